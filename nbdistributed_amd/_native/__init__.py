@@ -1,0 +1,160 @@
+"""Builders and loaders for the framework's native code.
+
+Two native artefacts live in this directory, both built in-tree so they travel with the
+repository snapshot (they are git-ignored, never pip-installed):
+
+* ``libnbd_transport.so`` — the C++17 ZMTP/3.1 DEALER/ROUTER control-plane transport
+  (``csrc/transport``).  Plain ``g++``; no GPU, no Python headers (C ABI, loaded with ctypes),
+  so the same library serves the PyTorch workers and a torch-less IPython coordinator.
+* ``libnbd_ops.so`` — the CDNA4 (gfx950) HIP kernels (``csrc/kernels``) registered as
+  ``torch.ops.nbd.*`` through ``TORCH_LIBRARY``; built with ``hipcc --offload-arch=gfx950`` and
+  loaded with ``torch.ops.load_library``.
+
+Builds are incremental: a library is rebuilt only when a source is newer than it.
+"""
+from __future__ import annotations
+
+import fcntl
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+from typing import List, Optional
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parent.parent
+CSRC = REPO / "csrc"
+
+TRANSPORT_LIB = HERE / "libnbd_transport.so"
+OPS_LIB = HERE / "libnbd_ops.so"
+
+TRANSPORT_SOURCES = [CSRC / "transport" / "nbd_transport.cpp"]
+TRANSPORT_HEADERS = [CSRC / "transport" / "nbd_transport.h"]
+
+OPS_HIP_SOURCES = sorted((CSRC / "kernels").glob("*.hip")) if (CSRC / "kernels").exists() else []
+OPS_CPP_SOURCES = sorted((CSRC / "kernels").glob("*.cpp")) if (CSRC / "kernels").exists() else []
+OPS_HEADERS = sorted((CSRC / "kernels").glob("*.h")) if (CSRC / "kernels").exists() else []
+
+GPU_ARCH = os.environ.get("NBD_GPU_ARCH", "gfx950")
+
+
+def _stale(target: Path, deps: List[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.exists() and d.stat().st_mtime > t for d in deps)
+
+
+class _BuildLock:
+    """Cross-process lock so parallel test workers don't race on the same output file."""
+
+    def __init__(self, name: str):
+        self.path = HERE / f".{name}.lock"
+
+    def __enter__(self):
+        self.fh = open(self.path, "w")
+        fcntl.flock(self.fh, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        fcntl.flock(self.fh, fcntl.LOCK_UN)
+        self.fh.close()
+
+
+def _run(cmd: List[str], env: Optional[dict] = None) -> None:
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+    if proc.returncode != 0:
+        raise RuntimeError(f"native build failed ({proc.returncode}):\n$ {' '.join(cmd)}\n{proc.stdout}")
+
+
+def build_transport(force: bool = False, sanitize: Optional[str] = None, out: Optional[Path] = None) -> Path:
+    """Compile libnbd_transport.so (g++, -O2, C++17).  ``sanitize`` = 'thread'|'address' builds
+    an instrumented copy at ``out`` (used by the host-side sanitizer tests)."""
+    target = Path(out) if out else TRANSPORT_LIB
+    with _BuildLock("transport"):
+        if not force and sanitize is None and not _stale(target, TRANSPORT_SOURCES + TRANSPORT_HEADERS):
+            return target
+        cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+        cmd = [cxx, "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall",
+               "-static-libstdc++", "-static-libgcc",
+               f"-I{CSRC / 'transport'}"]
+        if sanitize:
+            cmd += [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer"]
+        tmp = target.with_suffix(f".tmp{os.getpid()}.so")
+        cmd += ["-o", str(tmp)] + [str(s) for s in TRANSPORT_SOURCES]
+        _run(cmd)
+        os.replace(tmp, target)
+    return target
+
+
+def _torch_build_flags() -> tuple:
+    import torch
+    from torch.utils import cpp_extension
+
+    inc = cpp_extension.include_paths()
+    libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cflags = [f"-I{p}" for p in inc] + [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H"]
+    ldflags = [f"-L{libdir}", f"-Wl,-rpath,{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-lc10_hip", "-ltorch_hip"]
+    return cflags, ldflags
+
+
+def hipcc_path() -> str:
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    p = Path(rocm) / "bin" / "hipcc"
+    return str(p) if p.exists() else (shutil.which("hipcc") or "hipcc")
+
+
+def build_ops(force: bool = False, jobs: int = 4) -> Path:
+    """Compile the gfx950 HIP kernels + TORCH_LIBRARY registrations into libnbd_ops.so.
+
+    Each source is compiled separately (parallel) to an object, then linked.  hipcc
+    cross-compiles for gfx950 without a GPU present."""
+    deps = OPS_HIP_SOURCES + OPS_CPP_SOURCES + OPS_HEADERS
+    with _BuildLock("ops"):
+        if not force and not _stale(OPS_LIB, deps):
+            return OPS_LIB
+        cflags, ldflags = _torch_build_flags()
+        hipcc = hipcc_path()
+        objdir = HERE / "build"
+        objdir.mkdir(exist_ok=True)
+        common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'kernels'}", "-D__HIP_PLATFORM_AMD__",
+                  "-Wno-unused-result", "-Wno-deprecated-declarations"] + cflags
+        procs = []
+        objs = []
+        for src in OPS_HIP_SOURCES + OPS_CPP_SOURCES:
+            obj = objdir / (src.name + ".o")
+            objs.append(obj)
+            if not force and not _stale(obj, [src] + OPS_HEADERS):
+                continue
+            if src.suffix == ".hip":
+                cmd = [hipcc, f"--offload-arch={GPU_ARCH}", "-x", "hip", "-c", str(src), "-o", str(obj)] + common
+            else:
+                cmd = [hipcc, "-c", str(src), "-o", str(obj)] + common
+            procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+            if len(procs) >= jobs:
+                _wait(procs.pop(0))
+        while procs:
+            _wait(procs.pop(0))
+        tmp = OPS_LIB.with_suffix(f".tmp{os.getpid()}.so")
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={GPU_ARCH}", "-o", str(tmp)] + [str(o) for o in objs] + ldflags)
+        os.replace(tmp, OPS_LIB)
+    return OPS_LIB
+
+
+def _wait(item) -> None:
+    cmd, proc = item
+    out, _ = proc.communicate()
+    if proc.returncode != 0:
+        raise RuntimeError(f"native build failed ({proc.returncode}):\n$ {' '.join(cmd)}\n{out}")
+
+
+def build_all(force: bool = False) -> None:
+    build_transport(force=force)
+    build_ops(force=force)
+
+
+if __name__ == "__main__":  # python -m nbdistributed_amd._native [--force]
+    build_all(force="--force" in sys.argv)
+    print(TRANSPORT_LIB, OPS_LIB)

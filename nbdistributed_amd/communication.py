@@ -1,0 +1,394 @@
+"""Coordinator side of the control plane.
+
+Reference: ``src/nbdistributed/communication.py`` — a pyzmq ROUTER bound on ``tcp://*``
+(:121-125), a background thread that polls every 100 ms (:168-202), an ``Event`` that only ever
+fires for ``send_to_all`` (:193-197), a 10 ms sleep-poll for subset requests (:348-370),
+timeouts that leak table entries and drop partial results (:262, :359).
+
+Re-design:
+
+* native ROUTER (``transport``), bound to a private Unix socket (or loopback/explicit TCP for
+  attach mode) with a per-session token (D-17);
+* one receive thread blocked in native ``recv`` (no polling); every request — all ranks or a
+  subset — completes through the same lock-protected table of ``PendingRequest`` objects whose
+  completion and live events (stream chunks, responses, deaths) are pushed the instant they
+  arrive (D-4);
+* fail-fast: a rank that dies (process exit reported by the launcher, socket EOF, or heartbeat
+  timeout) resolves every request waiting on it with a ``dead`` entry, keeping the other ranks'
+  results (D-18); a send to a disconnected rank fails immediately (ROUTER_MANDATORY);
+* streamed output is decoded incrementally per (rank, stream) and routed by request id; output
+  that arrives outside a request (background threads) goes to ``output_callback``.
+
+The reference's programmatic API is kept: ``send_to_all``, ``send_to_rank``, ``send_to_ranks``,
+``set_output_callback``, ``shutdown``, ``Message``.
+"""
+from __future__ import annotations
+
+import codecs
+import itertools
+import os
+import queue
+import secrets
+import shutil
+import tempfile
+import threading
+import time
+from typing import Any, Callable, Dict, Iterable, List, Optional
+
+from . import protocol as P
+from .protocol import Message  # noqa: F401  (re-exported: reference API)
+from .transport import (EV_AUTH_FAILED, EV_CONNECTED, EV_DISCONNECTED, EV_HANDSHAKE_FAILED, EV_HEARTBEAT_TIMEOUT,
+                        ROUTER, HostUnreachable, Socket, TransportError)
+
+OutputCallback = Callable[[int, str, str], None]
+
+MAX_CAPTURED_OUTPUT = 1 << 20  # per rank per request, kept for programmatic callers
+
+
+class RankDied(RuntimeError):
+    def __init__(self, rank: int, reason: str):
+        super().__init__(f"rank {rank} died: {reason}")
+        self.rank = rank
+        self.reason = reason
+
+
+class RequestTimeout(TimeoutError):
+    def __init__(self, msg: str, partial: Dict[int, Any]):
+        super().__init__(msg)
+        self.partial = partial
+
+
+class PendingRequest:
+    """One request in flight to a set of ranks."""
+
+    def __init__(self, seq: int, msg_type: str, ranks: List[int], live: bool):
+        self.seq = seq
+        self.msg_type = msg_type
+        self.ranks = list(ranks)
+        self.responses: Dict[int, Any] = {}
+        self.errors: Dict[int, bool] = {}
+        self.dead: Dict[int, str] = {}
+        self.outputs: Dict[int, List[str]] = {r: [] for r in ranks}
+        self._out_bytes: Dict[int, int] = {r: 0 for r in ranks}
+        self.events: Optional[queue.SimpleQueue] = queue.SimpleQueue() if live else None
+        self.done = threading.Event()
+        self.t_sent = time.perf_counter()
+        self.t_done: Optional[float] = None
+        self.t_first_reply: Dict[int, float] = {}
+        self._lock = threading.Lock()
+
+    def _maybe_done(self) -> None:
+        if len(self.responses) + len(self.dead) >= len(self.ranks) and not self.done.is_set():
+            self.t_done = time.perf_counter()
+            self.done.set()
+            if self.events is not None:
+                self.events.put(("done",))
+
+    def on_response(self, rank: int, data: Any, error: bool) -> None:
+        with self._lock:
+            if rank not in self.outputs or rank in self.responses or rank in self.dead:
+                return
+            self.responses[rank] = data
+            self.errors[rank] = error
+            self.t_first_reply[rank] = time.perf_counter()
+            if self.events is not None:
+                self.events.put(("response", rank))
+            self._maybe_done()
+
+    def on_stream(self, rank: int, stream: str, text: str) -> None:
+        with self._lock:
+            if rank in self.outputs and self._out_bytes[rank] < MAX_CAPTURED_OUTPUT:
+                self.outputs[rank].append(text)
+                self._out_bytes[rank] += len(text)
+            if self.events is not None:
+                self.events.put(("stream", rank, stream, text))
+
+    def on_dead(self, rank: int, reason: str) -> None:
+        with self._lock:
+            if rank not in self.outputs or rank in self.responses or rank in self.dead:
+                return
+            self.dead[rank] = reason
+            if self.events is not None:
+                self.events.put(("dead", rank, reason))
+            self._maybe_done()
+
+    def results(self) -> Dict[int, Any]:
+        """Per-rank results; dead ranks get an error dict, execute results carry the streamed
+        output merged into ``output`` (reference semantics)."""
+        out: Dict[int, Any] = {}
+        for r in self.ranks:
+            if r in self.responses:
+                d = self.responses[r]
+                if self.msg_type == "execute" and isinstance(d, dict):
+                    d = dict(d)
+                    streamed = "".join(self.outputs.get(r, []))
+                    echo = d.get("output") or ""
+                    d["output"] = streamed + echo
+                    d["echo"] = echo
+                out[r] = d
+            elif r in self.dead:
+                out[r] = {"error": f"rank {r} died: {self.dead[r]}", "dead": True, "rank": r}
+        return out
+
+
+class CommunicationManager:
+    """Coordinator endpoint: ROUTER socket + receive thread + request table."""
+
+    def __init__(self, num_processes: int, base_port: Optional[int] = None, output_callback: Optional[OutputCallback] = None,
+                 default_timeout: Optional[float] = None, endpoint: Optional[str] = None, token: Optional[str] = None,
+                 heartbeat_ivl_ms: Optional[int] = None, heartbeat_timeout_ms: Optional[int] = None):
+        from .config import get_config
+
+        cfg = get_config()
+        self.num_processes = num_processes
+        self.output_callback = output_callback
+        self.default_timeout = default_timeout
+        self.token = token if token is not None else (secrets.token_hex(16) if cfg.use_token else None)
+        self._tmpdir: Optional[str] = None
+        if endpoint is None:
+            if base_port is not None:
+                endpoint = f"tcp://{cfg.bind_host}:{base_port}"
+            elif cfg.transport == "tcp":
+                endpoint = f"tcp://{cfg.bind_host}:0"
+            else:
+                base = tempfile.gettempdir()
+                if len(base) > 60:
+                    base = "/tmp"
+                self._tmpdir = tempfile.mkdtemp(prefix="nbd-", dir=base)
+                os.chmod(self._tmpdir, 0o700)
+                endpoint = f"ipc://{self._tmpdir}/coord.sock"
+        self.sock = Socket(ROUTER, token=self.token.encode() if self.token else None,
+                           heartbeat_ivl_ms=cfg.heartbeat_ivl_ms if heartbeat_ivl_ms is None else heartbeat_ivl_ms,
+                           heartbeat_timeout_ms=cfg.heartbeat_timeout_ms if heartbeat_timeout_ms is None else heartbeat_timeout_ms,
+                           mandatory=True)
+        self.endpoint = self.sock.bind(endpoint)
+        self._seq = itertools.count(1)
+        self._lock = threading.Lock()
+        self.pending: Dict[int, PendingRequest] = {}
+        self.ready: Dict[int, Dict[str, Any]] = {}
+        self.connected: Dict[int, float] = {}
+        self.dead: Dict[int, str] = {}
+        self.ready_cv = threading.Condition(self._lock)
+        self._decoders: Dict[tuple, Any] = {}
+        self.background: "queue.SimpleQueue" = queue.SimpleQueue()
+        self.event_log: List[tuple] = []
+        self.running = True
+        self._closing = False
+        self.thread = threading.Thread(target=self._message_handler, name="nbd-comm", daemon=True)
+        self.thread.start()
+
+    # ------------------------------------------------------------------ reference API
+    def set_output_callback(self, callback: Optional[OutputCallback]) -> None:
+        self.output_callback = callback
+
+    def send_to_all(self, msg_type: str, data: Any = None, timeout: Optional[float] = None,
+                    raise_on_error: bool = False) -> Dict[int, Any]:
+        return self.send_to_ranks(list(range(self.num_processes)), msg_type, data, timeout, raise_on_error)
+
+    def send_to_rank(self, rank: int, msg_type: str, data: Any = None, timeout: Optional[float] = None) -> Any:
+        return self.send_to_ranks([rank], msg_type, data, timeout).get(rank)
+
+    def send_to_ranks(self, ranks: Iterable[int], msg_type: str, data: Any = None, timeout: Optional[float] = None,
+                      raise_on_error: bool = False) -> Dict[int, Any]:
+        req = self.submit(list(ranks), msg_type, data, live=False)
+        self.wait(req, timeout)
+        res = req.results()
+        if req.outputs and self.output_callback is not None and msg_type == "execute":
+            for r in req.ranks:
+                txt = "".join(req.outputs.get(r, []))
+                if txt:
+                    self.output_callback(r, txt, "stdout")
+        if raise_on_error:
+            for r, v in res.items():
+                if isinstance(v, dict) and v.get("dead"):
+                    raise RankDied(r, req.dead[r])
+        return res
+
+    # ------------------------------------------------------------------ async API
+    def submit(self, ranks: List[int], msg_type: str, data: Any = None, flags: int = 0, live: bool = True) -> PendingRequest:
+        mtype = P.TYPE_CODES[msg_type]
+        seq = next(self._seq)
+        req = PendingRequest(seq, msg_type, ranks, live)
+        e, body = P.encode_body(data)
+        header = P.pack_header(mtype, P.COORDINATOR_RANK, seq, P.S_NONE, e, flags)
+        with self._lock:
+            self.pending[seq] = req
+            dead_now = {r: self.dead[r] for r in ranks if r in self.dead}
+        for r, why in dead_now.items():
+            req.on_dead(r, why)
+        for r in ranks:
+            if r in dead_now:
+                continue
+            try:
+                self.sock.send([P.worker_identity(r), header, body])
+            except HostUnreachable:
+                req.on_dead(r, "not connected")
+            except TransportError as ex:
+                req.on_dead(r, f"send failed: {ex}")
+        return req
+
+    def wait(self, req: PendingRequest, timeout: Optional[float] = None) -> PendingRequest:
+        t = self.default_timeout if timeout is None else timeout
+        ok = req.done.wait(t) if t is not None else _wait_forever(req.done)
+        self._forget(req)
+        if not ok:
+            missing = [r for r in req.ranks if r not in req.responses and r not in req.dead]
+            raise RequestTimeout(f"{req.msg_type}: no reply from ranks {missing} within {t}s", req.results())
+        return req
+
+    def _forget(self, req: PendingRequest) -> None:
+        with self._lock:
+            self.pending.pop(req.seq, None)
+
+    def interrupt(self, ranks: Optional[List[int]] = None) -> None:
+        """Out-of-band interrupt: the workers' native I/O thread raises SIGINT on arrival."""
+        ranks = list(range(self.num_processes)) if ranks is None else ranks
+        header = P.pack_header(P.T_INTERRUPT, P.COORDINATOR_RANK, 0, P.S_NONE, P.E_NONE, 0)
+        for r in ranks:
+            try:
+                self.sock.send([P.worker_identity(r), header, b""])
+            except TransportError:
+                pass
+
+    # ------------------------------------------------------------------ liveness
+    def mark_dead(self, rank: int, reason: str) -> None:
+        with self._lock:
+            if self._closing:
+                return
+            prev = self.dead.get(rank)
+            if prev is not None and "exit code" in prev:
+                return
+            self.dead[rank] = reason
+            reqs = list(self.pending.values())
+            self.ready_cv.notify_all()
+        for req in reqs:
+            req.on_dead(rank, reason)
+        self.event_log.append((time.time(), "dead", rank, reason))
+
+    def wait_ready(self, ranks: List[int], timeout: Optional[float], alive: Optional[Callable[[], Dict[int, int]]] = None) -> Dict[int, Dict[str, Any]]:
+        """Block until every rank has sent READY.  Raises RuntimeError with the worker's own
+        error if a bootstrap fails, or if a process exits first."""
+        deadline = None if timeout is None else time.monotonic() + timeout
+        with self._lock:
+            while True:
+                errs = {r: self.ready[r] for r in ranks if r in self.ready and "error" in self.ready[r]}
+                if errs:
+                    r, e = next(iter(errs.items()))
+                    raise RuntimeError(f"rank {r} failed to start: {e['error']}\n{e.get('traceback', '')}")
+                dead = {r: self.dead[r] for r in ranks if r in self.dead}
+                if dead:
+                    raise RuntimeError(f"workers exited during startup: {dead}")
+                if all(r in self.ready for r in ranks):
+                    return {r: self.ready[r] for r in ranks}
+                if alive is not None:
+                    exited = {r: c for r, c in alive().items() if r in ranks}
+                    if exited:
+                        raise RuntimeError(f"workers exited during startup (rank: exit code): {exited}")
+                remaining = None if deadline is None else deadline - time.monotonic()
+                if remaining is not None and remaining <= 0:
+                    missing = [r for r in ranks if r not in self.ready]
+                    raise TimeoutError(f"ranks {missing} not ready after {timeout}s")
+                self.ready_cv.wait(0.2 if remaining is None else min(0.2, remaining))
+
+    # ------------------------------------------------------------------ receive thread
+    def _decode_stream(self, rank: int, stream: int, body: bytes) -> str:
+        key = (rank, stream)
+        dec = self._decoders.get(key)
+        if dec is None:
+            dec = self._decoders[key] = codecs.getincrementaldecoder("utf-8")(errors="replace")
+        return dec.decode(body)
+
+    def _message_handler(self) -> None:
+        while self.running:
+            try:
+                m = self.sock.recv(timeout=None)
+            except TransportError:
+                break
+            if m is None:
+                continue
+            if m.is_event:
+                self._on_event(m.event, P.rank_of_identity(m.identity))
+                continue
+            if len(m.frames) < 2:
+                continue
+            rank = P.rank_of_identity(m.frames[0])
+            try:
+                h = P.unpack_header(m.frames[1])
+            except ValueError:
+                continue
+            body = m.frames[2] if len(m.frames) > 2 else b""
+            if rank is None:
+                rank = h.rank
+            if h.mtype == P.T_STREAM:
+                text = self._decode_stream(rank, h.stream, body)
+                if not text:
+                    continue
+                stream = P.STREAM_NAMES.get(h.stream, "stdout")
+                with self._lock:
+                    req = self.pending.get(h.seq)
+                if req is not None and rank in req.outputs:
+                    req.on_stream(rank, stream, text)
+                else:
+                    cb = self.output_callback
+                    if cb is not None:
+                        try:
+                            cb(rank, text, stream)
+                        except Exception:
+                            pass
+                    else:
+                        self.background.put((rank, stream, text))
+                continue
+            try:
+                data = P.decode_body(h.enc, body)
+            except Exception as e:
+                data = {"error": f"undecodable reply: {e}", "rank": rank}
+            if h.mtype == P.T_RESPONSE:
+                with self._lock:
+                    req = self.pending.get(h.seq)
+                if req is not None:
+                    req.on_response(rank, data, bool(h.flags & P.F_ERROR))
+            elif h.mtype == P.T_READY:
+                with self._lock:
+                    self.ready[rank] = data if isinstance(data, dict) else {"status": data}
+                    self.ready_cv.notify_all()
+
+    def _on_event(self, event: int, rank: Optional[int]) -> None:
+        if rank is None:
+            return
+        self.event_log.append((time.time(), event, rank))
+        if event == EV_CONNECTED:
+            with self._lock:
+                self.connected[rank] = time.time()
+                if rank in self.dead and "exit code" not in self.dead[rank]:
+                    self.dead.pop(rank)  # reconnected (attach mode)
+        elif event in (EV_DISCONNECTED, EV_HEARTBEAT_TIMEOUT):
+            with self._lock:
+                self.connected.pop(rank, None)
+                closing = self._closing
+            if not closing:
+                why = "heartbeat timeout (no traffic from the worker)" if event == EV_HEARTBEAT_TIMEOUT else "connection lost"
+                self.mark_dead(rank, why)
+        elif event in (EV_HANDSHAKE_FAILED, EV_AUTH_FAILED):
+            pass
+
+    # ------------------------------------------------------------------ teardown
+    def shutdown(self) -> None:
+        with self._lock:
+            self._closing = True
+            self.running = False
+            reqs = list(self.pending.values())
+        for req in reqs:
+            for r in req.ranks:
+                req.on_dead(r, "coordinator shut down")
+        self.sock.close()
+        self.thread.join(timeout=2.0)
+        if self._tmpdir:
+            shutil.rmtree(self._tmpdir, ignore_errors=True)
+
+
+def _wait_forever(ev: threading.Event) -> bool:
+    # Event.wait() without timeout is not interruptible on some Pythons; loop in slices so a
+    # KeyboardInterrupt in the kernel's main thread is delivered promptly.
+    while not ev.wait(0.5):
+        pass
+    return True

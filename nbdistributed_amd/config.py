@@ -1,0 +1,56 @@
+"""One place for every tunable, with ``NBD_*`` environment overrides.
+
+The reference has no configuration beyond magic flags and hard-codes its timings
+(100 ms display poll ``magic.py:1094``, 10 ms completion poll
+``communication.py:358``, 2 s startup sleep ``process_manager.py:137``, 5 s status timeout
+``process_manager.py:365``...).  Here none of those sleeps exist (everything is event-driven);
+what remains configurable is listed below.
+"""
+from __future__ import annotations
+
+import os
+import sys
+from dataclasses import dataclass, field, fields
+
+
+def _env(name: str, default, cast=str):
+    v = os.environ.get(name)
+    if v is None or v == "":
+        return default
+    if cast is bool:
+        return v.lower() in ("1", "true", "yes", "on")
+    return cast(v)
+
+
+@dataclass
+class Config:
+    # worker launch
+    worker_python: str = field(default_factory=lambda: _env("NBD_WORKER_PYTHON", sys.executable))
+    startup_timeout_s: float = field(default_factory=lambda: _env("NBD_STARTUP_TIMEOUT", 600.0, float))
+    # transport
+    transport: str = field(default_factory=lambda: _env("NBD_TRANSPORT", "ipc"))  # ipc | tcp
+    bind_host: str = field(default_factory=lambda: _env("NBD_BIND_HOST", "127.0.0.1"))
+    heartbeat_ivl_ms: int = field(default_factory=lambda: _env("NBD_HEARTBEAT_IVL_MS", 1000, int))
+    heartbeat_timeout_ms: int = field(default_factory=lambda: _env("NBD_HEARTBEAT_TIMEOUT_MS", 15000, int))
+    stream_flush_us: int = field(default_factory=lambda: _env("NBD_STREAM_FLUSH_US", 2000, int))
+    use_token: bool = field(default_factory=lambda: _env("NBD_TOKEN_AUTH", True, bool))
+    # data plane
+    backend: str = field(default_factory=lambda: _env("NBD_BACKEND", "auto"))  # auto | rccl | nccl | gloo
+    eager_comm_init: bool = field(default_factory=lambda: _env("NBD_EAGER_COMM_INIT", True, bool))
+    # interrupt handling: seconds after SIGINT before the worker aborts its communicator
+    interrupt_abort_s: float = field(default_factory=lambda: _env("NBD_INTERRUPT_ABORT_S", 10.0, float))
+    # REPL echo of tensors: auto | repr | summary
+    echo_mode: str = field(default_factory=lambda: _env("NBD_ECHO", "auto"))
+    echo_summary_min_numel: int = field(default_factory=lambda: _env("NBD_ECHO_SUMMARY_MIN_NUMEL", 1001, int))
+    # namespace -> local proxy sync after %%distributed cells (IDE support)
+    ide_sync: bool = field(default_factory=lambda: _env("NBD_IDE_SYNC", True, bool))
+    # timeline ring buffer
+    timeline_capacity: int = field(default_factory=lambda: _env("NBD_TIMELINE_CAPACITY", 2000, int))
+    log_level: str = field(default_factory=lambda: _env("NBD_LOG_LEVEL", "WARNING"))
+
+    def as_dict(self):
+        return {f.name: getattr(self, f.name) for f in fields(self)}
+
+
+def get_config() -> Config:
+    return Config()

@@ -1,0 +1,544 @@
+"""IPython magics — the notebook-facing API — as a thin adapter over ``Session``.
+
+Reference: ``src/nbdistributed/magic.py`` (``DistributedMagic``, :62-1870).  Every magic name,
+flag and default is kept:
+
+    %dist_init [-n N=2] [-a ADDR=localhost] [-g "0,1,..."] [-t SECONDS=None]
+    %%distributed            %%rank [spec]   (spec: [0,1,2] | [0-2] | [0-2,5]; "%%rank[0]" works too)
+    %sync   %dist_status   %dist_mode [-e|-d]   %dist_shutdown   %dist_reset [-n]
+    %dist_debug   %dist_sync_ide   %timeline_save [path]   %timeline_debug   %timeline_clear
+
+plus new ones: ``%dist_interrupt [--hard]``, ``%dist_recover``, ``%dist_pull``, ``%dist_push``,
+``%dist_profile start|stop``, ``%dist_bench``, ``%dist_attach``.
+
+The logic lives in ``MagicCore`` (no IPython import), so it runs — and is tested — in the
+PyTorch interpreter, which has no IPython; ``register()`` wraps it for a real shell.
+
+Behaviour fixes over the reference: working shutdown/unload (D-1); auto mode
+leaves ``!shell``, ``?help`` and frontend-internal cells local (D-7); ``%%rank[0]`` accepted
+(D-6); failures raise so the notebook marks the cell failed (D-9); one timeline record per
+cell, nothing re-serialised per cell (D-5); IDE proxies never clobber local names and use meta
+tensors (D-14); ``%dist_reset`` kills only this session's process groups (D-16).
+"""
+from __future__ import annotations
+
+import argparse
+import re
+import shlex
+import sys
+import time
+from typing import Any, Callable, Dict, List, Optional
+
+from .proxies import ProxyTable
+from .session import DistributedExecutionError, Session, _default_writer
+from .utils.ranks import RankSpecError, format_ranks, parse_ranks
+
+FRONTEND_MARKERS = ("__jupyter_exec_background__", "_VSCODE_", "__vsc_ipynb_file__", "_vscode_",
+                    "get_ipython().kernel", "_ipython_display_formatter")
+_RANK_NOSPACE = re.compile(r"^(\s*%%rank)\[")
+
+
+class MagicUsageError(Exception):
+    pass
+
+
+class _ArgParser(argparse.ArgumentParser):
+    def error(self, message):
+        raise MagicUsageError(f"{self.prog}: {message}")
+
+    def exit(self, status=0, message=None):
+        if message:
+            raise MagicUsageError(message)
+        raise MagicUsageError("")
+
+
+def _parser(prog: str) -> _ArgParser:
+    return _ArgParser(prog=prog, add_help=True)
+
+
+def _init_parser() -> _ArgParser:
+    p = _parser("%dist_init")
+    p.add_argument("--num-processes", "-n", type=int, default=2, help="Number of worker processes (one per GPU)")
+    p.add_argument("--master-addr", "-a", type=str, default="localhost", help="Master address")
+    p.add_argument("--gpu-ids", "-g", type=str, default=None, help="Comma-separated GPU ids, e.g. '0,1,3'")
+    p.add_argument("--timeout", "-t", type=float, default=None, help="Default request timeout in seconds (None = wait forever)")
+    p.add_argument("--backend", "-b", type=str, default="auto", help="auto | rccl | nccl | gloo")
+    p.add_argument("--python", type=str, default=None, help="worker interpreter (default: this kernel's)")
+    return p
+
+
+def auto_mode_transform(lines: List[str]) -> List[str]:
+    """Input transformer used in auto mode (reference magic.py:709-741): ship plain cells to
+    the workers by prefixing ``%%distributed``; leave magics, shell escapes, help requests and
+    frontend-internal cells alone."""
+    text = "".join(lines)
+    stripped_lines = [l.strip() for l in lines]
+    code_lines = [l for l in stripped_lines if l and not l.startswith("#")]
+    if not code_lines:
+        return lines
+    first = code_lines[0]
+    if first.startswith(("%", "!", "?")):
+        return lines
+    if len(code_lines) == 1 and first.endswith("?") and not first.endswith("??)"):
+        return lines  # obj? / obj?? help
+    if any(m in text for m in FRONTEND_MARKERS):
+        return lines
+    if lines and not lines[-1].endswith("\n"):
+        lines = lines[:-1] + [lines[-1] + "\n"]
+    return ["%%distributed\n"] + lines
+
+
+def rank_nospace_transform(lines: List[str]) -> List[str]:
+    """Accept ``%%rank[0]`` (IPython would look for a magic named ``rank[0]``; reference D-6)."""
+    if lines and _RANK_NOSPACE.match(lines[0]):
+        lines = [_RANK_NOSPACE.sub(r"\1 [", lines[0], count=1)] + lines[1:]
+    return lines
+
+
+class MagicCore:
+    """All magic behaviour, independent of IPython."""
+
+    def __init__(self, shell: Any = None, writer: Optional[Callable[[str], None]] = None):
+        self.shell = shell
+        self.write = writer or _default_writer
+        self.session = Session(writer=self.write)
+        self.proxies = ProxyTable()
+        self.auto_mode = False
+        self.ide_sync = self.session.cfg.ide_sync
+
+    # ------------------------------------------------------------------ helpers
+    def p(self, *args) -> None:
+        self.write(" ".join(str(a) for a in args) + "\n")
+
+    @property
+    def user_ns(self) -> Dict[str, Any]:
+        return getattr(self.shell, "user_ns", {}) if self.shell is not None else {}
+
+    def _transformers(self) -> Optional[list]:
+        return getattr(self.shell, "input_transformers_cleanup", None) if self.shell is not None else None
+
+    def enable_auto(self) -> None:
+        tr = self._transformers()
+        if tr is not None and auto_mode_transform not in tr:
+            tr.append(auto_mode_transform)
+        self.auto_mode = True
+
+    def disable_auto(self) -> None:
+        tr = self._transformers()
+        if tr is not None:
+            while auto_mode_transform in tr:
+                tr.remove(auto_mode_transform)
+        self.auto_mode = False
+
+    def _apply_delta(self, res) -> None:
+        if self.ide_sync and res is not None and res.ns_delta and self.shell is not None:
+            try:
+                self.proxies.apply(self.user_ns, res.ns_delta)
+            except Exception:
+                pass
+
+    # ------------------------------------------------------------------ %dist_init
+    def dist_init(self, line: str) -> None:
+        args = _init_parser().parse_args(shlex.split(line))
+        s = self.session
+        if s.active:
+            alive = s.alive_ranks()
+            if len(alive) == s.num_processes:
+                self.p("Distributed workers already running. Use %dist_shutdown to stop them first.")
+                return
+            self.p(f"⚠️  Replacing a degraded session ({len(alive)}/{s.num_processes} ranks alive)...")
+            s.shutdown(graceful=False)
+        gpu_ids = None
+        if args.gpu_ids:
+            try:
+                gpu_ids = [int(x.strip()) for x in args.gpu_ids.split(",") if x.strip()]
+            except ValueError:
+                self.p("❌ Invalid GPU IDs format. Use comma-separated integers (e.g., '0,1,3')")
+                return
+            from .utils.devices import visible_gpu_count
+
+            n = visible_gpu_count()
+            if n > 0:
+                bad = [g for g in gpu_ids if not 0 <= g < n]
+                if bad:
+                    self.p(f"❌ Invalid GPU IDs: {bad}")
+                    self.p(f"Available GPUs: {list(range(n))}")
+                    return
+                if len(gpu_ids) < args.num_processes:
+                    self.p(f"❌ Not enough GPU IDs specified. Need {args.num_processes}, got {len(gpu_ids)}")
+                    self.p("Either specify more GPU IDs or reduce --num-processes")
+                    return
+            else:
+                self.p("⚠️  No GPU visible: GPU IDs will be ignored")
+                gpu_ids = None
+            if gpu_ids:
+                self.p(f"Using GPU IDs: {gpu_ids}")
+        self.p(f"Starting {args.num_processes} distributed workers...")
+        t0 = time.perf_counter()
+        try:
+            ready = s.start(args.num_processes, args.master_addr, gpu_ids, timeout=args.timeout,
+                            backend=args.backend, python=args.python)
+        except Exception as e:
+            self.p(f"Failed to start distributed workers: {e}")
+            return
+        dt = time.perf_counter() - t0
+        self.p(f"✓ Successfully started {args.num_processes} workers in {dt:.2f}s "
+               f"(backend: {ready[0].get('backend')})")
+        for r in sorted(ready):
+            st = ready[r]
+            if st.get("cuda_available"):
+                self.p(f"  Rank {r} -> GPU {st.get('gpu_id')} ({st.get('gpu_name')}, {st.get('gcn_arch', '')}, "
+                       f"{st.get('gpu_memory_total', 0):.0f} GB HBM) pid {st.get('pid')}")
+            elif gpu_ids:
+                self.p(f"  Rank {r} -> GPU {gpu_ids[r]}")
+        self.p("Available commands:")
+        self.p("  %%distributed - Execute code on all ranks (explicit)")
+        self.p("  %%rank [0,n] - Execute code on specific ranks")
+        self.p("  %sync - Synchronize all ranks")
+        self.p("  %dist_status - Show worker status")
+        self.p("  %dist_mode - Toggle automatic distributed mode")
+        self.p("  %dist_interrupt - Interrupt running cells on the workers")
+        self.p("  %dist_shutdown - Shutdown workers")
+        self.p()
+        self.p("🚀 Distributed mode active: All cells will now execute on workers automatically!")
+        self.p("   Magic commands (%, %%) will still execute locally as normal.")
+        self.p()
+        self.p("🐍 Below are auto-imported and special variables auto-generated into the namespace to use")
+        self.p("  `torch`")
+        self.p("  `dist`: `torch.distributed` import alias")
+        self.p("  `rank` (`int`): The local rank")
+        self.p("  `world_size` (`int`): The global world size")
+        self.p("  `gpu_id` (`int`): The specific GPU ID assigned to this worker")
+        self.p("  `device` (`torch.device`): The current PyTorch device object (e.g. `cuda:1`)")
+        self.p("  `nbd`: this framework (nbd.ops HIP kernels, nbd.parallel, nbd.models)")
+        self.enable_auto()
+
+    # ------------------------------------------------------------------ cells
+    def distributed(self, line: str, cell: str) -> Any:
+        s = self.session
+        if not s.active:
+            self.p("No distributed workers running. Use %dist_init first.")
+            return None
+        res = s.execute(cell, ns_delta=self.ide_sync, raise_on_error=False)
+        self._apply_delta(res)
+        if not res.ok:
+            raise DistributedExecutionError(res)
+        return None
+
+    def rank(self, line: str, cell: str) -> Any:
+        s = self.session
+        if not s.active:
+            self.p("No distributed workers running. Use %dist_init first.")
+            return None
+        spec = line.strip()
+        try:
+            ranks = parse_ranks(spec, s.num_processes) if spec else []
+        except RankSpecError as e:
+            self.p(f"❌ {e}")
+            ranks = []
+        if not ranks:
+            self.p("Usage: %%rank [0,1,2] or %%rank [0-2]  (ranks in range 0.."
+                   f"{max(0, s.num_processes - 1)})")
+            return None
+        res = s.execute(cell, ranks=ranks, kind=f"rank[{format_ranks(ranks)}]", ns_delta=self.ide_sync and 0 in ranks,
+                        raise_on_error=False)
+        self._apply_delta(res)
+        if not res.ok:
+            raise DistributedExecutionError(res)
+        return None
+
+    # ------------------------------------------------------------------ line magics
+    def sync(self, line: str = "") -> None:
+        s = self.session
+        if not s.active:
+            self.p("No distributed workers running. Use %dist_init first.")
+            return
+        t0 = time.perf_counter()
+        try:
+            res = s.sync()
+        except Exception as e:
+            self.p(f"Error synchronizing ranks: {e}")
+            return
+        bad = {r: v for r, v in res.items() if isinstance(v, dict) and "error" in v}
+        if bad:
+            self.p(f"⚠️  Synchronized {len(res) - len(bad)} ranks; failed: " +
+                   ", ".join(f"rank {r}: {v['error']}" for r, v in bad.items()))
+        else:
+            self.p(f"✓ Synchronized {len(res)} ranks ({(time.perf_counter() - t0) * 1e3:.2f} ms)")
+
+    def dist_status(self, line: str = "") -> None:
+        s = self.session
+        if not s.active:
+            self.p("No distributed workers running")
+            return
+        st = s.status()
+        self.p(f"Distributed cluster status ({s.num_processes} processes):")
+        self.p("=" * 60)
+        for r in sorted(st):
+            info = st[r]
+            ok = info.get("running") and "dead_reason" not in info
+            self.p(f"Rank {r}: {'✓' if ok else '✗'} PID {info.get('pid')}")
+            if info.get("cuda_available"):
+                self.p(f"  ├─ GPU: {info.get('gpu_id')} ({info.get('gpu_name')} {info.get('gcn_arch', '')}) "
+                       f"local device {info.get('current_device')}")
+                tot = info.get("gpu_memory_total", 0.0) or 0.0
+                alloc = info.get("gpu_memory_allocated", 0.0)
+                used = info.get("gpu_memory_used", 0.0)
+                pct = alloc / tot * 100 if tot else 0.0
+                self.p(f"  ├─ Memory: {alloc:.1f}GB / {tot:.1f}GB ({pct:.1f}% used)")
+                self.p(f"  ├─ Reserved: {info.get('gpu_memory_reserved', 0.0):.1f}GB   HBM in use (all procs): {used:.1f}GB")
+                self.p(f"  ├─ Backend: {info.get('backend')} (RCCL {info.get('rccl_version')})  HIP {info.get('hip_version')}")
+            else:
+                self.p(f"  ├─ Device: {info.get('gpu_name', 'CPU')}  backend {info.get('backend')}")
+            if info.get("running") and "dead_reason" not in info:
+                self.p(f"  └─ Status: Running ({info.get('cells', 0)} cells)")
+            else:
+                why = info.get("dead_reason") or ""
+                self.p(f"  └─ Status: Stopped (exit code: {info.get('returncode', 'unknown')}) {why}")
+            self.p()
+        lc = s.last_cell
+        if lc is not None:
+            self.p(f"Last cell: {lc.duration_s * 1e3:.2f} ms round trip on ranks {format_ranks(lc.ranks)}")
+
+    def dist_mode(self, line: str = "") -> None:
+        p = _parser("%dist_mode")
+        p.add_argument("--enable", "-e", action="store_true")
+        p.add_argument("--disable", "-d", action="store_true")
+        args = p.parse_args(shlex.split(line))
+        if not self.session.active:
+            self.p("No distributed workers running. Use %dist_init first.")
+            return
+        if args.enable and args.disable:
+            self.p("Cannot specify both --enable and --disable")
+            return
+        if args.enable:
+            if not self.auto_mode:
+                self.enable_auto()
+                self.p("🚀 Distributed mode enabled: Regular cells will execute on workers")
+            else:
+                self.p("Distributed mode is already enabled")
+        elif args.disable:
+            if self.auto_mode:
+                self.disable_auto()
+                self.p("📱 Distributed mode disabled: Regular cells will execute locally")
+            else:
+                self.p("Distributed mode is already disabled")
+        else:
+            self.p(f"Distributed mode is currently {'enabled' if self.auto_mode else 'disabled'}")
+            self.p("Use %dist_mode --enable or %dist_mode --disable to toggle")
+
+    def dist_shutdown(self, line: str = "") -> None:
+        s = self.session
+        if not s.active:
+            self.p("No distributed workers running")
+            self.disable_auto()
+            return
+        n = s.num_processes
+        self.p(f"Shutting down {n} workers...")
+        s.shutdown(graceful=True)
+        self.disable_auto()
+        self.proxies.clear(self.user_ns)
+        self.p("✓ Distributed workers shut down")
+
+    def dist_reset(self, line: str = "") -> None:
+        p = _parser("%dist_reset")
+        p.add_argument("--nuclear", "-n", action="store_true", help="SIGKILL immediately")
+        args = p.parse_args(shlex.split(line))
+        s = self.session
+        self.p("🔄 Resetting distributed environment...")
+        if s.active:
+            s.shutdown(graceful=not args.nuclear)
+        self.disable_auto()
+        self.proxies.clear(self.user_ns)
+        self.session = Session(writer=self.write)
+        self.p("✓ Reset complete (only this session's worker process groups were signalled)")
+
+    def dist_debug(self, line: str = "") -> None:
+        s = self.session
+        self.p("=== Distributed Debug Information ===")
+        self.p(f"Session active: {s.active}")
+        self.p(f"Process manager exists: {s.pm is not None}")
+        self.p(f"Communication manager exists: {s.comm is not None}")
+        self.p(f"Number of processes: {s.num_processes}")
+        self.p(f"Distributed mode active: {self.auto_mode}")
+        if s.comm is not None:
+            self.p(f"Control endpoint: {s.comm.endpoint}  (token auth: {bool(s.comm.token)})")
+            self.p(f"Connected peers: {s.comm.sock.peer_count}  dead: {s.comm.dead or '{}'}")
+            self.p(f"Requests in flight: {len(s.comm.pending)}")
+        if s.pm is not None:
+            self.p(f"Process manager is_running(): {s.pm.is_running()}")
+            self.p(f"Number of processes tracked: {len(s.pm.workers)}")
+            for w in s.pm.workers:
+                rc = w.proc.poll()
+                self.p(f"  Process {w.rank} (PID: {w.pid}): {'Running' if rc is None else f'Dead (exit code: {rc})'}"
+                       f"  GPU {w.gpu_id} -> local device {w.device_index}")
+        if s.comm is not None and s.active:
+            try:
+                rt = s.ping(timeout=2.0)
+                self.p("Control-plane round trip: " + ", ".join(f"r{r} {t * 1e6:.0f} µs" for r, t in sorted(rt.items())))
+            except Exception as e:
+                self.p(f"ping failed: {e}")
+        self.p("=====================================")
+
+    def dist_sync_ide(self, line: str = "") -> None:
+        s = self.session
+        if not s.active:
+            self.p("No distributed workers running. Use %dist_init first.")
+            return
+        info = s.namespace_info(0)
+        if isinstance(info, dict) and "error" in info and "dead" in info:
+            self.p(f"❌ {info['error']}")
+            return
+        delta = {"changed": list(info.values()), "removed": [n for n in self.proxies.owned if n not in info]}
+        n = self.proxies.apply(self.user_ns, delta)
+        self.p(f"✓ Synchronized {n} names from rank 0 into the local namespace")
+
+    def timeline_save(self, line: str = "") -> None:
+        path = line.strip() or f"nbd_timeline_{int(time.time())}.json"
+        out = self.session.timeline.save(path)
+        self.p(f"✓ Timeline saved: {out['json']}  (Chrome trace: {out['trace']})")
+
+    def timeline_debug(self, line: str = "") -> None:
+        if self.session.active:
+            try:
+                self.session.status(timeout=2.0)  # pulls pending GPU timings
+            except Exception:
+                pass
+        self.p(self.session.timeline.summary())
+
+    def timeline_clear(self, line: str = "") -> None:
+        n = self.session.timeline.clear()
+        self.p(f"✓ Cleared {n} timeline records")
+
+    # ------------------------------------------------------------------ new magics
+    def dist_interrupt(self, line: str = "") -> None:
+        p = _parser("%dist_interrupt")
+        p.add_argument("--hard", action="store_true", help="send SIGINT to the worker processes directly")
+        p.add_argument("ranks", nargs="?", default=None)
+        args = p.parse_args(shlex.split(line))
+        s = self.session
+        if not s.active:
+            self.p("No distributed workers running")
+            return
+        ranks = parse_ranks(args.ranks, s.num_processes) if args.ranks else None
+        s.interrupt(ranks, hard=args.hard)
+        self.p(f"⚡ Interrupt sent to ranks {format_ranks(ranks or s.all_ranks())}")
+
+    def dist_recover(self, line: str = "") -> None:
+        s = self.session
+        if not s.active:
+            self.p("No distributed workers running")
+            return
+        res = s.recover()
+        bad = {r: v for r, v in res.items() if isinstance(v, dict) and "error" in v}
+        if bad:
+            self.p(f"❌ recovery failed on {sorted(bad)}: {bad}")
+        else:
+            self.p(f"✓ Process group rebuilt on {len(res)} ranks")
+
+    def dist_pull(self, line: str = "") -> None:
+        p = _parser("%dist_pull")
+        p.add_argument("name")
+        p.add_argument("--rank", "-r", type=int, default=0)
+        p.add_argument("--as", dest="as_name", default=None)
+        p.add_argument("--summary", action="store_true", help="on-device summary only (no copy)")
+        args = p.parse_args(shlex.split(line))
+        res = self.session.get_var(args.name, args.rank, summary=args.summary)
+        if isinstance(res, dict) and "error" in res:
+            self.p(f"❌ {res['error']}")
+            return
+        value = res
+        if isinstance(res, dict) and res.get("type") == "tensor":
+            if args.summary:
+                self.p(f"{args.name}: {res.get('summary')}")
+                return
+            value = res["value"]
+        self.user_ns[args.as_name or args.name] = value
+        self.proxies.owned.pop(args.as_name or args.name, None)
+        self.p(f"✓ {args.as_name or args.name} <- rank {args.rank}.{args.name} ({type(value).__name__})")
+
+    def dist_push(self, line: str = "") -> None:
+        p = _parser("%dist_push")
+        p.add_argument("name")
+        p.add_argument("--ranks", "-r", default=None)
+        p.add_argument("--as", dest="as_name", default=None)
+        args = p.parse_args(shlex.split(line))
+        if args.name not in self.user_ns:
+            self.p(f"❌ name {args.name!r} is not defined locally")
+            return
+        ranks = parse_ranks(args.ranks, self.session.num_processes) if args.ranks else None
+        self.session.set_var(args.as_name or args.name, self.user_ns[args.name], ranks)
+        self.p(f"✓ pushed {args.name} to ranks {format_ranks(ranks or self.session.all_ranks())}")
+
+    def dist_profile(self, line: str = "") -> None:
+        p = _parser("%dist_profile")
+        p.add_argument("action", choices=["start", "stop"])
+        p.add_argument("--out", default="nbd_trace_rank{rank}.json")
+        args = p.parse_args(shlex.split(line))
+        res = self.session.profile(args.action, path_template=args.out)
+        for r in sorted(res):
+            v = res[r]
+            if isinstance(v, dict) and "error" in v:
+                self.p(f"Rank {r}: ❌ {v['error']}")
+            elif args.action == "stop":
+                self.p(f"Rank {r}: trace -> {v.get('trace')}")
+                if r == 0 and v.get("table"):
+                    self.p(v["table"])
+            else:
+                self.p(f"Rank {r}: profiling")
+
+    def teardown(self) -> None:
+        if self.session.active:
+            self.session.shutdown(graceful=True)
+        self.disable_auto()
+        tr = self._transformers()
+        if tr is not None and rank_nospace_transform in tr:
+            tr.remove(rank_nospace_transform)
+
+
+LINE_MAGICS = ["dist_init", "sync", "dist_status", "dist_mode", "dist_shutdown", "dist_reset", "dist_debug",
+               "dist_sync_ide", "timeline_save", "timeline_debug", "timeline_clear", "dist_interrupt",
+               "dist_recover", "dist_pull", "dist_push", "dist_profile"]
+CELL_MAGICS = ["distributed", "rank"]
+
+
+def _safe(core: MagicCore, fn):
+    def call(*a):
+        try:
+            return fn(*a)
+        except MagicUsageError as e:
+            if str(e):
+                core.p(str(e))
+        except RankSpecError as e:
+            core.p(f"❌ {e}")
+    call.__doc__ = fn.__doc__
+    return call
+
+
+def register(shell) -> Any:
+    """Register the magics with an IPython shell (``%load_ext nbdistributed_amd``)."""
+    from IPython.core.magic import Magics, magics_class
+
+    core = MagicCore(shell)
+
+    @magics_class
+    class DistributedMagics(Magics):
+        pass
+
+    m = DistributedMagics(shell)
+    m.core = core
+    for name in LINE_MAGICS:
+        shell.register_magic_function(_safe(core, getattr(core, name)), magic_kind="line", magic_name=name)
+    for name in CELL_MAGICS:
+        shell.register_magic_function(_safe(core, getattr(core, name)), magic_kind="cell", magic_name=name)
+    tr = getattr(shell, "input_transformers_cleanup", None)
+    if tr is not None and rank_nospace_transform not in tr:
+        tr.insert(0, rank_nospace_transform)
+    try:
+        shell.events.register("shutdown_kernel", core.teardown) if "shutdown_kernel" in shell.events.callbacks else None
+    except Exception:
+        pass
+    import atexit
+
+    atexit.register(core.teardown)
+    return m

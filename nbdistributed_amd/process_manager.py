@@ -1,0 +1,271 @@
+"""Worker process lifecycle (spawn, placement, liveness, teardown).
+
+Reference: ``src/nbdistributed/process_manager.py`` — ``start_workers`` (:57-152) Popen's
+``["python", worker.py, …]`` with undrained pipes, sleeps a fixed 2 s and hopes; ``is_running``
+prunes dead processes (renumbering ranks, D-15); ``shutdown`` terminate/kill (:177-227); status
+merging (:260-374).
+
+Re-design:
+
+* ``sys.executable`` (or ``NBD_WORKER_PYTHON``) instead of whatever ``python`` is on PATH (D-11);
+* each worker in its own session (``start_new_session``) so teardown signals exactly our process
+  groups — never name patterns (D-16);
+* stdout/stderr pipes drained by reader threads and forwarded (D-10: a 200 KB stderr burst
+  wedged the reference's workers);
+* ranks keep their slot forever: a dead rank is reported as dead with its exit code, never
+  removed from the list (D-15);
+* a waiter thread per worker reports exits immediately (fail-fast for in-flight cells);
+* GPU placement: every worker gets the same ``HIP_VISIBLE_DEVICES`` (the assigned GPUs in rank
+  order, translated through any filter the kernel itself runs under) and binds local device
+  ``index(gpu_ids[rank])``, so LOCAL_RANK, torch's device and the physical GPU agree (D-12) and
+  peer GPUs stay visible for RCCL's xGMI P2P transport.
+
+There is no readiness sleep: the Session waits for each worker's READY message.
+"""
+from __future__ import annotations
+
+import os
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+from .utils.devices import local_device_index, visible_gpu_count, worker_visible_devices
+
+OutputCallback = Callable[[int, str, str], None]  # rank, text, stream
+
+
+def find_free_port(host: str = "127.0.0.1") -> int:
+    """Ephemeral port for the torch.distributed TCPStore (reference :154-175).  The rendezvous
+    itself retries on EADDRINUSE; the control plane never needs a port (it binds port 0 or a
+    Unix socket and reports the real endpoint)."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind((host if host not in ("localhost", "") else "127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@dataclass
+class WorkerProc:
+    rank: int
+    proc: subprocess.Popen
+    gpu_id: Optional[int]
+    device_index: Optional[int]
+    started: float = field(default_factory=time.time)
+    exit_code: Optional[int] = None
+    exited_at: Optional[float] = None
+
+    @property
+    def pid(self) -> int:
+        return self.proc.pid
+
+    @property
+    def running(self) -> bool:
+        return self.proc.poll() is None
+
+
+class ProcessManager:
+    """Spawns and supervises the local worker processes."""
+
+    def __init__(self, output_callback: Optional[OutputCallback] = None,
+                 exit_callback: Optional[Callable[[int, int], None]] = None):
+        self.workers: List[WorkerProc] = []
+        self.num_processes = 0
+        self.master_addr = "127.0.0.1"
+        self.master_port: Optional[int] = None
+        self.comm_endpoint: Optional[str] = None
+        self.gpu_assignments: Dict[int, Optional[int]] = {}
+        self.output_callback = output_callback
+        self.exit_callback = exit_callback
+        self._threads: List[threading.Thread] = []
+        self._shutting_down = False
+
+    # reference attribute name
+    @property
+    def processes(self) -> List[subprocess.Popen]:
+        return [w.proc for w in self.workers]
+
+    @staticmethod
+    def plan_gpus(num_processes: int, gpu_ids: Optional[List[int]] = None) -> List[Optional[int]]:
+        """GPU id per rank: explicit list (cycled if short, like the reference :106-115) or
+        round-robin over the visible GPUs; all None on a GPU-less host."""
+        if gpu_ids:
+            return [gpu_ids[r % len(gpu_ids)] for r in range(num_processes)]
+        n = visible_gpu_count()
+        if n == 0:
+            return [None] * num_processes
+        return [r % n for r in range(num_processes)]
+
+    def start_workers(self, num_processes: int, master_addr: str = "localhost", gpu_ids: Optional[List[int]] = None,
+                      comm_endpoint: Optional[str] = None, token: Optional[str] = None, backend: str = "auto",
+                      python: Optional[str] = None, extra_env: Optional[Dict[str, str]] = None,
+                      worker_args: Optional[List[str]] = None) -> str:
+        """Spawn ``num_processes`` workers that connect to ``comm_endpoint``.  Returns the endpoint
+        (the reference returned the ZMQ port)."""
+        if comm_endpoint is None:
+            raise ValueError("comm_endpoint is required: bind the coordinator socket before spawning")
+        from .config import get_config
+
+        cfg = get_config()
+        self.num_processes = num_processes
+        self.master_addr = "127.0.0.1" if master_addr in ("localhost", None, "") else master_addr
+        self.master_port = find_free_port(self.master_addr)
+        self.comm_endpoint = comm_endpoint
+        plan = self.plan_gpus(num_processes, gpu_ids)
+        gpus = [g for g in plan if g is not None]
+        env_base = dict(os.environ)
+        if extra_env:
+            env_base.update(extra_env)
+        if gpus:
+            vis = worker_visible_devices(gpus)
+            env_base["HIP_VISIBLE_DEVICES"] = vis
+            env_base["CUDA_VISIBLE_DEVICES"] = vis
+        env_base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL P2P
+        env_base["PYTHONUNBUFFERED"] = "1"
+        repo_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        env_base["PYTHONPATH"] = repo_root + (os.pathsep + env_base["PYTHONPATH"] if env_base.get("PYTHONPATH") else "")
+        if token:
+            env_base["NBD_TOKEN"] = token
+        exe = python or cfg.worker_python
+        for rank in range(num_processes):
+            gid = plan[rank]
+            didx = local_device_index(gpus, rank) if gid is not None else None
+            cmd = [exe, "-m", "nbdistributed_amd.worker", "--rank", str(rank), "--world-size", str(num_processes),
+                   "--master-addr", self.master_addr, "--master-port", str(self.master_port),
+                   "--coord", comm_endpoint, "--backend", backend]
+            if gid is not None:
+                cmd += ["--gpu-id", str(gid), "--device-index", str(didx)]
+            if worker_args:
+                cmd += worker_args
+            proc = subprocess.Popen(cmd, env=env_base, stdin=subprocess.DEVNULL, stdout=subprocess.PIPE,
+                                    stderr=subprocess.PIPE, start_new_session=True, cwd=os.getcwd())
+            w = WorkerProc(rank=rank, proc=proc, gpu_id=gid, device_index=didx)
+            self.workers.append(w)
+            self.gpu_assignments[rank] = gid
+            for stream, pipe in (("stdout", proc.stdout), ("stderr", proc.stderr)):
+                t = threading.Thread(target=self._drain, args=(rank, stream, pipe), daemon=True,
+                                     name=f"nbd-drain-{rank}-{stream}")
+                t.start()
+                self._threads.append(t)
+            t = threading.Thread(target=self._wait, args=(w,), daemon=True, name=f"nbd-wait-{rank}")
+            t.start()
+            self._threads.append(t)
+        return comm_endpoint
+
+    def _drain(self, rank: int, stream: str, pipe) -> None:
+        try:
+            for raw in iter(pipe.readline, b""):
+                text = raw.decode("utf-8", errors="replace")
+                cb = self.output_callback
+                if cb is not None:
+                    try:
+                        cb(rank, text, stream)
+                    except Exception:
+                        pass
+        except (OSError, ValueError):
+            pass
+        finally:
+            try:
+                pipe.close()
+            except Exception:
+                pass
+
+    def _wait(self, w: WorkerProc) -> None:
+        code = w.proc.wait()
+        w.exit_code = code
+        w.exited_at = time.time()
+        cb = self.exit_callback
+        if cb is not None and not self._shutting_down:
+            try:
+                cb(w.rank, code)
+            except Exception:
+                pass
+
+    # ------------------------------------------------------------------ queries
+    def is_running(self) -> bool:
+        """True while at least one worker is alive.  Unlike the reference (:250-256) this does
+        not mutate the worker list."""
+        return any(w.running for w in self.workers)
+
+    def all_running(self) -> bool:
+        return bool(self.workers) and all(w.running for w in self.workers)
+
+    def dead_ranks(self) -> Dict[int, int]:
+        return {w.rank: w.proc.returncode for w in self.workers if w.proc.poll() is not None}
+
+    def get_status(self) -> Dict[int, Dict]:
+        out = {}
+        for w in self.workers:
+            rc = w.proc.poll()
+            out[w.rank] = {"pid": w.pid, "running": rc is None, "returncode": rc, "gpu_id": w.gpu_id,
+                           "device_index": w.device_index}
+        return out
+
+    def get_detailed_status(self, comm_manager=None, timeout: float = 5.0) -> Dict[int, Dict]:
+        """Process status merged with each live worker's own report (reference :326-374).  Dead
+        ranks are skipped in the query, so one dead rank no longer costs the full timeout."""
+        status = self.get_status()
+        if comm_manager is not None:
+            alive = [r for r, s in status.items() if s["running"]]
+            if alive:
+                try:
+                    res = comm_manager.send_to_ranks(alive, "get_status", {}, timeout=timeout, raise_on_error=False)
+                except Exception:
+                    res = {}
+                for r, info in res.items():
+                    if isinstance(info, dict) and "error" not in info:
+                        status[r].update(info)
+        return status
+
+    # ------------------------------------------------------------------ teardown
+    def signal_all(self, sig: int) -> None:
+        for w in self.workers:
+            if w.running:
+                try:
+                    os.killpg(w.pid, sig)  # the worker's own session/group only
+                except (ProcessLookupError, PermissionError):
+                    pass
+
+    def interrupt(self, ranks: Optional[List[int]] = None) -> None:
+        for w in self.workers:
+            if (ranks is None or w.rank in ranks) and w.running:
+                try:
+                    os.kill(w.pid, signal.SIGINT)
+                except ProcessLookupError:
+                    pass
+
+    def shutdown(self, grace: float = 3.0, verbose: bool = False) -> None:
+        """Terminate the workers' process groups: SIGTERM, wait ``grace``, then SIGKILL."""
+        self._shutting_down = True
+        if verbose:
+            print(f"Shutting down {len(self.workers)} workers...")
+        self.signal_all(signal.SIGTERM)
+        deadline = time.time() + grace
+        for w in self.workers:
+            try:
+                w.proc.wait(timeout=max(0.0, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                pass
+        if any(w.running for w in self.workers):
+            self.signal_all(signal.SIGKILL)
+            for w in self.workers:
+                try:
+                    w.proc.wait(timeout=2.0)
+                except subprocess.TimeoutExpired:
+                    pass
+        for t in self._threads:
+            t.join(timeout=0.5)
+        if verbose:
+            print("All workers stopped")
+
+    def wait_exit(self, timeout: float) -> bool:
+        deadline = time.time() + timeout
+        for w in self.workers:
+            try:
+                w.proc.wait(timeout=max(0.0, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                return False
+        return True

@@ -1,0 +1,158 @@
+"""Bounded per-cell execution timeline with real per-rank timings.
+
+Reference (``magic.py:32-59, 123-395, 1316-1474``): every cell is tracked twice,
+per-line "durations" are invented from keyword heuristics, no worker-side time is collected, and
+on every cell end *all* timelines are re-serialised into a ``display(Javascript(...))`` — O(N)
+work per cell (113 → 138.5 ms per cell after 600 cells).
+
+Here one record per cell holds what actually happened: coordinator round-trip, each rank's own
+exec wall time (``perf_counter`` in the worker), its GPU time between HIP events recorded around
+the cell (collected lazily, never adding a sync), status and output volume.  Records live in a
+fixed-size ring buffer; nothing is serialised until asked (``%timeline_save``), which writes JSON
+and a Chrome/Perfetto trace (``chrome://tracing``) with one lane per rank.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import threading
+import time
+from collections import deque
+from dataclasses import asdict, dataclass, field
+from typing import Any, Dict, List, Optional
+
+
+@dataclass
+class CellRecord:
+    cell_id: str
+    seq: int
+    kind: str
+    ranks: List[int]
+    code_preview: str
+    code_sha1: str
+    t_start: float
+    t_end: Optional[float] = None
+    duration_s: Optional[float] = None
+    status: str = "running"
+    per_rank: Dict[int, Dict[str, Any]] = field(default_factory=dict)
+    output_bytes: int = 0
+
+
+class Timeline:
+    def __init__(self, capacity: int = 2000):
+        self.records: deque = deque(maxlen=capacity)
+        self.by_seq: Dict[int, CellRecord] = {}
+        self._lock = threading.Lock()
+        self._n = 0
+
+    def start(self, seq: int, kind: str, ranks: List[int], code: str) -> CellRecord:
+        with self._lock:
+            self._n += 1
+            rec = CellRecord(cell_id=f"cell_{self._n}", seq=seq, kind=kind, ranks=list(ranks),
+                             code_preview=code[:200], code_sha1=hashlib.sha1(code.encode()).hexdigest()[:12],
+                             t_start=time.time())
+            if len(self.records) == self.records.maxlen and self.records:
+                self.by_seq.pop(self.records[0].seq, None)
+            self.records.append(rec)
+            self.by_seq[seq] = rec
+            return rec
+
+    def end(self, rec: CellRecord, results: Dict[int, Any], duration_s: float, status: str, output_bytes: int = 0) -> None:
+        with self._lock:
+            rec.t_end = rec.t_start + duration_s
+            rec.duration_s = duration_s
+            rec.status = status
+            rec.output_bytes = output_bytes
+            for r, d in results.items():
+                if not isinstance(d, dict):
+                    continue
+                pr = rec.per_rank.setdefault(r, {})
+                for k in ("exec_s", "t_start", "t_end", "status"):
+                    if k in d:
+                        pr[k] = d[k]
+                if d.get("dead"):
+                    pr["status"] = "dead"
+                gpu = d.get("gpu_ms")
+                if gpu:
+                    self._attach_gpu_locked(r, gpu)
+
+    def attach_gpu(self, rank: int, gpu_ms: Dict[int, float]) -> None:
+        with self._lock:
+            self._attach_gpu_locked(rank, gpu_ms)
+
+    def _attach_gpu_locked(self, rank: int, gpu_ms: Dict[int, float]) -> None:
+        for seq, ms in gpu_ms.items():
+            rec = self.by_seq.get(int(seq))
+            if rec is not None:
+                rec.per_rank.setdefault(rank, {})["gpu_ms"] = ms
+
+    def clear(self) -> int:
+        with self._lock:
+            n = len(self.records)
+            self.records.clear()
+            self.by_seq.clear()
+            return n
+
+    def to_list(self) -> List[Dict[str, Any]]:
+        with self._lock:
+            return [asdict(r) for r in self.records]
+
+    def to_chrome_trace(self) -> Dict[str, Any]:
+        events: List[Dict[str, Any]] = []
+        ranks = set()
+        with self._lock:
+            recs = list(self.records)
+        for rec in recs:
+            if rec.duration_s is None:
+                continue
+            events.append({"name": f"{rec.kind}:{rec.cell_id}", "ph": "X", "pid": 0, "tid": 0,
+                           "ts": rec.t_start * 1e6, "dur": rec.duration_s * 1e6,
+                           "args": {"code": rec.code_preview, "status": rec.status, "seq": rec.seq}})
+            for r, pr in rec.per_rank.items():
+                ranks.add(r)
+                if "t_start" in pr and "exec_s" in pr:
+                    events.append({"name": rec.cell_id, "ph": "X", "pid": 1 + r, "tid": 0,
+                                   "ts": pr["t_start"] * 1e6, "dur": pr["exec_s"] * 1e6,
+                                   "args": {"status": pr.get("status"), "gpu_ms": pr.get("gpu_ms")}})
+                if "gpu_ms" in pr and "t_start" in pr:
+                    events.append({"name": f"{rec.cell_id} (gpu)", "ph": "X", "pid": 1 + r, "tid": 1,
+                                   "ts": pr["t_start"] * 1e6, "dur": pr["gpu_ms"] * 1e3})
+        meta = [{"name": "process_name", "ph": "M", "pid": 0, "args": {"name": "coordinator"}}]
+        for r in sorted(ranks):
+            meta.append({"name": "process_name", "ph": "M", "pid": 1 + r, "args": {"name": f"rank {r}"}})
+            meta.append({"name": "thread_name", "ph": "M", "pid": 1 + r, "tid": 0, "args": {"name": "exec (host)"}})
+            meta.append({"name": "thread_name", "ph": "M", "pid": 1 + r, "tid": 1, "args": {"name": "GPU"}})
+        return {"traceEvents": meta + events, "displayTimeUnit": "ms"}
+
+    def save(self, path: str) -> Dict[str, str]:
+        """Write ``path`` (JSON records) and ``<path>.trace.json`` (Chrome trace)."""
+        base = path[:-5] if path.endswith(".json") else path
+        jp = base + ".json"
+        tp = base + ".trace.json"
+        with open(jp, "w") as f:
+            json.dump({"records": self.to_list(), "saved_at": time.time()}, f, indent=1, default=str)
+        with open(tp, "w") as f:
+            json.dump(self.to_chrome_trace(), f, default=str)
+        return {"json": jp, "trace": tp}
+
+    def summary(self, last: int = 20) -> str:
+        with self._lock:
+            recs = list(self.records)[-last:]
+            total = len(self.records)
+        lines = [f"Timeline: {total} cell(s) recorded (showing last {len(recs)})"]
+        for rec in recs:
+            dur = f"{rec.duration_s * 1e3:8.2f} ms" if rec.duration_s is not None else "  running"
+            per = []
+            for r in sorted(rec.per_rank):
+                pr = rec.per_rank[r]
+                s = f"r{r}:{pr.get('exec_s', 0) * 1e3:.2f}ms"
+                if "gpu_ms" in pr:
+                    s += f"/gpu {pr['gpu_ms']:.2f}ms"
+                per.append(s)
+            preview = rec.code_preview.strip().splitlines()[0][:40] if rec.code_preview.strip() else ""
+            lines.append(f"  {rec.cell_id:>9} {rec.kind:<11} {dur} {rec.status:<11} {' '.join(per)}  | {preview}")
+        if recs:
+            ds = sorted(r.duration_s for r in recs if r.duration_s is not None)
+            if ds:
+                lines.append(f"  p50 {ds[len(ds) // 2] * 1e3:.2f} ms   min {ds[0] * 1e3:.2f} ms   max {ds[-1] * 1e3:.2f} ms")
+        return "\n".join(lines)

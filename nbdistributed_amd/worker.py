@@ -1,0 +1,541 @@
+"""Worker runtime: one process per GPU, executing notebook cells on request.
+
+Reference: ``src/nbdistributed/worker.py`` (DistributedWorker, :72-580; entry point :583-601).
+Same contract — a persistent per-rank namespace seeded with ``torch, dist, rank, world_size,
+__rank__, __world_size__, gpu_id, device`` (:160-177), message handlers ``execute / get_var /
+set_var / sync / get_status / get_namespace_info / shutdown`` (:205-221), streamed stdout and the
+echo of a cell's last expression — re-designed:
+
+* transport: native DEALER (``libnbd_transport.so``) with heartbeats; the process's fd 1/fd 2
+  are captured natively, so Python prints, C/C++ library output (RCCL ``NCCL_DEBUG``, hipcc,
+  ``os.system``) and stderr (warnings, tqdm) all stream to the coordinator, line-coalesced by
+  the I/O thread (reference: per-``write()`` pickled messages, stdout only, :30-69; D-8, D-10);
+* READY handshake after the data plane is up (reference: none, D-2);
+* device binding via HIP_VISIBLE_DEVICES ordering, ``device`` is a ``torch.device`` (D-12, D-13);
+* ``backend="rccl"`` registered and eagerly initialised (``parallel/backend.py``);
+* out-of-band interrupt: an INTERRUPT message raises SIGINT from the native I/O thread; a
+  watchdog aborts the RCCL communicator if the cell stays stuck inside a collective;
+* REPL echo of large GPU tensors adds a one-pass on-device summary (HIP kernel
+  ``nbd::tensor_summary``) instead of relying on host copies;
+* attach mode: workers launched by torchrun/srun/mpirun connect to a coordinator endpoint
+  (multi-node), reading RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* from the environment.
+
+Run as ``python -m nbdistributed_amd.worker --rank R --world-size N --master-addr A
+--master-port P --coord ENDPOINT [--gpu-id G --device-index I]`` (spawned mode) or
+``python -m nbdistributed_amd.worker --attach --coord ENDPOINT`` (attach mode).
+"""
+from __future__ import annotations
+
+import argparse
+import faulthandler
+import io
+import os
+import signal
+import socket as pysocket
+import sys
+import threading
+import time
+import traceback
+from typing import Any, Dict, Optional
+
+from . import protocol as P
+from .config import get_config
+from .executor import CellExecutor
+from .namespace import NamespaceTracker, namespace_info
+from .transport import DEALER, EV_DISCONNECTED, EV_HEARTBEAT_TIMEOUT, OPT_SIGNAL_PREFIX, OPT_STREAM_FLUSH_US, Socket, TransportError
+
+
+class DistributedWorker:
+    def __init__(self, rank: int, world_size: int, master_addr: str, master_port: int, coord: str,
+                 gpu_id: Optional[int] = None, device_index: Optional[int] = None, backend: str = "auto",
+                 token: Optional[str] = None, attach: bool = False, capture: bool = True,
+                 local_rank: Optional[int] = None, local_world_size: Optional[int] = None):
+        self.rank = rank
+        self.world_size = world_size
+        self.master_addr = master_addr
+        self.master_port = master_port
+        self.coord = coord
+        self.gpu_id = gpu_id
+        self.device_index = device_index
+        self.backend_req = backend
+        self.attach = attach
+        self.capture = capture
+        self.local_rank = rank if local_rank is None else local_rank
+        self.local_world_size = world_size if local_world_size is None else local_world_size
+        self.cfg = get_config()
+        self.token = token
+        self.stop = False
+        self.in_cell = False
+        self.cell_seq = 0
+        self.interrupt_at: Optional[float] = None
+        self.pg_aborted = False
+        self.device = None
+        self.backend = None
+        self.ppid = os.getppid()
+        self._profiler = None
+        self._pending_gpu: list = []
+        self.tracker = NamespaceTracker()
+        self.executor = CellExecutor(tag=f"cell-r{rank}")
+        self.ns = self.executor.ns
+        self.sock: Optional[Socket] = None
+        self.console_err = sys.__stderr__
+
+    # ------------------------------------------------------------------ bootstrap
+    def connect(self) -> None:
+        s = Socket(DEALER, identity=P.worker_identity(self.rank),
+                   token=self.token.encode() if self.token else None,
+                   heartbeat_ivl_ms=self.cfg.heartbeat_ivl_ms,
+                   heartbeat_timeout_ms=max(self.cfg.heartbeat_timeout_ms * 4, 60000))
+        s.set_bytes(OPT_SIGNAL_PREFIX, P.INTERRUPT_PREFIX)
+        s.set_int(OPT_STREAM_FLUSH_US, self.cfg.stream_flush_us)
+        s.connect(self.coord)
+        self.sock = s
+        self._set_stream_seq(0)
+        if self.capture:
+            _, saved_err = s.capture_fds(stdout=True, stderr=True)
+            if saved_err >= 0:
+                # crash reports must survive the death of the capture thread: send them to the
+                # original stderr (drained by the launcher) instead of the pipe.
+                self.console_err = io.TextIOWrapper(os.fdopen(saved_err, "wb", buffering=0), write_through=True)
+                faulthandler.enable(file=self.console_err)
+            for stream in (sys.stdout, sys.stderr):
+                try:
+                    stream.reconfigure(line_buffering=True, write_through=True)
+                except Exception:
+                    pass
+
+    def _set_stream_seq(self, seq: int) -> None:
+        self.sock.stream_header(1, P.pack_header(P.T_STREAM, self.rank, seq, P.S_STDOUT, P.E_BYTES, ts=0.0))
+        self.sock.stream_header(2, P.pack_header(P.T_STREAM, self.rank, seq, P.S_STDERR, P.E_BYTES, ts=0.0))
+
+    def bootstrap(self) -> Dict[str, Any]:
+        t0 = time.time()
+        if not self.attach:
+            os.environ["RANK"] = str(self.rank)
+            os.environ["LOCAL_RANK"] = str(self.local_rank)
+            os.environ["WORLD_SIZE"] = str(self.world_size)
+            os.environ["LOCAL_WORLD_SIZE"] = str(self.local_world_size)
+            os.environ["MASTER_ADDR"] = self.master_addr
+            os.environ["MASTER_PORT"] = str(self.master_port)
+        import torch
+        import torch.distributed as dist
+
+        from .parallel import backend as B
+
+        cuda = torch.cuda.is_available()
+        self.backend = B.resolve_backend(self.backend_req if self.backend_req != "auto" else self.cfg.backend, cuda)
+        if self.backend == "gloo" and not cuda:
+            self.device = torch.device("cpu")
+        else:
+            idx = self.device_index if self.device_index is not None else self.local_rank
+            self.device = B.bind_device(idx)
+        B.init_data_plane(self.backend, self.rank, self.world_size, self.device,
+                          eager=self.cfg.eager_comm_init)
+        import nbdistributed_amd as nbd
+
+        self.ns.update({
+            "torch": torch, "dist": dist, "rank": self.rank, "world_size": self.world_size,
+            "__rank__": self.rank, "__world_size__": self.world_size,
+            "gpu_id": self.gpu_id if self.gpu_id is not None else (self.device.index if self.device.type == "cuda" else None),
+            "device": self.device, "local_rank": self.local_rank, "nbd": nbd,
+        })
+        status = self.status()
+        status["init_s"] = time.time() - t0
+        return status
+
+    # ------------------------------------------------------------------ status
+    def status(self) -> Dict[str, Any]:
+        st: Dict[str, Any] = {
+            "rank": self.rank, "world_size": self.world_size, "gpu_id": self.gpu_id, "pid": os.getpid(),
+            "hostname": pysocket.gethostname(), "backend": self.backend, "local_rank": self.local_rank,
+            "cuda_available": False, "current_device": None, "gpu_name": "CPU",
+            "gpu_memory_allocated": 0.0, "gpu_memory_reserved": 0.0, "gpu_memory_total": 0.0,
+            "gpu_memory_used": 0.0, "pg_aborted": self.pg_aborted, "cells": self.executor.count,
+        }
+        torch = sys.modules.get("torch")
+        if torch is not None and self.device is not None and self.device.type == "cuda":
+            gib = float(1 << 30)
+            d = self.device
+            props = torch.cuda.get_device_properties(d)
+            free, total = torch.cuda.mem_get_info(d)
+            st.update(cuda_available=True, current_device=torch.cuda.current_device(),
+                      gpu_name=props.name, gcn_arch=getattr(props, "gcnArchName", ""),
+                      multi_processor_count=props.multi_processor_count,
+                      gpu_memory_allocated=torch.cuda.memory_allocated(d) / gib,
+                      gpu_memory_reserved=torch.cuda.memory_reserved(d) / gib,
+                      gpu_memory_total=total / gib, gpu_memory_used=(total - free) / gib,
+                      visible_devices=os.environ.get("HIP_VISIBLE_DEVICES"))
+            from .parallel.backend import rccl_version
+
+            st["rccl_version"] = rccl_version()
+        if torch is not None:
+            st["torch_version"] = torch.__version__
+            st["hip_version"] = getattr(torch.version, "hip", None)
+        return st
+
+    # ------------------------------------------------------------------ signals / watchdog
+    def _install_signal_handlers(self) -> None:
+        if threading.current_thread() is not threading.main_thread():
+            return
+        r, w = os.pipe()
+        os.set_blocking(w, False)
+        signal.set_wakeup_fd(w, warn_on_full_buffer=False)
+
+        def _on_sigint(signum, frame):
+            if self.in_cell:
+                raise KeyboardInterrupt
+            # idle: nothing to interrupt
+
+        signal.signal(signal.SIGINT, _on_sigint)
+        t = threading.Thread(target=self._watchdog, args=(r,), name="nbd-interrupt-watchdog", daemon=True)
+        t.start()
+
+    def _watchdog(self, rfd: int) -> None:
+        """Runs off the main thread: sees every SIGINT through the wakeup fd even while the main
+        thread is stuck in native code (e.g. waiting on a collective some rank never joins)."""
+        while not self.stop:
+            try:
+                data = os.read(rfd, 64)
+            except OSError:
+                return
+            if signal.SIGINT not in data or not self.in_cell:
+                continue
+            seq = self.cell_seq
+            deadline = time.monotonic() + self.cfg.interrupt_abort_s
+            while time.monotonic() < deadline and self.in_cell and self.cell_seq == seq:
+                time.sleep(0.05)
+            if self.in_cell and self.cell_seq == seq and not self.pg_aborted:
+                from .parallel.backend import abort_process_group
+
+                print(f"[nbd] rank {self.rank}: cell still running {self.cfg.interrupt_abort_s:.0f}s after "
+                      "interrupt — aborting the communicator (use %dist_recover to rebuild it)",
+                      file=sys.stderr, flush=True)
+                self.pg_aborted = abort_process_group()
+
+    # ------------------------------------------------------------------ handlers
+    def format_value(self, value: Any) -> str:
+        torch = sys.modules.get("torch")
+        mode = self.cfg.echo_mode
+        if torch is not None and isinstance(value, torch.Tensor) and mode != "repr":
+            big = value.numel() >= self.cfg.echo_summary_min_numel
+            if mode == "summary" or (big and value.device.type == "cuda"):
+                try:
+                    from .ops import tensor_summary_text
+
+                    s = tensor_summary_text(value)
+                    return s if mode == "summary" else repr(value) + "\n" + s
+                except Exception as e:  # never lose the echo because of the summary path
+                    return repr(value) + f"\n<summary unavailable: {e}>"
+        return repr(value)
+
+    def _gpu_events(self):
+        torch = sys.modules.get("torch")
+        if torch is None or self.device is None or self.device.type != "cuda" or not torch.cuda.is_initialized():
+            return None
+        try:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        except Exception:
+            return None
+
+    def _collect_gpu_times(self) -> Dict[int, float]:
+        done: Dict[int, float] = {}
+        keep = []
+        for seq, a, b in self._pending_gpu:
+            try:
+                if b.query():
+                    done[seq] = a.elapsed_time(b)
+                else:
+                    keep.append((seq, a, b))
+            except Exception:
+                pass
+        self._pending_gpu = keep[-64:]
+        return done
+
+    def handle_execute(self, seq: int, code: str, flags: int) -> Dict[str, Any]:
+        self._set_stream_seq(seq)
+        gpu_prev = self._collect_gpu_times()
+        ev0 = self._gpu_events()
+        self.cell_seq = seq
+        self.in_cell = True
+        try:
+            res = self.executor.run(code, echo=not (flags & P.F_NO_ECHO))
+        finally:
+            self.in_cell = False
+        out = ""
+        if res.has_value:
+            try:
+                out = self.format_value(res.value)
+            except Exception as e:
+                out = f"<repr failed: {type(e).__name__}: {e}>"
+        ev1 = self._gpu_events()
+        if ev0 is not None and ev1 is not None:
+            self._pending_gpu.append((seq, ev0, ev1))
+        try:
+            sys.stdout.flush()
+            sys.stderr.flush()
+        except Exception:
+            pass
+        self.sock.stream_flush()
+        resp: Dict[str, Any] = {"status": "success" if res.status == "ok" else res.status, "rank": self.rank,
+                                "output": out, "exec_s": res.exec_s, "t_start": res.t_start, "t_end": res.t_end}
+        if gpu_prev:
+            resp["gpu_ms"] = gpu_prev
+        if res.status != "ok":
+            resp["error"] = res.error
+            resp["ename"] = res.ename
+            resp["traceback"] = res.traceback
+        if self.pg_aborted:
+            resp["pg_aborted"] = True
+        if flags & P.F_NS_DELTA:
+            try:
+                resp["ns_delta"] = self.tracker.delta(self.ns)
+            except Exception as e:
+                resp["ns_delta_error"] = str(e)
+        return resp
+
+    def handle_get_var(self, data: Any) -> Dict[str, Any]:
+        opts = data if isinstance(data, dict) else {"name": data}
+        name = opts["name"]
+        if name not in self.ns:
+            raise NameError(f"name {name!r} is not defined on rank {self.rank}")
+        value = self.ns[name]
+        torch = sys.modules.get("torch")
+        if torch is not None and isinstance(value, torch.Tensor):
+            info = {"type": "tensor", "device": str(value.device), "dtype": str(value.dtype),
+                    "shape": list(value.shape)}
+            if opts.get("summary"):
+                from .ops import tensor_summary
+
+                info["summary"] = tensor_summary(value)
+            if not opts.get("summary_only"):
+                info["value"] = value.detach().cpu()
+            return info
+        return value
+
+    def handle_set_var(self, data: Dict[str, Any]) -> Dict[str, Any]:
+        name = data["name"]
+        value = data["value"]
+        torch = sys.modules.get("torch")
+        if torch is not None and isinstance(value, torch.Tensor) and data.get("to_device", True) and self.device is not None:
+            value = value.to(self.device, non_blocking=False)
+        self.ns[name] = value
+        return {"status": "success", "name": name}
+
+    def handle_sync(self) -> Dict[str, Any]:
+        import torch
+        import torch.distributed as dist
+
+        t0 = time.perf_counter()
+        if self.device is not None and self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+            dist.barrier(device_ids=[self.device.index])
+            torch.cuda.synchronize(self.device)
+        else:
+            dist.barrier()
+        return {"status": "synced", "rank": self.rank, "barrier_s": time.perf_counter() - t0}
+
+    def handle_recover(self, data: Dict[str, Any]) -> Dict[str, Any]:
+        """Rebuild the process group (after an abort) on a fresh rendezvous port."""
+        import torch.distributed as dist
+
+        from .parallel import backend as B
+
+        try:
+            if dist.is_initialized():
+                dist.destroy_process_group()
+        except Exception:
+            pass
+        os.environ["MASTER_PORT"] = str(data["master_port"])
+        if data.get("master_addr"):
+            os.environ["MASTER_ADDR"] = data["master_addr"]
+        B.init_data_plane(self.backend, self.rank, self.world_size, self.device, eager=True)
+        self.pg_aborted = False
+        self.ns["dist"] = dist
+        return {"status": "recovered", "rank": self.rank}
+
+    def handle_profile(self, data: Dict[str, Any]) -> Dict[str, Any]:
+        import torch
+
+        action = data.get("action")
+        if action == "start":
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if self.device is not None and self.device.type == "cuda":
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            self._profiler = torch.profiler.profile(activities=acts, record_shapes=bool(data.get("record_shapes")))
+            self._profiler.__enter__()
+            return {"status": "profiling", "rank": self.rank}
+        if action == "stop":
+            if self._profiler is None:
+                raise RuntimeError("profiler not running")
+            self._profiler.__exit__(None, None, None)
+            path = data.get("path_template", "nbd_trace_rank{rank}.json").format(rank=self.rank)
+            self._profiler.export_chrome_trace(path)
+            table = self._profiler.key_averages().table(sort_by="self_cuda_time_total" if self.device is not None and self.device.type == "cuda" else "self_cpu_time_total", row_limit=int(data.get("row_limit", 15)))
+            self._profiler = None
+            return {"status": "stopped", "rank": self.rank, "trace": os.path.abspath(path), "table": table}
+        raise ValueError(f"unknown profile action {action!r}")
+
+    def dispatch(self, h: P.Header, data: Any) -> Any:
+        t = h.mtype
+        if t == P.T_EXECUTE:
+            return self.handle_execute(h.seq, data, h.flags)
+        if t == P.T_GET_VAR:
+            return self.handle_get_var(data)
+        if t == P.T_SET_VAR:
+            return self.handle_set_var(data)
+        if t == P.T_SYNC:
+            return self.handle_sync()
+        if t == P.T_GET_STATUS:
+            st = self.status()
+            st["gpu_ms"] = self._collect_gpu_times()
+            return st
+        if t == P.T_GET_NAMESPACE_INFO:
+            return namespace_info(self.ns)
+        if t == P.T_PING:
+            return {"pong": time.time(), "rank": self.rank}
+        if t == P.T_RECOVER:
+            return self.handle_recover(data)
+        if t == P.T_PROFILE:
+            return self.handle_profile(data)
+        if t == P.T_INTERRUPT:
+            return None  # the signal already did the work; nothing to answer
+        raise ValueError(f"unknown message type {h.mtype}")
+
+    # ------------------------------------------------------------------ main loop
+    def reply(self, seq: int, data: Any, error: bool = False) -> None:
+        try:
+            frames = P.encode(P.T_RESPONSE, self.rank, seq, data, flags=P.F_ERROR if error else 0)
+        except Exception as e:  # unpicklable result: say so instead of hanging the coordinator
+            frames = P.encode(P.T_RESPONSE, self.rank, seq,
+                              {"error": f"could not serialise reply: {type(e).__name__}: {e}",
+                               "traceback": traceback.format_exc(), "rank": self.rank}, flags=P.F_ERROR)
+        self.sock.send(frames)
+
+    def run(self) -> None:
+        self._install_signal_handlers()
+        while not self.stop:
+            try:
+                m = self.sock.recv(timeout=0.5)
+            except KeyboardInterrupt:
+                continue
+            except TransportError:
+                break
+            if m is None:
+                if not self.attach and os.getppid() != self.ppid:
+                    break  # the coordinator died without telling us
+                continue
+            if m.is_event:
+                if m.event in (EV_DISCONNECTED, EV_HEARTBEAT_TIMEOUT) and not self.attach:
+                    break
+                continue
+            try:
+                h = P.unpack_header(m.frames[0])
+                data = P.decode_body(h.enc, m.frames[1] if len(m.frames) > 1 else b"")
+            except Exception:
+                continue
+            if h.mtype == P.T_SHUTDOWN:
+                self.reply(h.seq, {"status": "shutdown", "rank": self.rank})
+                break
+            if h.mtype == P.T_INTERRUPT:
+                continue
+            try:
+                result = self.dispatch(h, data)
+                self.reply(h.seq, result)
+            except KeyboardInterrupt:
+                self.reply(h.seq, {"error": "interrupted", "status": "interrupted", "rank": self.rank}, error=True)
+            except BaseException as e:  # noqa: BLE001
+                self.reply(h.seq, {"error": f"{type(e).__name__}: {e}", "traceback": traceback.format_exc(),
+                                   "rank": self.rank}, error=True)
+        self.stop = True
+
+    def shutdown(self) -> None:
+        self.stop = True
+        torch = sys.modules.get("torch")
+        if torch is not None:
+            try:
+                import torch.distributed as dist
+
+                if dist.is_initialized():
+                    done = threading.Event()
+
+                    def _destroy():
+                        try:
+                            dist.destroy_process_group()
+                        except Exception:
+                            pass
+                        done.set()
+
+                    threading.Thread(target=_destroy, daemon=True).start()
+                    done.wait(10.0)
+            except Exception:
+                pass
+        if self.sock is not None:
+            try:
+                sys.stdout.flush()
+                sys.stderr.flush()
+            except Exception:
+                pass
+            self.sock.close()
+
+
+def _parse_args(argv=None):
+    ap = argparse.ArgumentParser(prog="python -m nbdistributed_amd.worker")
+    ap.add_argument("--rank", type=int)
+    ap.add_argument("--world-size", type=int)
+    ap.add_argument("--master-addr", default=None)
+    ap.add_argument("--master-port", type=int, default=None)
+    ap.add_argument("--coord", required=True, help="coordinator endpoint (ipc:// or tcp://)")
+    ap.add_argument("--gpu-id", type=int, default=None)
+    ap.add_argument("--device-index", type=int, default=None)
+    ap.add_argument("--backend", default="auto")
+    ap.add_argument("--attach", action="store_true", help="take RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* from env")
+    ap.add_argument("--no-capture", action="store_true")
+    return ap.parse_args(argv)
+
+
+def worker_from_env(coord: str, backend: str = "auto", token: Optional[str] = None, capture: bool = True) -> DistributedWorker:
+    """Attach-mode constructor (torchrun / srun launched processes)."""
+    env = os.environ
+    rank = int(env["RANK"])
+    world = int(env["WORLD_SIZE"])
+    local = int(env.get("LOCAL_RANK", rank))
+    lws = int(env.get("LOCAL_WORLD_SIZE", world))
+    return DistributedWorker(rank, world, env.get("MASTER_ADDR", "127.0.0.1"), int(env.get("MASTER_PORT", 29500)),
+                             coord, gpu_id=None, device_index=local, backend=backend, token=token, attach=True,
+                             capture=capture, local_rank=local, local_world_size=lws)
+
+
+def main(argv=None) -> int:
+    args = _parse_args(argv)
+    token = os.environ.pop("NBD_TOKEN", None)
+    if args.attach:
+        w = worker_from_env(args.coord, args.backend, token, capture=not args.no_capture)
+    else:
+        w = DistributedWorker(args.rank, args.world_size, args.master_addr, args.master_port, args.coord,
+                              gpu_id=args.gpu_id, device_index=args.device_index, backend=args.backend,
+                              token=token, capture=not args.no_capture)
+    code = 0
+    try:
+        w.connect()
+        try:
+            status = w.bootstrap()
+        except BaseException as e:  # tell the coordinator why, then die
+            w.sock.send(P.encode(P.T_READY, w.rank, 0, {"error": f"{type(e).__name__}: {e}",
+                                                          "traceback": traceback.format_exc(), "rank": w.rank}))
+            time.sleep(0.2)
+            return 3
+        w.sock.send(P.encode(P.T_READY, w.rank, 0, status))
+        w.run()
+    except KeyboardInterrupt:
+        code = 130
+    finally:
+        w.shutdown()
+    return code
+
+
+if __name__ == "__main__":
+    code = main()
+    sys.stdout.flush()
+    os._exit(code)
