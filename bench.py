@@ -1,0 +1,135 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of nbdistributed_amd (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--sweep]
+
+Single GPU (default): this process plays rank 0.  Multi-GPU: launched by the driver as
+``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`` — every torchrun
+process becomes a framework worker in *attach* mode (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* from
+the environment, ``backend="rccl"``), and rank 0 additionally starts the coordinator as a child
+process that never touches the GPU (exactly what a notebook kernel is).  The coordinator drives
+the benchmark as ``%%distributed`` cells through the native control plane; each worker runs them
+in its REPL engine with RCCL over xGMI as the data plane.
+
+Printed by rank 0: one JSON line (value = trivial ``%%distributed`` cell p50 round trip in ms,
+reference 111.6 ms; plus 1 GiB bf16 all_reduce algbw/busbw).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+
+def _args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--sweep", action="store_true", help="also run the 1 KiB..1 GiB all_reduce sweep")
+    ap.add_argument("--no-allreduce", action="store_true")
+    ap.add_argument("--ar-bytes", type=int, default=1 << 30)
+    ap.add_argument("--coordinator", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--endpoint", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--world", type=int, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--out", default=None, help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+def coordinator_main(a) -> int:
+    """Child process: the notebook-kernel role.  No torch import, no GPU."""
+    from nbdistributed_amd.benchmarking import run_all
+    from nbdistributed_amd.session import Session
+
+    sess = Session(writer=lambda s: sys.stderr.write(s))
+    try:
+        sess.attach(a.world, bind=a.endpoint, token=None, startup_timeout=900)
+        res = run_all(sess, a.steps, a.warmup, allreduce=not a.no_allreduce, sweep=a.sweep, ar_bytes=a.ar_bytes)
+        res["init_ready"] = {r: sess.ready[r].get("init_s") for r in sess.ready}
+        res["device"] = sess.ready[0].get("gpu_name")
+        res["rccl_version"] = sess.ready[0].get("rccl_version")
+        with open(a.out, "w") as f:
+            json.dump(res, f)
+        return 0
+    finally:
+        sess.shutdown(graceful=True)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def main(argv=None) -> int:
+    a = _args(argv)
+    if a.coordinator:
+        return coordinator_main(a)
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", str(a.gpus or 1))
+    os.environ.setdefault("LOCAL_RANK", os.environ["RANK"])
+    os.environ.setdefault("LOCAL_WORLD_SIZE", os.environ["WORLD_SIZE"])
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        os.environ["MASTER_PORT"] = str(_free_port())
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    if a.gpus is not None and a.gpus != world:
+        print(f"--gpus {a.gpus} disagrees with WORLD_SIZE {world}", file=sys.stderr)
+        return 2
+    tag = f"{os.environ['MASTER_PORT']}-{os.getuid()}"
+    endpoint = f"ipc://{tempfile.gettempdir() if len(tempfile.gettempdir()) < 60 else '/tmp'}/nbd-bench-{tag}.sock"
+    out_path = os.path.join(tempfile.gettempdir(), f"nbd-bench-{tag}.json")
+    child = None
+    if rank == 0:
+        # started before this process touches the GPU; a child, never an exec
+        cmd = [sys.executable, os.path.abspath(__file__), "--coordinator", "--endpoint", endpoint, "--world", str(world),
+               "--steps", str(a.steps), "--warmup", str(a.warmup), "--out", out_path, "--ar-bytes", str(a.ar_bytes)]
+        if a.sweep:
+            cmd.append("--sweep")
+        if a.no_allreduce:
+            cmd.append("--no-allreduce")
+        child = subprocess.Popen(cmd, stdin=subprocess.DEVNULL)
+    from nbdistributed_amd import protocol as P
+    from nbdistributed_amd.worker import worker_from_env
+
+    w = worker_from_env(endpoint, backend="auto", token=None, capture=True)
+    rc = 0
+    try:
+        w.connect()
+        status = w.bootstrap()
+        w.sock.send(P.encode(P.T_READY, w.rank, 0, status))
+        w.run()
+    finally:
+        w.shutdown()  # restores fd 1/2
+    if child is not None:
+        rc = child.wait(timeout=600)
+        if rc != 0 or not os.path.exists(out_path):
+            print(f"coordinator failed (exit {rc})", file=sys.stderr)
+            return rc or 1
+        from nbdistributed_amd.benchmarking import result_line
+
+        with open(out_path) as f:
+            res = json.load(f)
+        os.unlink(out_path)
+        line = result_line(res, world, a.steps, a.warmup)
+        line["device"] = res.get("device")
+        line["rccl_version"] = res.get("rccl_version")
+        print(json.dumps(line), flush=True)
+    return rc
+
+
+if __name__ == "__main__":
+    code = main()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(code)

@@ -1,0 +1,12 @@
+// nbd_ops.cpp — operator schemas of the nbdistributed_amd HIP kernels (torch.ops.nbd.*).
+// The GPU implementations are registered next to their kernels (bucket.hip, summary.hip) under
+// the CUDA dispatch key (HIP on ROCm).  CPU tensors are served by the PyTorch reference
+// implementations in nbdistributed_amd/ops (same semantics; used by the CPU test-suite).
+#include <torch/library.h>
+
+TORCH_LIBRARY(nbd, m) {
+  m.def("bucket_flatten(Tensor[] tensors, Tensor(a!) bucket, int[] offsets, float scale) -> ()");
+  m.def("bucket_unflatten(Tensor bucket, Tensor(a!)[] tensors, int[] offsets, float scale, bool accumulate) -> ()");
+  m.def("local_prereduce(Tensor[] inputs, Tensor(a!) out, float scale) -> ()");
+  m.def("tensor_summary(Tensor x) -> Tensor");
+}

@@ -119,7 +119,7 @@ def build_ops(force: bool = False, jobs: int = 4) -> Path:
         hipcc = hipcc_path()
         objdir = HERE / "build"
         objdir.mkdir(exist_ok=True)
-        common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'kernels'}", "-D__HIP_PLATFORM_AMD__",
+        common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'kernels'}", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                   "-Wno-unused-result", "-Wno-deprecated-declarations"] + cflags
         procs = []
         objs = []

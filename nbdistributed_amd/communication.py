@@ -136,14 +136,17 @@ class CommunicationManager:
 
     def __init__(self, num_processes: int, base_port: Optional[int] = None, output_callback: Optional[OutputCallback] = None,
                  default_timeout: Optional[float] = None, endpoint: Optional[str] = None, token: Optional[str] = None,
-                 heartbeat_ivl_ms: Optional[int] = None, heartbeat_timeout_ms: Optional[int] = None):
+                 heartbeat_ivl_ms: Optional[int] = None, heartbeat_timeout_ms: Optional[int] = None,
+                 use_token: Optional[bool] = None):
         from .config import get_config
 
         cfg = get_config()
         self.num_processes = num_processes
         self.output_callback = output_callback
         self.default_timeout = default_timeout
-        self.token = token if token is not None else (secrets.token_hex(16) if cfg.use_token else None)
+        if use_token is None:
+            use_token = cfg.use_token
+        self.token = token if token is not None else (secrets.token_hex(16) if use_token else None)
         self._tmpdir: Optional[str] = None
         if endpoint is None:
             if base_port is not None:

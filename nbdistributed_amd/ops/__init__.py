@@ -1,0 +1,224 @@
+"""Hot-path GPU ops: hand-written gfx950 HIP kernels exposed as ``torch.ops.nbd.*``.
+
+=====================  ==============================================  =========================
+op                     what it fuses                                    kernel (csrc/kernels)
+=====================  ==============================================  =========================
+bucket_flatten (K1)    N grads -> 1 bucket + cast (fp32->bf16) + scale  bucket.hip multi_copy
+bucket_unflatten (K2)  bucket -> N grads + scale (1/world) + cast (+=)  bucket.hip multi_copy
+local_prereduce (K3)   sum of k buffers, fp32 accumulate, scale, cast   bucket.hip prereduce
+tensor_summary (K4)    count/sum/mean/std/norm/min/max/absmax/nan/inf   summary.hip (MFMA Σx, Σx²)
+=====================  ==============================================  =========================
+
+GPU tensors always go to the HIP kernels; if ``libnbd_ops.so`` cannot be loaded on a GPU box the
+call raises (no silent eager fallback).  CPU tensors use the PyTorch reference implementations
+below — the same semantics, and the oracle the GPU numerics tests compare against.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
+
+_lock = threading.Lock()
+_loaded: Optional[bool] = None
+_load_error: Optional[str] = None
+
+
+def load_library(build: bool = True) -> bool:
+    """Load libnbd_ops.so into this process (building it first if stale and ``build``)."""
+    global _loaded, _load_error
+    if _loaded is not None:
+        return _loaded
+    with _lock:
+        if _loaded is not None:
+            return _loaded
+        import torch
+
+        from .._native import OPS_HIP_SOURCES, OPS_LIB, build_ops
+
+        try:
+            path = os.environ.get("NBD_OPS_LIB")
+            if not path:
+                path = str(build_ops()) if build and OPS_HIP_SOURCES else str(OPS_LIB)
+            torch.ops.load_library(path)
+            _loaded = True
+        except Exception as e:  # pragma: no cover - reported by native_available()/_require
+            _loaded = False
+            _load_error = f"{type(e).__name__}: {e}"
+    return _loaded
+
+
+def native_available() -> bool:
+    return load_library()
+
+
+def _require() -> None:
+    if not load_library():
+        raise RuntimeError(f"nbdistributed_amd HIP ops unavailable ({_load_error}); "
+                           "run `python -m nbdistributed_amd._native` to build libnbd_ops.so")
+
+
+def plan_offsets(numels: Sequence[int], align: int = 64) -> Tuple[List[int], int]:
+    """Bucket layout: each tensor starts at a multiple of ``align`` elements (128 B for bf16,
+    256 B for fp32) so every tensor takes the kernels' 16-B vector path.  Returns (offsets,
+    total numel)."""
+    offs = []
+    pos = 0
+    for n in numels:
+        offs.append(pos)
+        pos += (int(n) + align - 1) // align * align
+    return offs, pos
+
+
+# ---------------------------------------------------------------- reference implementations
+def _ref_flatten(tensors, bucket, offsets, scale):
+    for t, o in zip(tensors, offsets):
+        n = t.numel()
+        bucket[o:o + n].copy_((t.reshape(-1).float() * scale).to(bucket.dtype))
+
+
+def _ref_unflatten(bucket, tensors, offsets, scale, accumulate):
+    for t, o in zip(tensors, offsets):
+        n = t.numel()
+        v = bucket[o:o + n].float() * scale
+        if accumulate:
+            v = v + t.reshape(-1).float()
+        t.view(-1).copy_(v.to(t.dtype))
+
+
+def _ref_prereduce(inputs, out, scale):
+    acc = inputs[0].reshape(-1).float().clone()
+    for x in inputs[1:]:
+        acc += x.reshape(-1).float()
+    out.view(-1).copy_((acc * scale).to(out.dtype))
+
+
+def _ref_summary(x):
+    import torch
+
+    xf = x.detach().reshape(-1).double()
+    n = xf.numel()
+    nan = torch.isnan(xf)
+    inf = torch.isinf(xf)
+    fin = xf[~nan]
+    mn = float(fin.min()) if fin.numel() else float("inf")
+    mx = float(fin.max()) if fin.numel() else float("-inf")
+    amx = float(fin.abs().max()) if fin.numel() else 0.0
+    s = float(xf.sum())
+    mean = s / n if n else float("nan")
+    std = float(xf.std()) if n > 1 else float("nan")
+    norm = float(xf.square().sum().sqrt())
+    return torch.tensor([n, s, mean, std, norm, mn, mx, amx, float(nan.sum()), float(inf.sum()),
+                         n - float(nan.sum()) - float(inf.sum()), 0.0], dtype=torch.float64)
+
+
+# ---------------------------------------------------------------- public API
+def bucket_flatten(tensors: Sequence, bucket=None, offsets: Optional[Sequence[int]] = None, dtype=None,
+                   scale: float = 1.0, align: int = 64):
+    """Copy ``tensors`` into one flat ``bucket`` (allocated if None), casting to the bucket's dtype
+    and multiplying by ``scale``.  Returns (bucket, offsets)."""
+    import torch
+
+    tensors = list(tensors)
+    if offsets is None:
+        offsets, total = plan_offsets([t.numel() for t in tensors], align)
+    else:
+        total = max((o + t.numel() for o, t in zip(offsets, tensors)), default=0)
+    if bucket is None:
+        dev = tensors[0].device if tensors else "cpu"
+        bucket = torch.zeros(total, dtype=dtype or (tensors[0].dtype if tensors else torch.float32), device=dev)
+    if not tensors:
+        return bucket, list(offsets)
+    flat = [t if t.is_contiguous() else t.contiguous() for t in tensors]
+    if bucket.is_cuda:
+        _require()
+        torch.ops.nbd.bucket_flatten(flat, bucket, list(offsets), float(scale))
+    else:
+        _ref_flatten(flat, bucket, offsets, scale)
+    return bucket, list(offsets)
+
+
+def bucket_unflatten(bucket, tensors: Sequence, offsets: Sequence[int], scale: float = 1.0,
+                     accumulate: bool = False) -> None:
+    """Scatter ``bucket`` back into ``tensors`` (in place), times ``scale``, cast to each
+    tensor's dtype, optionally accumulating (``t += scale * bucket[...]``)."""
+    import torch
+
+    tensors = list(tensors)
+    if not tensors:
+        return
+    for t in tensors:
+        if not t.is_contiguous():
+            raise ValueError("bucket_unflatten targets must be contiguous")
+    if bucket.is_cuda:
+        _require()
+        torch.ops.nbd.bucket_unflatten(bucket, tensors, list(offsets), float(scale), bool(accumulate))
+    else:
+        _ref_unflatten(bucket, tensors, offsets, scale, accumulate)
+
+
+def local_prereduce(inputs: Sequence, out=None, scale: float = 1.0, dtype=None):
+    """``out = scale * Σ inputs`` with fp32 accumulation.  Returns ``out``."""
+    import torch
+
+    inputs = [x if x.is_contiguous() else x.contiguous() for x in inputs]
+    if not inputs:
+        raise ValueError("local_prereduce needs at least one input")
+    if out is None:
+        out = torch.empty_like(inputs[0], dtype=dtype or inputs[0].dtype)
+    if out.is_cuda:
+        _require()
+        if len(inputs) > 16:
+            partials = []
+            for i in range(0, len(inputs), 16):
+                p = torch.empty(out.shape, dtype=torch.float32, device=out.device)
+                torch.ops.nbd.local_prereduce(inputs[i:i + 16], p, 1.0)
+                partials.append(p)
+            return local_prereduce(partials, out, scale)
+        torch.ops.nbd.local_prereduce(inputs, out, float(scale))
+    else:
+        _ref_prereduce(inputs, out, scale)
+    return out
+
+
+SUMMARY_FIELDS = ("count", "sum", "mean", "std", "norm", "min", "max", "absmax", "nan", "inf", "finite", "shift")
+
+
+def tensor_summary_raw(x):
+    """float64[12] on x's device: see ``SUMMARY_FIELDS``."""
+    import torch
+
+    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16, torch.float16):
+        _require()
+        return torch.ops.nbd.tensor_summary(x.detach())
+    if x.is_cuda:
+        return _ref_summary(x).to(x.device)
+    return _ref_summary(x)
+
+
+def tensor_summary(x) -> Dict[str, float]:
+    """One-pass statistics of ``x`` (HIP kernel on GPU); one 96-byte device->host copy."""
+    import torch
+
+    if not x.is_floating_point():
+        x = x.float() if not x.is_cuda else x.to(torch.float32)
+    raw = tensor_summary_raw(x).cpu().tolist()
+    d = dict(zip(SUMMARY_FIELDS, raw))
+    for k in ("count", "nan", "inf", "finite"):
+        d[k] = int(d[k])
+    d.pop("shift", None)
+    return d
+
+
+def tensor_summary_text(x) -> str:
+    s = tensor_summary(x)
+    shape = "x".join(str(d) for d in x.shape) or "scalar"
+    parts = [f"mean={s['mean']:.6g}", f"std={s['std']:.6g}", f"min={s['min']:.6g}", f"max={s['max']:.6g}",
+             f"norm={s['norm']:.6g}"]
+    if s["nan"] or s["inf"]:
+        parts.append(f"nan={s['nan']} inf={s['inf']}")
+    return f"[{shape} {str(x.dtype).replace('torch.', '')} {x.device}] " + " ".join(parts)
+
+
+__all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "tensor_summary", "tensor_summary_text",
+           "tensor_summary_raw", "plan_offsets", "native_available", "load_library", "SUMMARY_FIELDS"]

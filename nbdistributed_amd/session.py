@@ -209,7 +209,8 @@ class Session:
         if self.active:
             raise RuntimeError("session already running; shut it down first")
         comm = CommunicationManager(world_size, output_callback=self._background_output, default_timeout=timeout,
-                                    endpoint=bind or f"tcp://{self.cfg.bind_host}:0", token=token)
+                                    endpoint=bind or f"tcp://{self.cfg.bind_host}:0", token=token,
+                                    use_token=token is not None)
         self.comm = comm
         self.num_processes = self.world_size = world_size
         self.attached = True

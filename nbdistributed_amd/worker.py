@@ -117,6 +117,8 @@ class DistributedWorker:
             os.environ["LOCAL_WORLD_SIZE"] = str(self.local_world_size)
             os.environ["MASTER_ADDR"] = self.master_addr
             os.environ["MASTER_PORT"] = str(self.master_port)
+        if "torch" not in sys.modules:
+            os.environ.setdefault("TORCH_CPP_LOG_LEVEL", "ERROR")  # c10d hostname warnings, gloo chatter
         import torch
         import torch.distributed as dist
 

@@ -1,0 +1,131 @@
+"""GPU numerics: the HIP kernels (torch.ops.nbd.*) against plain PyTorch fp32 references."""
+import math
+
+import pytest
+import torch
+
+from nbdistributed_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+DT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}
+
+
+@pytest.fixture(scope="module")
+def dev(require_gpu):
+    assert ops.native_available(), ops._load_error
+    return torch.device("cuda", 0)
+
+
+def _tensors(dev, dtype, sizes, misalign=False):
+    g = torch.Generator(device="cpu").manual_seed(0)
+    out = []
+    for i, n in enumerate(sizes):
+        if misalign and i % 3 == 1:
+            big = torch.randn(n + 1, generator=g).to(dev, dtype)
+            out.append(big[1:])  # contiguous, data pointer not 16-B aligned
+        else:
+            out.append(torch.randn(n, generator=g).to(dev, dtype))
+    return out
+
+
+SIZES = [1, 7, 8, 9, 1000, 16383, 16384, 16385, 100003, 3 * 16384 + 5]
+
+
+@pytest.mark.parametrize("src", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("dst", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("misalign", [False, True])
+def test_bucket_flatten_matches_reference(dev, src, dst, misalign):
+    ts = _tensors(dev, DT[src], SIZES, misalign)
+    offsets, total = ops.plan_offsets([t.numel() for t in ts])
+    if misalign:
+        offsets = [o + (i % 2) for i, o in enumerate(offsets)]  # odd bucket offsets too
+        total += 1
+    b = torch.full((total,), 7.0, device=dev, dtype=DT[dst])
+    ref = b.clone()
+    ops.bucket_flatten(ts, b, offsets, scale=0.25)
+    ops._ref_flatten(ts, ref, offsets, 0.25)
+    torch.testing.assert_close(b.float(), ref.float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("src,dst", [("bf16", "f32"), ("f32", "f32"), ("f32", "bf16"), ("f16", "f32")])
+def test_bucket_unflatten_matches_reference(dev, src, dst, accumulate):
+    sizes = SIZES + [5] * 70  # > 64 tensors: several launches
+    offsets, total = ops.plan_offsets(sizes)
+    bucket = torch.randn(total, device=dev).to(DT[src])
+    outs = _tensors(dev, DT[dst], sizes)
+    refs = [t.clone() for t in outs]
+    ops.bucket_unflatten(bucket, outs, offsets, scale=1.0 / 8, accumulate=accumulate)
+    ops._ref_unflatten(bucket, refs, offsets, 1.0 / 8, accumulate)
+    tol = 0 if not accumulate else (1e-6 if dst == "f32" else 1e-2)
+    for a, r in zip(outs, refs):
+        torch.testing.assert_close(a.float(), r.float(), rtol=tol, atol=tol)
+
+
+def test_flatten_unflatten_roundtrip_many_tensors(dev):
+    ts = _tensors(dev, torch.float32, [(i * 37) % 5000 + 1 for i in range(200)])
+    b, offs = ops.bucket_flatten(ts, dtype=torch.float32)
+    outs = [torch.empty_like(t) for t in ts]
+    ops.bucket_unflatten(b, outs, offs)
+    for a, t in zip(outs, ts):
+        assert torch.equal(a, t)
+
+
+@pytest.mark.parametrize("k", [1, 2, 5, 16, 21])
+@pytest.mark.parametrize("src,dst", [("bf16", "bf16"), ("f32", "f32"), ("bf16", "f32"), ("f16", "f16")])
+def test_local_prereduce_matches_reference(dev, k, src, dst):
+    n = 1_000_003
+    xs = [torch.randn(n, device=dev).to(DT[src]) for _ in range(k)]
+    out = torch.empty(n, device=dev, dtype=DT[dst])
+    ops.local_prereduce(xs, out, scale=1.0 / k)
+    ref = torch.stack([x.float() for x in xs]).sum(0) / k
+    tol = 1e-5 if dst == "f32" else 1e-2
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
+
+
+def _check_summary(x):
+    got = ops.tensor_summary(x)
+    ref = dict(zip(ops.SUMMARY_FIELDS, ops._ref_summary(x.cpu()).tolist()))
+    n = x.numel()
+    assert got["count"] == n
+    assert got["nan"] == int(ref["nan"]) and got["inf"] == int(ref["inf"])
+    if n == 0:
+        return got
+    scale = float(x.detach().double().abs().sum()) + 1e-12
+    if got["nan"] == 0 and got["inf"] == 0:
+        assert abs(got["sum"] - ref["sum"]) <= 2e-6 * scale + 1e-6
+        assert math.isclose(got["norm"], ref["norm"], rel_tol=2e-5, abs_tol=1e-6)
+        if n > 1:
+            assert math.isclose(got["std"], ref["std"], rel_tol=1e-3, abs_tol=1e-6)
+    assert got["min"] == ref["min"] and got["max"] == ref["max"] and got["absmax"] == ref["absmax"]
+    return got
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("n", [0, 1, 511, 512, 513, 4099, 1_000_003, 50_000_017])
+def test_tensor_summary_matches_reference(dev, dtype, n):
+    x = (torch.randn(n, device=dev) * 3 + 0.5).to(DT[dtype])
+    _check_summary(x)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+def test_tensor_summary_misaligned_and_nonfinite(dev, dtype):
+    big = torch.randn(100_000, device=dev).to(DT[dtype])
+    x = big[3:]  # misaligned start
+    x[10] = float("nan")
+    x[20] = float("inf")
+    x[5000] = float("-inf")
+    got = _check_summary(x)
+    assert got["nan"] == 1 and got["inf"] == 2 and math.isnan(got["sum"])
+
+
+def test_tensor_summary_large_mean_small_spread_f32(dev):
+    x = 1000.0 + 1e-3 * torch.randn(4_000_000, device=dev)
+    got = ops.tensor_summary(x)
+    assert math.isclose(got["std"], float(x.double().std()), rel_tol=1e-3)
+
+
+def test_tensor_summary_2d_noncontiguous(dev):
+    x = torch.randn(1024, 2048, device=dev, dtype=torch.bfloat16).t()
+    _check_summary(x)
