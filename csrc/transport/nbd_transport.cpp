@@ -82,7 +82,7 @@ enum class PState { Connecting, Greeting, Handshake, Active, Closed };
 struct Peer {
   uint64_t tok = 0;
   int fd = -1;
-  PState st = PState::Greeting;
+  std::atomic<PState> st{PState::Greeting};
   int connect_idx = -1;  // DEALER: index of the ConnectRec that owns this peer
   RBuf rb;
   size_t want = 0;  // bytes needed to complete the frame being parsed (reservation hint)
@@ -201,13 +201,15 @@ struct nbd_msg {
 
 struct nbd_socket {
   int type;
-  // options
+  // options: numeric ones are atomics (set from API threads, read by the I/O thread);
+  // string ones are guarded by optmu and copied out under it.
+  std::mutex optmu;
   std::string identity, token, sig_prefix;
-  int hb_ivl_ms = 0, hb_timeout_ms = 0, reconnect_ivl_ms = 100;
-  bool mandatory = false;
-  int64_t flush_us = 2000;
-  size_t stream_max = 1 << 16;
-  size_t hwm = 0;
+  std::atomic<int> hb_ivl_ms{0}, hb_timeout_ms{0}, reconnect_ivl_ms{100};
+  std::atomic<bool> mandatory{false};
+  std::atomic<int64_t> flush_us{2000};
+  std::atomic<size_t> stream_max{1 << 16};
+  std::atomic<size_t> hwm{0};
 
   int ep = -1, evfd = -1;
   std::thread io;
@@ -317,8 +319,9 @@ struct nbd_socket {
   // Queue bytes for a peer and try to write them right away from the calling thread.
   int enqueue(const PeerP& p, std::string&& data, bool may_block) {
     std::unique_lock<std::mutex> lk(p->omu);
-    if (may_block && hwm > 0) {
-      while (!p->closed && !closing.load() && p->oqbytes > hwm) p->ocv.wait_for(lk, std::chrono::milliseconds(50));
+    const size_t lim = hwm.load();
+    if (may_block && lim > 0) {
+      while (!p->closed && !closing.load() && p->oqbytes > lim) p->ocv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(50));
     }
     if (p->closed) return fail("EPIPE: peer connection closed");
     p->oqbytes += data.size();
@@ -410,7 +413,7 @@ struct nbd_socket {
         auto& rec = connects[(size_t)p->connect_idx];
         if (rec.peer_tok == p->tok) {
           rec.peer_tok = 0;
-          rec.next_try = Clock::now() + std::chrono::milliseconds(reconnect_ivl_ms);
+          rec.next_try = Clock::now() + std::chrono::milliseconds(reconnect_ivl_ms.load());
         }
       }
     }
@@ -421,10 +424,15 @@ struct nbd_socket {
   }
 
   void send_ready(const PeerP& p) {
-    std::string props;
+    std::string props, id, tok;
+    {
+      std::lock_guard<std::mutex> lk(optmu);
+      id = identity;
+      tok = token;
+    }
     put_prop(props, "Socket-Type", type == NBD_ROUTER ? "ROUTER" : "DEALER");
-    put_prop(props, "Identity", identity);
-    if (!token.empty()) put_prop(props, "X-Nbd-Token", token);
+    put_prop(props, "Identity", id);
+    if (!tok.empty()) put_prop(props, "X-Nbd-Token", tok);
     enqueue(p, command("READY", props), false);
   }
 
@@ -461,7 +469,12 @@ struct nbd_socket {
         enqueue(p, command("ERROR", std::string(1, (char)22) + "Incompatible socket"), false);
         return NBD_EV_HANDSHAKE_FAILED;
       }
-      if (!token.empty() && (!has_tok || ptok != token)) {
+      std::string mytok;
+      {
+        std::lock_guard<std::mutex> lk(optmu);
+        mytok = token;
+      }
+      if (!mytok.empty() && (!has_tok || ptok != mytok)) {
         enqueue(p, command("ERROR", std::string(1, (char)13) + "Invalid token"), false);
         return NBD_EV_AUTH_FAILED;
       }
@@ -510,10 +523,14 @@ struct nbd_socket {
     if (type == NBD_ROUTER) m->frames.push_back(p->identity);
     for (auto& f : p->cur) m->frames.push_back(std::move(f));
     p->cur.clear();
-    if (!sig_prefix.empty()) {
+    std::string prefix;
+    {
+      std::lock_guard<std::mutex> lk(optmu);
+      prefix = sig_prefix;
+    }
+    if (!prefix.empty()) {
       size_t k = (type == NBD_ROUTER) ? 1 : 0;
-      if (m->frames.size() > k && m->frames[k].compare(0, sig_prefix.size(), sig_prefix) == 0)
-        ::kill(::getpid(), SIGINT);
+      if (m->frames.size() > k && m->frames[k].compare(0, prefix.size(), prefix) == 0) ::kill(::getpid(), SIGINT);
     }
     push_inbox(m);
   }
@@ -688,13 +705,13 @@ struct nbd_socket {
       else {
         ::close(fd);
         std::lock_guard<std::mutex> lk(mu);
-        connects[idx].next_try = Clock::now() + std::chrono::milliseconds(reconnect_ivl_ms);
+        connects[idx].next_try = Clock::now() + std::chrono::milliseconds(reconnect_ivl_ms.load());
       }
       return;
     }
     if (fd >= 0) ::close(fd);
     std::lock_guard<std::mutex> lk(mu);
-    connects[idx].next_try = Clock::now() + std::chrono::milliseconds(reconnect_ivl_ms);
+    connects[idx].next_try = Clock::now() + std::chrono::milliseconds(reconnect_ivl_ms.load());
   }
 
   // ---------------------------------------------------------------- capture
@@ -740,7 +757,8 @@ struct nbd_socket {
         if (kv.second->st != PState::Active) timers = true;
       if (timers) t = 50;
       if ((hb_ivl_ms > 0 || hb_timeout_ms > 0) && !peers.empty()) {
-        int h = std::max(10, std::min(hb_ivl_ms > 0 ? hb_ivl_ms : 1000, hb_timeout_ms > 0 ? hb_timeout_ms : 1000) / 4);
+        const int ivl = hb_ivl_ms.load(), tmo = hb_timeout_ms.load();
+        int h = std::max(10, std::min(ivl > 0 ? ivl : 1000, tmo > 0 ? tmo : 1000) / 4);
         t = t < 0 ? h : std::min(t, h);
       }
     }
@@ -748,7 +766,7 @@ struct nbd_socket {
       std::lock_guard<std::mutex> lk(cmu);
       for (auto& c : cap) {
         if (c.buf.empty()) continue;
-        auto due = c.first + std::chrono::microseconds(flush_us);
+        auto due = c.first + std::chrono::microseconds(flush_us.load());
         int ms = (int)std::chrono::duration_cast<std::chrono::milliseconds>(due - now).count();
         ms = std::max(ms, 0);
         if (due > now && ms == 0) ms = 1;
@@ -785,7 +803,7 @@ struct nbd_socket {
       if (hb_ivl_ms > 0 && p->minor >= 1 &&
           std::chrono::duration_cast<std::chrono::milliseconds>(now - p->last_ping).count() >= hb_ivl_ms) {
         p->last_ping = now;
-        uint16_t ttl = htobe16((uint16_t)std::min(65535, hb_timeout_ms / 100));
+        uint16_t ttl = htobe16((uint16_t)std::min(65535, hb_timeout_ms.load() / 100));
         enqueue(p, command("PING", std::string(reinterpret_cast<char*>(&ttl), 2)), false);
       }
     }
@@ -793,7 +811,7 @@ struct nbd_socket {
       std::lock_guard<std::mutex> lk(cmu);
       for (int k = 0; k < 2; ++k) {
         Capture& c = cap[k];
-        if (!c.buf.empty() && now - c.first >= std::chrono::microseconds(flush_us)) emit_locked(k);
+        if (!c.buf.empty() && now - c.first >= std::chrono::microseconds(flush_us.load())) emit_locked(k);
       }
     }
   }
@@ -952,6 +970,7 @@ int nbd_setopt_bytes(nbd_socket* s, int opt, const void* data, size_t len) {
   Guard g(s);
   if (!g.ok) return fail("ECLOSED");
   std::string v(static_cast<const char*>(data), len);
+  std::lock_guard<std::mutex> lk(s->optmu);
   switch (opt) {
     case NBD_OPT_IDENTITY:
       if (len > 255) return fail("EINVAL: identity longer than 255 bytes");
@@ -1073,7 +1092,10 @@ int nbd_recv(nbd_socket* s, int timeout_ms, nbd_msg** out) {
   std::unique_lock<std::mutex> lk(s->imu);
   auto pred = [s] { return !s->inbox.empty() || s->inbox_closed; };
   if (timeout_ms < 0) s->icv.wait(lk, pred);
-  else if (!s->icv.wait_for(lk, std::chrono::milliseconds(timeout_ms), pred)) return 1;
+  // system_clock deadline -> pthread_cond_timedwait (steady_clock would use
+  // pthread_cond_clockwait, which older ThreadSanitizer runtimes do not intercept)
+  else if (!s->icv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms), pred))
+    return 1;
   if (s->inbox.empty()) return -1;
   Msg* m = s->inbox.front();
   s->inbox.pop_front();
