@@ -36,6 +36,14 @@ from .timeline import Timeline
 
 Writer = Callable[[str], None]
 
+# Library chatter printed outside any cell (worker bring-up) that carries no information for the
+# notebook user.  Everything else from a worker is shown.
+_NOISE = ("[Gloo] Rank ", "amdgpu.ids: No such file or directory")
+
+
+def _is_noise(line: str) -> bool:
+    return any(n in line for n in _NOISE)
+
 
 def _default_writer(text: str) -> None:
     out = sys.stdout  # resolved per call: IPython swaps sys.stdout per cell
@@ -168,12 +176,16 @@ class Session:
         """Worker output that bypassed the transport (before capture started, or crash reports
         written to the original stderr)."""
         with self._native_lock:
-            self.write("".join(f"[rank {rank} {stream}] {l}\n" for l in text.rstrip("\n").split("\n")))
+            lines = [l for l in text.rstrip("\n").split("\n") if not _is_noise(l)]
+            if lines:
+                self.write("".join(f"[rank {rank} {stream}] {l}\n" for l in lines))
 
     def _background_output(self, rank: int, text: str, stream: str) -> None:
         """Output from a worker that belongs to no request in flight (background threads)."""
         with self._native_lock:
-            self.write("".join(f"[rank {rank}] {l}\n" for l in text.rstrip("\n").split("\n") if l))
+            lines = [l for l in text.rstrip("\n").split("\n") if l and not _is_noise(l)]
+            if lines:
+                self.write("".join(f"[rank {rank}] {l}\n" for l in lines))
 
     def start(self, num_processes: int = 2, master_addr: str = "localhost", gpu_ids: Optional[List[int]] = None,
               timeout: Optional[float] = None, backend: str = "auto", python: Optional[str] = None,

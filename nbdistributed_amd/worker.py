@@ -45,6 +45,26 @@ from .namespace import NamespaceTracker, namespace_info
 from .transport import DEALER, EV_DISCONNECTED, EV_HEARTBEAT_TIMEOUT, OPT_SIGNAL_PREFIX, OPT_STREAM_FLUSH_US, Socket, TransportError
 
 
+def plain(obj: Any) -> Any:
+    """Convert to builtin types only, so a torch-less coordinator can unpickle it (e.g.
+    ``torch.__version__`` is a ``TorchVersion`` str subclass that pickles by reference)."""
+    if obj is None or type(obj) in (bool, int, float, str, bytes):
+        return obj
+    if isinstance(obj, bool):
+        return bool(obj)
+    if isinstance(obj, int):
+        return int(obj)
+    if isinstance(obj, float):
+        return float(obj)
+    if isinstance(obj, str):
+        return str.__str__(obj) if type(obj) is str else "".join(obj)
+    if isinstance(obj, dict):
+        return {plain(k): plain(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(plain(v) for v in obj) if type(obj) in (list, tuple) else [plain(v) for v in obj]
+    return str(obj)
+
+
 class DistributedWorker:
     def __init__(self, rank: int, world_size: int, master_addr: str, master_port: int, coord: str,
                  gpu_id: Optional[int] = None, device_index: Optional[int] = None, backend: str = "auto",
@@ -173,7 +193,7 @@ class DistributedWorker:
         if torch is not None:
             st["torch_version"] = torch.__version__
             st["hip_version"] = getattr(torch.version, "hip", None)
-        return st
+        return plain(st)
 
     # ------------------------------------------------------------------ signals / watchdog
     def _install_signal_handlers(self) -> None:

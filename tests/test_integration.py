@@ -1,0 +1,293 @@
+"""CPU/gloo multi-process integration: every magic through a notebook-shaped shell, with real
+worker processes (BASELINE config 1 and the reference's notebook flow)."""
+import os
+import time
+
+import pytest
+
+from nbdistributed_amd.session import DistributedExecutionError, Session
+from nbdistributed_amd.utils.fakeshell import HeadlessShell
+
+
+class Capture:
+    def __init__(self):
+        self.buf = []
+
+    def __call__(self, s):
+        self.buf.append(s)
+
+    def take(self):
+        out = "".join(self.buf)
+        self.buf.clear()
+        return out
+
+
+@pytest.fixture(scope="module")
+def nb():
+    """A 2-rank session driven like a notebook: %load_ext + %dist_init -n 2."""
+    sh = HeadlessShell()
+    core = sh.load_extension()
+    cap = Capture()
+    core.write = cap
+    core.session.write = cap
+    sh.run_cell("%dist_init -n 2 --backend gloo", raise_errors=True)
+    assert core.session.active, cap.take()
+    out = cap.take()
+    assert "Successfully started 2 workers" in out
+    yield sh, core, cap
+    sh.run_cell("%dist_shutdown")
+
+
+def test_first_cell_right_after_init_is_not_lost(nb):
+    # reference D-2: the first message after %dist_init could be dropped (no READY handshake)
+    sh, core, cap = nb
+    r = sh.run_cell("first = rank * 10\nfirst")
+    assert r.success
+    out = cap.take()
+    assert "🔹 Rank 0:" in out and "🔹 Rank 1:" in out and "10" in out
+
+
+def test_baseline_config1_allreduce_on_gloo(nb):
+    sh, core, cap = nb
+    sh.run_cell("x = torch.ones(4)\ndist.all_reduce(x)\nx")
+    out = cap.take()
+    assert out.count("tensor([2., 2., 2., 2.])") == 2
+
+
+def test_namespace_contract(nb):
+    sh, core, cap = nb
+    res = core.session.execute("(rank, world_size, __rank__, __world_size__, str(device), __name__, dist.get_backend())",
+                               render=False)
+    assert res.results[0]["output"] == "(0, 2, 0, 2, 'cpu', '__main__', 'gloo')"
+    assert res.results[1]["output"] == "(1, 2, 1, 2, 'cpu', '__main__', 'gloo')"
+
+
+def test_print_with_several_args_is_one_line(nb):
+    # reference D-8: print(a, b, c) became 3 lines (one per write() chunk)
+    sh, core, cap = nb
+    sh.run_cell("print('a', 'b', 3)")
+    out = cap.take()
+    assert out.count("  a b 3\n") == 2
+
+
+def test_stderr_and_c_level_output_are_streamed(nb):
+    sh, core, cap = nb
+    sh.run_cell("import sys, os\nprint('err line', file=sys.stderr)\nos.system('echo from-shell-$RANK')")
+    out = cap.take()
+    assert out.count("err line") == 2 and "from-shell-0" in out and "from-shell-1" in out
+
+
+def test_stderr_flood_does_not_wedge(nb):
+    # reference §5.3: 200 KB of stderr filled an undrained pipe and wedged the worker forever
+    sh, core, cap = nb
+    t = time.time()
+    r = sh.run_cell("import sys\nsys.stderr.write('x' * 300_000 + '\\n')\nsys.stderr.flush()\n'alive'")
+    assert r.success and time.time() - t < 20
+    assert cap.take().count("'alive'") == 2
+
+
+def test_rank_magic_both_forms_and_subset(nb):
+    sh, core, cap = nb
+    sh.run_cell("%%rank [0]\nsolo = 'r0'\nprint('only', rank)")
+    out = cap.take()
+    assert "only 0" in out and "only 1" not in out
+    sh.run_cell("%%rank[1]\nprint('nospace', rank)")  # reference D-6: this form raised UsageError
+    out = cap.take()
+    assert "nospace 1" in out and "nospace 0" not in out
+    res = core.session.execute("'solo' in dir()", render=False)
+    assert res.results[0]["output"] == "True" and res.results[1]["output"] == "False"
+    sh.run_cell("%%rank [0-1]\nprint('both', rank)")
+    assert cap.take().count("both") == 2
+    sh.run_cell("%%rank\nprint('x')")
+    assert "Usage" in cap.take()
+
+
+def test_selective_build_then_broadcast(nb):
+    # BASELINE config 3 (CPU-sized): build on rank 0, broadcast params to all ranks
+    sh, core, cap = nb
+    sh.run_cell("torch.manual_seed(rank)\nmodel = torch.nn.Linear(64, 64)")
+    sh.run_cell("%%rank [0]\nref_sum = float(sum(p.detach().sum() for p in model.parameters()))")
+    sh.run_cell("for p in model.parameters():\n    dist.broadcast(p.data, src=0)\n"
+                "s = torch.tensor([float(sum(p.sum() for p in model.parameters()))])\n"
+                "g = [torch.zeros(1) for _ in range(world_size)]\ndist.all_gather(g, s)\n"
+                "bool(torch.allclose(g[0], g[1]))")
+    assert cap.take().count("  True\n") == 2
+
+
+def test_errors_fail_the_cell_with_per_rank_tracebacks(nb):
+    sh, core, cap = nb
+    r = sh.run_cell("if rank == 1:\n    raise ValueError('only rank 1 fails')\n'fine'")
+    assert isinstance(r.error_in_exec, DistributedExecutionError)
+    res = r.error_in_exec.result
+    assert list(res.errors) == [1] and res.results[0]["output"].endswith("'fine'")
+    assert "only rank 1 fails" in "\n".join(r.error_in_exec._render_traceback_())
+
+
+def test_ide_sync_proxies(nb):
+    sh, core, cap = nb
+    sh.run_cell("weights = torch.zeros(128, 256)\ncount = 7\ndef helper(a, b=2):\n    'doc'\n    return a\n")
+    ns = sh.user_ns
+    assert ns["count"] == 7
+    assert ns["weights"].device.type == "meta" and tuple(ns["weights"].shape) == (128, 256)
+    import inspect
+
+    assert str(inspect.signature(ns["helper"])) == "(a, b=2)"
+    ns["count"] = "mine"
+    sh.run_cell("count = 8")
+    assert ns["count"] == "mine"  # never clobbers a local definition
+    sh.run_cell("%dist_sync_ide")
+    assert "Synchronized" in cap.take()
+
+
+def test_sync_status_debug_mode_timeline(nb, tmp_path):
+    sh, core, cap = nb
+    sh.run_cell("%sync")
+    assert "✓ Synchronized 2 ranks" in cap.take()
+    sh.run_cell("%dist_status")
+    out = cap.take()
+    assert "Rank 0: ✓ PID" in out and "Rank 1: ✓ PID" in out and "Status: Running" in out
+    sh.run_cell("%dist_debug")
+    out = cap.take()
+    assert "Connected peers: 2" in out and "Control-plane round trip" in out
+    sh.run_cell("%dist_mode --disable")
+    assert "disabled" in cap.take()
+    sh.run_cell("local_only = 1")
+    assert sh.user_ns.get("local_only") == 1
+    sh.run_cell("%dist_mode -e")
+    assert "enabled" in cap.take()
+    sh.run_cell("%timeline_debug")
+    assert "Timeline:" in cap.take()
+    p = tmp_path / "tl.json"
+    sh.run_cell(f"%timeline_save {p}")
+    assert p.exists() and (tmp_path / "tl.trace.json").exists()
+    sh.run_cell("%timeline_clear")
+    assert "Cleared" in cap.take()
+
+
+def test_pull_push(nb):
+    sh, core, cap = nb
+    sh.run_cell("arr = torch.arange(6.).reshape(2, 3) + rank")
+    sh.run_cell("%dist_pull arr --rank 1 --as arr1")
+    import torch
+
+    assert torch.equal(sh.user_ns["arr1"], torch.arange(6.).reshape(2, 3) + 1)
+    sh.user_ns["cfg"] = {"lr": 0.1}
+    sh.run_cell("%dist_push cfg")
+    res = core.session.execute("cfg['lr']", render=False)
+    assert res.results[1]["output"] == "0.1"
+
+
+def test_interrupt_running_python_cell(nb):
+    sh, core, cap = nb
+    import threading
+
+    s = core.session
+    threading.Timer(0.5, lambda: s.interrupt()).start()
+    t = time.time()
+    r = sh.run_cell("import time\nwhile True:\n    time.sleep(0.01)")
+    assert time.time() - t < 10
+    assert isinstance(r.error_in_exec, DistributedExecutionError)
+    assert all(e.get("status") == "interrupted" for e in r.error_in_exec.result.errors.values())
+    assert sh.run_cell("'still alive'").success  # workers survive the interrupt
+
+
+def test_cell_latency_is_sub_millisecond_scale(nb):
+    sh, core, cap = nb
+    lat = []
+    for _ in range(30):
+        t = time.perf_counter()
+        core.session.execute("1", render=False)
+        lat.append(time.perf_counter() - t)
+    lat.sort()
+    assert lat[15] < 0.02  # reference: 111.6 ms
+
+
+# ------------------------------------------------------------------ lifecycle / faults
+def _alive(pid):
+    try:
+        os.kill(pid, 0)
+        return True
+    except ProcessLookupError:
+        return False
+
+
+def test_dist_shutdown_really_stops_workers():
+    # reference D-1: %dist_shutdown left the workers running
+    sh = HeadlessShell()
+    core = sh.load_extension()
+    core.write = core.session.write = Capture()
+    sh.run_cell("%dist_init -n 2 --backend gloo", raise_errors=True)
+    pids = [w.pid for w in core.session.pm.workers]
+    assert all(_alive(p) for p in pids)
+    sh.run_cell("%dist_shutdown")
+    time.sleep(0.5)
+    assert not any(_alive(p) for p in pids)
+    assert not core.auto_mode
+
+
+def test_rank_crash_mid_cell_fails_fast_with_partial_results():
+    s = Session(writer=lambda t: None)
+    s.start(2, backend="gloo")
+    try:
+        t = time.time()
+        with pytest.raises(DistributedExecutionError) as ei:
+            s.execute("import os, time\nif rank == 1:\n    os._exit(7)\ntime.sleep(0.2)\n'rank0 ok'")
+        assert time.time() - t < 5
+        res = ei.value.result
+        assert 1 in res.dead and "exit code 7" in res.dead[1] or "connection lost" in res.dead[1]
+        assert res.results[0]["output"] == "'rank0 ok'"
+        # later cells fail fast on the dead rank instead of hanging
+        t = time.time()
+        r2 = s.execute("rank", raise_on_error=False)
+        assert 1 in r2.dead and time.time() - t < 2
+        assert r2.results[0]["output"] == "0"
+        st = s.status()
+        assert st[1]["running"] is False and st[1]["returncode"] == 7
+    finally:
+        s.shutdown()
+
+
+def test_dist_init_replaces_degraded_cluster():
+    sh = HeadlessShell()
+    core = sh.load_extension()
+    cap = Capture()
+    core.write = core.session.write = cap
+    sh.run_cell("%dist_init -n 2 --backend gloo", raise_errors=True)
+    sh.run_cell("%%rank [1]\nimport os\nos._exit(1)")
+    cap.take()
+    sh.run_cell("%dist_init -n 2 --backend gloo")
+    out = cap.take()
+    assert "Replacing a degraded session" in out and "Successfully started 2 workers" in out
+    assert sh.run_cell("rank").success
+    sh.run_cell("%dist_reset")
+    assert "Reset complete" in cap.take()
+    assert not core.session.active
+
+
+def test_bootstrap_failure_is_reported():
+    s = Session(writer=lambda t: None)
+    with pytest.raises(RuntimeError, match="failed to start|exited"):
+        s.start(1, backend="rccl")  # no GPU here: rank 0 must report why it cannot start
+    assert not s.active
+
+
+@pytest.mark.parametrize("n", [1, 4, 8])
+def test_scale_world_sizes(n):
+    s = Session(writer=lambda t: None)
+    t0 = time.time()
+    s.start(n, backend="gloo")
+    try:
+        init_s = time.time() - t0
+        res = s.execute("x = torch.ones(8) * (rank + 1)\ndist.all_reduce(x)\nint(x[0])", render=False)
+        want = str(n * (n + 1) // 2)
+        assert all(res.results[r]["output"] == want for r in range(n))
+        lat = []
+        for _ in range(20):
+            t = time.perf_counter()
+            s.execute("1", render=False)
+            lat.append(time.perf_counter() - t)
+        lat.sort()
+        assert lat[10] < 0.05, lat
+        assert init_s < 120
+    finally:
+        s.shutdown()
