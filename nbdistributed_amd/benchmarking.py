@@ -51,6 +51,100 @@ def _nbd_ar_check():
 """
 
 
+DDP_SETUP = """
+import time as _t
+from nbdistributed_amd.models import GPT2, GPT2Config, linear_4096
+from nbdistributed_amd.parallel import DistributedDataParallel as _NbdDDP
+from torch.nn.parallel import DistributedDataParallel as _TorchDDP
+
+def _nbd_time_steps(step, steps, warm):
+    for _ in range(warm):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier(device_ids=[device.index])
+    torch.cuda.synchronize()
+    t = _t.perf_counter()
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    return (_t.perf_counter() - t) / steps * 1e3, float(out)
+
+def _nbd_gpt2_bench(steps, warm, B, T, impl):
+    torch.manual_seed(0)
+    m = GPT2(GPT2Config.small()).to(device)
+    if impl == "nbd":
+        model = _NbdDDP(m, comm_dtype=torch.bfloat16)
+    else:
+        model = _TorchDDP(m, device_ids=[device.index], bucket_cap_mb=25)
+    opt = torch.optim.AdamW(m.parameters(), lr=3e-4, fused=True)
+    x = torch.randint(0, m.config.vocab_size, (B, T), device=device)
+    def step():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            _, loss = model(x, x)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=False)
+        return loss.detach()
+    ms, loss = _nbd_time_steps(step, steps, warm)
+    del model, opt, m, x
+    torch.cuda.empty_cache()
+    return ms, loss
+
+def _nbd_linear_bench(steps, warm, rows, impl):
+    torch.manual_seed(0)
+    m = linear_4096().to(device)
+    model = _NbdDDP(m) if impl == "nbd" else _TorchDDP(m, device_ids=[device.index])
+    opt = torch.optim.SGD(m.parameters(), lr=1e-3)
+    x = torch.randn(rows, 4096, device=device)
+    def step():
+        loss = model(x).square().mean()
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=False)
+        return loss.detach()
+    ms, loss = _nbd_time_steps(step, steps, warm)
+    del model, opt, m, x
+    torch.cuda.empty_cache()
+    return ms, loss
+"""
+
+
+def _max_over_ranks(res) -> float:
+    vals = []
+    for r in res.ranks:
+        out = res.results[r]["output"]
+        vals.append(float(out.strip("()").split(",")[0]))
+    return max(vals)
+
+
+def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 1024, compare_torch: bool = True,
+              linear_rows: int = 8192) -> Dict[str, Any]:
+    """BASELINE configs 4 and 5 as notebook cells: DDP steps timed inside each worker (max over
+    ranks).  GPT-2 small: fp32 master weights, bf16 autocast, bf16 gradient wire format through
+    the fused HIP bucket kernels; synthetic tokens."""
+    n = session.world_size
+    session.execute(DDP_SETUP, render=False)
+    out: Dict[str, Any] = {"model": "gpt2-small (124,439,808 params)", "per_gpu_batch": B, "seq_len": T,
+                           "global_batch": B * n, "steps": steps, "warmup": warmup}
+    r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'nbd')", render=False)
+    ms = _max_over_ranks(r)
+    toks = n * B * T / (ms / 1e3)
+    out.update(ms_per_step=ms, tokens_per_s=toks, tokens_per_s_per_gpu=toks / n,
+               mfu=6 * 124_439_808 * toks / (2.5e15 * n))
+    if compare_torch:
+        r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'torch')", render=False)
+        tms = _max_over_ranks(r)
+        out.update(torch_ddp_ms_per_step=tms, torch_ddp_tokens_per_s=n * B * T / (tms / 1e3),
+                   speedup_vs_torch_ddp=tms / ms)
+    r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'nbd')", render=False)
+    lin = {"rows": linear_rows, "ms_per_step": _max_over_ranks(r)}
+    if compare_torch:
+        r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'torch')", render=False)
+        lin["torch_ddp_ms_per_step"] = _max_over_ranks(r)
+    out["linear4096"] = lin
+    return out
+
+
 def _log(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
@@ -110,7 +204,7 @@ def bench_sweep(session, dtype: str = "bfloat16", max_bytes: int = 1 << 30, min_
 
 
 def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: bool = False,
-            ar_bytes: int = 1 << 30) -> Dict[str, Any]:
+            ar_bytes: int = 1 << 30, ddp: bool = True, ddp_steps: int = 20) -> Dict[str, Any]:
     n = session.world_size
     _log(f"phase 1: {warmup}+{steps} trivial %%distributed cells on {n} rank(s)")
     cells = bench_cells(session, steps, warmup)
@@ -124,6 +218,10 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
     if sweep and gpu:
         _log("phase 3: all_reduce sweep")
         out["sweep"] = bench_sweep(session)
+    if ddp and gpu:
+        _log("phase 4: DDP steps (GPT-2 small bf16 config 5, Linear 4096 config 4)")
+        out["ddp"] = bench_ddp(session, steps=ddp_steps)
+        _log(f"gpt2 ddp {out['ddp']['ms_per_step']:.2f} ms/step {out['ddp']['tokens_per_s']:.0f} tok/s")
     return out
 
 

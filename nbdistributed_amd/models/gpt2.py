@@ -1,0 +1,123 @@
+"""GPT-2 (124M "small" by default) for the BASELINE config-5 DDP loop.
+
+BASELINE.json config 5: "00_accelerate.ipynb-style GPT-2-small DDP loop, bf16, synthetic tokens"
+(124,439,808 parameters with the tied LM head).  Plain PyTorch modules; on
+MI355X the GEMMs go to hipBLASLt and attention to PyTorch's fused SDPA (AOTriton/CK flash
+kernels), the MLP's bias+GELU and the residual LayerNorms run through torch's fused ROCm kernels.
+Random init (no checkpoints: no network), GPT-2 initialisation scheme.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+@dataclass
+class GPT2Config:
+    vocab_size: int = 50257
+    n_positions: int = 1024
+    n_embd: int = 768
+    n_layer: int = 12
+    n_head: int = 12
+    dropout: float = 0.0
+    bias: bool = True
+    tie_weights: bool = True
+
+    @classmethod
+    def small(cls):
+        return cls()
+
+    @classmethod
+    def tiny(cls):
+        return cls(vocab_size=512, n_positions=128, n_embd=64, n_layer=2, n_head=4)
+
+
+class CausalSelfAttention(nn.Module):
+    def __init__(self, c: GPT2Config):
+        super().__init__()
+        assert c.n_embd % c.n_head == 0
+        self.n_head = c.n_head
+        self.c_attn = nn.Linear(c.n_embd, 3 * c.n_embd, bias=c.bias)
+        self.c_proj = nn.Linear(c.n_embd, c.n_embd, bias=c.bias)
+        self.dropout = c.dropout
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, T, C = x.shape
+        q, k, v = self.c_attn(x).split(C, dim=2)
+        hd = C // self.n_head
+        q = q.view(B, T, self.n_head, hd).transpose(1, 2)
+        k = k.view(B, T, self.n_head, hd).transpose(1, 2)
+        v = v.view(B, T, self.n_head, hd).transpose(1, 2)
+        y = F.scaled_dot_product_attention(q, k, v, is_causal=True, dropout_p=self.dropout if self.training else 0.0)
+        y = y.transpose(1, 2).reshape(B, T, C)
+        return self.c_proj(y)
+
+
+class MLP(nn.Module):
+    def __init__(self, c: GPT2Config):
+        super().__init__()
+        self.c_fc = nn.Linear(c.n_embd, 4 * c.n_embd, bias=c.bias)
+        self.c_proj = nn.Linear(4 * c.n_embd, c.n_embd, bias=c.bias)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
+
+
+class Block(nn.Module):
+    def __init__(self, c: GPT2Config):
+        super().__init__()
+        self.ln_1 = nn.LayerNorm(c.n_embd, bias=c.bias)
+        self.attn = CausalSelfAttention(c)
+        self.ln_2 = nn.LayerNorm(c.n_embd, bias=c.bias)
+        self.mlp = MLP(c)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = x + self.attn(self.ln_1(x))
+        return x + self.mlp(self.ln_2(x))
+
+
+class GPT2(nn.Module):
+    def __init__(self, config: Optional[GPT2Config] = None):
+        super().__init__()
+        c = config or GPT2Config()
+        self.config = c
+        self.wte = nn.Embedding(c.vocab_size, c.n_embd)
+        self.wpe = nn.Embedding(c.n_positions, c.n_embd)
+        self.h = nn.ModuleList([Block(c) for _ in range(c.n_layer)])
+        self.ln_f = nn.LayerNorm(c.n_embd, bias=c.bias)
+        self.lm_head = nn.Linear(c.n_embd, c.vocab_size, bias=False)
+        if c.tie_weights:
+            self.lm_head.weight = self.wte.weight
+        self.apply(self._init)
+        for n, p in self.named_parameters():
+            if n.endswith("c_proj.weight"):
+                nn.init.normal_(p, mean=0.0, std=0.02 / math.sqrt(2 * c.n_layer))
+
+    @staticmethod
+    def _init(m: nn.Module) -> None:
+        if isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, mean=0.0, std=0.02)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, mean=0.0, std=0.02)
+
+    def num_params(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None):
+        B, T = idx.shape
+        pos = torch.arange(T, device=idx.device)
+        x = self.wte(idx) + self.wpe(pos)
+        for blk in self.h:
+            x = blk(x)
+        logits = self.lm_head(self.ln_f(x))
+        loss = None
+        if targets is not None:
+            loss = F.cross_entropy(logits.float().view(-1, logits.size(-1)), targets.view(-1))
+        return logits, loss

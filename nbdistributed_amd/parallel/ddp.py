@@ -1,0 +1,244 @@
+"""Data parallelism for notebook cells: bucketed gradient all-reduce overlapped with backward.
+
+Reference: the reference has no parallelism of its own — its notebook wraps the model with HF
+accelerate, i.e. torch DDP (notebook exec 32/35: ``accelerator.prepare`` /
+``accelerator.backward``).  ``DistributedDataParallel`` here is a drop-in for that pattern,
+designed for MI355X + RCCL over xGMI:
+
+* gradients are grouped into buckets in reverse registration order (≈ backward order); the
+  bucket cap defaults to 64 MiB of wire bytes — large enough that each RCCL all-reduce runs in
+  its bandwidth regime on a point-to-point xGMI ring (per-link bound), with a small
+  first bucket (4 MiB) so communication starts early in backward;
+* when the last gradient of a bucket is accumulated (``register_post_accumulate_grad_hook``),
+  the bucket is launched on a dedicated high-priority HIP stream: one fused HIP kernel
+  (``nbd::bucket_flatten``) gathers the grads into the bucket while casting to the wire dtype
+  (fp32 -> bf16 halves the xGMI bytes) and pre-dividing by the world size; RCCL all-reduces the
+  bucket; a second fused kernel (``nbd::bucket_unflatten``) scatters back, casting to the grads'
+  dtype — all overlapped with the rest of backward on the compute stream;
+* buckets are launched strictly in bucket order on every rank (a bucket that becomes ready early
+  waits for its predecessors), so ranks always issue the same collective sequence;
+* parameters that got no gradient this step (unused branches) are flattened as zeros at the end
+  of backward so no rank ever waits on a missing bucket;
+* ``no_sync()`` for gradient accumulation, buffers broadcast from rank 0 in forward, parameters
+  broadcast from rank 0 at construction (coalesced through the same flatten kernel).
+
+Also provides DDP communication hooks for stock ``torch.nn.parallel.DistributedDataParallel``
+(``bf16_compress_hook``) built on the same fused kernels.
+"""
+from __future__ import annotations
+
+import contextlib
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+
+
+@dataclass
+class _Bucket:
+    index: int
+    params: List[torch.nn.Parameter]
+    offsets: List[int]
+    numel: int
+    buffer: Optional[torch.Tensor] = None
+    pending: int = 0
+    ready: bool = False
+    launched: bool = False
+    work: Any = None
+    grads: List[torch.Tensor] = field(default_factory=list)
+
+
+class DistributedDataParallel(torch.nn.Module):
+    def __init__(self, module: torch.nn.Module, process_group=None, bucket_cap_mb: float = 64.0,
+                 first_bucket_mb: float = 4.0, comm_dtype: Optional[torch.dtype] = None,
+                 broadcast_buffers: bool = True, init_sync: bool = True, align: int = 64):
+        super().__init__()
+        self.module = module
+        self.pg = process_group if process_group is not None else dist.group.WORLD
+        self.world = dist.get_world_size(self.pg)
+        self.broadcast_buffers = broadcast_buffers
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        if not self.params:
+            raise ValueError("module has no trainable parameters")
+        self.device = self.params[0].device
+        self.cuda = self.device.type == "cuda"
+        self.comm_dtype = comm_dtype or self.params[0].dtype
+        self._require_sync = True
+        self._in_backward = False
+        self._next_launch = 0
+        self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1) if self.cuda else None
+        self.buckets = self._plan(bucket_cap_mb, first_bucket_mb, align)
+        self._bucket_of: Dict[int, _Bucket] = {}
+        for b in self.buckets:
+            b.buffer = torch.zeros(b.numel, dtype=self.comm_dtype, device=self.device)
+            for p in b.params:
+                self._bucket_of[id(p)] = b
+        self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in self.params]
+        if init_sync and self.world > 1:
+            self._broadcast_tensors([p.data for p in module.parameters()])
+            self._broadcast_tensors(list(module.buffers()))
+        self.stats = {"buckets": len(self.buckets), "bucket_numels": [b.numel for b in self.buckets],
+                      "comm_dtype": str(self.comm_dtype)}
+
+    # ------------------------------------------------------------------ planning
+    def _plan(self, cap_mb: float, first_mb: float, align: int) -> List[_Bucket]:
+        esz = torch.tensor([], dtype=self.comm_dtype).element_size()
+        buckets: List[_Bucket] = []
+        cur: List[torch.nn.Parameter] = []
+        cur_bytes = 0
+        limit = first_mb * 2 ** 20
+        for p in reversed(self.params):
+            nbytes = p.numel() * esz
+            if cur and cur_bytes + nbytes > limit:
+                buckets.append(self._make_bucket(len(buckets), cur, align))
+                cur, cur_bytes = [], 0
+                limit = cap_mb * 2 ** 20
+            cur.append(p)
+            cur_bytes += nbytes
+        if cur:
+            buckets.append(self._make_bucket(len(buckets), cur, align))
+        return buckets
+
+    @staticmethod
+    def _make_bucket(i: int, params: List[torch.nn.Parameter], align: int) -> _Bucket:
+        offs, total = ops.plan_offsets([p.numel() for p in params], align)
+        return _Bucket(index=i, params=list(params), offsets=offs, numel=total)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, *args, **kwargs):
+        if self._require_sync and self.broadcast_buffers and self.world > 1:
+            bufs = [b for b in self.module.buffers() if b.is_floating_point() or b.dtype in (torch.int64, torch.int32)]
+            if bufs:
+                self._broadcast_tensors(bufs)
+        return self.module(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        prev = self._require_sync
+        self._require_sync = False
+        try:
+            yield
+        finally:
+            self._require_sync = prev
+
+    # ------------------------------------------------------------------ backward hooks
+    def _start_backward(self) -> None:
+        self._in_backward = True
+        self._next_launch = 0
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.ready = b.launched = False
+            b.work = None
+        torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+
+    def _grad_ready(self, p: torch.nn.Parameter) -> None:
+        if not self._require_sync:
+            return
+        if not self._in_backward:
+            self._start_backward()
+        b = self._bucket_of[id(p)]
+        b.pending -= 1
+        if b.pending == 0:
+            b.ready = True
+            self._launch_ready()
+
+    def _launch_ready(self) -> None:
+        while self._next_launch < len(self.buckets) and self.buckets[self._next_launch].ready:
+            self._launch(self.buckets[self._next_launch])
+            self._next_launch += 1
+
+    def _bucket_grads(self, b: _Bucket) -> List[torch.Tensor]:
+        grads = []
+        for p in b.params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            grads.append(p.grad)
+        return grads
+
+    def _launch(self, b: _Bucket) -> None:
+        grads = self._bucket_grads(b)
+        b.grads = grads
+        scale = 1.0 / self.world
+        if self.cuda:
+            cur = torch.cuda.current_stream(self.device)
+            self.comm_stream.wait_stream(cur)  # the grads were produced on the compute stream
+            with torch.cuda.stream(self.comm_stream):
+                ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
+                b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)
+                b.work.wait()  # device-side: the comm stream waits for RCCL's stream
+                ops.bucket_unflatten(b.buffer, grads, b.offsets)
+            for g in grads:
+                g.record_stream(self.comm_stream)
+        else:
+            ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
+            b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)
+        b.launched = True
+
+    def _finalize(self) -> None:
+        # buckets whose params got no gradient this step (unused parameters): zeros
+        for b in self.buckets:
+            if not b.ready:
+                b.ready = True
+        self._launch_ready()
+        if self.cuda:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+        else:
+            for b in self.buckets:
+                if b.work is not None:
+                    b.work.wait()
+                    ops.bucket_unflatten(b.buffer, b.grads, b.offsets)
+        for b in self.buckets:
+            b.grads = []
+            b.work = None
+        self._in_backward = False
+
+    # ------------------------------------------------------------------ broadcast
+    def _broadcast_tensors(self, tensors: List[torch.Tensor]) -> None:
+        groups: Dict[torch.dtype, List[torch.Tensor]] = {}
+        for t in tensors:
+            groups.setdefault(t.dtype, []).append(t)
+        for dt, ts in groups.items():
+            if dt in (torch.float32, torch.bfloat16, torch.float16):
+                flat = [t if t.is_contiguous() else t.contiguous() for t in ts]
+                buf, offs = ops.bucket_flatten(flat, dtype=dt)
+                dist.broadcast(buf, src=dist.get_global_rank(self.pg, 0) if self.pg is not dist.group.WORLD else 0,
+                               group=self.pg)
+                ops.bucket_unflatten(buf, flat, offs)
+                for t, f in zip(ts, flat):
+                    if t.data_ptr() != f.data_ptr():
+                        t.copy_(f)
+            else:
+                for t in ts:
+                    dist.broadcast(t, src=0, group=self.pg)
+
+
+# ---------------------------------------------------------------------- comm hooks for torch DDP
+def bf16_compress_hook(process_group, bucket):
+    """Fused replacement for torch's bf16_compress_hook: one HIP kernel casts fp32 -> bf16 and
+    pre-divides, RCCL all-reduces the bf16 bucket, one HIP kernel casts back into the fp32
+    bucket (torch's version runs three eager kernels plus a copy)."""
+    group = process_group if process_group is not None else dist.group.WORLD
+    world = dist.get_world_size(group)
+    buf = bucket.buffer()
+    comp = torch.empty(buf.numel(), dtype=torch.bfloat16, device=buf.device)
+    ops.bucket_flatten([buf], comp, [0], scale=1.0 / world)
+    fut = dist.all_reduce(comp, group=group, async_op=True).get_future()
+
+    def _decompress(f):
+        ops.bucket_unflatten(comp, [buf], [0])
+        return buf
+
+    return fut.then(_decompress)
+
+
+def allreduce_hook(process_group, bucket):
+    """Plain averaging all-reduce with the pre-divide fused into one HIP pass."""
+    group = process_group if process_group is not None else dist.group.WORLD
+    world = dist.get_world_size(group)
+    buf = bucket.buffer()
+    ops.bucket_unflatten(buf, [buf], [0], scale=1.0 / world)  # in-place scale (same-dtype copy)
+    fut = dist.all_reduce(buf, group=group, async_op=True).get_future()
+    return fut.then(lambda f: f.value()[0])

@@ -53,3 +53,32 @@ def test_cell_latency_on_gpu_worker(gpu_session):
         lat.append(time.perf_counter() - t)
     lat.sort()
     assert lat[len(lat) // 2] < 0.005  # < 5 ms p50 (reference: 111.6 ms)
+
+
+def test_nbd_ddp_on_gpu_matches_plain_backward(gpu_session):
+    code = (
+        "import copy\n"
+        "from nbdistributed_amd.models import GPT2, GPT2Config\n"
+        "from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP\n"
+        "torch.manual_seed(0)\n"
+        "base = GPT2(GPT2Config.tiny()).to(device)\n"
+        "plain = copy.deepcopy(base)\n"
+        "d32 = NbdDDP(copy.deepcopy(base), bucket_cap_mb=0.05, first_bucket_mb=0.01)\n"
+        "d16 = NbdDDP(copy.deepcopy(base), comm_dtype=torch.bfloat16)\n"
+        "idx = torch.randint(0, 512, (4, 64), device=device)\n"
+        "for m in (plain, d32, d16):\n"
+        "    m(idx, idx)[1].backward()\n"
+        "torch.cuda.synchronize()\n"
+        "e32 = max(float((p.grad - q.grad).abs().max()) for p, q in zip(plain.parameters(), d32.module.parameters()))\n"
+        "e16 = max(float(((p.grad - q.grad).abs().max() / (p.grad.abs().max() + 1e-12))) "
+        "for p, q in zip(plain.parameters(), d16.module.parameters()))\n"
+        "(len(d32.buckets) > 1, e32 == 0.0, e16 < 1e-2)"
+    )
+    r = gpu_session.execute(code, render=False)
+    assert r.results[0]["output"] == "(True, True, True)", r.results[0]
+
+
+def test_tensor_echo_uses_device_summary(gpu_session):
+    r = gpu_session.execute("big = torch.ones(1 << 20, device=device, dtype=torch.bfloat16) * 2\nbig", render=False)
+    out = r.results[0]["output"]
+    assert "mean=2" in out and "std=0" in out and "cuda:0" in out
