@@ -8,8 +8,9 @@ MI355X-native version:
 
 * ``"rccl"`` is registered as a first-class backend name (stock torch rejects it: SURVEY §0.1).
   On ROCm, torch's ProcessGroupNCCL *is* RCCL, so the creator builds a ProcessGroupNCCL with our
-  options (high-priority streams by default so collectives are scheduled ahead of compute
-  kernels on the same CU pool).
+  options.  Collective streams use NORMAL priority: measured on MI355X (ROCm 7, GPT-2 small
+  bf16 DDP step, benchmarks/ddp_compare.py), high-priority RCCL streams doubled the step time
+  (55 ms vs 26 ms) — opt in with NBD_RCCL_HIGH_PRIORITY=1.
 * The communicator is initialised eagerly during ``%dist_init`` with one tiny all-reduce, so the
   first collective inside a cell does not pay ncclCommInitRank (topology discovery + xGMI ring
   setup) — that cost moves to worker bring-up, where it belongs.
@@ -39,7 +40,7 @@ def register_rccl_backend() -> bool:
     except ImportError:
         return False
 
-    high_prio = os.environ.get("NBD_RCCL_HIGH_PRIORITY", "1") not in ("0", "false", "False")
+    high_prio = os.environ.get("NBD_RCCL_HIGH_PRIORITY", "0") not in ("0", "false", "False")
 
     def _create_rccl(store, rank, world_size, timeout):
         opts = ProcessGroupNCCL.Options(is_high_priority_stream=high_prio)

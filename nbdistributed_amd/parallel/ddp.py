@@ -10,7 +10,7 @@ designed for MI355X + RCCL over xGMI:
   its bandwidth regime on a point-to-point xGMI ring (per-link bound), with a small
   first bucket (4 MiB) so communication starts early in backward;
 * when the last gradient of a bucket is accumulated (``register_post_accumulate_grad_hook``),
-  the bucket is launched on a dedicated high-priority HIP stream: one fused HIP kernel
+  the bucket is launched on a dedicated HIP stream (normal priority — see __init__): one fused HIP kernel
   (``nbd::bucket_flatten``) gathers the grads into the bucket while casting to the wire dtype
   (fp32 -> bf16 halves the xGMI bytes) and pre-dividing by the world size; RCCL all-reduces the
   bucket; a second fused kernel (``nbd::bucket_unflatten``) scatters back, casting to the grads'
@@ -69,7 +69,15 @@ class DistributedDataParallel(torch.nn.Module):
         self._require_sync = True
         self._in_backward = False
         self._next_launch = 0
-        self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1) if self.cuda else None
+        import os
+
+        # normal | high | none.  A high-priority stream measured 2.2x slower end to end on
+        # MI355X (GPT-2 small DDP step 55 ms vs 25.5 ms, benchmarks/ddp_compare.py).
+        mode = os.environ.get("NBD_DDP_COMM_STREAM", "normal")
+        if not self.cuda or mode == "none":
+            self.comm_stream = None
+        else:
+            self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1 if mode == "high" else 0)
         self.buckets = self._plan(bucket_cap_mb, first_bucket_mb, align)
         self._bucket_of: Dict[int, _Bucket] = {}
         for b in self.buckets:
@@ -162,7 +170,12 @@ class DistributedDataParallel(torch.nn.Module):
         grads = self._bucket_grads(b)
         b.grads = grads
         scale = 1.0 / self.world
-        if self.cuda:
+        if self.cuda and self.comm_stream is None:
+            ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
+            b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)
+            b.work.wait()
+            ops.bucket_unflatten(b.buffer, grads, b.offsets)
+        elif self.cuda:
             cur = torch.cuda.current_stream(self.device)
             self.comm_stream.wait_stream(cur)  # the grads were produced on the compute stream
             with torch.cuda.stream(self.comm_stream):
@@ -183,7 +196,7 @@ class DistributedDataParallel(torch.nn.Module):
             if not b.ready:
                 b.ready = True
         self._launch_ready()
-        if self.cuda:
+        if self.cuda and self.comm_stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
         else:
             for b in self.buckets:
