@@ -414,6 +414,7 @@ class MagicCore:
     def dist_interrupt(self, line: str = "") -> None:
         p = _parser("%dist_interrupt")
         p.add_argument("--hard", action="store_true", help="send SIGINT to the worker processes directly")
+        p.add_argument("--kill", action="store_true", help="SIGKILL the ranks (last resort; then %%dist_init)")
         p.add_argument("ranks", nargs="?", default=None)
         args = p.parse_args(shlex.split(line))
         s = self.session
@@ -421,8 +422,9 @@ class MagicCore:
             self.p("No distributed workers running")
             return
         ranks = parse_ranks(args.ranks, s.num_processes) if args.ranks else None
-        s.interrupt(ranks, hard=args.hard)
-        self.p(f"⚡ Interrupt sent to ranks {format_ranks(ranks or s.all_ranks())}")
+        s.interrupt(ranks, hard=args.hard, kill=args.kill)
+        what = "Killed" if args.kill else "Interrupt sent to"
+        self.p(f"⚡ {what} ranks {format_ranks(ranks or s.all_ranks())}")
 
     def dist_recover(self, line: str = "") -> None:
         s = self.session

@@ -276,7 +276,8 @@ class Session:
         ranks = self.all_ranks() if ranks is None else list(ranks)
         flags = (P.F_NS_DELTA if ns_delta and 0 in ranks else 0) | (0 if echo else P.F_NO_ECHO)
         t0 = time.perf_counter()
-        req = comm.submit(ranks, "execute", code, flags=flags, live=render)
+        payload: Any = code if len(ranks) == self.num_processes else {"code": code, "ranks": list(ranks)}
+        req = comm.submit(ranks, "execute", payload, flags=flags, live=render)
         rec = self.timeline.start(req.seq, kind, ranks, code)
         renderer = _Renderer(self.write, show_header=show_header) if render else None
         interrupted = False
@@ -393,9 +394,22 @@ class Session:
         comm = self._require()
         return comm.send_to_ranks([rank], "get_namespace_info", "", timeout=timeout)[rank]
 
-    def interrupt(self, ranks: Optional[List[int]] = None, hard: bool = False) -> None:
+    def interrupt(self, ranks: Optional[List[int]] = None, hard: bool = False, kill: bool = False) -> None:
+        """Interrupt running cells.  Default: out-of-band message (SIGINT raised natively in the
+        worker).  ``hard``: SIGINT straight to the processes.  ``kill``: SIGKILL the ranks (last
+        resort for a rank blocked inside a non-abortable collective); the session becomes
+        degraded and ``%dist_init`` replaces it."""
         comm = self._require()
-        if hard and self.pm is not None:
+        if kill and self.pm is not None:
+            import signal as _signal
+
+            for w in self.pm.workers:
+                if (ranks is None or w.rank in ranks) and w.running:
+                    try:
+                        os.killpg(w.pid, _signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
+        elif hard and self.pm is not None:
             self.pm.interrupt(ranks)
         else:
             comm.interrupt(ranks)

@@ -41,6 +41,7 @@ from typing import Any, Dict, Optional
 from . import protocol as P
 from .config import get_config
 from .executor import CellExecutor
+from .guard import CollectiveGuard
 from .namespace import NamespaceTracker, namespace_info
 from .transport import DEALER, EV_DISCONNECTED, EV_HEARTBEAT_TIMEOUT, OPT_SIGNAL_PREFIX, OPT_STREAM_FLUSH_US, Socket, TransportError
 
@@ -95,6 +96,7 @@ class DistributedWorker:
         self._profiler = None
         self._pending_gpu: list = []
         self.tracker = NamespaceTracker()
+        self.guard = CollectiveGuard()
         self.executor = CellExecutor(tag=f"cell-r{rank}")
         self.ns = self.executor.ns
         self.sock: Optional[Socket] = None
@@ -155,6 +157,8 @@ class DistributedWorker:
                           eager=self.cfg.eager_comm_init)
         import nbdistributed_amd as nbd
 
+        if os.environ.get("NBD_COLLECTIVE_GUARD", "1") != "0":
+            self.guard.install()
         self.ns.update({
             "torch": torch, "dist": dist, "rank": self.rank, "world_size": self.world_size,
             "__rank__": self.rank, "__world_size__": self.world_size,
@@ -227,12 +231,19 @@ class DistributedWorker:
             while time.monotonic() < deadline and self.in_cell and self.cell_seq == seq:
                 time.sleep(0.05)
             if self.in_cell and self.cell_seq == seq and not self.pg_aborted:
-                from .parallel.backend import abort_process_group
+                if self.backend in ("rccl", "nccl"):
+                    from .parallel.backend import abort_process_group
 
-                print(f"[nbd] rank {self.rank}: cell still running {self.cfg.interrupt_abort_s:.0f}s after "
-                      "interrupt — aborting the communicator (use %dist_recover to rebuild it)",
-                      file=sys.stderr, flush=True)
-                self.pg_aborted = abort_process_group()
+                    print(f"[nbd] rank {self.rank}: cell still running {self.cfg.interrupt_abort_s:.0f}s after "
+                          "interrupt — aborting the RCCL communicator (use %dist_recover to rebuild it)",
+                          file=sys.stderr, flush=True)
+                    self.pg_aborted = abort_process_group()
+                else:
+                    # gloo has no thread-safe abort: calling it from here deadlocks with the blocked op
+                    print(f"[nbd] rank {self.rank}: still blocked {self.cfg.interrupt_abort_s:.0f}s after interrupt "
+                          f"(probably inside a {self.backend} collective some rank never joined). "
+                          "Use %dist_interrupt --kill to stop this rank, then %dist_init to rebuild the cluster.",
+                          file=sys.stderr, flush=True)
 
     # ------------------------------------------------------------------ handlers
     def format_value(self, value: Any) -> str:
@@ -275,7 +286,13 @@ class DistributedWorker:
         self._pending_gpu = keep[-64:]
         return done
 
-    def handle_execute(self, seq: int, code: str, flags: int) -> Dict[str, Any]:
+    def handle_execute(self, seq: int, data: Any, flags: int) -> Dict[str, Any]:
+        if isinstance(data, dict):  # subset cell: {"code": ..., "ranks": [...]}
+            code = data["code"]
+            self.guard.enter(data.get("ranks"), self.world_size)
+        else:
+            code = data
+            self.guard.exit()
         self._set_stream_seq(seq)
         gpu_prev = self._collect_gpu_times()
         ev0 = self._gpu_events()
@@ -285,6 +302,7 @@ class DistributedWorker:
             res = self.executor.run(code, echo=not (flags & P.F_NO_ECHO))
         finally:
             self.in_cell = False
+            self.guard.exit()
         out = ""
         if res.has_value:
             try:

@@ -82,3 +82,11 @@ def test_tensor_echo_uses_device_summary(gpu_session):
     r = gpu_session.execute("big = torch.ones(1 << 20, device=device, dtype=torch.bfloat16) * 2\nbig", render=False)
     out = r.results[0]["output"]
     assert "mean=2" in out and "std=0" in out and "cuda:0" in out
+
+
+def test_accelerate_on_rccl_backend(gpu_session):
+    from test_accelerate import ACCEL
+
+    r = gpu_session.execute(ACCEL, render=False)
+    assert r.ok, r.errors
+    assert r.results[0]["echo"].endswith("'cuda:0')"), r.results[0]

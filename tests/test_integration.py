@@ -291,3 +291,37 @@ def test_scale_world_sizes(n):
         assert init_s < 120
     finally:
         s.shutdown()
+
+
+def test_subset_collective_fails_fast_instead_of_hanging(nb):
+    # reference: %%rank [0] + dist.all_reduce blocks forever
+    sh, core, cap = nb
+    t = time.time()
+    r = sh.run_cell("%%rank [0]\nx = torch.ones(4)\ndist.all_reduce(x)")
+    assert time.time() - t < 5
+    err = r.error_in_exec.result.errors[0]
+    assert err["ename"] == "SubsetCollectiveError" and "ranks [1] are not executing" in err["error"]
+    r = sh.run_cell("%%rank [0]\nimport torch.distributed as D\nD.send(torch.ones(1), dst=1)")
+    assert r.error_in_exec.result.errors[0]["ename"] == "SubsetCollectiveError"
+    # subgroups of the executing ranks are fine; full-world cells are unaffected
+    sh.run_cell("g01 = dist.new_group([0, 1])")
+    assert sh.run_cell("%%rank [0-1]\ny = torch.ones(2)\ndist.all_reduce(y, group=g01)\nint(y[0])").success
+    assert sh.run_cell("z = torch.ones(2)\ndist.all_reduce(z)\nint(z[0])").success
+    assert cap.take().count("  2\n") == 4
+
+
+def test_interrupt_kill_then_reinit():
+    sh = HeadlessShell()
+    core = sh.load_extension()
+    cap = Capture()
+    core.write = core.session.write = cap
+    sh.run_cell("%dist_init -n 2 --backend gloo", raise_errors=True)
+    sh.run_cell("%dist_interrupt --kill [1]")
+    assert "Killed ranks 1" in cap.take()
+    time.sleep(0.5)
+    r = sh.run_cell("rank")
+    assert 1 in r.error_in_exec.result.dead
+    sh.run_cell("%dist_init -n 2 --backend gloo")
+    assert "Replacing a degraded session" in cap.take()
+    assert sh.run_cell("rank").success
+    sh.run_cell("%dist_shutdown")
