@@ -46,6 +46,6 @@ def __getattr__(name):
         return importlib.import_module(".process_manager", __name__).ProcessManager
     if name in ("CommunicationManager", "Message"):
         return getattr(importlib.import_module(".communication", __name__), name)
-    if name in ("ops", "parallel", "models", "utils", "transport", "timeline"):
+    if name in ("ops", "parallel", "models", "utils", "transport", "timeline", "checkpoint", "benchmarking", "guard"):
         return importlib.import_module(f".{name}", __name__)
     raise AttributeError(name)

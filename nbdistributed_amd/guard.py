@@ -22,7 +22,8 @@ COLLECTIVES = ["all_reduce", "broadcast", "all_gather", "all_gather_into_tensor"
                "reduce_scatter_tensor", "all_to_all", "all_to_all_single", "barrier", "reduce", "gather", "scatter",
                "broadcast_object_list", "all_gather_object", "gather_object", "scatter_object_list",
                "monitored_barrier", "all_reduce_coalesced", "all_gather_coalesced"]
-P2P = {"send": "dst", "recv": "src", "isend": "dst", "irecv": "src"}
+# isend/irecv are not wrapped: dist.P2POp checks them by identity (batch_isend_irecv)
+P2P = {"send": "dst", "recv": "src"}
 
 
 class SubsetCollectiveError(RuntimeError):

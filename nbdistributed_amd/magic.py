@@ -489,6 +489,52 @@ class MagicCore:
             else:
                 self.p(f"Rank {r}: profiling")
 
+    def dist_checkpoint(self, line: str = "") -> None:
+        p = _parser("%dist_checkpoint")
+        p.add_argument("action", choices=["save", "load"])
+        p.add_argument("path")
+        p.add_argument("names", nargs="*")
+        p.add_argument("--replicated", action="store_true", help="state is identical on all ranks: store once")
+        args = p.parse_args(shlex.split(line))
+        s = self.session
+        if not s.active:
+            self.p("No distributed workers running. Use %dist_init first.")
+            return
+        if args.action == "save" and not args.names:
+            self.p("Usage: %dist_checkpoint save PATH name [name ...]")
+            return
+        import os
+
+        path = os.path.abspath(args.path)
+        t0 = time.perf_counter()
+        extra = ", replicated=True" if (args.replicated and args.action == "save") else ""
+        res = s.execute(f"nbd.checkpoint.{args.action}(globals(), {args.names!r}, {path!r}{extra})", render=False,
+                        raise_on_error=False, echo=False, kind=f"checkpoint_{args.action}")
+        if not res.ok:
+            raise DistributedExecutionError(res)
+        verb = "Saved" if args.action == "save" else "Loaded"
+        what = ", ".join(args.names) if args.names else "all names in the checkpoint"
+        self.p(f"✓ {verb} {what} on {len(res.ranks)} ranks ({path}, {time.perf_counter() - t0:.2f}s)")
+
+    def dist_topology(self, line: str = "") -> None:
+        """xGMI / PCIe link table between the GPUs of this node (KFD topology)."""
+        from .utils.devices import kfd_gpus, xgmi_matrix
+
+        gpus = kfd_gpus()
+        if not gpus:
+            self.p("No GPUs in the KFD topology of this host")
+            return
+        m = xgmi_matrix(gpus)
+        self.p(f"{len(gpus)} GPU(s): " + ", ".join(f"{i}:{g.gfx_arch}" for i, g in enumerate(gpus)))
+        n = len(gpus)
+        grid = [["." if i == j else "-" for j in range(n)] for i in range(n)]
+        for l in m["links"]:
+            grid[l["src"]][l["dst"]] = "X" if l["type"] == "xgmi" else "P"
+        self.p("     " + " ".join(f"{j:>2}" for j in range(n)))
+        for i in range(n):
+            self.p(f"  {i:>2} " + " ".join(f"{c:>2}" for c in grid[i]))
+        self.p("  X = xGMI link, P = PCIe, . = self")
+
     def teardown(self) -> None:
         if self.session.active:
             self.session.shutdown(graceful=True)
@@ -500,7 +546,7 @@ class MagicCore:
 
 LINE_MAGICS = ["dist_init", "sync", "dist_status", "dist_mode", "dist_shutdown", "dist_reset", "dist_debug",
                "dist_sync_ide", "timeline_save", "timeline_debug", "timeline_clear", "dist_interrupt",
-               "dist_recover", "dist_pull", "dist_push", "dist_profile"]
+               "dist_recover", "dist_pull", "dist_push", "dist_profile", "dist_checkpoint", "dist_topology"]
 CELL_MAGICS = ["distributed", "rank"]
 
 

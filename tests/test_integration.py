@@ -325,3 +325,37 @@ def test_interrupt_kill_then_reinit():
     assert "Replacing a degraded session" in cap.take()
     assert sh.run_cell("rank").success
     sh.run_cell("%dist_shutdown")
+
+
+def test_checkpoint_save_and_load_roundtrip(nb, tmp_path):
+    sh, core, cap = nb
+    sh.run_cell("torch.manual_seed(7 + rank)\nnet = torch.nn.Linear(8, 4)\nopt = torch.optim.SGD(net.parameters(), lr=0.1)\n"
+                "step = 41 + rank\nbuf = torch.arange(5.) * (rank + 1)\nw0 = net.weight.detach().clone()")
+    sh.run_cell(f"%dist_checkpoint save {tmp_path}/ck net opt step buf")
+    assert "Saved net, opt, step, buf on 2 ranks" in cap.take()
+    sh.run_cell("with torch.no_grad():\n    net.weight.zero_()\nstep = 0\nbuf.zero_()")
+    sh.run_cell(f"%dist_checkpoint load {tmp_path}/ck net opt step buf")
+    assert "Loaded" in cap.take()
+    res = core.session.execute("(bool(torch.equal(net.weight, w0)), step, buf.tolist())", render=False)
+    assert res.results[0]["output"] == "(True, 41, [0.0, 1.0, 2.0, 3.0, 4.0])"
+    assert res.results[1]["output"] == "(True, 42, [0.0, 2.0, 4.0, 6.0, 8.0])"
+
+
+def test_collective_primitives_from_cells(nb):
+    # everything a user-written TP/SP/EP/PP cell needs works from cells
+    sh, core, cap = nb
+    code = (
+        "out = []\n"
+        "t = torch.tensor([float(rank)])\n"
+        "g = [torch.zeros(1) for _ in range(world_size)]\ndist.all_gather(g, t)\nout.append([x.item() for x in g])\n"
+        "b = torch.tensor([rank * 10.])\ndist.broadcast(b, src=1)\nout.append(b.item())\n"
+        "r = torch.tensor([1.])\ndist.reduce(r, dst=0)\nout.append(r.item() if rank == 0 else None)\n"
+        "if rank == 0:\n    dist.send(torch.tensor([5.]), dst=1)\nelse:\n    q = torch.zeros(1); dist.recv(q, src=0); out.append(q.item())\n"
+        "ops = [dist.P2POp(dist.isend, torch.tensor([float(rank)]), (rank + 1) % 2), dist.P2POp(dist.irecv, rr := torch.zeros(1), (rank + 1) % 2)]\n"
+        "[w.wait() for w in dist.batch_isend_irecv(ops)]\nout.append(rr.item())\n"
+        "objs = [None, None]\ndist.all_gather_object(objs, {'r': rank})\nout.append(objs)\n"
+        "out"
+    )
+    res = core.session.execute(code, render=False)
+    assert res.results[0]["output"] == "[[0.0, 1.0], 10.0, 2.0, 1.0, [{'r': 0}, {'r': 1}]]"
+    assert res.results[1]["output"] == "[[0.0, 1.0], 10.0, None, 5.0, 0.0, [{'r': 0}, {'r': 1}]]"
