@@ -359,3 +359,11 @@ def test_collective_primitives_from_cells(nb):
     res = core.session.execute(code, render=False)
     assert res.results[0]["output"] == "[[0.0, 1.0], 10.0, 2.0, 1.0, [{'r': 0}, {'r': 1}]]"
     assert res.results[1]["output"] == "[[0.0, 1.0], 10.0, None, 5.0, 0.0, [{'r': 0}, {'r': 1}]]"
+
+
+def test_dist_recover_rebuilds_process_group(nb):
+    sh, core, cap = nb
+    sh.run_cell("%dist_recover")
+    assert "Process group rebuilt on 2 ranks" in cap.take()
+    r = sh.run_cell("x = torch.ones(3)\ndist.all_reduce(x)\nint(x.sum())")
+    assert r.success and cap.take().count("  6\n") == 2
