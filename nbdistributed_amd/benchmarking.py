@@ -26,20 +26,33 @@ METRIC = "all_reduce bus GB/s + %%distributed cell p50 round-trip (ms) at 1/2/4/
 
 AR_SETUP = """
 import time as _t
+def _nbd_sync():
+    if device.type == 'cuda':
+        torch.cuda.synchronize()
+
+def _nbd_barrier():
+    _nbd_sync()
+    dist.barrier(device_ids=[device.index]) if device.type == 'cuda' else dist.barrier()
+    _nbd_sync()
+
 def _nbd_ar_time(numel, dtype, iters, warm):
     x = torch.zeros(numel, dtype=dtype, device=device)
     for _ in range(warm):
         dist.all_reduce(x)
-    torch.cuda.synchronize()
-    dist.barrier(device_ids=[device.index]) if device.type == 'cuda' else dist.barrier()
-    torch.cuda.synchronize()
-    s = torch.cuda.Event(enable_timing=True); e = torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        dist.all_reduce(x)
-    e.record()
-    torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / iters
+    _nbd_barrier()
+    if device.type == 'cuda':
+        s = torch.cuda.Event(enable_timing=True); e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            dist.all_reduce(x)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / iters
+    else:
+        t = _t.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(x)
+        ms = (_t.perf_counter() - t) / iters * 1e3
     del x
     return ms
 
@@ -60,51 +73,53 @@ from torch.nn.parallel import DistributedDataParallel as _TorchDDP
 def _nbd_time_steps(step, steps, warm):
     for _ in range(warm):
         step()
-    torch.cuda.synchronize()
-    dist.barrier(device_ids=[device.index])
-    torch.cuda.synchronize()
+    _nbd_barrier()
     t = _t.perf_counter()
     for _ in range(steps):
         out = step()
-    torch.cuda.synchronize()
+    _nbd_sync()
     return (_t.perf_counter() - t) / steps * 1e3, float(out)
 
-def _nbd_gpt2_bench(steps, warm, B, T, impl):
-    torch.manual_seed(0)
-    m = GPT2(GPT2Config.small()).to(device)
+def _nbd_wrap(m, impl, **kw):
     if impl == "nbd":
-        model = _NbdDDP(m, comm_dtype=torch.bfloat16)
-    else:
-        model = _TorchDDP(m, device_ids=[device.index], bucket_cap_mb=25)
-    opt = torch.optim.AdamW(m.parameters(), lr=3e-4, fused=True)
+        return _NbdDDP(m, **kw)
+    return _TorchDDP(m, device_ids=[device.index] if device.type == "cuda" else None, bucket_cap_mb=25)
+
+def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small"):
+    torch.manual_seed(0)
+    m = GPT2(getattr(GPT2Config, config)()).to(device)
+    model = _nbd_wrap(m, impl, comm_dtype=torch.bfloat16)
+    opt = torch.optim.AdamW(m.parameters(), lr=3e-4, fused=device.type == "cuda")
     x = torch.randint(0, m.config.vocab_size, (B, T), device=device)
     def step():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast(device.type, dtype=torch.bfloat16):
             _, loss = model(x, x)
         loss.backward()
         opt.step()
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=True)
         return loss.detach()
     ms, loss = _nbd_time_steps(step, steps, warm)
     del model, opt, m, x
-    torch.cuda.empty_cache()
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
     return ms, loss
 
-def _nbd_linear_bench(steps, warm, rows, impl):
+def _nbd_linear_bench(steps, warm, rows, impl, dim=4096):
     torch.manual_seed(0)
-    m = linear_4096().to(device)
-    model = _NbdDDP(m) if impl == "nbd" else _TorchDDP(m, device_ids=[device.index])
+    m = torch.nn.Linear(dim, dim).to(device)
+    model = _nbd_wrap(m, impl)
     opt = torch.optim.SGD(m.parameters(), lr=1e-3)
-    x = torch.randn(rows, 4096, device=device)
+    x = torch.randn(rows, dim, device=device)
     def step():
         loss = model(x).square().mean()
         loss.backward()
         opt.step()
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=True)
         return loss.detach()
     ms, loss = _nbd_time_steps(step, steps, warm)
     del model, opt, m, x
-    torch.cuda.empty_cache()
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
     return ms, loss
 """
 
@@ -118,28 +133,30 @@ def _max_over_ranks(res) -> float:
 
 
 def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 1024, compare_torch: bool = True,
-              linear_rows: int = 8192) -> Dict[str, Any]:
+              linear_rows: int = 8192, config: str = "small", linear_dim: int = 4096) -> Dict[str, Any]:
     """BASELINE configs 4 and 5 as notebook cells: DDP steps timed inside each worker (max over
     ranks).  GPT-2 small: fp32 master weights, bf16 autocast, bf16 gradient wire format through
     the fused HIP bucket kernels; synthetic tokens."""
     n = session.world_size
+    session.execute(AR_SETUP, render=False)
     session.execute(DDP_SETUP, render=False)
-    out: Dict[str, Any] = {"model": "gpt2-small (124,439,808 params)", "per_gpu_batch": B, "seq_len": T,
+    out: Dict[str, Any] = {"model": f"gpt2-{config}", "per_gpu_batch": B, "seq_len": T,
                            "global_batch": B * n, "steps": steps, "warmup": warmup}
-    r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'nbd')", render=False)
+    r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'nbd', {config!r})", render=False)
     ms = _max_over_ranks(r)
     toks = n * B * T / (ms / 1e3)
-    out.update(ms_per_step=ms, tokens_per_s=toks, tokens_per_s_per_gpu=toks / n,
-               mfu=6 * 124_439_808 * toks / (2.5e15 * n))
+    out.update(ms_per_step=ms, tokens_per_s=toks, tokens_per_s_per_gpu=toks / n)
+    if config == "small":  # 6·N·tokens FLOPs over the 2.5 PFLOP/s dense bf16 peak per GPU
+        out["mfu"] = 6 * 124_439_808 * toks / (2.5e15 * n)
     if compare_torch:
-        r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'torch')", render=False)
+        r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'torch', {config!r})", render=False)
         tms = _max_over_ranks(r)
         out.update(torch_ddp_ms_per_step=tms, torch_ddp_tokens_per_s=n * B * T / (tms / 1e3),
                    speedup_vs_torch_ddp=tms / ms)
-    r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'nbd')", render=False)
-    lin = {"rows": linear_rows, "ms_per_step": _max_over_ranks(r)}
+    r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'nbd', {linear_dim})", render=False)
+    lin = {"rows": linear_rows, "dim": linear_dim, "ms_per_step": _max_over_ranks(r)}
     if compare_torch:
-        r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'torch')", render=False)
+        r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'torch', {linear_dim})", render=False)
         lin["torch_ddp_ms_per_step"] = _max_over_ranks(r)
     out["linear4096"] = lin
     return out

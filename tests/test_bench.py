@@ -1,0 +1,58 @@
+"""The benchmark harness itself, multi-rank on CPU/gloo: the same cells the driver's 2/4/8-GPU
+runs execute (all-reduce timing, DDP phases) and bench.py's JSON contract."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from nbdistributed_amd import benchmarking as B
+from nbdistributed_amd.session import Session
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def sess():
+    s = Session(writer=lambda t: None)
+    s.start(2, backend="gloo")
+    yield s
+    s.shutdown()
+
+
+def test_allreduce_phase_multi_rank(sess):
+    r = B.bench_allreduce(sess, nbytes=1 << 16, iters=3, warm=1)
+    assert r["correct"] and r["busbw_GBps"] is not None and r["busbw_GBps"] > 0
+    assert set(r["per_rank_ms"]) == {0, 1}
+
+
+def test_ddp_phase_multi_rank(sess):
+    r = B.bench_ddp(sess, steps=2, warmup=1, B=2, T=32, config="tiny", linear_rows=16, linear_dim=64)
+    assert r["ms_per_step"] > 0 and r["tokens_per_s"] > 0 and r["global_batch"] == 4
+    assert r["torch_ddp_ms_per_step"] > 0 and r["linear4096"]["ms_per_step"] > 0
+
+
+def test_cells_phase_and_result_line(sess):
+    cells = B.bench_cells(sess, steps=10, warmup=2)
+    line = B.result_line({"cell": cells}, 2, 10, 2)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in line
+    assert line["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert line["higher_is_better"] is False and line["n_gpus"] == 2
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_bench_py_contract_cpu(n):
+    if n == 1:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "20", "--warmup", "2"]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", "29655", os.path.join(ROOT, "bench.py"),
+               "--gpus", str(n), "--steps", "20", "--warmup", "2"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd="/tmp")
+    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
+    assert res.returncode == 0 and len(lines) == 1, res.stdout[-2000:] + res.stderr[-3000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["steps"] == 20 and d["value"] > 0 and d["config"]["parallelism"] == f"dp{n}"

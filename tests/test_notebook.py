@@ -1,0 +1,35 @@
+"""Execute examples/00_accelerate_mi355x.ipynb headlessly (CPU/gloo, tiny config): the reference
+notebook's workflow end to end through the magics."""
+import json
+import os
+
+import pytest
+
+from nbdistributed_amd.utils.fakeshell import HeadlessShell
+
+NB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "00_accelerate_mi355x.ipynb")
+
+
+def test_example_notebook_runs_end_to_end(monkeypatch):
+    pytest.importorskip("transformers")
+    pytest.importorskip("accelerate")
+    monkeypatch.setenv("NBD_NOTEBOOK_TINY", "1")
+    cells = [c for c in json.load(open(NB))["cells"] if c["cell_type"] == "code"]
+    sh = HeadlessShell()
+    core = sh.load_extension()
+    out = []
+    core.write = core.session.write = out.append
+    try:
+        for c in cells:
+            src = "".join(c["source"])
+            if src.startswith("%load_ext"):
+                continue
+            if src.startswith("%dist_init"):
+                src += " --backend gloo"
+            r = sh.run_cell(src)
+            assert r.success, (src, r.error_in_exec, "".join(out)[-3000:])
+        text = "".join(out)
+        assert "accuracy" in text and "epoch time" in text and "Distributed cluster status" in text
+    finally:
+        if core.session.active:
+            core.session.shutdown()
