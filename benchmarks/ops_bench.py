@@ -38,6 +38,19 @@ def timeit(fn, iters=20, warm=5):
     return statistics.median(ts)
 
 
+def host_us(fn, n=50):
+    """CPU wall time of one call (launch + argument marshalling), no device sync inside."""
+    import time
+
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(n):
+        fn()
+    dt = (time.perf_counter() - t) / n * 1e6
+    torch.cuda.synchronize()
+    return dt
+
+
 def gpt2_like_shapes(total_params: int = 124_439_808):
     # GPT-2 small parameter tensors (wte, wpe, 12 x block, ln_f); used as the bucket contents
     d, v, ctx = 768, 50257, 1024
@@ -70,7 +83,21 @@ def main():
     t_torch = timeit(torch_flat)
     res["flatten_fp32_to_bf16"] = {"numel": numel, "hip_ms": t_hip, "torch_ms": t_torch,
                                    "hip_GBps": byts / t_hip / 1e6, "torch_GBps": byts / t_torch / 1e6,
-                                   "speedup": t_torch / t_hip}
+                                   "speedup": t_torch / t_hip,
+                                   "host_us": host_us(lambda: ops.bucket_flatten(grads, bucket, offs, scale=0.125))}
+
+    # same bytes as ONE tensor: isolates the per-block chunk->tensor lookup and tensor-tail cost
+    one = torch.randn(numel, device=dev)
+    t_one = timeit(lambda: ops.bucket_flatten([one], bucket, [0], scale=0.125))
+    res["flatten_single_tensor"] = {"hip_ms": t_one, "hip_GBps": byts / t_one / 1e6}
+    # 148 tensors that are views into that one allocation: same lookup work, contiguous memory
+    views, pos = [], 0
+    for g in grads:
+        views.append(one[pos:pos + g.numel()])
+        pos += (g.numel() + 63) // 64 * 64 if pos + (g.numel() + 63) // 64 * 64 <= one.numel() else g.numel()
+    t_views = timeit(lambda: ops.bucket_flatten(views, bucket, offs, scale=0.125))
+    res["flatten_views_one_alloc"] = {"hip_ms": t_views, "hip_GBps": byts / t_views / 1e6}
+    del one, views
 
     # K2: unflatten bf16 bucket -> fp32 grads, x 1/8 (DDP average) ; torch: per-tensor copy_
     def torch_unflat():

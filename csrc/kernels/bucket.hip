@@ -11,9 +11,14 @@
 // separate cast / divide / copy-back kernels (torch nn/parallel/distributed.py).
 //
 // Design (MI355X): pure HBM streaming, so the only levers are bytes and launches.
-//  * one launch per <= 64 tensors: the tensor table travels in the kernel arguments (no H2D
-//    metadata copy); work is cut in 16 Ki-element chunks and the chunk->tensor lookup is a
-//    block-uniform binary search over the prefix table (scalar ALU);
+//  * one launch per <= 256 tensors: the tensor table (7 KiB) travels in the kernel arguments —
+//    gfx950/HIP accepts >= 16 KiB of arguments (csrc/kernels/bench/kernarg.hip), so a whole
+//    GPT-2 gradient set is one launch with no H2D metadata copy; work is cut in 8 Ki-element
+//    chunks (measured best block footprint, csrc/kernels/bench/copy_bw.hip: 16-32 KiB per block
+//    5.6-5.7 TB/s vs 64 KiB 5.3) and the chunk->tensor lookup is a block-uniform binary search
+//    over the prefix table (scalar ALU);
+//  * 16-bit destinations written with non-temporal stores (streamed once; measured +3-6 %;
+//    fp32 NT stores were 20 % slower and are not used);
 //  * 16 B per lane per access (8 elements), loads for a whole unrolled group issued before the
 //    converts/stores so each wave keeps several KiB in flight;
 //  * misaligned tensors (storage offsets not multiple of 16 B) fall back to a scalar path inside
@@ -30,36 +35,37 @@
 
 namespace nbd {
 
-constexpr int kMaxT = 64;
-constexpr int64_t kChunk = 16384;
+constexpr int kMaxT = 256;
+constexpr int64_t kChunk = 8192;
 constexpr int kThreads = 256;
 constexpr int kUnroll = 2;
+
+constexpr int kHint = 2048;  // coarse chunk-group -> tensor table (uint8: kMaxT <= 256)
 
 struct CopyTable {
   const void* src[kMaxT];
   void* dst[kMaxT];
   int64_t numel[kMaxT];
   int32_t chunk_prefix[kMaxT + 1];
-  uint64_t aligned_mask;  // bit t: both src[t] and dst[t] are 16 B aligned
+  int32_t group_chunks;    // chunks per hint group
+  uint8_t hint[kHint];     // tensor owning the first chunk of each group
+  uint64_t aligned_mask[kMaxT / 64];  // bit t: both src[t] and dst[t] are 16 B aligned
 };
 
 template <typename S, typename D, bool ACC>
 __global__ __launch_bounds__(kThreads) void multi_copy_kernel(CopyTable tab, int nt, float scale) {
   const int chunk = blockIdx.x;
-  // block-uniform binary search: largest t with chunk_prefix[t] <= chunk
-  int lo = 0, hi = nt - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (tab.chunk_prefix[mid] <= chunk) lo = mid;
-    else hi = mid - 1;
-  }
-  const int t = lo;
+  // chunk -> tensor: coarse hint, then a short forward scan (block-uniform, scalar loads).
+  // A binary search over the prefix table (8 dependent scalar loads per block) cost 18 % of
+  // the kernel on the GPT-2 gradient set (4.5 vs 5.5 TB/s single tensor, ops_bench.py).
+  int t = tab.hint[chunk / tab.group_chunks];
+  while (t + 1 < nt && tab.chunk_prefix[t + 1] <= chunk) ++t;
   const int64_t begin = (int64_t)(chunk - tab.chunk_prefix[t]) * kChunk;
   const int64_t end = min(begin + kChunk, tab.numel[t]);
   const S* __restrict__ src = static_cast<const S*>(tab.src[t]);
   D* __restrict__ dst = static_cast<D*>(tab.dst[t]);
 
-  if ((tab.aligned_mask >> t) & 1ull) {
+  if ((tab.aligned_mask[t >> 6] >> (t & 63)) & 1ull) {
     const int64_t stride = (int64_t)kThreads * 8;
     int64_t i = begin + (int64_t)threadIdx.x * 8;
     for (; i + (kUnroll - 1) * stride + 8 <= end; i += kUnroll * stride) {
@@ -81,7 +87,12 @@ __global__ __launch_bounds__(kThreads) void multi_copy_kernel(CopyTable tab, int
           for (int j = 0; j < 8; ++j) v[u][j] *= scale;
       }
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) store8<D>(dst + i + u * stride, v[u]);
+      for (int u = 0; u < kUnroll; ++u) {
+        // non-temporal only for 16-bit destinations: +3-6 % there, but fp32 NT stores measured
+        // 20 % slower (unflatten 3.4 vs 4.2 TB/s); accumulate is read-modify-write: keep cached
+        if (!ACC && sizeof(D) == 2) store8_nt<D>(dst + i + u * stride, v[u]);
+        else store8<D>(dst + i + u * stride, v[u]);
+      }
     }
     for (; i + 8 <= end; i += stride) {
       float v[8];
@@ -129,7 +140,6 @@ static void launch_copy(const std::vector<CopyItem>& items, float scale, bool ac
     CopyTable tab{};
     int nt = 0;
     int32_t chunks = 0;
-    tab.aligned_mask = 0;
     for (; pos < items.size() && nt < kMaxT; ++pos) {
       const CopyItem& it = items[pos];
       if (it.numel == 0) continue;
@@ -137,7 +147,8 @@ static void launch_copy(const std::vector<CopyItem>& items, float scale, bool ac
       tab.dst[nt] = it.dst;
       tab.numel[nt] = it.numel;
       tab.chunk_prefix[nt] = chunks;
-      if (((uintptr_t)it.src % 16 == 0) && ((uintptr_t)it.dst % 16 == 0)) tab.aligned_mask |= (1ull << nt);
+      if (((uintptr_t)it.src % 16 == 0) && ((uintptr_t)it.dst % 16 == 0))
+        tab.aligned_mask[nt >> 6] |= (1ull << (nt & 63));
       const int64_t c = (it.numel + kChunk - 1) / kChunk;
       TORCH_CHECK(chunks + c < (int64_t)INT32_MAX, "nbd bucket: too many chunks in one launch");
       chunks += (int32_t)c;
@@ -145,6 +156,13 @@ static void launch_copy(const std::vector<CopyItem>& items, float scale, bool ac
     }
     if (nt == 0) continue;
     tab.chunk_prefix[nt] = chunks;
+    tab.group_chunks = (chunks + kHint - 1) / kHint;
+    if (tab.group_chunks < 1) tab.group_chunks = 1;
+    for (int g = 0, t = 0; g < kHint; ++g) {
+      const int32_t first = g * tab.group_chunks;
+      while (t + 1 < nt && tab.chunk_prefix[t + 1] <= first) ++t;
+      tab.hint[g] = (uint8_t)t;
+    }
     if (acc)
       hipLaunchKernelGGL((multi_copy_kernel<S, D, true>), dim3(chunks), dim3(kThreads), 0, stream, tab, nt, scale);
     else
@@ -246,7 +264,8 @@ __global__ __launch_bounds__(kThreads) void prereduce_kernel(ReduceArgs a, int k
           for (int e = 0; e < 8; ++e) acc[e] += x[j][e];
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] *= scale;
-      store8<D>(out + v * 8, acc);
+      if (sizeof(D) == 2) store8_nt<D>(out + v * 8, acc);
+      else store8<D>(out + v * 8, acc);
     }
     for (int64_t i = nv * 8 + tid; i < n; i += nthreads) {
       float s = 0.f;
