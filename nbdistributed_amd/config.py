@@ -26,6 +26,7 @@ def _env(name: str, default, cast=str):
 class Config:
     # worker launch
     worker_python: str = field(default_factory=lambda: _env("NBD_WORKER_PYTHON", sys.executable))
+    zygote: bool = field(default_factory=lambda: _env("NBD_ZYGOTE", True, bool))
     startup_timeout_s: float = field(default_factory=lambda: _env("NBD_STARTUP_TIMEOUT", 600.0, float))
     # transport
     transport: str = field(default_factory=lambda: _env("NBD_TRANSPORT", "ipc"))  # ipc | tcp

@@ -105,6 +105,15 @@ class MagicCore:
         self.proxies = ProxyTable()
         self.auto_mode = False
         self.ide_sync = self.session.cfg.ide_sync
+        if self.session.cfg.zygote:
+            # pre-warm the worker fork server while the user reads the notebook: %dist_init then
+            # forks workers that already have torch imported
+            try:
+                from .zygote import get_zygote
+
+                get_zygote(self.session.cfg.worker_python)
+            except Exception:
+                pass
 
     # ------------------------------------------------------------------ helpers
     def p(self, *args) -> None:

@@ -82,6 +82,7 @@ class ProcessManager:
         self.exit_callback = exit_callback
         self._threads: List[threading.Thread] = []
         self._shutting_down = False
+        self.zygote_used = False
 
     # reference attribute name
     @property
@@ -130,6 +131,17 @@ class ProcessManager:
         if token:
             env_base["NBD_TOKEN"] = token
         exe = python or cfg.worker_python
+        zyg = None
+        if cfg.zygote:
+            from .zygote import get_zygote
+
+            try:
+                zyg = get_zygote(exe)
+                if not zyg.wait_ready(cfg.startup_timeout_s):
+                    zyg = None
+            except Exception:
+                zyg = None
+        self.zygote_used = zyg is not None
         for rank in range(num_processes):
             gid = plan[rank]
             didx = local_device_index(gpus, rank) if gid is not None else None
@@ -140,8 +152,15 @@ class ProcessManager:
                 cmd += ["--gpu-id", str(gid), "--device-index", str(didx)]
             if worker_args:
                 cmd += worker_args
-            proc = subprocess.Popen(cmd, env=env_base, stdin=subprocess.DEVNULL, stdout=subprocess.PIPE,
-                                    stderr=subprocess.PIPE, start_new_session=True, cwd=os.getcwd())
+            proc = None
+            if zyg is not None:
+                try:
+                    proc = zyg.spawn(cmd[3:], env_base, os.getcwd())  # argv after "-m nbdistributed_amd.worker"
+                except Exception:
+                    proc = None
+            if proc is None:
+                proc = subprocess.Popen(cmd, env=env_base, stdin=subprocess.DEVNULL, stdout=subprocess.PIPE,
+                                        stderr=subprocess.PIPE, start_new_session=True, cwd=os.getcwd())
             w = WorkerProc(rank=rank, proc=proc, gpu_id=gid, device_index=didx)
             self.workers.append(w)
             self.gpu_assignments[rank] = gid

@@ -43,6 +43,8 @@ from .config import get_config
 from .executor import CellExecutor
 from .guard import CollectiveGuard
 from .namespace import NamespaceTracker, namespace_info
+_PROCESS_T0 = time.time()  # module import time ~ interpreter start of a spawned worker
+
 from .transport import DEALER, EV_DISCONNECTED, EV_HEARTBEAT_TIMEOUT, OPT_SIGNAL_PREFIX, OPT_STREAM_FLUSH_US, Socket, TransportError
 
 
@@ -141,11 +143,15 @@ class DistributedWorker:
             os.environ["MASTER_PORT"] = str(self.master_port)
         if "torch" not in sys.modules:
             os.environ.setdefault("TORCH_CPP_LOG_LEVEL", "ERROR")  # c10d hostname warnings, gloo chatter
+        phases: Dict[str, float] = {}
+        tp = time.perf_counter()
         import torch
         import torch.distributed as dist
 
         from .parallel import backend as B
 
+        phases["import_torch_s"] = time.perf_counter() - tp
+        tp = time.perf_counter()
         cuda = torch.cuda.is_available()
         self.backend = B.resolve_backend(self.backend_req if self.backend_req != "auto" else self.cfg.backend, cuda)
         if self.backend == "gloo" and not cuda:
@@ -153,8 +159,11 @@ class DistributedWorker:
         else:
             idx = self.device_index if self.device_index is not None else self.local_rank
             self.device = B.bind_device(idx)
+        phases["bind_device_s"] = time.perf_counter() - tp
+        tp = time.perf_counter()
         B.init_data_plane(self.backend, self.rank, self.world_size, self.device,
                           eager=self.cfg.eager_comm_init)
+        phases["init_process_group_s"] = time.perf_counter() - tp
         import nbdistributed_amd as nbd
 
         if os.environ.get("NBD_COLLECTIVE_GUARD", "1") != "0":
@@ -167,6 +176,8 @@ class DistributedWorker:
         })
         status = self.status()
         status["init_s"] = time.time() - t0
+        status["init_phases"] = phases
+        status["process_start_to_ready_s"] = time.time() - _PROCESS_T0
         return status
 
     # ------------------------------------------------------------------ status
