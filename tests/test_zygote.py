@@ -10,14 +10,16 @@ from nbdistributed_amd.zygote import get_zygote
 def test_zygote_spawn_exit_code_and_pipes():
     z = get_zygote(sys.executable)
     assert z.wait_ready(120)
-    code = "import sys; print('out-line'); print('err-line', file=sys.stderr); sys.exit(5)"
-    # argv for worker.main is irrelevant here: run a tiny program through the same fork path
+    # a worker whose bootstrap fails (no rendezvous port) exits with code 3: the code must travel
+    # back through the zygote
     p = z.spawn(["--rank", "0", "--world-size", "1", "--coord", "ipc:///nonexistent/x.sock", "--backend", "gloo"],
-                dict(os.environ, NBD_STARTUP_TIMEOUT="1"), "/tmp")
+                dict(os.environ), "/tmp")
     assert p.pid > 0
-    # no coordinator at that endpoint: the worker keeps retrying; kill it and see the code
-    time.sleep(0.5)
-    assert p.poll() is None
+    assert p.wait(30) == 3
+    # a live worker killed from outside reports the signal
+    p = z.spawn(["--rank", "0", "--world-size", "2", "--master-addr", "127.0.0.1", "--master-port", "1",
+                 "--coord", "ipc:///nonexistent/y.sock", "--backend", "gloo"], dict(os.environ), "/tmp")
+    time.sleep(0.3)
     os.killpg(p.pid, 9)
     assert p.wait(10) == -9
 
