@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import codecs
 import itertools
+import logging
 import os
 import queue
 import secrets
@@ -43,6 +44,8 @@ from .transport import (EV_AUTH_FAILED, EV_CONNECTED, EV_DISCONNECTED, EV_HANDSH
 OutputCallback = Callable[[int, str, str], None]
 
 MAX_CAPTURED_OUTPUT = 1 << 20  # per rank per request, kept for programmatic callers
+
+log = logging.getLogger("nbdistributed_amd.comm")
 
 
 class RankDied(RuntimeError):
@@ -236,6 +239,7 @@ class CommunicationManager:
         self._forget(req)
         if not ok:
             missing = [r for r in req.ranks if r not in req.responses and r not in req.dead]
+            log.warning("%s seq %d timed out after %ss; no reply from %s", req.msg_type, req.seq, t, missing)
             raise RequestTimeout(f"{req.msg_type}: no reply from ranks {missing} within {t}s", req.results())
         return req
 
@@ -267,6 +271,7 @@ class CommunicationManager:
         for req in reqs:
             req.on_dead(rank, reason)
         self.event_log.append((time.time(), "dead", rank, reason))
+        log.warning("rank %d marked dead: %s (%d request(s) resolved)", rank, reason, len(reqs))
 
     def wait_ready(self, ranks: List[int], timeout: Optional[float], alive: Optional[Callable[[], Dict[int, int]]] = None) -> Dict[int, Dict[str, Any]]:
         """Block until every rank has sent READY.  Raises RuntimeError with the worker's own

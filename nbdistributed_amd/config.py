@@ -53,5 +53,21 @@ class Config:
         return {f.name: getattr(self, f.name) for f in fields(self)}
 
 
+_logging_configured = False
+
+
 def get_config() -> Config:
-    return Config()
+    global _logging_configured
+    cfg = Config()
+    if not _logging_configured:
+        import logging
+
+        logger = logging.getLogger("nbdistributed_amd")
+        logger.setLevel(getattr(logging, cfg.log_level.upper(), logging.WARNING))
+        if not logger.handlers:
+            h = logging.StreamHandler()
+            h.setFormatter(logging.Formatter("[nbd %(levelname)s %(name)s] %(message)s"))
+            logger.addHandler(h)
+            logger.propagate = False
+        _logging_configured = True
+    return cfg

@@ -307,7 +307,17 @@ class MagicCore:
             self.p()
         lc = s.last_cell
         if lc is not None:
-            self.p(f"Last cell: {lc.duration_s * 1e3:.2f} ms round trip on ranks {format_ranks(lc.ranks)}")
+            per = []
+            for r in sorted(lc.results):
+                d = lc.results[r]
+                if isinstance(d, dict) and "exec_s" in d:
+                    per.append(f"r{r} {d['exec_s'] * 1e3:.2f} ms")
+            self.p(f"Last cell: {lc.duration_s * 1e3:.2f} ms round trip on ranks {format_ranks(lc.ranks)}"
+                   + (f" (exec: {', '.join(per)})" if per else ""))
+        if s.ready.get(0, {}).get("init_phases"):
+            ph = s.ready[0]["init_phases"]
+            self.p("Bring-up (rank 0): " + ", ".join(f"{k.replace('_s', '')} {v:.2f}s" for k, v in ph.items())
+                   + (" [forked from the zygote]" if s.pm is not None and s.pm.zygote_used else ""))
 
     def dist_mode(self, line: str = "") -> None:
         p = _parser("%dist_mode")

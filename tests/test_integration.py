@@ -4,6 +4,7 @@ import os
 import time
 
 import pytest
+import torch  # noqa: F401  (loaded in this "kernel": proxies become meta tensors)
 
 from nbdistributed_amd.session import DistributedExecutionError, Session
 from nbdistributed_amd.utils.fakeshell import HeadlessShell
