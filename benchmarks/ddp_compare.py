@@ -18,6 +18,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from nbdistributed_amd.models import GPT2, GPT2Config  # noqa: E402
+from nbdistributed_amd.optim import FlatAdamW  # noqa: E402
 from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP  # noqa: E402
 from nbdistributed_amd.parallel.backend import init_data_plane  # noqa: E402
 
@@ -29,7 +30,8 @@ def main():
     ap.add_argument("--warm", type=int, default=3)
     ap.add_argument("--B", type=int, default=8)
     ap.add_argument("--T", type=int, default=1024)
-    ap.add_argument("--impls", default="none,torch,nbd,nbd32")
+    ap.add_argument("--impls", default="none,torch,nbd,nbd32,flat")
+    ap.add_argument("--clip", type=float, default=0.0, help="clip_grad_norm_ max norm (0: off)")
     ap.add_argument("--backend", default="rccl")
     a = ap.parse_args()
     os.environ.setdefault("RANK", "0")
@@ -49,6 +51,14 @@ def main():
 
     for impl in a.impls.split(","):
         m = copy.deepcopy(base)
+        amp = True
+        if impl == "flat":
+            # bf16 parameters re-homed into the DDP buckets, fp32 master/moments inside FlatAdamW,
+            # one fused HIP AdamW kernel per bucket; no autocast casts in the forward
+            m = m.to(torch.bfloat16)
+            w = NbdDDP(m, flat_params=True, grad_mode="bucket")
+            models[impl] = (w, FlatAdamW(w, lr=3e-4), False)
+            continue
         if impl == "torch":
             w = torch.nn.parallel.DistributedDataParallel(m, device_ids=[local])
         elif impl == "nbd":
@@ -58,29 +68,38 @@ def main():
         else:
             w = m
         opt = torch.optim.AdamW(m.parameters(), lr=3e-4, fused=True)
-        models[impl] = (w, opt)
+        models[impl] = (w, opt, amp)
 
-    def step(w, opt):
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+    def step(w, opt, amp):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             _, loss = w(x, x)
         loss.backward()
+        if a.clip > 0:
+            if isinstance(opt, FlatAdamW):
+                opt.clip_grad_norm_(a.clip)
+            else:
+                torch.nn.utils.clip_grad_norm_(w.parameters(), a.clip)
         opt.step()
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=True)
+        return loss
 
     res = {k: [] for k in models}
+    losses = {}
     for r in range(a.rounds):
-        for k, (w, opt) in models.items():
+        for k, (w, opt, amp) in models.items():
             for _ in range(a.warm):
-                step(w, opt)
+                step(w, opt, amp)
             torch.cuda.synchronize()
             t = time.perf_counter()
             for _ in range(a.steps):
-                step(w, opt)
+                loss = step(w, opt, amp)
             torch.cuda.synchronize()
             res[k].append((time.perf_counter() - t) / a.steps * 1e3)
+            losses[k] = float(loss.detach())
     if rank == 0:
         for k, v in res.items():
-            print(f"{k:8s} ms/step " + " ".join(f"{x:.2f}" for x in v) + f"   tok/s {world * a.B * a.T / (min(v) / 1e3):.0f}")
+            print(f"{k:8s} ms/step " + " ".join(f"{x:.2f}" for x in v) +
+                  f"   tok/s {world * a.B * a.T / (min(v) / 1e3):.0f}   loss {losses[k]:.4f}")
     dist.destroy_process_group()
 
 

@@ -68,6 +68,7 @@ DDP_SETUP = """
 import time as _t
 from nbdistributed_amd.models import GPT2, GPT2Config, linear_4096
 from nbdistributed_amd.parallel import DistributedDataParallel as _NbdDDP
+from nbdistributed_amd.optim import FlatAdamW as _FlatAdamW
 from torch.nn.parallel import DistributedDataParallel as _TorchDDP
 
 def _nbd_time_steps(step, steps, warm):
@@ -88,11 +89,17 @@ def _nbd_wrap(m, impl, **kw):
 def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small"):
     torch.manual_seed(0)
     m = GPT2(getattr(GPT2Config, config)()).to(device)
-    model = _nbd_wrap(m, impl, comm_dtype=torch.bfloat16)
-    opt = torch.optim.AdamW(m.parameters(), lr=3e-4, fused=device.type == "cuda")
+    amp = impl != "flat"
+    if impl == "flat":   # bf16 params in the DDP buckets + fp32 master/moments in FlatAdamW
+        m = m.to(torch.bfloat16)
+        model = _NbdDDP(m, flat_params=True, grad_mode="bucket")
+        opt = _FlatAdamW(model, lr=3e-4)
+    else:
+        model = _nbd_wrap(m, impl, comm_dtype=torch.bfloat16)
+        opt = torch.optim.AdamW(m.parameters(), lr=3e-4, fused=device.type == "cuda")
     x = torch.randint(0, m.config.vocab_size, (B, T), device=device)
     def step():
-        with torch.autocast(device.type, dtype=torch.bfloat16):
+        with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
             _, loss = model(x, x)
         loss.backward()
         opt.step()

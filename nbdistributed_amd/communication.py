@@ -180,6 +180,7 @@ class CommunicationManager:
         self.event_log: List[tuple] = []
         self.running = True
         self._closing = False
+        self.stopping = False  # set by Session.shutdown: worker exits are expected from here on
         self.thread = threading.Thread(target=self._message_handler, name="nbd-comm", daemon=True)
         self.thread.start()
 
@@ -271,7 +272,7 @@ class CommunicationManager:
         for req in reqs:
             req.on_dead(rank, reason)
         self.event_log.append((time.time(), "dead", rank, reason))
-        log.warning("rank %d marked dead: %s (%d request(s) resolved)", rank, reason, len(reqs))
+        (log.debug if self.stopping else log.warning)("rank %d marked dead: %s (%d request(s) resolved)", rank, reason, len(reqs))
 
     def wait_ready(self, ranks: List[int], timeout: Optional[float], alive: Optional[Callable[[], Dict[int, int]]] = None) -> Dict[int, Dict[str, Any]]:
         """Block until every rank has sent READY.  Raises RuntimeError with the worker's own

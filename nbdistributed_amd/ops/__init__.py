@@ -7,6 +7,8 @@ bucket_flatten (K1)    N grads -> 1 bucket + cast (fp32->bf16) + scale  bucket.h
 bucket_unflatten (K2)  bucket -> N grads + scale (1/world) + cast (+=)  bucket.hip multi_copy
 local_prereduce (K3)   sum of k buffers, fp32 accumulate, scale, cast   bucket.hip prereduce
 tensor_summary (K4)    count/sum/mean/std/norm/min/max/absmax/nan/inf   summary.hip (MFMA Σx, Σx²)
+adamw_flat (K5)        AdamW step over a DDP bucket: fp32 master/m/v,   optim.hip
+                       param cast, optional device clip coefficient
 =====================  ==============================================  =========================
 
 GPU tensors always go to the HIP kernels; if ``libnbd_ops.so`` cannot be loaded on a GPU box the
@@ -181,6 +183,40 @@ def local_prereduce(inputs: Sequence, out=None, scale: float = 1.0, dtype=None):
     return out
 
 
+def _ref_adamw(grad, param, master, m, v, lr, beta1, beta2, eps, wd, step, grad_scale, grad_scale_t=None):
+    import math
+
+    n = param.numel()
+    g = grad.reshape(-1)[:n].float() * grad_scale
+    if grad_scale_t is not None:
+        g = g * grad_scale_t.float().reshape(())
+    master.mul_(1 - lr * wd)
+    m.mul_(beta1).add_(g, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+    master.addcdiv_(m, denom, value=-lr / bc1)
+    param.view(-1).copy_(master.to(param.dtype))
+
+
+def adamw_flat(grad, param, master, exp_avg, exp_avg_sq, lr: float, beta1: float, beta2: float, eps: float,
+               weight_decay: float, step: int, grad_scale: float = 1.0, grad_scale_t=None) -> None:
+    """One fused AdamW step over flat buffers (see csrc/kernels/optim.hip): fp32 master weights
+    and moments, ``param`` (any float dtype) rewritten from the master copy.  The gradient is
+    multiplied by ``grad_scale`` and, if given, by the 1-element device tensor ``grad_scale_t``
+    (a clip coefficient computed on the GPU — no host sync)."""
+    import torch
+
+    if param.is_cuda:
+        _require()
+        torch.ops.nbd.adamw_flat(grad, param, master, exp_avg, exp_avg_sq, float(lr), float(beta1), float(beta2),
+                                 float(eps), float(weight_decay), int(step), float(grad_scale), grad_scale_t)
+    else:
+        _ref_adamw(grad, param, master, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step, grad_scale,
+                   grad_scale_t)
+
+
 SUMMARY_FIELDS = ("count", "sum", "mean", "std", "norm", "min", "max", "absmax", "nan", "inf", "finite", "shift")
 
 
@@ -220,5 +256,5 @@ def tensor_summary_text(x) -> str:
     return f"[{shape} {str(x.dtype).replace('torch.', '')} {x.device}] " + " ".join(parts)
 
 
-__all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "tensor_summary", "tensor_summary_text",
+__all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "tensor_summary", "tensor_summary_text",
            "tensor_summary_raw", "plan_offsets", "native_available", "load_library", "SUMMARY_FIELDS"]

@@ -49,12 +49,19 @@ class _Bucket:
     launched: bool = False
     work: Any = None
     grads: List[torch.Tensor] = field(default_factory=list)
+    param_flat: Optional[torch.Tensor] = None  # flat_params: the parameters live here (views)
 
 
 class DistributedDataParallel(torch.nn.Module):
     def __init__(self, module: torch.nn.Module, process_group=None, bucket_cap_mb: float = 64.0,
                  first_bucket_mb: float = 4.0, comm_dtype: Optional[torch.dtype] = None,
-                 broadcast_buffers: bool = True, init_sync: bool = True, align: int = 64):
+                 broadcast_buffers: bool = True, init_sync: bool = True, align: int = 64,
+                 flat_params: bool = False, grad_mode: str = "unflatten"):
+        """``flat_params``: re-home each bucket's parameters into one contiguous buffer (the
+        nn.Parameters become views) so a flat optimizer (``nbdistributed_amd.optim.FlatAdamW``)
+        can update a whole bucket in one pass.  ``grad_mode="bucket"``: leave the averaged
+        gradients in the bucket buffers (no unflatten, ``p.grad`` released after the flatten) —
+        only for optimizers that read the buckets (FlatAdamW)."""
         super().__init__()
         self.module = module
         self.pg = process_group if process_group is not None else dist.group.WORLD
@@ -66,6 +73,10 @@ class DistributedDataParallel(torch.nn.Module):
         self.device = self.params[0].device
         self.cuda = self.device.type == "cuda"
         self.comm_dtype = comm_dtype or self.params[0].dtype
+        if grad_mode not in ("unflatten", "bucket"):
+            raise ValueError("grad_mode must be 'unflatten' or 'bucket'")
+        self.grad_mode = grad_mode
+        self.flat_params = flat_params
         self._require_sync = True
         self._in_backward = False
         self._next_launch = 0
@@ -84,6 +95,8 @@ class DistributedDataParallel(torch.nn.Module):
             b.buffer = torch.zeros(b.numel, dtype=self.comm_dtype, device=self.device)
             for p in b.params:
                 self._bucket_of[id(p)] = b
+        if flat_params:
+            self._rehome_params()
         self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in self.params]
         if init_sync and self.world > 1:
             self._broadcast_tensors([p.data for p in module.parameters()])
@@ -114,6 +127,19 @@ class DistributedDataParallel(torch.nn.Module):
     def _make_bucket(i: int, params: List[torch.nn.Parameter], align: int) -> _Bucket:
         offs, total = ops.plan_offsets([p.numel() for p in params], align)
         return _Bucket(index=i, params=list(params), offsets=offs, numel=total)
+
+    def _rehome_params(self) -> None:
+        for b in self.buckets:
+            dts = {p.dtype for p in b.params}
+            if len(dts) != 1:
+                raise ValueError(f"flat_params needs one dtype per bucket, got {dts}")
+            flat = torch.zeros(b.numel, dtype=dts.pop(), device=self.device)
+            with torch.no_grad():
+                for p, o in zip(b.params, b.offsets):
+                    n = p.numel()
+                    flat[o:o + n].copy_(p.data.reshape(-1))
+                    p.data = flat[o:o + n].view_as(p)
+            b.param_flat = flat
 
     # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
@@ -170,11 +196,13 @@ class DistributedDataParallel(torch.nn.Module):
         grads = self._bucket_grads(b)
         b.grads = grads
         scale = 1.0 / self.world
+        unflatten = self.grad_mode == "unflatten"
         if self.cuda and self.comm_stream is None:
             ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
             b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)
             b.work.wait()
-            ops.bucket_unflatten(b.buffer, grads, b.offsets)
+            if unflatten:
+                ops.bucket_unflatten(b.buffer, grads, b.offsets)
         elif self.cuda:
             cur = torch.cuda.current_stream(self.device)
             self.comm_stream.wait_stream(cur)  # the grads were produced on the compute stream
@@ -182,12 +210,20 @@ class DistributedDataParallel(torch.nn.Module):
                 ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
                 b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)
                 b.work.wait()  # device-side: the comm stream waits for RCCL's stream
-                ops.bucket_unflatten(b.buffer, grads, b.offsets)
+                if unflatten:
+                    ops.bucket_unflatten(b.buffer, grads, b.offsets)
             for g in grads:
                 g.record_stream(self.comm_stream)
         else:
             ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
             b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)
+        if not unflatten:
+            # the averaged gradients live in b.buffer; release the per-parameter grads now
+            # (the caching allocator will not reuse them before the comm stream is done)
+            for p in b.params:
+                p.grad = None
+            if not self.cuda:
+                b.grads = []
         b.launched = True
 
     def _finalize(self) -> None:
@@ -202,7 +238,8 @@ class DistributedDataParallel(torch.nn.Module):
             for b in self.buckets:
                 if b.work is not None:
                     b.work.wait()
-                    ops.bucket_unflatten(b.buffer, b.grads, b.offsets)
+                    if self.grad_mode == "unflatten":
+                        ops.bucket_unflatten(b.buffer, b.grads, b.offsets)
         for b in self.buckets:
             b.grads = []
             b.work = None

@@ -242,6 +242,8 @@ class Session:
         comm, pm = self.comm, self.pm
         self.comm = None
         self.pm = None
+        if comm is not None:
+            comm.stopping = True
         if comm is not None and graceful:
             alive = [r for r in range(self.num_processes) if r not in comm.dead]
             if alive:

@@ -129,3 +129,25 @@ def test_tensor_summary_large_mean_small_spread_f32(dev):
 def test_tensor_summary_2d_noncontiguous(dev):
     x = torch.randn(1024, 2048, device=dev, dtype=torch.bfloat16).t()
     _check_summary(x)
+
+
+@pytest.mark.parametrize("gdt", ["f32", "bf16"])
+@pytest.mark.parametrize("pdt", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("n", [1, 7, 8, 1000, 16389, 1 << 20])
+@pytest.mark.parametrize("clip", [False, True])
+def test_adamw_flat_matches_reference(dev, gdt, pdt, n, clip):
+    g = torch.Generator(device="cpu").manual_seed(n)
+    master = torch.randn(n, generator=g)
+    grads = [torch.randn(n, generator=g).to(DT[gdt]) for _ in range(3)]
+    coef = torch.tensor([0.37]) if clip else None
+    ref = [master.clone(), torch.zeros(n), torch.zeros(n), master.to(DT[pdt])]
+    gpu = [t.clone().to(dev) for t in ref]
+    for step, gr in enumerate(grads, 1):
+        ops._ref_adamw(gr, ref[3], ref[0], ref[1], ref[2], 1e-3, 0.9, 0.95, 1e-8, 0.1, step, 0.5, coef)
+        ops.adamw_flat(gr.to(dev), gpu[3], gpu[0], gpu[1], gpu[2], 1e-3, 0.9, 0.95, 1e-8, 0.1, step, 0.5,
+                       coef.to(dev) if clip else None)
+    torch.cuda.synchronize()
+    for name, a, b in zip(("master", "exp_avg", "exp_avg_sq"), ref[:3], gpu[:3]):
+        assert torch.allclose(b.cpu(), a, atol=1e-6, rtol=1e-5), name
+    # the param copy is the master cast to its dtype (round-to-nearest both ways)
+    assert torch.equal(gpu[3].cpu(), gpu[0].cpu().to(DT[pdt]))

@@ -90,3 +90,35 @@ def test_accelerate_on_rccl_backend(gpu_session):
     r = gpu_session.execute(ACCEL, render=False)
     assert r.ok, r.errors
     assert r.results[0]["echo"].endswith("'cuda:0')"), r.results[0]
+
+
+def test_flat_adamw_bf16_tracks_fp32_training(gpu_session):
+    """GPT-2 tiny: bf16 params + FlatAdamW (fused HIP optimizer reading the DDP buckets) vs fp32
+    params + autocast + torch fused AdamW: the loss curves agree."""
+    code = (
+        "import copy\n"
+        "from nbdistributed_amd.models import GPT2, GPT2Config\n"
+        "from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP\n"
+        "from nbdistributed_amd.optim import FlatAdamW\n"
+        "torch.manual_seed(0)\n"
+        "base = GPT2(GPT2Config.tiny()).to(device)\n"
+        "ref = NbdDDP(copy.deepcopy(base))\n"
+        "oref = torch.optim.AdamW(ref.parameters(), lr=1e-3, fused=True)\n"
+        "flat = NbdDDP(copy.deepcopy(base).to(torch.bfloat16), flat_params=True, grad_mode='bucket')\n"
+        "oflat = FlatAdamW(flat, lr=1e-3)\n"
+        "idx = torch.randint(0, 512, (4, 64), device=device)\n"
+        "lr_, lf_ = [], []\n"
+        "for i in range(30):\n"
+        "    with torch.autocast('cuda', dtype=torch.bfloat16):\n"
+        "        l1 = ref(idx, idx)[1]\n"
+        "    l1.backward(); oref.step(); oref.zero_grad()\n"
+        "    l2 = flat(idx, idx)[1]\n"
+        "    l2.backward(); oflat.clip_grad_norm_(10.0); oflat.step()\n"
+        "    lr_.append(float(l1.detach())); lf_.append(float(l2.detach()))\n"
+        "(lr_[0], lr_[-1], lf_[0], lf_[-1])"
+    )
+    r = gpu_session.execute(code, render=False)
+    r0, r1, f0, f1 = eval(r.results[0]["echo"])
+    assert abs(r0 - f0) < 0.05 * r0, (r0, f0)  # same init, bf16 vs fp32-autocast forward
+    assert r1 < r0 - 0.5, (r0, r1)             # memorising one batch: the loss falls
+    assert abs(r1 - f1) < 0.1 * r1 + 0.1, (r1, f1)
