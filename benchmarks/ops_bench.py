@@ -64,11 +64,34 @@ def gpt2_like_shapes(total_params: int = 124_439_808):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default="", help="comma list of: flatten,unflatten,prereduce,summary,adamw")
     a = ap.parse_args()
+    only = set(filter(None, a.only.split(",")))
+
+    def want(k):
+        return not only or k in only
+
     dev = torch.device("cuda", 0)
     assert ops.native_available(), ops._load_error
     res = {}
 
+    if want("flatten") or want("unflatten"):
+        bench_bucket(res, dev)
+    if want("prereduce"):
+        bench_prereduce(res, dev)
+    if want("summary"):
+        bench_summary(res, dev)
+    if want("adamw"):
+        bench_adamw(res, dev)
+    torch.cuda.synchronize()
+    for k, v in res.items():
+        print(f"{k:28s} " + " ".join(f"{kk}={vv:.4g}" if isinstance(vv, float) else f"{kk}={vv}" for kk, vv in v.items()))
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+def bench_bucket(res, dev):
     # K1: flatten 124M fp32 grads (GPT-2 small) -> bf16 bucket, scale 1/8
     grads = [torch.randn(s, device=dev) for s in gpt2_like_shapes()]
     numel = sum(g.numel() for g in grads)
@@ -110,8 +133,9 @@ def main():
                                      "torch_GBps": byts / t_torch / 1e6, "speedup": t_torch / t_hip}
     t_hip = timeit(lambda: ops.bucket_unflatten(bucket, grads, offs, scale=0.125, accumulate=True))
     res["unflatten_accumulate"] = {"hip_ms": t_hip, "hip_GBps": (numel * 2 + numel * 8) / t_hip / 1e6}
-    del grads, bucket
 
+
+def bench_prereduce(res, dev):
     # K3: pre-reduce 4 bf16 buffers of 128 Mi elements -> bf16
     n = 128 << 20
     xs = [torch.randn(n, device=dev, dtype=torch.bfloat16) for _ in range(4)]
@@ -128,8 +152,9 @@ def main():
     t_torch = timeit(torch_pre)
     res["prereduce_4x_bf16"] = {"numel": n, "hip_ms": t_hip, "torch_ms": t_torch, "hip_GBps": byts / t_hip / 1e6,
                                 "torch_GBps": byts / t_torch / 1e6, "speedup": t_torch / t_hip}
-    del xs, out
 
+
+def bench_summary(res, dev):
     # K4: summary of 1 GiB bf16 and 512 MiB f32 vs torch's separate reductions
     for name, dt, numel in (("summary_bf16_1GiB", torch.bfloat16, 512 << 20), ("summary_f32_512MiB", torch.float32, 128 << 20)):
         x = torch.randn(numel, device=dev, dtype=dt)
@@ -145,12 +170,35 @@ def main():
         res[name] = {"numel": numel, "hip_ms": t_hip, "torch_ms": t_torch, "hip_GBps": byts / t_hip / 1e6,
                      "torch_GBps": byts / t_torch / 1e6, "speedup": t_torch / t_hip}
         del x
-    torch.cuda.synchronize()
-    for k, v in res.items():
-        print(f"{k:28s} " + " ".join(f"{kk}={vv:.4g}" if isinstance(vv, float) else f"{kk}={vv}" for kk, vv in v.items()))
-    if a.json:
-        with open(a.json, "w") as f:
-            json.dump(res, f, indent=1)
+
+
+def bench_adamw(res, dev):
+    # K5: one AdamW step over GPT-2 small.  HIP: one flat bucket (bf16 grad + bf16 param, fp32
+    # master/m/v: 28 B/param).  torch: fused AdamW over the 148 fp32 parameters (fp32 grads;
+    # also 28 B/param) — the mixed-precision recipe the flat path replaces.
+    shapes = gpt2_like_shapes()
+    numels = [int(torch.Size(s).numel()) for s in shapes]
+    offs, total = ops.plan_offsets(numels)
+    grad = torch.randn(total, device=dev, dtype=torch.bfloat16)
+    param = torch.randn(total, device=dev, dtype=torch.bfloat16)
+    master = param.float()
+    m, v = torch.zeros_like(master), torch.zeros_like(master)
+    step = [0]
+
+    def hip_step():
+        step[0] += 1
+        ops.adamw_flat(grad, param, master, m, v, 1e-4, 0.9, 0.999, 1e-8, 0.1, step[0])
+
+    t_hip = timeit(hip_step)
+    byts = total * 28
+    ps = [torch.nn.Parameter(torch.randn(s, device=dev)) for s in shapes]
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    opt = torch.optim.AdamW(ps, lr=1e-4, weight_decay=0.1, fused=True)
+    t_torch = timeit(opt.step)
+    res["adamw_gpt2_small"] = {"numel": total, "hip_ms": t_hip, "torch_fused_ms": t_torch,
+                               "hip_GBps": byts / t_hip / 1e6, "torch_GBps": byts / t_torch / 1e6,
+                               "speedup": t_torch / t_hip}
 
 
 if __name__ == "__main__":
