@@ -72,7 +72,7 @@ def main():
 
     def step(w, opt, amp):
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
-            _, loss = w(x, x)
+            _, loss = w(x, x, return_logits=False)
         loss.backward()
         if a.clip > 0:
             if isinstance(opt, FlatAdamW):

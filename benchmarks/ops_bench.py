@@ -64,7 +64,7 @@ def gpt2_like_shapes(total_params: int = 124_439_808):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
-    ap.add_argument("--only", default="", help="comma list of: flatten,unflatten,prereduce,summary,adamw")
+    ap.add_argument("--only", default="", help="comma list of: flatten,unflatten,prereduce,summary,adamw,xent")
     a = ap.parse_args()
     only = set(filter(None, a.only.split(",")))
 
@@ -83,6 +83,8 @@ def main():
         bench_summary(res, dev)
     if want("adamw"):
         bench_adamw(res, dev)
+    if want("xent"):
+        bench_xent(res, dev)
     torch.cuda.synchronize()
     for k, v in res.items():
         print(f"{k:28s} " + " ".join(f"{kk}={vv:.4g}" if isinstance(vv, float) else f"{kk}={vv}" for kk, vv in v.items()))
@@ -199,6 +201,39 @@ def bench_adamw(res, dev):
     res["adamw_gpt2_small"] = {"numel": total, "hip_ms": t_hip, "torch_fused_ms": t_torch,
                                "hip_GBps": byts / t_hip / 1e6, "torch_GBps": byts / t_torch / 1e6,
                                "speedup": t_torch / t_hip}
+
+
+
+def bench_xent(res, dev):
+    # K6: GPT-2 small LM-head loss, logits [8192, 50257] bf16: forward + backward.
+    # HIP: logsumexp pass + gradient pass (2 reads + 1 write of the logits);  torch: the model's
+    # previous path F.cross_entropy(logits.float()) + backward (fp32 copy, log_softmax, ...).
+    import torch.nn.functional as F
+
+    N, V = 8192, 50257
+    base = (torch.randn(N, V, device=dev) * 2).to(torch.bfloat16)
+    tgt = torch.randint(0, V, (N,), device=dev)
+
+    def hip():
+        x = base.detach().requires_grad_(True)
+        ops.cross_entropy(x, tgt).backward()
+
+    def hip_inplace():
+        x = base.detach().requires_grad_(True)
+        y = x.view(N, V)  # non-leaf alias: the gradient is written over y's storage (copy of base)
+        ops.cross_entropy(y * 1, tgt, inplace_backward=True).backward()
+
+    def eager():
+        x = base.detach().requires_grad_(True)
+        F.cross_entropy(x.float(), tgt).backward()
+
+    t_hip = timeit(hip)
+    t_eager = timeit(eager)
+    fb = timeit(lambda: torch.ops.nbd.xent_fwd(base, tgt, -100))
+    byts = N * V * 2
+    res["xent_gpt2_fwd_bwd"] = {"rows": N, "vocab": V, "hip_ms": t_hip, "torch_ms": t_eager, "speedup": t_eager / t_hip,
+                                "fwd_ms": fb, "fwd_GBps": byts / fb / 1e6,
+                                "bwd_GBps_est": 2 * byts / max(t_hip - fb, 1e-6) / 1e6}
 
 
 if __name__ == "__main__":

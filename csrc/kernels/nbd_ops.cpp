@@ -9,6 +9,8 @@ TORCH_LIBRARY(nbd, m) {
   m.def("bucket_unflatten(Tensor bucket, Tensor(a!)[] tensors, int[] offsets, float scale, bool accumulate) -> ()");
   m.def("local_prereduce(Tensor[] inputs, Tensor(a!) out, float scale) -> ()");
   m.def("tensor_summary(Tensor x) -> Tensor");
+  m.def("xent_fwd(Tensor logits, Tensor target, int ignore_index) -> (Tensor, Tensor)");
+  m.def("xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor scale, int ignore_index, Tensor(a!) dlogits) -> ()");
   m.def("adamw_flat(Tensor grad, Tensor(a!) param, Tensor(b!) master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "
         "float lr, float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, Tensor? grad_scale_t=None) -> ()");
 }

@@ -100,7 +100,7 @@ def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small"):
     x = torch.randint(0, m.config.vocab_size, (B, T), device=device)
     def step():
         with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
-            _, loss = model(x, x)
+            _, loss = model(x, x, return_logits=False)
         loss.backward()
         opt.step()
         opt.zero_grad(set_to_none=True)
@@ -142,19 +142,28 @@ def _max_over_ranks(res) -> float:
 def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 1024, compare_torch: bool = True,
               linear_rows: int = 8192, config: str = "small", linear_dim: int = 4096) -> Dict[str, Any]:
     """BASELINE configs 4 and 5 as notebook cells: DDP steps timed inside each worker (max over
-    ranks).  GPT-2 small: fp32 master weights, bf16 autocast, bf16 gradient wire format through
-    the fused HIP bucket kernels; synthetic tokens."""
+    ranks).  GPT-2 small, synthetic tokens.  Primary number: bf16 parameters living in the DDP
+    buckets, fp32 master weights and moments in ``FlatAdamW`` (fused HIP AdamW per bucket).  Also
+    reported: fp32 params + bf16 autocast + torch fused AdamW through nbd DDP (``amp_*``) and
+    through torch DDP (``torch_ddp_*``)."""
     n = session.world_size
     session.execute(AR_SETUP, render=False)
     session.execute(DDP_SETUP, render=False)
     out: Dict[str, Any] = {"model": f"gpt2-{config}", "per_gpu_batch": B, "seq_len": T,
                            "global_batch": B * n, "steps": steps, "warmup": warmup}
-    r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'nbd', {config!r})", render=False)
+    # primary: bf16 params re-homed into the DDP buckets + FlatAdamW (fp32 master/moments, one
+    # fused HIP kernel per bucket reading the all-reduced bucket); secondary: fp32 params +
+    # autocast + torch fused AdamW through nbd DDP (bf16 wire)
+    r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flat', {config!r})", render=False)
     ms = _max_over_ranks(r)
     toks = n * B * T / (ms / 1e3)
-    out.update(ms_per_step=ms, tokens_per_s=toks, tokens_per_s_per_gpu=toks / n)
+    out.update(recipe="bf16 params + fp32 master weights/moments (FlatAdamW), bf16 grad all_reduce",
+               ms_per_step=ms, tokens_per_s=toks, tokens_per_s_per_gpu=toks / n)
     if config == "small":  # 6·N·tokens FLOPs over the 2.5 PFLOP/s dense bf16 peak per GPU
         out["mfu"] = 6 * 124_439_808 * toks / (2.5e15 * n)
+    r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'nbd', {config!r})", render=False)
+    ams = _max_over_ranks(r)
+    out.update(amp_ms_per_step=ams, amp_tokens_per_s=n * B * T / (ams / 1e3))
     if compare_torch:
         r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'torch', {config!r})", render=False)
         tms = _max_over_ranks(r)
@@ -227,8 +236,65 @@ def bench_sweep(session, dtype: str = "bfloat16", max_bytes: int = 1 << 30, min_
     return out
 
 
+BCAST_BUILD = """
+model = torch.nn.Linear({dim}, {dim}, device=device)   # %%rank[0]: only rank 0 builds (random init)
+"""
+
+BCAST_RECV = """
+model = torch.nn.Linear({dim}, {dim}, device="meta").to_empty(device=device)  # receivers: storage only
+"""
+
+BCAST_CELL = """
+def _nbd_bcast_bench(iters, warm, coalesced):
+    from nbdistributed_amd.parallel import broadcast_params
+    def one():
+        if coalesced:
+            broadcast_params(model, src=0)
+        else:
+            for p in model.parameters():      # the reference README pattern (README.md:115-125)
+                dist.broadcast(p.data, src=0)
+    for _ in range(warm):
+        one()
+    _nbd_barrier()
+    t = _t.perf_counter()
+    for _ in range(iters):
+        one()
+    _nbd_sync()
+    return (_t.perf_counter() - t) / iters * 1e3
+"""
+
+
+def bench_rank_broadcast(session, dim: int = 4096, iters: int = 20, warm: int = 3) -> Dict[str, Any]:
+    """BASELINE config 3: ``%%rank[0]`` builds ``nn.Linear(dim, dim)``, then a ``%%distributed``
+    cell broadcasts its parameters to every rank (per-parameter loop as in the reference README,
+    and the coalesced ``broadcast_params``).  Reports the cell round-trips and in-worker times."""
+    n = session.world_size
+    session.execute(AR_SETUP, render=False)
+    session.execute("import time as _t", render=False)
+    t = time.perf_counter()
+    session.execute(BCAST_BUILD.format(dim=dim), ranks=[0], render=False)
+    build_ms = (time.perf_counter() - t) * 1e3
+    if n > 1:
+        session.execute(BCAST_RECV.format(dim=dim), ranks=list(range(1, n)), render=False)
+    session.execute(BCAST_CELL, render=False)
+    t = time.perf_counter()
+    session.execute("for p in model.parameters():\n    dist.broadcast(p.data, src=0)\n_nbd_sync()", render=False)
+    first_cell_ms = (time.perf_counter() - t) * 1e3
+    chk = session.execute("w = model.weight.detach().float(); t = torch.stack([w.sum(), w.square().sum()])\n"
+                          "ref = t.clone(); dist.broadcast(ref, src=0); bool(torch.equal(t, ref))", render=False)
+    correct = all(chk.results[r].get("output") == "True" for r in chk.ranks)
+    per_param = _max_over_ranks(session.execute(f"_nbd_bcast_bench({iters}, {warm}, False)", render=False))
+    coalesced = _max_over_ranks(session.execute(f"_nbd_bcast_bench({iters}, {warm}, True)", render=False))
+    nbytes = (dim * dim + dim) * 4
+    session.execute("del model", render=False)
+    return {"dim": dim, "bytes": nbytes, "build_cell_ms": build_ms, "broadcast_cell_ms": first_cell_ms,
+            "per_param_ms": per_param, "coalesced_ms": coalesced,
+            "per_param_GBps": nbytes / (per_param * 1e-3) / 1e9, "coalesced_GBps": nbytes / (coalesced * 1e-3) / 1e9,
+            "correct": correct}
+
+
 def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: bool = False,
-            ar_bytes: int = 1 << 30, ddp: bool = True, ddp_steps: int = 20) -> Dict[str, Any]:
+            ar_bytes: int = 1 << 30, ddp: bool = True, ddp_steps: int = 20, bcast: bool = True) -> Dict[str, Any]:
     n = session.world_size
     _log(f"phase 1: {warmup}+{steps} trivial %%distributed cells on {n} rank(s)")
     cells = bench_cells(session, steps, warmup)
@@ -242,6 +308,11 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
     if sweep and gpu:
         _log("phase 3: all_reduce sweep")
         out["sweep"] = bench_sweep(session)
+    if bcast and gpu:
+        _log("phase 3b: %%rank[0] Linear(4096) build + broadcast (config 3)")
+        out["rank_broadcast"] = bench_rank_broadcast(session)
+        _log(f"broadcast per-param {out['rank_broadcast']['per_param_ms']:.3f} ms, coalesced "
+             f"{out['rank_broadcast']['coalesced_ms']:.3f} ms")
     if ddp and gpu:
         _log("phase 4: DDP steps (GPT-2 small bf16 config 5, Linear 4096 config 4)")
         out["ddp"] = bench_ddp(session, steps=ddp_steps)
@@ -281,7 +352,7 @@ def result_line(res: Dict[str, Any], n: int, steps: int, warmup: int) -> Dict[st
         line["allreduce_correct"] = ar["correct"]
     if res.get("sweep"):
         line["allreduce_sweep"] = res["sweep"]
-    for k in ("ddp",):
+    for k in ("ddp", "rank_broadcast"):
         if k in res:
             line[k] = res[k]
     return line

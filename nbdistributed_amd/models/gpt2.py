@@ -3,7 +3,8 @@
 BASELINE.json config 5: "00_accelerate.ipynb-style GPT-2-small DDP loop, bf16, synthetic tokens"
 (124,439,808 parameters with the tied LM head).  Plain PyTorch modules; on
 MI355X the GEMMs go to hipBLASLt and attention to PyTorch's fused SDPA (AOTriton/CK flash
-kernels), the MLP's bias+GELU and the residual LayerNorms run through torch's fused ROCm kernels.
+kernels); the LM-head loss is the fused HIP cross-entropy (``ops.cross_entropy``, no fp32 copy
+of the 8192 x 50257 logits).
 Random init (no checkpoints: no network), GPT-2 initialisation scheme.
 """
 from __future__ import annotations
@@ -27,6 +28,7 @@ class GPT2Config:
     dropout: float = 0.0
     bias: bool = True
     tie_weights: bool = True
+    fused_ce: bool = True  # GPU: nbd.ops.cross_entropy (HIP) instead of F.cross_entropy(logits.float())
 
     @classmethod
     def small(cls):
@@ -110,7 +112,9 @@ class GPT2(nn.Module):
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
-    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None):
+    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None, return_logits: bool = True):
+        """Returns (logits, loss).  With ``targets`` and ``return_logits=False`` the logits are
+        not returned (None) and the fused loss writes its gradient over their storage."""
         B, T = idx.shape
         pos = torch.arange(T, device=idx.device)
         x = self.wte(idx) + self.wpe(pos)
@@ -119,5 +123,11 @@ class GPT2(nn.Module):
         logits = self.lm_head(self.ln_f(x))
         loss = None
         if targets is not None:
-            loss = F.cross_entropy(logits.float().view(-1, logits.size(-1)), targets.view(-1))
-        return logits, loss
+            flat, tgt = logits.view(-1, logits.size(-1)), targets.reshape(-1)
+            if self.config.fused_ce and logits.is_cuda:
+                from .. import ops
+
+                loss = ops.cross_entropy(flat, tgt, inplace_backward=not return_logits)
+            else:
+                loss = F.cross_entropy(flat.float(), tgt)
+        return (logits if return_logits or targets is None else None), loss

@@ -247,22 +247,48 @@ class DistributedDataParallel(torch.nn.Module):
 
     # ------------------------------------------------------------------ broadcast
     def _broadcast_tensors(self, tensors: List[torch.Tensor]) -> None:
-        groups: Dict[torch.dtype, List[torch.Tensor]] = {}
-        for t in tensors:
+        broadcast_tensors(tensors, src=0, group=self.pg)
+
+
+def broadcast_tensors(tensors: List[torch.Tensor], src: int = 0, group=None, coalesce_max_bytes: int = 4 << 20) -> None:
+    """In-place broadcast of ``tensors`` from ``src`` (a rank of ``group``).
+
+    Tensors smaller than ``coalesce_max_bytes`` are latency-bound one by one (one RCCL launch and
+    ring traversal each — the README pattern ``for p in model.parameters(): dist.broadcast(...)``,
+    reference ``README.md:115-125``); they are packed per dtype by one fused HIP kernel
+    (``nbd::bucket_flatten``) into one buffer, sent as ONE broadcast and scattered back by
+    ``nbd::bucket_unflatten``.  Larger contiguous tensors are bandwidth-bound and go out directly
+    in place (no copies)."""
+    pg = group if group is not None else dist.group.WORLD
+    gsrc = src if pg is dist.group.WORLD else dist.get_global_rank(pg, src)
+    groups: Dict[torch.dtype, List[torch.Tensor]] = {}
+    for t in tensors:
+        big = t.numel() * t.element_size() >= coalesce_max_bytes and t.is_contiguous()
+        if big or t.dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            dist.broadcast(t, src=gsrc, group=pg)
+        else:
             groups.setdefault(t.dtype, []).append(t)
-        for dt, ts in groups.items():
-            if dt in (torch.float32, torch.bfloat16, torch.float16):
-                flat = [t if t.is_contiguous() else t.contiguous() for t in ts]
-                buf, offs = ops.bucket_flatten(flat, dtype=dt)
-                dist.broadcast(buf, src=dist.get_global_rank(self.pg, 0) if self.pg is not dist.group.WORLD else 0,
-                               group=self.pg)
-                ops.bucket_unflatten(buf, flat, offs)
-                for t, f in zip(ts, flat):
-                    if t.data_ptr() != f.data_ptr():
-                        t.copy_(f)
-            else:
-                for t in ts:
-                    dist.broadcast(t, src=0, group=self.pg)
+    for dt, ts in groups.items():
+        if len(ts) == 1 and ts[0].is_contiguous():
+            dist.broadcast(ts[0], src=gsrc, group=pg)
+            continue
+        flat = [t if t.is_contiguous() else t.contiguous() for t in ts]
+        buf, offs = ops.bucket_flatten(flat, dtype=dt)
+        dist.broadcast(buf, src=gsrc, group=pg)
+        ops.bucket_unflatten(buf, flat, offs)
+        for t, f in zip(ts, flat):
+            if t.data_ptr() != f.data_ptr():
+                t.copy_(f)
+
+
+def broadcast_params(module: torch.nn.Module, src: int = 0, group=None, buffers: bool = True) -> None:
+    """Make every rank's ``module`` parameters (and buffers) equal to rank ``src``'s — the
+    ``%%rank[0]`` build-then-broadcast pattern in one call."""
+    with torch.no_grad():
+        ts = [p.data for p in module.parameters()]
+        if buffers:
+            ts += list(module.buffers())
+        broadcast_tensors(ts, src=src, group=group)
 
 
 # ---------------------------------------------------------------------- comm hooks for torch DDP

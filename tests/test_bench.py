@@ -30,7 +30,14 @@ def test_allreduce_phase_multi_rank(sess):
 def test_ddp_phase_multi_rank(sess):
     r = B.bench_ddp(sess, steps=2, warmup=1, B=2, T=32, config="tiny", linear_rows=16, linear_dim=64)
     assert r["ms_per_step"] > 0 and r["tokens_per_s"] > 0 and r["global_batch"] == 4
+    assert r["amp_ms_per_step"] > 0 and "FlatAdamW" in r["recipe"]
     assert r["torch_ddp_ms_per_step"] > 0 and r["linear4096"]["ms_per_step"] > 0
+
+
+def test_rank_broadcast_phase_multi_rank(sess):
+    r = B.bench_rank_broadcast(sess, dim=128, iters=3, warm=1)
+    assert r["correct"], r
+    assert r["per_param_ms"] > 0 and r["coalesced_ms"] > 0 and r["bytes"] == (128 * 128 + 128) * 4
 
 
 def test_cells_phase_and_result_line(sess):

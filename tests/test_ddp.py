@@ -116,3 +116,19 @@ ids, mask, labels = synthetic_mrpc(n=8, seq_len=16, vocab=100)
 """
     r = sess.execute(code, render=False)
     assert r.results[0]["output"] == "((2, 32, 512), True, (8, 16), 8)"
+
+
+def test_broadcast_params_coalesced(sess):
+    code = """
+from nbdistributed_amd.parallel import broadcast_params
+torch.manual_seed(rank)
+net = nn.Sequential(nn.Linear(8, 8), nn.BatchNorm1d(8), nn.Linear(8, 3).to(torch.bfloat16))
+net[1].num_batches_tracked += 5 * rank
+broadcast_params(net, src=1)
+sig = torch.cat([t.detach().float().reshape(-1) for t in list(net.parameters()) + list(net.buffers())])
+ref = sig.clone(); dist.broadcast(ref, src=1)
+(bool(torch.equal(sig, ref)), int(net[1].num_batches_tracked))
+"""
+    r = sess.execute(code, render=False)
+    for rank in (0, 1):
+        assert r.results[rank]["output"] == "(True, 5)", r.results[rank]

@@ -151,3 +151,40 @@ def test_adamw_flat_matches_reference(dev, gdt, pdt, n, clip):
         assert torch.allclose(b.cpu(), a, atol=1e-6, rtol=1e-5), name
     # the param copy is the master cast to its dtype (round-to-nearest both ways)
     assert torch.equal(gpu[3].cpu(), gpu[0].cpu().to(DT[pdt]))
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("V", [1, 7, 64, 1000, 50257])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_cross_entropy_matches_reference(dev, dt, V, inplace):
+    import torch.nn.functional as F
+
+    g = torch.Generator(device="cpu").manual_seed(V)
+    N = 67
+    x32 = (torch.randn(N, V, generator=g) * 3).to(DT[dt]).float()
+    tgt = torch.randint(0, V, (N,), generator=g)
+    tgt[::5] = -100  # ignored rows
+    ref_x = x32.clone().requires_grad_(True)
+    ref = F.cross_entropy(ref_x, tgt)
+    (ref * 2.5).backward()
+    x = x32.to(dev, DT[dt]).requires_grad_(True)
+    y = x * 1.0 if inplace else x  # in-place backward needs a non-leaf (it overwrites the storage)
+    loss = ops.cross_entropy(y, tgt.to(dev), inplace_backward=inplace)
+    (loss * 2.5).backward()
+    torch.cuda.synchronize()
+    tol = 1e-5 if dt == "f32" else 2e-2
+    loss, ref = float(loss.detach()), float(ref.detach())
+    assert abs(loss - ref) <= 1e-4 * max(1.0, abs(ref)), (loss, ref)
+    gref = ref_x.grad
+    assert torch.allclose(x.grad.float().cpu(), gref, atol=tol * float(gref.abs().max()) + 1e-7, rtol=tol)
+
+
+def test_cross_entropy_strided_rows_and_sum(dev):
+    import torch.nn.functional as F
+
+    base = torch.randn(33, 1030, device=dev, dtype=torch.bfloat16)
+    x = base[:, 3:1003]  # row stride 1030, misaligned start, unit column stride
+    tgt = torch.randint(0, 1000, (33,), device=dev)
+    got = ops.cross_entropy(x, tgt, reduction="sum")
+    ref = F.cross_entropy(x.float(), tgt, reduction="sum")
+    assert abs(float(got) - float(ref)) < 1e-3 * abs(float(ref))

@@ -258,3 +258,17 @@ def test_reference_ops_cpu():
     s = ops.tensor_summary(torch.tensor([1.0, 2.0, float("nan"), float("inf")]))
     assert s["count"] == 4 and s["nan"] == 1 and s["inf"] == 1 and s["min"] == 1.0 and s["max"] == float("inf")
     assert "mean=" in ops.tensor_summary_text(torch.arange(10.0))
+
+
+def test_gpt2_return_logits_flag_cpu():
+    import torch
+
+    from nbdistributed_amd.models import GPT2, GPT2Config
+
+    torch.manual_seed(0)
+    m = GPT2(GPT2Config.tiny())
+    idx = torch.randint(0, 512, (2, 16))
+    logits, loss = m(idx, idx)
+    none, loss2 = m(idx, idx, return_logits=False)
+    assert logits.shape == (2, 16, 512) and none is None and torch.equal(loss, loss2)
+    assert m(idx)[1] is None
