@@ -64,7 +64,7 @@ def gpt2_like_shapes(total_params: int = 124_439_808):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
-    ap.add_argument("--only", default="", help="comma list of: flatten,unflatten,prereduce,summary,adamw,xent")
+    ap.add_argument("--only", default="", help="comma list of: flatten,unflatten,prereduce,summary,adamw,xent,attn")
     a = ap.parse_args()
     only = set(filter(None, a.only.split(",")))
 
@@ -85,6 +85,8 @@ def main():
         bench_adamw(res, dev)
     if want("xent"):
         bench_xent(res, dev)
+    if want("attn"):
+        bench_attn(res, dev)
     torch.cuda.synchronize()
     for k, v in res.items():
         print(f"{k:28s} " + " ".join(f"{kk}={vv:.4g}" if isinstance(vv, float) else f"{kk}={vv}" for kk, vv in v.items()))
@@ -234,6 +236,30 @@ def bench_xent(res, dev):
     res["xent_gpt2_fwd_bwd"] = {"rows": N, "vocab": V, "hip_ms": t_hip, "torch_ms": t_eager, "speedup": t_eager / t_hip,
                                 "fwd_ms": fb, "fwd_GBps": byts / fb / 1e6,
                                 "bwd_GBps_est": 2 * byts / max(t_hip - fb, 1e-6) / 1e6}
+
+
+def bench_attn(res, dev):
+    # K7: GPT-2 small attention, B=8 H=12 T=1024 D=64 causal, bf16: HIP flash vs torch SDPA
+    import torch.nn.functional as F
+
+    B, H, T, D = 8, 12, 1024, 64
+    q, k, v, do = (torch.randn(B, H, T, D, device=dev, dtype=torch.bfloat16) for _ in range(4))
+    flops_fwd = 4 * B * H * T * T * D / 2  # causal: half the score matrix
+    for name, fn in (("hip", lambda a, b, c: ops.flash_attention(a, b, c, causal=True)),
+                     ("sdpa", lambda a, b, c: F.scaled_dot_product_attention(a, b, c, is_causal=True))):
+        t_f = timeit(lambda: fn(q, k, v))
+        qq, kk, vv = (t.detach().requires_grad_(True) for t in (q, k, v))
+
+        def fb():
+            fn(qq, kk, vv).backward(do)
+
+        t_fb = timeit(fb)
+        res.setdefault("attn_gpt2_causal", {}).update({
+            f"{name}_fwd_ms": t_f, f"{name}_fwd_bwd_ms": t_fb, f"{name}_fwd_TFs": flops_fwd / t_f / 1e9,
+            f"{name}_bwd_TFs": 2.5 * flops_fwd / (t_fb - t_f) / 1e9})
+    r = res["attn_gpt2_causal"]
+    r["speedup_fwd"] = r["sdpa_fwd_ms"] / r["hip_fwd_ms"]
+    r["speedup_fwd_bwd"] = r["sdpa_fwd_bwd_ms"] / r["hip_fwd_bwd_ms"]
 
 
 if __name__ == "__main__":

@@ -1,0 +1,515 @@
+// attn.hip — flash attention (forward + backward) for gfx950, head dim 64, bf16, optional causal.
+//
+// Used by the GPT-2 DDP workload (12 heads x 64, T = 1024): torch's SDPA path on this image ran
+// at 5–7 % of the MFMA roof there (rocprof: attn_fwd 77 µs, bwd_kernel_dk_dv + dq 272 µs per
+// layer, profiles/gpt2_step_rocprof_r1.md).  Everything below is v_mfma_f32_32x32x16_bf16 with
+// the operand maps of cdna_hip_programming.md §3:
+//   A: lane l (r = l&31, h = l>>5) holds A[r][8h + j];  B: lane l holds B[8h + j][r];
+//   C/D (16 f32 per lane): col = l&31, row = (i&3) + 8(i>>2) + 4h  for register i.
+//
+// Forward (one workgroup = 4 waves = 128 queries of one (batch, head); a wave owns 32 queries):
+//   S^T[key][q] = K·Q^T with the query on the lane, so each lane owns one query row's scores
+//   (softmax max / sum = in-lane over 32 registers + one lane^32 exchange) and the S^T
+//   accumulator, packed to bf16, is directly the B operand of O^T[d][q] += V^T[d][key]·P[key][q]
+//   (§3 "accumulator tile as the next MFMA's operand").  Q lives in registers; K tiles in LDS
+//   (144-B rows: conflict-free ds_read_b128 row reads); V tiles in LDS read transposed with
+//   ds_read_b64_tr_b16 (T10).  The next K/V tile is fetched into registers while the current one
+//   is computed (T14 issue-early / write-late), one LDS buffer.
+// Backward (FA2 split, no atomics, deterministic):
+//   pre   δ[q] = Σ_d dO·O
+//   dkdv  one workgroup = 128 keys, wave = 32 keys on the lane; sweeps 64-query tiles:
+//         S = Q·K^T, P = exp2(S·c − lse₂), dV^T += dO^T·P, dP = dO·V^T, dS = P(dP − δ),
+//         dK^T += Q^T·dS — dK/dV stay in 64 accumulator registers; K, V in registers.
+//   dq    one workgroup = 128 queries, wave = 32 queries on the lane; sweeps 64-key tiles:
+//         S^T = K·Q^T, dP^T = V·dO^T, dS^T = P^T(dP^T − δ), dQ^T += K^T·dS^T.
+// Causal: workgroups are launched heaviest-first; fully masked tiles are skipped per wave.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include <cmath>
+#include <tuple>
+
+#include "nbd_common.h"
+
+namespace nbd {
+namespace attn {
+
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef float f16x __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) s4v lds_s4v;
+
+constexpr int D = 64;
+constexpr int NT = 256;     // threads per workgroup (4 waves)
+constexpr int BLK = 128;    // rows owned by a workgroup (queries in fwd/dq, keys in dkdv)
+constexpr int TILE = 64;    // rows per swept tile
+constexpr int RS = 72;      // LDS row stride (elements) of row-read images: 144 B
+constexpr int RSV = 96;     // LDS row stride of transpose-only images: 192 B (tr reads conflict-free)
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+struct View {
+  const uint16_t* p;
+  int64_t sb, sh, st;  // element strides of batch, head, row; d is contiguous
+  __device__ __forceinline__ const uint16_t* row(int b, int h, int t) const { return p + b * sb + h * sh + t * st; }
+};
+struct MView {
+  uint16_t* p;
+  int64_t sb, sh, st;
+  __device__ __forceinline__ uint16_t* row(int b, int h, int t) const { return p + b * sb + h * sh + t * st; }
+};
+
+__device__ __forceinline__ f16x mfma(s8v a, s8v b, f16x c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ s8v ld16(const uint16_t* p) { return *reinterpret_cast<const s8v*>(p); }
+__device__ __forceinline__ void st16(uint16_t* p, s8v v) { *reinterpret_cast<s8v*>(p) = v; }
+__device__ __forceinline__ s4v tr4(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p));
+}
+__device__ __forceinline__ s8v cat(s4v a, s4v b) {
+  s8v r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+__device__ __forceinline__ uint16_t bf(float x) { return f32_to_bf16(x); }
+// registers 8s .. 8s+7 of a C tile -> bf16 B/A fragment of k-step s (k order as §3)
+__device__ __forceinline__ s8v pack_half(const f16x& c, int s) {
+  s8v r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (short)bf(c[8 * s + j]);
+  return r;
+}
+__device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+__device__ __forceinline__ f16x zero16() {
+  f16x z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// store a 32x32 C tile whose rows are d (= db*32 + row) and columns a row index of `out`
+// (lane&31): 4 consecutive d per 8-byte store
+__device__ __forceinline__ void store_dT(uint16_t* rowp, const f16x& c, int db, int h, float mul) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    uint32_t lo = (uint32_t)bf(c[4 * g] * mul) | ((uint32_t)bf(c[4 * g + 1] * mul) << 16);
+    uint32_t hi = (uint32_t)bf(c[4 * g + 2] * mul) | ((uint32_t)bf(c[4 * g + 3] * mul) << 16);
+    const int d = db * 32 + 8 * g + 4 * h;
+    *reinterpret_cast<uint2*>(rowp + d) = make_uint2(lo, hi);
+  }
+}
+
+// cooperative tile staging: 64 rows x 64 d, 512 16-B chunks, 2 per thread
+struct Stage2 {
+  s8v a[2];
+  __device__ __forceinline__ void load(const uint16_t* base, int64_t st, int tid) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * NT;
+      a[i] = ld16(base + (c >> 3) * st + (c & 7) * 8);
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* lds, int stride, int tid) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * NT;
+      st16(lds + (c >> 3) * stride + (c & 7) * 8, a[i]);
+    }
+  }
+};
+
+// ============================================================================ forward
+template <bool CAUSAL>
+__global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MView o, float* __restrict__ lse,
+                                                     int H, int T, int nblk, float sc2) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[TILE * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[TILE * RSV];
+  const int bh = blockIdx.x % (gridDim.x / nblk);
+  const int qb = CAUSAL ? nblk - 1 - blockIdx.x / (gridDim.x / nblk) : blockIdx.x / (gridDim.x / nblk);
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int q0 = qb * BLK + w * 32;  // this wave's first query
+  const int qi = q0 + r;             // this lane's query
+  s8v qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = ld16(q.row(b, hh, qi) + 16 * s + 8 * h);
+  f16x acc_o[2] = {zero16(), zero16()};
+  float m = -INFINITY, l = 0.f;
+  const int ntiles = CAUSAL ? (qb * BLK + BLK) / TILE : T / TILE;
+  Stage2 sk, sv;
+  sk.load(k.row(b, hh, 0), k.st, tid);
+  sv.load(v.row(b, hh, 0), v.st, tid);
+  sk.store(Ks, RS, tid);
+  sv.store(Vs, RSV, tid);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) {  // issue the next tile's loads now, write them after this tile
+      sk.load(k.row(b, hh, (t + 1) * TILE), k.st, tid);
+      sv.load(v.row(b, hh, (t + 1) * TILE), v.st, tid);
+    }
+    const int k0 = t * TILE;
+    if (!CAUSAL || k0 <= q0 + 31) {
+      f16x sacc[2] = {zero16(), zero16()};
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) sacc[kb] = mfma(ld16(Ks + (kb * 32 + r) * RS + 16 * s + 8 * h), qf[s], sacc[kb]);
+      const bool diag = CAUSAL && (k0 + TILE - 1 > q0);
+      float mt = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float x = sacc[kb][i] * sc2;
+          if (diag && k0 + kb * 32 + crow(i, h) > qi) x = -INFINITY;
+          sacc[kb][i] = x;
+          mt = fmaxf(mt, x);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m, mt);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      float rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(sacc[kb][i] - mn);
+          sacc[kb][i] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mn;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc_o[db][i] *= alpha;
+      // O^T[d][q] += V^T[d][key] . P[key][q]
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const s8v pb = pack_half(sacc[kb], s);
+          const int key = kb * 32 + 16 * s + 4 * h + (lane & 15) / 4;
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const uint16_t* base = Vs + key * RSV + db * 32 + (lane & 16) + 4 * (lane & 3);
+            acc_o[db] = mfma(cat(tr4(base), tr4(base + 8 * RSV)), pb, acc_o[db]);
+          }
+        }
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      sk.store(Ks, RS, tid);
+      sv.store(Vs, RSV, tid);
+      __syncthreads();
+    }
+  }
+  const float inv = 1.f / l;
+  uint16_t* orow = o.row(b, hh, qi);
+  store_dT(orow, acc_o[0], 0, h, inv);
+  store_dT(orow, acc_o[1], 1, h, inv);
+  if (h == 0) lse[(int64_t)bh * T + qi] = (m + __log2f(l)) * kLn2;
+}
+
+// ============================================================================ backward: δ
+__global__ __launch_bounds__(NT) void bwd_pre_kernel(View dout, View out, float* __restrict__ delta, int H, int T,
+                                                     int64_t rows) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= rows) return;
+  const int t = (int)(i % T);
+  const int64_t bh = i / T;
+  const int b = (int)(bh / H), hh = (int)(bh % H);
+  const uint16_t* a = dout.row(b, hh, t);
+  const uint16_t* c = out.row(b, hh, t);
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < D; j += 8) {
+    float x[8], y[8];
+    load8<bf16_t>(reinterpret_cast<const bf16_t*>(a + j), x);
+    load8<bf16_t>(reinterpret_cast<const bf16_t*>(c + j), y);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc = fmaf(x[e], y[e], acc);
+  }
+  delta[i] = acc;
+}
+
+// ============================================================================ backward: dK, dV
+template <bool CAUSAL>
+__global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v, View dout,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta, MView dk, MView dv, int H,
+                                                          int T, int nblk, float sc2, float scale) {
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[TILE * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Os[TILE * RS];  // dO tile
+  __shared__ __attribute__((aligned(16))) float Ls[TILE];           // lse * log2(e)
+  __shared__ __attribute__((aligned(16))) float Ds[TILE];           // delta
+  const int per = gridDim.x / nblk;
+  const int bh = blockIdx.x % per;
+  const int kb0 = blockIdx.x / per;  // key block; block 0 has the most query tiles under a causal mask
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int key0 = kb0 * BLK + w * 32;
+  const int ki = key0 + r;  // this lane's key
+  s8v kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = ld16(k.row(b, hh, ki) + 16 * s + 8 * h);
+    vf[s] = ld16(v.row(b, hh, ki) + 16 * s + 8 * h);
+  }
+  f16x dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
+  const int t0 = CAUSAL ? (kb0 * BLK) / TILE : 0;
+  const int nt = T / TILE;
+  const float* lse_bh = lse + (int64_t)bh * T;
+  const float* del_bh = delta + (int64_t)bh * T;
+  Stage2 sq, so;
+  float lv = 0.f, dlv = 0.f;
+  sq.load(q.row(b, hh, t0 * TILE), q.st, tid);
+  so.load(dout.row(b, hh, t0 * TILE), dout.st, tid);
+  if (tid < TILE) {
+    lv = lse_bh[t0 * TILE + tid] * kLog2e;
+    dlv = del_bh[t0 * TILE + tid];
+  }
+  sq.store(Qs, RS, tid);
+  so.store(Os, RS, tid);
+  if (tid < TILE) {
+    Ls[tid] = lv;
+    Ds[tid] = dlv;
+  }
+  __syncthreads();
+  for (int t = t0; t < nt; ++t) {
+    if (t + 1 < nt) {
+      sq.load(q.row(b, hh, (t + 1) * TILE), q.st, tid);
+      so.load(dout.row(b, hh, (t + 1) * TILE), dout.st, tid);
+      if (tid < TILE) {
+        lv = lse_bh[(t + 1) * TILE + tid] * kLog2e;
+        dlv = del_bh[(t + 1) * TILE + tid];
+      }
+    }
+    const int qt0 = t * TILE;
+    if (!CAUSAL || qt0 + TILE - 1 >= key0) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const int qr0 = qt0 + qb * 32;
+        if (CAUSAL && qr0 + 31 < key0) continue;  // this 32-query block sees none of our keys
+        // S[q][key] = Q . K^T (key on the lane)
+        f16x sacc = zero16(), dp = zero16();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sacc = mfma(ld16(Qs + (qb * 32 + r) * RS + 16 * s + 8 * h), kf[s], sacc);
+          dp = mfma(ld16(Os + (qb * 32 + r) * RS + 16 * s + 8 * h), vf[s], dp);
+        }
+        const bool diag = CAUSAL && (qr0 < key0 + 31);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qrow = qb * 32 + crow(i, h);
+          float p = __builtin_amdgcn_exp2f(sacc[i] * sc2 - Ls[qrow]);
+          if (diag && ki > qt0 + qrow) p = 0.f;
+          sacc[i] = p;                      // P
+          dp[i] = p * (dp[i] - Ds[qrow]);   // dS
+        }
+        // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . dS[q][key]
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const s8v pb = pack_half(sacc, s);
+          const s8v sb = pack_half(dp, s);
+          const int qrow = qb * 32 + 16 * s + 4 * h + (lane & 15) / 4;
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const int col = db * 32 + (lane & 16) + 4 * (lane & 3);
+            const uint16_t* ob = Os + qrow * RS + col;
+            const uint16_t* qb_ = Qs + qrow * RS + col;
+            dvt[db] = mfma(cat(tr4(ob), tr4(ob + 8 * RS)), pb, dvt[db]);
+            dkt[db] = mfma(cat(tr4(qb_), tr4(qb_ + 8 * RS)), sb, dkt[db]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (t + 1 < nt) {
+      sq.store(Qs, RS, tid);
+      so.store(Os, RS, tid);
+      if (tid < TILE) {
+        Ls[tid] = lv;
+        Ds[tid] = dlv;
+      }
+      __syncthreads();
+    }
+  }
+  uint16_t* dkr = dk.row(b, hh, ki);
+  uint16_t* dvr = dv.row(b, hh, ki);
+  store_dT(dkr, dkt[0], 0, h, scale);
+  store_dT(dkr, dkt[1], 1, h, scale);
+  store_dT(dvr, dvt[0], 0, h, 1.f);
+  store_dT(dvr, dvt[1], 1, h, 1.f);
+}
+
+// ============================================================================ backward: dQ
+template <bool CAUSAL>
+__global__ __launch_bounds__(NT, 2) void bwd_dq_kernel(View q, View k, View v, View dout,
+                                                        const float* __restrict__ lse, const float* __restrict__ delta,
+                                                        MView dq, int H, int T, int nblk, float sc2, float scale) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[TILE * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[TILE * RS];
+  const int per = gridDim.x / nblk;
+  const int bh = blockIdx.x % per;
+  const int qb = CAUSAL ? nblk - 1 - blockIdx.x / per : blockIdx.x / per;
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int q0 = qb * BLK + w * 32;
+  const int qi = q0 + r;
+  s8v qf[4], of[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = ld16(q.row(b, hh, qi) + 16 * s + 8 * h);
+    of[s] = ld16(dout.row(b, hh, qi) + 16 * s + 8 * h);
+  }
+  const float l2 = lse[(int64_t)bh * T + qi] * kLog2e;
+  const float dl = delta[(int64_t)bh * T + qi];
+  f16x dqt[2] = {zero16(), zero16()};
+  const int ntiles = CAUSAL ? (qb * BLK + BLK) / TILE : T / TILE;
+  Stage2 sk, sv;
+  sk.load(k.row(b, hh, 0), k.st, tid);
+  sv.load(v.row(b, hh, 0), v.st, tid);
+  sk.store(Ks, RS, tid);
+  sv.store(Vs, RS, tid);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) {
+      sk.load(k.row(b, hh, (t + 1) * TILE), k.st, tid);
+      sv.load(v.row(b, hh, (t + 1) * TILE), v.st, tid);
+    }
+    const int k0 = t * TILE;
+    if (!CAUSAL || k0 <= q0 + 31) {
+      const bool diag = CAUSAL && (k0 + TILE - 1 > q0);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        f16x sacc = zero16(), dp = zero16();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sacc = mfma(ld16(Ks + (kb * 32 + r) * RS + 16 * s + 8 * h), qf[s], sacc);
+          dp = mfma(ld16(Vs + (kb * 32 + r) * RS + 16 * s + 8 * h), of[s], dp);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = __builtin_amdgcn_exp2f(sacc[i] * sc2 - l2);
+          if (diag && k0 + kb * 32 + crow(i, h) > qi) p = 0.f;
+          dp[i] = p * (dp[i] - dl);  // dS^T[key][q]
+        }
+        // dQ^T[d][q] += K^T[d][key] . dS^T[key][q]
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const s8v sb = pack_half(dp, s);
+          const int key = kb * 32 + 16 * s + 4 * h + (lane & 15) / 4;
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const uint16_t* base = Ks + key * RS + db * 32 + (lane & 16) + 4 * (lane & 3);
+            dqt[db] = mfma(cat(tr4(base), tr4(base + 8 * RS)), sb, dqt[db]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      sk.store(Ks, RS, tid);
+      sv.store(Vs, RS, tid);
+      __syncthreads();
+    }
+  }
+  uint16_t* dqr = dq.row(b, hh, qi);
+  store_dT(dqr, dqt[0], 0, h, scale);
+  store_dT(dqr, dqt[1], 1, h, scale);
+}
+
+// ============================================================================ host
+static View view_of(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.size(3) == D && t.stride(3) == 1, "attn: ", name,
+              " must be a [B, H, T, 64] GPU view with a contiguous last dim");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "attn: ", name, " must be bfloat16");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0 &&
+                  ((uintptr_t)t.data_ptr() & 15) == 0,
+              "attn: ", name, " strides must be multiples of 8 elements and its base 16-B aligned");
+  return View{static_cast<const uint16_t*>(t.data_ptr()), t.stride(0), t.stride(1), t.stride(2)};
+}
+static MView mview_of(const at::Tensor& t, const char* name) {
+  View v = view_of(t, name);
+  return MView{const_cast<uint16_t*>(v.p), v.sb, v.sh, v.st};
+}
+static void check_shapes(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
+  TORCH_CHECK(q.sizes() == k.sizes() && q.sizes() == v.sizes(), "attn: q, k, v shapes must match (no GQA yet)");
+  TORCH_CHECK(q.size(2) % BLK == 0 && q.size(2) >= BLK, "attn: sequence length must be a positive multiple of 128");
+  TORCH_CHECK(q.size(0) * q.size(1) * (q.size(2) / BLK) < (1LL << 31), "attn: grid too large");
+}
+
+std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                                bool causal, double scale) {
+  check_shapes(q, k, v);
+  const int B = q.size(0), H = q.size(1), T = q.size(2);
+  View qv = view_of(q, "q"), kv = view_of(k, "k"), vv = view_of(v, "v");
+  // output stored [B, T, H, D] (what the projection after attention reads), returned as [B, H, T, D]
+  at::Tensor o = at::empty({B, T, H, D}, q.options()).permute({0, 2, 1, 3});
+  at::Tensor lse = at::empty({B, H, T}, q.options().dtype(at::kFloat));
+  MView ov = mview_of(o, "out");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  const int nblk = T / BLK;
+  const dim3 grid((unsigned)(B * H * nblk));
+  const float sc2 = (float)scale * kLog2e;
+  if (causal)
+    hipLaunchKernelGGL((fwd_kernel<true>), grid, dim3(NT), 0, st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
+                       sc2);
+  else
+    hipLaunchKernelGGL((fwd_kernel<false>), grid, dim3(NT), 0, st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
+                       sc2);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return {o, lse};
+}
+
+void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                  const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
+                  const at::Tensor& dk, const at::Tensor& dv) {
+  check_shapes(q, k, v);
+  TORCH_CHECK(dout.sizes() == q.sizes() && out.sizes() == q.sizes() && dq.sizes() == q.sizes() &&
+                  dk.sizes() == q.sizes() && dv.sizes() == q.sizes(),
+              "attn_bwd: shape mismatch");
+  const int B = q.size(0), H = q.size(1), T = q.size(2);
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == (int64_t)B * H * T,
+              "attn_bwd: lse must be float32 [B, H, T]");
+  View qv = view_of(q, "q"), kv = view_of(k, "k"), vv = view_of(v, "v"), dov = view_of(dout, "dout"),
+       ov = view_of(out, "out");
+  MView dqv = mview_of(dq, "dq"), dkv = mview_of(dk, "dk"), dvv = mview_of(dv, "dv");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  at::Tensor delta = at::empty({B, H, T}, lse.options());
+  const int64_t rows = (int64_t)B * H * T;
+  hipLaunchKernelGGL(bwd_pre_kernel, dim3((unsigned)((rows + NT - 1) / NT)), dim3(NT), 0, st, dov, ov,
+                     delta.data_ptr<float>(), H, T, rows);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  const int nblk = T / BLK;
+  const dim3 grid((unsigned)(B * H * nblk));
+  const float sc2 = (float)scale * kLog2e;
+  if (causal) {
+    hipLaunchKernelGGL((bwd_dkdv_kernel<true>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), dkv, dvv, H, T, nblk, sc2, (float)scale);
+    hipLaunchKernelGGL((bwd_dq_kernel<true>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale);
+  } else {
+    hipLaunchKernelGGL((bwd_dkdv_kernel<false>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), dkv, dvv, H, T, nblk, sc2, (float)scale);
+    hipLaunchKernelGGL((bwd_dq_kernel<false>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale);
+  }
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+}  // namespace attn
+}  // namespace nbd
+
+TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
+  m.impl("attn_fwd", &nbd::attn::attn_fwd_hip);
+  m.impl("attn_bwd", &nbd::attn::attn_bwd_hip);
+}

@@ -3,7 +3,8 @@
 BASELINE.json config 5: "00_accelerate.ipynb-style GPT-2-small DDP loop, bf16, synthetic tokens"
 (124,439,808 parameters with the tied LM head).  Plain PyTorch modules; on
 MI355X the GEMMs go to hipBLASLt and attention to PyTorch's fused SDPA (AOTriton/CK flash
-kernels); the LM-head loss is the fused HIP cross-entropy (``ops.cross_entropy``, no fp32 copy
+kernels) — or, for bf16 with head dim 64, the HIP flash-attention kernels (``ops.attention_qkv``);
+the LM-head loss is the fused HIP cross-entropy (``ops.cross_entropy``, no fp32 copy
 of the 8192 x 50257 logits).
 Random init (no checkpoints: no network), GPT-2 initialisation scheme.
 """
@@ -29,6 +30,7 @@ class GPT2Config:
     bias: bool = True
     tie_weights: bool = True
     fused_ce: bool = True  # GPU: nbd.ops.cross_entropy (HIP) instead of F.cross_entropy(logits.float())
+    fused_attn: bool = True  # GPU bf16: nbd.ops.attention_qkv (HIP flash fwd/bwd) instead of SDPA
 
     @classmethod
     def small(cls):
@@ -44,13 +46,19 @@ class CausalSelfAttention(nn.Module):
         super().__init__()
         assert c.n_embd % c.n_head == 0
         self.n_head = c.n_head
+        self.fused = c.fused_attn
         self.c_attn = nn.Linear(c.n_embd, 3 * c.n_embd, bias=c.bias)
         self.c_proj = nn.Linear(c.n_embd, c.n_embd, bias=c.bias)
         self.dropout = c.dropout
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, T, C = x.shape
-        q, k, v = self.c_attn(x).split(C, dim=2)
+        qkv = self.c_attn(x)
+        if self.fused and qkv.is_cuda and (self.dropout == 0.0 or not self.training):
+            from .. import ops
+
+            return self.c_proj(ops.attention_qkv(qkv, self.n_head, causal=True))
+        q, k, v = qkv.split(C, dim=2)
         hd = C // self.n_head
         q = q.view(B, T, self.n_head, hd).transpose(1, 2)
         k = k.view(B, T, self.n_head, hd).transpose(1, 2)

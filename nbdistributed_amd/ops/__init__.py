@@ -11,6 +11,8 @@ adamw_flat (K5)        AdamW step over a DDP bucket: fp32 master/m/v,   optim.hi
                        param cast, optional device clip coefficient
 cross_entropy (K6)     online-softmax logsumexp fwd + softmax-onehot    xent.hip
                        bwd over [N, V] logits, no fp32 copy
+flash_attention (K7)   QKᵀ→online softmax→PV fwd; FA2 dK/dV + dQ bwd    attn.hip (MFMA 32x32x16,
+                       (bf16, head dim 64, causal or not)               LDS tr-reads)
 =====================  ==============================================  =========================
 
 GPU tensors always go to the HIP kernels; if ``libnbd_ops.so`` cannot be loaded on a GPU box the
@@ -275,6 +277,111 @@ def cross_entropy(logits, target, ignore_index: int = -100, reduction: str = "me
     return _xent_fn().apply(logits, target.contiguous().long(), int(ignore_index), reduction, bool(inplace_backward))
 
 
+_AttnFns = None
+
+
+def _attn_fns():
+    global _AttnFns
+    if _AttnFns is not None:
+        return _AttnFns
+    import torch
+
+    def _ok_view(t):
+        return t.stride(-1) == 1 and all(st % 8 == 0 for st in t.stride()[:-1]) and t.data_ptr() % 16 == 0
+
+    def _fix(t):
+        return t if _ok_view(t) else t.contiguous()
+
+    class _FlashAttention(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, q, k, v, causal, scale):
+            q, k, v = _fix(q), _fix(k), _fix(v)
+            o, lse = torch.ops.nbd.attn_fwd(q, k, v, causal, scale)
+            ctx.save_for_backward(q, k, v, o, lse)
+            ctx.causal, ctx.scale = causal, scale
+            return o
+
+        @staticmethod
+        def backward(ctx, do):
+            q, k, v, o, lse = ctx.saved_tensors
+            B, H, T, D = q.shape
+            dqkv = torch.empty(B, T, 3, H, D, dtype=q.dtype, device=q.device)
+            dq, dk, dv = (dqkv[:, :, i].transpose(1, 2) for i in range(3))
+            torch.ops.nbd.attn_bwd(_fix(do), q, k, v, o, lse, ctx.causal, ctx.scale, dq, dk, dv)
+            return dq, dk, dv, None, None
+
+    class _FlashAttentionQKV(torch.autograd.Function):
+        """[B, T, 3·H·D] packed projection in, [B, T, H·D] out; the backward writes the packed
+        [B, T, 3·H·D] gradient directly (no split/cat, no transposes)."""
+
+        @staticmethod
+        def forward(ctx, qkv, n_head, causal, scale):
+            B, T, C3 = qkv.shape
+            C = C3 // 3
+            D = C // n_head
+            q, k, v = (qkv[:, :, i * C:(i + 1) * C].view(B, T, n_head, D).transpose(1, 2) for i in range(3))
+            o, lse = torch.ops.nbd.attn_fwd(q, k, v, causal, scale)
+            ctx.save_for_backward(qkv, o, lse)
+            ctx.n_head, ctx.causal, ctx.scale = n_head, causal, scale
+            return o.transpose(1, 2).reshape(B, T, C)  # o is stored [B, T, H, D]: a view
+
+        @staticmethod
+        def backward(ctx, dy):
+            qkv, o, lse = ctx.saved_tensors
+            B, T, C3 = qkv.shape
+            C, H = C3 // 3, ctx.n_head
+            D = C // H
+            q, k, v = (qkv[:, :, i * C:(i + 1) * C].view(B, T, H, D).transpose(1, 2) for i in range(3))
+            dy = dy if dy.is_contiguous() else dy.contiguous()
+            dqkv = torch.empty_like(qkv, memory_format=torch.contiguous_format)
+            dq, dk, dv = (dqkv[:, :, i * C:(i + 1) * C].view(B, T, H, D).transpose(1, 2) for i in range(3))
+            do = dy.view(B, T, H, D).transpose(1, 2)
+            torch.ops.nbd.attn_bwd(do, q, k, v, o, lse, ctx.causal, ctx.scale, dq, dk, dv)
+            return dqkv, None, None, None
+
+    _AttnFns = (_FlashAttention, _FlashAttentionQKV)
+    return _AttnFns
+
+
+def flash_supported(q) -> bool:
+    """The HIP kernels cover bf16, head dim 64, T a multiple of 128 (GPT-2's shapes)."""
+    import torch
+
+    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] == 64 and q.shape[-2] % 128 == 0
+            and q.shape[-2] >= 128)
+
+
+def flash_attention(q, k, v, causal: bool = False, scale: Optional[float] = None):
+    """softmax(q·kᵀ·scale [+ causal mask])·v for [B, H, T, D] tensors — the HIP flash kernels
+    (``csrc/kernels/attn.hip``) where :func:`flash_supported`, else PyTorch SDPA."""
+    import torch.nn.functional as F
+
+    sc = float(scale) if scale is not None else q.shape[-1] ** -0.5
+    if flash_supported(q) and q.shape == k.shape == v.shape and k.dtype == v.dtype == q.dtype:
+        _require()
+        return _attn_fns()[0].apply(q, k, v, bool(causal), sc)
+    return F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=sc)
+
+
+def attention_qkv(qkv, n_head: int, causal: bool = True, scale: Optional[float] = None):
+    """Multi-head attention straight from a packed [B, T, 3·C] projection (GPT-2 ``c_attn``
+    output) to [B, T, C]."""
+    import torch
+    import torch.nn.functional as F
+
+    B, T, C3 = qkv.shape
+    C = C3 // 3
+    D = C // n_head
+    sc = float(scale) if scale is not None else D ** -0.5
+    if (qkv.is_cuda and qkv.dtype == torch.bfloat16 and D == 64 and T % 128 == 0 and qkv.stride(-1) == 1
+            and qkv.stride(1) % 8 == 0 and qkv.stride(0) % 8 == 0 and qkv.data_ptr() % 16 == 0):
+        _require()
+        return _attn_fns()[1].apply(qkv, int(n_head), bool(causal), sc)
+    q, k, v = (qkv[:, :, i * C:(i + 1) * C].view(B, T, n_head, D).transpose(1, 2) for i in range(3))
+    y = F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=sc)
+    return y.transpose(1, 2).reshape(B, T, C)
+
+
 SUMMARY_FIELDS = ("count", "sum", "mean", "std", "norm", "min", "max", "absmax", "nan", "inf", "finite", "shift")
 
 
@@ -314,5 +421,6 @@ def tensor_summary_text(x) -> str:
     return f"[{shape} {str(x.dtype).replace('torch.', '')} {x.device}] " + " ".join(parts)
 
 
-__all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "cross_entropy", "tensor_summary", "tensor_summary_text",
+__all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "cross_entropy",
+           "flash_attention", "attention_qkv", "flash_supported", "tensor_summary", "tensor_summary_text",
            "tensor_summary_raw", "plan_offsets", "native_available", "load_library", "SUMMARY_FIELDS"]
