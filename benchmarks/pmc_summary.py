@@ -20,6 +20,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name)  # drop the parameter list
     return name[:90]
 

@@ -13,6 +13,7 @@ import re
 
 
 def short(name: str, n: int = 110) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name) if name.startswith("void ") or "(" in name else name
     return name if len(name) <= n else name[: n - 3] + "..."
 

@@ -12,6 +12,9 @@ TORCH_LIBRARY(nbd, m) {
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale, "
         "Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
+  m.def("ln_fwd(Tensor x, Tensor? delta, Tensor weight, Tensor bias, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("ln_bwd(Tensor x, Tensor dy, Tensor? dres, Tensor weight, Tensor mean, Tensor rstd) -> (Tensor, Tensor, Tensor)");
+  m.def("colsum(Tensor x, ScalarType dtype) -> Tensor");
   m.def("xent_fwd(Tensor logits, Tensor target, int ignore_index) -> (Tensor, Tensor)");
   m.def("xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor scale, int ignore_index, Tensor(a!) dlogits) -> ()");
   m.def("adamw_flat(Tensor grad, Tensor(a!) param, Tensor(b!) master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "

@@ -1,0 +1,490 @@
+// norm.hip — LayerNorm (with fused residual add) forward/backward and column sums, gfx950.
+//
+// GPT-2 small runs 25 LayerNorms over [8192, 768] bf16 rows per step plus a residual add before
+// each; torch's kernels took ≈1.5 ms/step for the norms and 0.37 ms for the adds, and Linear's
+// bias gradients (column sums of dY) another 1.0 ms through the generic reduce kernel
+// (profiles/gpt2_step_rocprof_r1b.md) — all memory-bound work well below the HBM roof.
+//
+//   ln_fwd      one wave per row (4 rows per 256-thread workgroup); a lane owns 4-element
+//               (8-B) chunks c = 4·lane + 256·k, held in registers between the mean and
+//               variance passes (two wave64 reductions, no LDS); optional fused residual add
+//               (writes x + delta once, normalises it) — 1 read (2 with the residual) + 1–2 writes.
+//   ln_bwd      each workgroup sweeps 32 rows (8 per wave): dx = rstd·(g·dy − mean(g·dy) −
+//               x̂·mean(g·dy·x̂)) (+ the residual stream's gradient, fused), and per-lane column
+//               partials Σdy·x̂, Σdy reduced over the 4 waves in LDS → one [C] partial row per
+//               workgroup; col_reduce sums the partials (fp32) into dγ, dβ.
+//   colsum      bias gradients: [rows, C] → per-workgroup column partials (a lane owns 8
+//               columns = one 16-B load per row) → col_reduce.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include <tuple>
+#include <type_traits>
+
+#include "nbd_common.h"
+
+namespace nbd {
+namespace norm {
+
+constexpr int NT = 256;
+constexpr int kMaxCh = 8;  // 4-element chunks per lane: C <= 64 * 4 * 8 = 2048 (kernels are
+                           // instantiated per chunk count NCH = ceil(C / 256) to keep registers low)
+
+template <typename T>
+__device__ __forceinline__ float round_to(float v) { return v; }
+template <>
+__device__ __forceinline__ float round_to<bf16_t>(float v) { return bf16_to_f32(f32_to_bf16(v)); }
+template <>
+__device__ __forceinline__ float round_to<f16_t>(float v) { return f16_to_f32(f32_to_f16(v)); }
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float (&v)[4]);
+template <>
+__device__ __forceinline__ void load4<bf16_t>(const bf16_t* p, float (&v)[4]) {
+  const uint2 w = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(w.x << 16);
+  v[1] = __uint_as_float(w.x & 0xffff0000u);
+  v[2] = __uint_as_float(w.y << 16);
+  v[3] = __uint_as_float(w.y & 0xffff0000u);
+}
+template <>
+__device__ __forceinline__ void load4<f16_t>(const f16_t* p, float (&v)[4]) {
+  const uint2 w = *reinterpret_cast<const uint2*>(p);
+  v[0] = f16_to_f32((uint16_t)(w.x & 0xffffu));
+  v[1] = f16_to_f32((uint16_t)(w.x >> 16));
+  v[2] = f16_to_f32((uint16_t)(w.y & 0xffffu));
+  v[3] = f16_to_f32((uint16_t)(w.y >> 16));
+}
+template <>
+__device__ __forceinline__ void load4<float>(const float* p, float (&v)[4]) {
+  const float4 w = *reinterpret_cast<const float4*>(p);
+  v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+}
+template <typename T>
+__device__ __forceinline__ void store4(T* p, const float (&v)[4]);
+template <>
+__device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float (&v)[4]) {
+  *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16),
+                                            (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16));
+}
+template <>
+__device__ __forceinline__ void store4<f16_t>(f16_t* p, const float (&v)[4]) {
+  *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)f32_to_f16(v[0]) | ((uint32_t)f32_to_f16(v[1]) << 16),
+                                            (uint32_t)f32_to_f16(v[2]) | ((uint32_t)f32_to_f16(v[3]) << 16));
+}
+template <>
+__device__ __forceinline__ void store4<float>(float* p, const float (&v)[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// ============================================================================ forward
+template <typename T, typename W, bool RES, int NCH>
+__global__ __launch_bounds__(NT) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ delta,
+                                                    T* __restrict__ xsum, const W* __restrict__ gamma,
+                                                    const W* __restrict__ beta, T* __restrict__ y,
+                                                    float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                    int64_t rows, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (NT / kWave) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int64_t base = row * C;
+  float v[NCH][4];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * lane + 256 * k;
+    if (c < C) {
+      load4<T>(x + base + c, v[k]);
+      if (RES) {
+        float d[4];
+        load4<T>(delta + base + c, d);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[k][e] += d[e];
+        store4<T>(xsum + base + c, v[k]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[k][e] = round_to<T>(v[k][e]);  // normalise what was stored
+      }
+      s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
+    }
+  }
+  const float mean = wsum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * lane + 256 * k;
+    if (c < C) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[k][e] - mean;
+        q = fmaf(d, d, q);
+      }
+    }
+  }
+  const float rstd = rsqrtf(wsum(q) / (float)C + eps);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * lane + 256 * k;
+    if (c < C) {
+      float g[4], b[4], o[4];
+      load4<W>(gamma + c, g);
+      load4<W>(beta + c, b);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = fmaf((v[k][e] - mean) * rstd, g[e], b[e]);
+      store4<T>(y + base + c, o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// ============================================================================ backward
+constexpr int kBwdRows = 32;  // rows per workgroup (8 per wave)
+
+template <typename T, typename W, bool RES, int NCH>
+__global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                    const T* __restrict__ dres, const W* __restrict__ gamma,
+                                                    const float* __restrict__ mean_in,
+                                                    const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                    float* __restrict__ part_g, int64_t rows, int C) {
+  __shared__ float red[2][NT / kWave - 1][NCH * 256];  // waves 1..3 hand their column partials to wave 0
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float g[NCH][4], ag[NCH][4], ab[NCH][4];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * lane + 256 * k;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ag[k][e] = ab[k][e] = 0.f;
+    if (c < C) load4<W>(gamma + c, g[k]);
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * kBwdRows;
+  for (int i = wave; i < kBwdRows; i += NT / kWave) {
+    const int64_t row = r0 + i;
+    if (row >= rows) break;
+    const int64_t base = row * C;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NCH][4], gy[NCH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = 4 * lane + 256 * k;
+      if (c < C) {
+        float xv[4], dv[4];
+        load4<T>(x + base + c, xv);
+        load4<T>(dy + base + c, dv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[k][e] = (xv[e] - mean) * rstd;
+          gy[k][e] = dv[e] * g[k][e];
+          s1 += gy[k][e];
+          s2 = fmaf(gy[k][e], xh[k][e], s2);
+          ag[k][e] = fmaf(dv[e], xh[k][e], ag[k][e]);
+          ab[k][e] += dv[e];
+        }
+      }
+    }
+    const float m1 = wsum(s1) / (float)C, m2 = wsum(s2) / (float)C;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = 4 * lane + 256 * k;
+      if (c < C) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rstd * (gy[k][e] - m1 - xh[k][e] * m2);
+        if (RES) {
+          float rv[4];
+          load4<T>(dres + base + c, rv);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += rv[e];
+        }
+        store4<T>(dx + base + c, o);
+      }
+    }
+  }
+  // column partials of this workgroup: waves 1..3 -> LDS -> wave 0 sums and writes one row
+  if (wave > 0) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = 4 * lane + 256 * k;
+      if (c < C)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          red[0][wave - 1][c + e] = ag[k][e];
+          red[1][wave - 1][c + e] = ab[k][e];
+        }
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = 4 * lane + 256 * k;
+      if (c < C) {
+#pragma unroll
+        for (int w = 0; w < NT / kWave - 1; ++w)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ag[k][e] += red[0][w][c + e];
+            ab[k][e] += red[1][w][c + e];
+          }
+        store4<float>(part_g + (int64_t)blockIdx.x * 2 * C + c, ag[k]);      // [blk][0, C)
+        store4<float>(part_g + (int64_t)blockIdx.x * 2 * C + C + c, ab[k]);  // [blk][C, 2C)
+      }
+    }
+  }
+}
+
+// ============================================================================ column sums
+constexpr int kColRows = 64;  // rows per workgroup
+
+template <typename T>
+__global__ __launch_bounds__(NT) void colsum_kernel(const T* __restrict__ x, int64_t rows, int C,
+                                                    float* __restrict__ part) {
+  // a lane owns 8 columns (one 16-B load per row); 256 threads = 2048 columns per workgroup
+  // tile; blockIdx.y = column tile, blockIdx.x = row block
+  const int c = (blockIdx.y * NT + threadIdx.x) * 8;
+  if (c >= C) return;
+  const int64_t r0 = (int64_t)blockIdx.x * kColRows;
+  const int64_t r1 = r0 + kColRows < rows ? r0 + kColRows : rows;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int64_t r = r0;
+  for (; r + 4 <= r1; r += 4) {  // four rows in flight per lane
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load8<T>(x + (r + u) * C + c, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[u][e];
+  }
+  for (; r < r1; ++r) {
+    float v[8];
+    load8<T>(x + r * C + c, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += v[e];
+  }
+  store8<float>(part + (int64_t)blockIdx.x * C + c, acc);
+}
+
+// Sum of `nparts` partial rows of width W (= C, or 2C for LayerNorm's [dγ | dβ] partials) into
+// out0[c] (c < C) / out1[c - C].  Workgroup = 16 columns x 16 partial-row groups: every thread's
+// loads are independent and issued together, the 16 groups are combined in LDS — no serial
+// per-column loop (a one-thread-per-column version spent 18 µs per call, latency-bound).
+template <typename O>
+__global__ __launch_bounds__(NT) void col_reduce_kernel(const float* __restrict__ part, int nparts, int W, int C,
+                                                        O* __restrict__ out0, O* __restrict__ out1) {
+  __shared__ float red[16][17];
+  const int cx = threadIdx.x & 15, pg = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cx;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < W) {
+    int p = pg;
+    for (; p + 48 < nparts; p += 64) {
+      a0 += part[(int64_t)p * W + c];
+      a1 += part[(int64_t)(p + 16) * W + c];
+      a2 += part[(int64_t)(p + 32) * W + c];
+      a3 += part[(int64_t)(p + 48) * W + c];
+    }
+    for (; p < nparts; p += 16) a0 += part[(int64_t)p * W + c];
+  }
+  red[pg][cx] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (pg == 0 && c < W) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) s += red[g][cx];
+    if (c < C) Elem<O>::store(out0, c, s);
+    else Elem<O>::store(out1, c - C, s);
+  }
+}
+
+// ============================================================================ host
+static void check_rows(const at::Tensor& t, int64_t C, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.size(-1) == C, "norm: ", name, " must be contiguous [..., C]");
+  TORCH_CHECK(((uintptr_t)t.data_ptr() & 15) == 0, "norm: ", name, " must be 16-B aligned");
+}
+
+template <typename F>
+static void dispatch_nch(int64_t C, F&& f) {
+  const int64_t n = (C + 255) / 256;
+  if (n <= 1) f(std::integral_constant<int, 1>{});
+  else if (n == 2) f(std::integral_constant<int, 2>{});
+  else if (n == 3) f(std::integral_constant<int, 3>{});
+  else if (n == 4) f(std::integral_constant<int, 4>{});
+  else if (n <= 6) f(std::integral_constant<int, 6>{});
+  else f(std::integral_constant<int, 8>{});
+}
+
+template <typename F>
+static void dispatch_tw(at::ScalarType t, at::ScalarType w, F&& f) {
+  TORCH_CHECK(t == at::kBFloat16 || t == at::kHalf || t == at::kFloat, "norm: unsupported dtype ", t);
+  TORCH_CHECK(w == t, "norm: weight dtype must match the input dtype");
+  if (t == at::kBFloat16) f(bf16_t{}, bf16_t{});
+  else if (t == at::kHalf) f(f16_t{}, f16_t{});
+  else f(float{}, float{});
+}
+
+template <typename O>
+static void launch_reduce(const at::Tensor& part, int nparts, int W, int C, const at::Tensor& out0,
+                          const at::Tensor& out1, hipStream_t st) {
+  hipLaunchKernelGGL((col_reduce_kernel<O>), dim3((W + 15) / 16), dim3(NT), 0, st, part.data_ptr<float>(), nparts, W,
+                     C, static_cast<O*>(out0.data_ptr()), static_cast<O*>(out1.data_ptr()));
+}
+// part [nparts, W] -> out0 = columns [0, C), out1 = columns [C, W) (same dtype)
+static void reduce_into(const at::Tensor& part, int nparts, int W, int C, const at::Tensor& out0,
+                        const at::Tensor& out1, hipStream_t st) {
+  switch (out0.scalar_type()) {
+    case at::kFloat: launch_reduce<float>(part, nparts, W, C, out0, out1, st); break;
+    case at::kBFloat16: launch_reduce<bf16_t>(part, nparts, W, C, out0, out1, st); break;
+    case at::kHalf: launch_reduce<f16_t>(part, nparts, W, C, out0, out1, st); break;
+    default: TORCH_CHECK(false, "norm: unsupported output dtype");
+  }
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+// returns (y, xsum or undefined, mean, rstd)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ln_fwd_hip(const at::Tensor& x,
+                                                                      const c10::optional<at::Tensor>& delta,
+                                                                      const at::Tensor& weight,
+                                                                      const at::Tensor& bias, double eps) {
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 4 == 0 && C <= 256 * kMaxCh && C > 0, "ln_fwd: C must be a multiple of 4 and <= 2048");
+  check_rows(x, C, "x");
+  TORCH_CHECK(weight.is_contiguous() && bias.is_contiguous() && weight.numel() == C && bias.numel() == C,
+              "ln_fwd: weight/bias must be [C]");
+  const bool res = delta.has_value() && delta->defined();
+  if (res) {
+    check_rows(*delta, C, "delta");
+    TORCH_CHECK(delta->sizes() == x.sizes() && delta->scalar_type() == x.scalar_type(), "ln_fwd: delta mismatch");
+  }
+  const int64_t rows = x.numel() / C;
+  at::Tensor y = at::empty_like(x);
+  at::Tensor xsum = res ? at::empty_like(x) : at::Tensor();
+  auto fo = x.options().dtype(at::kFloat);
+  at::Tensor mean = at::empty({rows}, fo), rstd = at::empty({rows}, fo);
+  if (rows == 0) return {y, xsum, mean, rstd};
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  dispatch_tw(x.scalar_type(), weight.scalar_type(), [&](auto t, auto w) {
+   dispatch_nch(C, [&](auto nch) {
+    using T = decltype(t);
+    using W = decltype(w);
+    constexpr int N = decltype(nch)::value;
+    if (res)
+      hipLaunchKernelGGL((ln_fwd_kernel<T, W, true, N>), grid, dim3(NT), 0, st, static_cast<const T*>(x.data_ptr()),
+                         static_cast<const T*>(delta->data_ptr()), static_cast<T*>(xsum.data_ptr()),
+                         static_cast<const W*>(weight.data_ptr()), static_cast<const W*>(bias.data_ptr()),
+                         static_cast<T*>(y.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, (int)C,
+                         (float)eps);
+    else
+      hipLaunchKernelGGL((ln_fwd_kernel<T, W, false, N>), grid, dim3(NT), 0, st, static_cast<const T*>(x.data_ptr()),
+                         nullptr, nullptr, static_cast<const W*>(weight.data_ptr()),
+                         static_cast<const W*>(bias.data_ptr()), static_cast<T*>(y.data_ptr()),
+                         mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, (int)C, (float)eps);
+   });
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return {y, xsum, mean, rstd};
+}
+
+// returns (dx, dweight, dbias); dx includes dres when given
+std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_hip(const at::Tensor& x, const at::Tensor& dy,
+                                                          const c10::optional<at::Tensor>& dres,
+                                                          const at::Tensor& weight, const at::Tensor& mean,
+                                                          const at::Tensor& rstd) {
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 4 == 0 && C <= 256 * kMaxCh && C > 0, "ln_bwd: C must be a multiple of 4 and <= 2048");
+  check_rows(x, C, "x");
+  check_rows(dy, C, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "ln_bwd: dy mismatch");
+  const bool res = dres.has_value() && dres->defined();
+  if (res) {
+    check_rows(*dres, C, "dres");
+    TORCH_CHECK(dres->sizes() == x.sizes() && dres->scalar_type() == x.scalar_type(), "ln_bwd: dres mismatch");
+  }
+  const int64_t rows = x.numel() / C;
+  TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows && mean.scalar_type() == at::kFloat &&
+                  rstd.scalar_type() == at::kFloat,
+              "ln_bwd: mean/rstd must be float32 [rows]");
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dw = at::empty({C}, weight.options()), db = at::empty({C}, weight.options());
+  const int nblk = (int)((rows + kBwdRows - 1) / kBwdRows);
+  if (rows == 0) return {dx, dw.zero_(), db.zero_()};
+  auto fo = x.options().dtype(at::kFloat);
+  at::Tensor pg = at::empty({nblk, 2 * C}, fo);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  dispatch_tw(x.scalar_type(), weight.scalar_type(), [&](auto t, auto w) {
+   dispatch_nch(C, [&](auto nch) {
+    using T = decltype(t);
+    using W = decltype(w);
+    constexpr int N = decltype(nch)::value;
+    const T* dr = res ? static_cast<const T*>(dres->data_ptr()) : nullptr;
+    if (res)
+      hipLaunchKernelGGL((ln_bwd_kernel<T, W, true, N>), dim3(nblk), dim3(NT), 0, st,
+                         static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
+                         static_cast<const W*>(weight.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C);
+    else
+      hipLaunchKernelGGL((ln_bwd_kernel<T, W, false, N>), dim3(nblk), dim3(NT), 0, st,
+                         static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
+                         static_cast<const W*>(weight.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C);
+   });
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  reduce_into(pg, nblk, (int)(2 * C), (int)C, dw, db, st);
+  return {dx, dw, db};
+}
+
+// Σ over rows of a contiguous [..., C] tensor -> [C] in `dtype` (fp32 accumulation)
+at::Tensor colsum_hip(const at::Tensor& x, at::ScalarType dtype) {
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0 && C > 0, "colsum: C must be a multiple of 8");
+  check_rows(x, C, "x");
+  const int64_t rows = x.numel() / C;
+  at::Tensor out = at::empty({C}, x.options().dtype(dtype));
+  if (rows == 0) return out.zero_();
+  const int nblk = (int)((rows + kColRows - 1) / kColRows);
+  at::Tensor part = at::empty({nblk, C}, x.options().dtype(at::kFloat));
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  const dim3 grid((unsigned)nblk, (unsigned)((C / 8 + NT - 1) / NT));
+  switch (x.scalar_type()) {
+    case at::kFloat:
+      hipLaunchKernelGGL((colsum_kernel<float>), grid, dim3(NT), 0, st, x.data_ptr<float>(), rows, (int)C,
+                         part.data_ptr<float>());
+      break;
+    case at::kBFloat16:
+      hipLaunchKernelGGL((colsum_kernel<bf16_t>), grid, dim3(NT), 0, st, static_cast<const bf16_t*>(x.data_ptr()),
+                         rows, (int)C, part.data_ptr<float>());
+      break;
+    case at::kHalf:
+      hipLaunchKernelGGL((colsum_kernel<f16_t>), grid, dim3(NT), 0, st, static_cast<const f16_t*>(x.data_ptr()), rows,
+                         (int)C, part.data_ptr<float>());
+      break;
+    default: TORCH_CHECK(false, "colsum: unsupported dtype ", x.scalar_type());
+  }
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  reduce_into(part, nblk, (int)C, (int)C, out, out, st);
+  return out;
+}
+
+}  // namespace norm
+}  // namespace nbd
+
+TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
+  m.impl("ln_fwd", &nbd::norm::ln_fwd_hip);
+  m.impl("ln_bwd", &nbd::norm::ln_bwd_hip);
+  m.impl("colsum", &nbd::norm::colsum_hip);
+}

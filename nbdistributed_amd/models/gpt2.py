@@ -31,6 +31,7 @@ class GPT2Config:
     tie_weights: bool = True
     fused_ce: bool = True  # GPU: nbd.ops.cross_entropy (HIP) instead of F.cross_entropy(logits.float())
     fused_attn: bool = True  # GPU bf16: nbd.ops.attention_qkv (HIP flash fwd/bwd) instead of SDPA
+    fused_norm: bool = True  # GPU, no autocast: HIP residual-add+LayerNorm and bias-grad kernels
 
     @classmethod
     def small(cls):
@@ -51,8 +52,13 @@ class CausalSelfAttention(nn.Module):
         self.c_proj = nn.Linear(c.n_embd, c.n_embd, bias=c.bias)
         self.dropout = c.dropout
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, fast: bool = False) -> torch.Tensor:
         B, T, C = x.shape
+        if fast:  # HIP path: bias grads by the column-sum kernel, flash attention on the packed QKV
+            from .. import ops
+
+            qkv = ops.linear(x, self.c_attn.weight, self.c_attn.bias)
+            return ops.linear(ops.attention_qkv(qkv, self.n_head, causal=True), self.c_proj.weight, self.c_proj.bias)
         qkv = self.c_attn(x)
         if self.fused and qkv.is_cuda and (self.dropout == 0.0 or not self.training):
             from .. import ops
@@ -74,7 +80,12 @@ class MLP(nn.Module):
         self.c_fc = nn.Linear(c.n_embd, 4 * c.n_embd, bias=c.bias)
         self.c_proj = nn.Linear(4 * c.n_embd, c.n_embd, bias=c.bias)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, fast: bool = False) -> torch.Tensor:
+        if fast:
+            from .. import ops
+
+            h = F.gelu(ops.linear(x, self.c_fc.weight, self.c_fc.bias), approximate="tanh")
+            return ops.linear(h, self.c_proj.weight, self.c_proj.bias)
         return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
 
 
@@ -117,6 +128,17 @@ class GPT2(nn.Module):
         elif isinstance(m, nn.Embedding):
             nn.init.normal_(m.weight, mean=0.0, std=0.02)
 
+    @property
+    def fused_attn_ok(self) -> bool:
+        c = self.config
+        return c.fused_attn and c.n_embd // c.n_head == 64 and (c.dropout == 0.0 or not self.training)
+
+    def _fast(self, x: torch.Tensor) -> bool:
+        c = self.config
+        return (c.fused_norm and c.bias and x.is_cuda and not torch.is_autocast_enabled()
+                and x.dtype in (torch.bfloat16, torch.float16) and c.n_embd % 8 == 0 and c.n_embd <= 2048
+                and x.shape[1] % 128 == 0)
+
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
@@ -126,9 +148,24 @@ class GPT2(nn.Module):
         B, T = idx.shape
         pos = torch.arange(T, device=idx.device)
         x = self.wte(idx) + self.wpe(pos)
-        for blk in self.h:
-            x = blk(x)
-        logits = self.lm_head(self.ln_f(x))
+        if self._fast(x):
+            # residual stream through the HIP add+LayerNorm kernels: each block's two residual adds
+            # are fused with the LayerNorm that follows them (ln_2, then the next block's ln_1 / ln_f)
+            from .. import ops
+
+            c = self.config
+            ln = self.h[0].ln_1
+            h = ops.layer_norm(x, ln.weight, ln.bias, ln.eps)
+            for i, blk in enumerate(self.h):
+                x, h = ops.add_layer_norm(x, blk.attn(h, fast=self.fused_attn_ok), blk.ln_2.weight, blk.ln_2.bias,
+                                          blk.ln_2.eps)
+                nxt = self.h[i + 1].ln_1 if i + 1 < c.n_layer else self.ln_f
+                x, h = ops.add_layer_norm(x, blk.mlp(h, fast=True), nxt.weight, nxt.bias, nxt.eps)
+            logits = self.lm_head(h)
+        else:
+            for blk in self.h:
+                x = blk(x)
+            logits = self.lm_head(self.ln_f(x))
         loss = None
         if targets is not None:
             flat, tgt = logits.view(-1, logits.size(-1)), targets.reshape(-1)
