@@ -9,7 +9,7 @@
 //               (8-B) chunks c = 4·lane + 256·k, held in registers between the mean and
 //               variance passes (two wave64 reductions, no LDS); optional fused residual add
 //               (writes x + delta once, normalises it) — 1 read (2 with the residual) + 1–2 writes.
-//   ln_bwd      each workgroup sweeps 32 rows (8 per wave): dx = rstd·(g·dy − mean(g·dy) −
+//   ln_bwd      each workgroup sweeps 16 rows (4 per wave, loads of two rows in flight at once): dx = rstd·(g·dy − mean(g·dy) −
 //               x̂·mean(g·dy·x̂)) (+ the residual stream's gradient, fused), and per-lane column
 //               partials Σdy·x̂, Σdy reduced over the 4 waves in LDS → one [C] partial row per
 //               workgroup; col_reduce sums the partials (fp32) into dγ, dβ.
@@ -148,7 +148,8 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const T* __restrict__ x, con
 }
 
 // ============================================================================ backward
-constexpr int kBwdRows = 32;  // rows per workgroup (8 per wave)
+constexpr int kBwdRows = 16;  // rows per workgroup (4 per wave, two at a time)
+constexpr int kRpi = 2;       // rows per wave iteration
 
 template <typename T, typename W, bool RES, int NCH>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
@@ -167,46 +168,63 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, con
     if (c < C) load4<W>(gamma + c, g[k]);
   }
   const int64_t r0 = (int64_t)blockIdx.x * kBwdRows;
-  for (int i = wave; i < kBwdRows; i += NT / kWave) {
-    const int64_t row = r0 + i;
-    if (row >= rows) break;
-    const int64_t base = row * C;
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[NCH][4], gy[NCH][4];
-    float s1 = 0.f, s2 = 0.f;
+  // each wave takes kRpi rows at a time and issues all their loads before any arithmetic
+  for (int i = wave * kRpi; i < kBwdRows; i += (NT / kWave) * kRpi) {
+    float xv[kRpi][NCH][4], dv[kRpi][NCH][4], rv[kRpi][NCH][4];
+    float mean[kRpi], rstd[kRpi];
+    bool live[kRpi];
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      const int c = 4 * lane + 256 * k;
-      if (c < C) {
-        float xv[4], dv[4];
-        load4<T>(x + base + c, xv);
-        load4<T>(dy + base + c, dv);
+    for (int j = 0; j < kRpi; ++j) {
+      const int64_t row = r0 + i + j;
+      live[j] = row < rows;
+      const int64_t rr = live[j] ? row : r0;  // dead rows re-read a live one; their results are dropped
+      mean[j] = mean_in[rr];
+      rstd[j] = rstd_in[rr];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          xh[k][e] = (xv[e] - mean) * rstd;
-          gy[k][e] = dv[e] * g[k][e];
-          s1 += gy[k][e];
-          s2 = fmaf(gy[k][e], xh[k][e], s2);
-          ag[k][e] = fmaf(dv[e], xh[k][e], ag[k][e]);
-          ab[k][e] += dv[e];
+      for (int k = 0; k < NCH; ++k) {
+        const int c = 4 * lane + 256 * k;
+        if (c < C) {
+          load4<T>(x + rr * C + c, xv[j][k]);
+          load4<T>(dy + rr * C + c, dv[j][k]);
+          if (RES) load4<T>(dres + rr * C + c, rv[j][k]);
         }
       }
     }
-    const float m1 = wsum(s1) / (float)C, m2 = wsum(s2) / (float)C;
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      const int c = 4 * lane + 256 * k;
-      if (c < C) {
-        float o[4];
+    for (int j = 0; j < kRpi; ++j) {
+      if (!live[j]) continue;
+      const int64_t base = (r0 + i + j) * C;
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = rstd * (gy[k][e] - m1 - xh[k][e] * m2);
-        if (RES) {
-          float rv[4];
-          load4<T>(dres + base + c, rv);
+      for (int k = 0; k < NCH; ++k) {
+        const int c = 4 * lane + 256 * k;
+        if (c < C) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] += rv[e];
+          for (int e = 0; e < 4; ++e) {
+            const float xh = (xv[j][k][e] - mean[j]) * rstd[j];
+            const float gy = dv[j][k][e] * g[k][e];
+            xv[j][k][e] = xh;  // keep x̂ and g·dy in the load registers
+            s1 += gy;
+            s2 = fmaf(gy, xh, s2);
+            ag[k][e] = fmaf(dv[j][k][e], xh, ag[k][e]);
+            ab[k][e] += dv[j][k][e];
+            dv[j][k][e] = gy;
+          }
         }
-        store4<T>(dx + base + c, o);
+      }
+      const float m1 = wsum(s1) / (float)C, m2 = wsum(s2) / (float)C;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int c = 4 * lane + 256 * k;
+        if (c < C) {
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o[e] = rstd[j] * (dv[j][k][e] - m1 - xv[j][k][e] * m2);
+            if (RES) o[e] += rv[j][k][e];
+          }
+          store4<T>(dx + base + c, o);
+        }
       }
     }
   }
