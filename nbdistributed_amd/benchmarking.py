@@ -293,8 +293,35 @@ def bench_rank_broadcast(session, dim: int = 4096, iters: int = 20, warm: int = 
             "correct": correct}
 
 
+def _phase(session, out: Dict[str, Any], name: str, fn, timeout_s: float) -> None:
+    """Run one optional benchmark phase; failures are recorded in ``out[name]`` instead of
+    losing the whole result line.  A timeout means ranks are stuck (e.g. inside a collective):
+    interrupt them (out-of-band SIGINT; the worker watchdog aborts the RCCL communicator) and
+    skip the remaining phases."""
+    if out.get("aborted"):
+        out[name] = {"skipped": "an earlier phase timed out"}
+        return
+    prev = session.default_timeout
+    session.default_timeout = timeout_s
+    try:
+        out[name] = fn()
+    except Exception as e:  # noqa: BLE001 - recorded in the result line
+        out[name] = {"error": f"{type(e).__name__}: {e}"[:800]}
+        _log(f"phase {name} failed: {type(e).__name__}: {str(e)[:300]}")
+        if isinstance(e, TimeoutError):
+            out["aborted"] = name
+            try:
+                session.interrupt()
+                time.sleep(session.cfg.interrupt_abort_s + 5.0)
+            except Exception:  # noqa: BLE001
+                pass
+    finally:
+        session.default_timeout = prev
+
+
 def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: bool = False,
-            ar_bytes: int = 1 << 30, ddp: bool = True, ddp_steps: int = 20, bcast: bool = True) -> Dict[str, Any]:
+            ar_bytes: int = 1 << 30, ddp: bool = True, ddp_steps: int = 20, bcast: bool = True,
+            phase_timeout_s: float = 900.0) -> Dict[str, Any]:
     n = session.world_size
     _log(f"phase 1: {warmup}+{steps} trivial %%distributed cells on {n} rank(s)")
     cells = bench_cells(session, steps, warmup)
@@ -303,20 +330,25 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
     gpu = bool(session.ready.get(0, {}).get("cuda_available"))
     if allreduce and gpu:
         _log(f"phase 2: {ar_bytes / 2**30:.2f} GiB bf16 all_reduce")
-        out["allreduce"] = bench_allreduce(session, ar_bytes)
-        _log(f"all_reduce {out['allreduce']['time_ms']:.3f} ms busbw {out['allreduce']['busbw_GBps']}")
+        _phase(session, out, "allreduce", lambda: bench_allreduce(session, ar_bytes), phase_timeout_s)
+        ar = out["allreduce"]
+        if "time_ms" in ar:
+            _log(f"all_reduce {ar['time_ms']:.3f} ms busbw {ar['busbw_GBps']}")
     if sweep and gpu:
         _log("phase 3: all_reduce sweep")
-        out["sweep"] = bench_sweep(session)
+        _phase(session, out, "sweep", lambda: bench_sweep(session), phase_timeout_s)
     if bcast and gpu:
         _log("phase 3b: %%rank[0] Linear(4096) build + broadcast (config 3)")
-        out["rank_broadcast"] = bench_rank_broadcast(session)
-        _log(f"broadcast per-param {out['rank_broadcast']['per_param_ms']:.3f} ms, coalesced "
-             f"{out['rank_broadcast']['coalesced_ms']:.3f} ms")
+        _phase(session, out, "rank_broadcast", lambda: bench_rank_broadcast(session), phase_timeout_s)
+        rb = out["rank_broadcast"]
+        if "per_param_ms" in rb:
+            _log(f"broadcast per-param {rb['per_param_ms']:.3f} ms, coalesced {rb['coalesced_ms']:.3f} ms")
     if ddp and gpu:
         _log("phase 4: DDP steps (GPT-2 small bf16 config 5, Linear 4096 config 4)")
-        out["ddp"] = bench_ddp(session, steps=ddp_steps)
-        _log(f"gpt2 ddp {out['ddp']['ms_per_step']:.2f} ms/step {out['ddp']['tokens_per_s']:.0f} tok/s")
+        _phase(session, out, "ddp", lambda: bench_ddp(session, steps=ddp_steps), phase_timeout_s)
+        d = out["ddp"]
+        if "ms_per_step" in d:
+            _log(f"gpt2 ddp {d['ms_per_step']:.2f} ms/step {d['tokens_per_s']:.0f} tok/s")
     return out
 
 
@@ -344,7 +376,9 @@ def result_line(res: Dict[str, Any], n: int, steps: int, warmup: int) -> Dict[st
         "baseline_cell_p50_ms": BASELINE_CELL_P50_MS,
         "speedup_vs_baseline": round(BASELINE_CELL_P50_MS / cells["p50_ms"], 1),
     }
-    if ar:
+    if ar and ("error" in ar or "skipped" in ar):
+        line["allreduce_error"] = ar.get("error") or ar.get("skipped")
+    elif ar:
         line["allreduce_bytes"] = ar["bytes"]
         line["allreduce_time_ms"] = round(ar["time_ms"], 4)
         line["allreduce_algbw_GBps"] = round(ar["algbw_GBps"], 2)
@@ -352,6 +386,8 @@ def result_line(res: Dict[str, Any], n: int, steps: int, warmup: int) -> Dict[st
         line["allreduce_correct"] = ar["correct"]
     if res.get("sweep"):
         line["allreduce_sweep"] = res["sweep"]
+    if res.get("aborted"):
+        line["aborted_phase"] = res["aborted"]
     for k in ("ddp", "rank_broadcast"):
         if k in res:
             line[k] = res[k]

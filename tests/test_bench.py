@@ -50,6 +50,32 @@ def test_cells_phase_and_result_line(sess):
     assert line["higher_is_better"] is False and line["n_gpus"] == 2
 
 
+def test_failed_phase_is_recorded_and_timeout_aborts_the_rest():
+    class _Cfg:
+        interrupt_abort_s = 0.0
+
+    class _Sess:
+        default_timeout = None
+        cfg = _Cfg()
+        interrupts = 0
+
+        def interrupt(self):
+            self.interrupts += 1
+
+    def _timeout():
+        raise TimeoutError("ranks stuck")
+
+    s, out = _Sess(), {}
+    B._phase(s, out, "a", lambda: 1 / 0, 5.0)
+    B._phase(s, out, "b", _timeout, 5.0)
+    B._phase(s, out, "c", lambda: {"ok": 1}, 5.0)
+    assert "ZeroDivisionError" in out["a"]["error"] and out["aborted"] == "b"
+    assert "skipped" in out["c"] and s.interrupts == 1 and s.default_timeout is None
+    cells = {"p50_ms": 1.0, "p90_ms": 1.0, "min_ms": 1.0, "mean_ms": 1.0}
+    line = B.result_line({"cell": cells, "allreduce": out["a"], "aborted": "b"}, 2, 1, 1)
+    assert line["allreduce_error"].startswith("ZeroDivisionError") and line["aborted_phase"] == "b"
+
+
 @pytest.mark.parametrize("n", [1, 2])
 def test_bench_py_contract_cpu(n):
     if n == 1:
