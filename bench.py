@@ -41,6 +41,7 @@ def _args(argv=None):
     ap.add_argument("--no-ddp", action="store_true", help="skip the DDP phases (configs 4 and 5)")
     ap.add_argument("--ddp-steps", type=int, default=20)
     ap.add_argument("--no-bcast", action="store_true", help="skip the %%%%rank[0] build + broadcast phase (config 3)")
+    ap.add_argument("--no-notebook", action="store_true", help="skip the reference notebook workload (SmolLM2)")
     ap.add_argument("--coordinator", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--endpoint", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--world", type=int, default=None, help=argparse.SUPPRESS)
@@ -57,7 +58,8 @@ def coordinator_main(a) -> int:
     try:
         sess.attach(a.world, bind=a.endpoint, token=None, startup_timeout=900)
         res = run_all(sess, a.steps, a.warmup, allreduce=not a.no_allreduce, sweep=a.sweep, ar_bytes=a.ar_bytes,
-                      ddp=not a.no_ddp, ddp_steps=a.ddp_steps, bcast=not a.no_bcast)
+                      ddp=not a.no_ddp, ddp_steps=a.ddp_steps, bcast=not a.no_bcast,
+                      notebook=not a.no_notebook)
         res["init_ready"] = {r: sess.ready[r].get("init_s") for r in sess.ready}
         res["device"] = sess.ready[0].get("gpu_name")
         res["rccl_version"] = sess.ready[0].get("rccl_version")
@@ -106,6 +108,8 @@ def main(argv=None) -> int:
             cmd.append("--no-ddp")
         if a.no_bcast:
             cmd.append("--no-bcast")
+        if a.no_notebook:
+            cmd.append("--no-notebook")
         cmd += ["--ddp-steps", str(a.ddp_steps)]
         child = subprocess.Popen(cmd, stdin=subprocess.DEVNULL)
     from nbdistributed_amd import protocol as P

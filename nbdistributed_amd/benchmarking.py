@@ -134,7 +134,8 @@ def _nbd_linear_bench(steps, warm, rows, impl, dim=4096):
 def _max_over_ranks(res) -> float:
     vals = []
     for r in res.ranks:
-        out = res.results[r]["output"]
+        d = res.results[r]
+        out = d.get("echo") or d["output"].strip().splitlines()[-1]  # echo = the last expression only
         vals.append(float(out.strip("()").split(",")[0]))
     return max(vals)
 
@@ -236,6 +237,81 @@ def bench_sweep(session, dtype: str = "bfloat16", max_bytes: int = 1 << 30, min_
     return out
 
 
+NOTEBOOK_SETUP = """
+def _nbd_notebook_bench(steps, warm, bs=16, seq=128, mode="reference", small=False):
+    # the reference notebook's training loop (00_accelerate.ipynb exec 22-35): SmolLM2-135M
+    # sequence classifier, AdamW lr 2e-5 + linear warmup, bs 16/rank, max_length 128, through
+    # accelerate -> DDP.  Random init + synthetic MRPC-shaped batches (no network here).
+    import gc
+    from torch.utils.data import DataLoader, TensorDataset
+    from transformers import get_linear_schedule_with_warmup
+    from nbdistributed_amd.models import smollm2_135m_classifier, synthetic_mrpc
+    torch.manual_seed(42)
+    over = dict(num_hidden_layers=2, hidden_size=64, intermediate_size=128, num_attention_heads=4,
+                num_key_value_heads=2, vocab_size=512) if small else {}
+    n = bs * world_size * (steps + warm + 2)
+    ids, mask, labels = synthetic_mrpc(n=n, seq_len=seq, vocab=over.get("vocab_size", 49152))
+    model = smollm2_135m_classifier(**over)
+    if mode == "reference":       # the notebook's recipe: fp32, accelerate-prepared torch DDP
+        from accelerate import Accelerator
+        acc = Accelerator(cpu=device.type == "cpu")
+        opt = torch.optim.AdamW(model.parameters(), lr=2e-5)
+        dl = DataLoader(TensorDataset(ids, mask, labels), batch_size=bs, shuffle=True)
+        sched = get_linear_schedule_with_warmup(opt, 100, 3 * len(dl))
+        model, opt, dl, sched = acc.prepare(model, opt, dl, sched)
+        it = iter(dl)
+        def step():
+            x, m, y = next(it)
+            out = model(input_ids=x, attention_mask=m, labels=y)
+            acc.backward(out.loss)
+            opt.step(); sched.step(); opt.zero_grad()
+            return out.loss.detach()
+    else:                         # nbd: bf16 params in DDP buckets + FlatAdamW (fp32 master)
+        model = _NbdDDP(model.to(device, torch.bfloat16 if device.type == "cuda" else torch.float32),
+                        flat_params=True, grad_mode="bucket")
+        opt = _FlatAdamW(model, lr=2e-5)
+        sched = get_linear_schedule_with_warmup(opt, 100, 3 * (n // (bs * world_size)))
+        sl = slice(rank * (n // world_size), (rank + 1) * (n // world_size))
+        ids, mask, labels = ids[sl].to(device), mask[sl].to(device), labels[sl].to(device)
+        pos = [0]
+        def step():
+            i = pos[0]; pos[0] += bs
+            out = model(input_ids=ids[i:i + bs], attention_mask=mask[i:i + bs], labels=labels[i:i + bs])
+            out.loss.backward()
+            opt.step(); sched.step(); opt.zero_grad()
+            return out.loss.detach()
+    ms, loss = _nbd_time_steps(step, steps, warm)
+    del model, opt
+    gc.collect()
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
+    return ms, loss
+"""
+
+REFERENCE_NOTEBOOK_MS_PER_STEP = 126.6  # BASELINE.md: 1 epoch = 14.56 s / 115 steps, 2 GPUs
+
+
+def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = False) -> Dict[str, Any]:
+    """The reference's own measured workload (SmolLM2-135M-cls fine-tune, 126.6
+    ms/step, ≈252 samples/s on 2 GPUs) as notebook cells, max over ranks."""
+    n = session.world_size
+    session.execute(AR_SETUP, render=False)
+    session.execute(DDP_SETUP, render=False)
+    session.execute(NOTEBOOK_SETUP, render=False)
+    out: Dict[str, Any] = {"model": "SmolLM2-135M sequence classifier (random init)", "per_gpu_batch": 16,
+                           "seq_len": 128, "data": "synthetic MRPC-shaped",
+                           "reference_ms_per_step": REFERENCE_NOTEBOOK_MS_PER_STEP,
+                           "reference_samples_per_s": 32 / (REFERENCE_NOTEBOOK_MS_PER_STEP / 1e3)}
+    for mode in ("reference", "nbd"):
+        r = session.execute(f"_nbd_notebook_bench({steps}, {warmup}, mode={mode!r}, small={small})", render=False)
+        ms = _max_over_ranks(r)
+        out[mode] = {"ms_per_step": ms, "samples_per_s": n * 16 / (ms / 1e3),
+                     "recipe": "fp32, accelerate DDP, torch AdamW" if mode == "reference"
+                     else "bf16 params + fp32 master (FlatAdamW), nbd DDP"}
+    out["speedup_vs_reference_per_step"] = REFERENCE_NOTEBOOK_MS_PER_STEP / out["reference"]["ms_per_step"]
+    return out
+
+
 BCAST_BUILD = """
 model = torch.nn.Linear({dim}, {dim}, device=device)   # %%rank[0]: only rank 0 builds (random init)
 """
@@ -321,7 +397,7 @@ def _phase(session, out: Dict[str, Any], name: str, fn, timeout_s: float) -> Non
 
 def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: bool = False,
             ar_bytes: int = 1 << 30, ddp: bool = True, ddp_steps: int = 20, bcast: bool = True,
-            phase_timeout_s: float = 900.0) -> Dict[str, Any]:
+            notebook: bool = True, phase_timeout_s: float = 900.0) -> Dict[str, Any]:
     n = session.world_size
     _log(f"phase 1: {warmup}+{steps} trivial %%distributed cells on {n} rank(s)")
     cells = bench_cells(session, steps, warmup)
@@ -349,6 +425,12 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
         d = out["ddp"]
         if "ms_per_step" in d:
             _log(f"gpt2 ddp {d['ms_per_step']:.2f} ms/step {d['tokens_per_s']:.0f} tok/s")
+    if notebook and gpu:
+        _log("phase 5: reference notebook workload (SmolLM2-135M-cls, bs16, seq128)")
+        _phase(session, out, "notebook", lambda: bench_notebook(session, steps=ddp_steps), phase_timeout_s)
+        nb = out["notebook"]
+        if "reference" in nb:
+            _log(f"notebook fp32 {nb['reference']['ms_per_step']:.2f} ms/step, nbd {nb['nbd']['ms_per_step']:.2f}")
     return out
 
 
@@ -388,7 +470,7 @@ def result_line(res: Dict[str, Any], n: int, steps: int, warmup: int) -> Dict[st
         line["allreduce_sweep"] = res["sweep"]
     if res.get("aborted"):
         line["aborted_phase"] = res["aborted"]
-    for k in ("ddp", "rank_broadcast"):
+    for k in ("ddp", "rank_broadcast", "notebook"):
         if k in res:
             line[k] = res[k]
     return line

@@ -15,21 +15,24 @@ import torch
 from . import ops
 
 
-class FlatAdamW:
+class FlatAdamW(torch.optim.Optimizer):
+    """A ``torch.optim.Optimizer`` (so LR schedulers and hooks work) whose state lives per DDP
+    bucket: ``flat_state[i]`` = fp32 master / exp_avg / exp_avg_sq of bucket i.  One param group
+    (the bucket kernels apply one lr / weight decay to the whole model)."""
+
     def __init__(self, ddp, lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 1e-2):
         if not getattr(ddp, "flat_params", False) or ddp.grad_mode != "bucket":
             raise ValueError("FlatAdamW needs DistributedDataParallel(..., flat_params=True, grad_mode='bucket')")
+        super().__init__(list(ddp.params), dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.ddp = ddp
-        self.defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
-        self.param_groups = [dict(self.defaults, params=list(ddp.params))]  # LR schedulers poke lr here
         self.step_count = 0
         self._clip_coef = None
-        self.state: List[Dict[str, torch.Tensor]] = []
+        self.flat_state: List[Dict[str, torch.Tensor]] = []
         for b in ddp.buckets:
             master = b.param_flat.detach().float().clone()
-            self.state.append({"master": master, "exp_avg": torch.zeros_like(master),
-                               "exp_avg_sq": torch.zeros_like(master)})
+            self.flat_state.append({"master": master, "exp_avg": torch.zeros_like(master),
+                                    "exp_avg_sq": torch.zeros_like(master)})
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -37,7 +40,7 @@ class FlatAdamW:
         g = self.param_groups[0]
         self.step_count += 1
         b1, b2 = g["betas"]
-        for b, st in zip(self.ddp.buckets, self.state):
+        for b, st in zip(self.ddp.buckets, self.flat_state):
             ops.adamw_flat(b.buffer, b.param_flat, st["master"], st["exp_avg"], st["exp_avg_sq"], g["lr"], b1, b2,
                            g["eps"], g["weight_decay"], self.step_count, grad_scale_t=self._clip_coef)
         self._clip_coef = None
@@ -63,13 +66,14 @@ class FlatAdamW:
 
     def state_dict(self) -> Dict[str, Any]:
         return {"step": self.step_count, "param_groups": [{k: v for k, v in self.param_groups[0].items() if k != "params"}],
-                "buckets": [{k: v for k, v in st.items()} for st in self.state]}
+                "buckets": [{k: v for k, v in st.items()} for st in self.flat_state]}
 
+    @torch.no_grad()
     def load_state_dict(self, sd: Dict[str, Any]) -> None:
         self.step_count = int(sd["step"])
         self.param_groups[0].update(sd["param_groups"][0])
-        for st, src in zip(self.state, sd["buckets"]):
+        for st, src in zip(self.flat_state, sd["buckets"]):
             for k in st:
                 st[k].copy_(src[k])
-        for b, st in zip(self.ddp.buckets, self.state):
+        for b, st in zip(self.ddp.buckets, self.flat_state):
             b.param_flat.copy_(st["master"].to(b.param_flat.dtype))

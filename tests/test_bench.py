@@ -34,6 +34,13 @@ def test_ddp_phase_multi_rank(sess):
     assert r["torch_ddp_ms_per_step"] > 0 and r["linear4096"]["ms_per_step"] > 0
 
 
+def test_notebook_phase_multi_rank(sess):
+    r = B.bench_notebook(sess, steps=2, warmup=1, small=True)
+    for mode in ("reference", "nbd"):
+        assert r[mode]["ms_per_step"] > 0 and r[mode]["samples_per_s"] > 0
+    assert r["reference_ms_per_step"] == 126.6
+
+
 def test_rank_broadcast_phase_multi_rank(sess):
     r = B.bench_rank_broadcast(sess, dim=128, iters=3, warm=1)
     assert r["correct"], r

@@ -97,7 +97,7 @@ sd = opt.state_dict()
 opt2 = FlatAdamW(ours, lr=1.0)
 opt2.load_state_dict(sd)
 (opt2.step_count == opt.step_count, opt2.param_groups[0]["lr"] == 3e-3,
- all(torch.equal(a["exp_avg"], b["exp_avg"]) for a, b in zip(opt.state, opt2.state)))
+ all(torch.equal(a["exp_avg"], b["exp_avg"]) for a, b in zip(opt.flat_state, opt2.flat_state)))
 """
 
 
@@ -120,6 +120,14 @@ def test_flat_adamw_ddp_matches_torch_ddp_adamw(sess):
         assert r.results[rank]["output"] == "(True, True, True, 4)", r.results[rank]
     r = sess.execute(STATE, render=False)
     assert r.results[0]["output"] == "(True, True, True)", r.results[0]
+
+
+def test_flat_adamw_drives_lr_scheduler(sess):
+    code = ("sch = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 0.5)\n"
+            "sch.step()\n"
+            "(isinstance(opt, torch.optim.Optimizer), opt.param_groups[0]['lr'])")
+    r = sess.execute(code, render=False)
+    assert r.results[0]["echo"] == "(True, 0.0015)", r.results[0]
 
 
 def test_flat_adamw_requires_bucket_mode(sess):
