@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--warm", type=int, default=3)
     ap.add_argument("--B", type=int, default=8)
     ap.add_argument("--T", type=int, default=1024)
-    ap.add_argument("--impls", default="none,torch,nbd,nbd32,flat")
+    ap.add_argument("--impls", default="none,torch,nbd,nbd32,flat,flatgraph")
     ap.add_argument("--clip", type=float, default=0.0, help="clip_grad_norm_ max norm (0: off)")
     ap.add_argument("--backend", default="rccl")
     a = ap.parse_args()
@@ -52,12 +52,12 @@ def main():
     for impl in a.impls.split(","):
         m = copy.deepcopy(base)
         amp = True
-        if impl == "flat":
+        if impl in ("flat", "flatgraph"):
             # bf16 parameters re-homed into the DDP buckets, fp32 master/moments inside FlatAdamW,
             # one fused HIP AdamW kernel per bucket; no autocast casts in the forward
             m = m.to(torch.bfloat16)
             w = NbdDDP(m, flat_params=True, grad_mode="bucket")
-            models[impl] = (w, FlatAdamW(w, lr=3e-4), False)
+            models[impl] = (w, FlatAdamW(w, lr=3e-4, capturable=impl == "flatgraph"), False)
             continue
         if impl == "torch":
             w = torch.nn.parallel.DistributedDataParallel(m, device_ids=[local])
@@ -70,9 +70,10 @@ def main():
         opt = torch.optim.AdamW(m.parameters(), lr=3e-4, fused=True)
         models[impl] = (w, opt, amp)
 
-    def step(w, opt, amp):
+    def step(w, opt, amp, inp=None):
+        inp = x if inp is None else inp
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
-            _, loss = w(x, x, return_logits=False)
+            _, loss = w(inp, inp, return_logits=False)
         loss.backward()
         if a.clip > 0:
             if isinstance(opt, FlatAdamW):
@@ -81,18 +82,30 @@ def main():
                 torch.nn.utils.clip_grad_norm_(w.parameters(), a.clip)
         opt.step()
         opt.zero_grad(set_to_none=True)
-        return loss
+        return loss.detach()
+
+    graphs = {}
+    if "flatgraph" in models:
+        from nbdistributed_amd.graphs import GraphedStep
+
+        w, opt, amp = models["flatgraph"]
+        graphs["flatgraph"] = GraphedStep(lambda xx: step(w, opt, amp, xx), (x,), warmup=3, optimizers=[opt])
+
+    def run(k, w, opt, amp):
+        if k in graphs:
+            return graphs[k](x)
+        return step(w, opt, amp)
 
     res = {k: [] for k in models}
     losses = {}
     for r in range(a.rounds):
         for k, (w, opt, amp) in models.items():
             for _ in range(a.warm):
-                step(w, opt, amp)
+                run(k, w, opt, amp)
             torch.cuda.synchronize()
             t = time.perf_counter()
             for _ in range(a.steps):
-                loss = step(w, opt, amp)
+                loss = run(k, w, opt, amp)
             torch.cuda.synchronize()
             res[k].append((time.perf_counter() - t) / a.steps * 1e3)
             losses[k] = float(loss.detach())

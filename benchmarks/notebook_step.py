@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""The reference notebook's training step (SmolLM2-135M sequence classifier, bs 16, seq 128)
+in one process on one GPU, in several recipes, for profiling:
+
+    python benchmarks/notebook_step.py [--modes fp32,bf16flat,graph] [--steps 20]
+
+fp32      : fp32 params, torch AdamW (the notebook's recipe, minus accelerate/DDP wrappers)
+bf16flat  : bf16 params in nbd DDP buckets (world 1) + FlatAdamW
+graph     : bf16flat captured once into a HIP graph (nbdistributed_amd.graphs) and replayed
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--modes", default="fp32,bf16flat")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warm", type=int, default=5)
+    ap.add_argument("--bs", type=int, default=16)
+    ap.add_argument("--seq", type=int, default=128)
+    a = ap.parse_args()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29541")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from nbdistributed_amd.parallel.backend import init_data_plane
+
+    init_data_plane("rccl", 0, 1, dev)
+    from nbdistributed_amd.models import smollm2_135m_classifier, synthetic_mrpc
+    from nbdistributed_amd.optim import FlatAdamW
+    from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP
+
+    ids, mask, labels = synthetic_mrpc(n=a.bs * 8, seq_len=a.seq)
+    ids, mask, labels = ids.to(dev), mask.to(dev), labels.to(dev)
+    for mode in a.modes.split(","):
+        torch.manual_seed(42)
+        model = smollm2_135m_classifier()
+        if mode == "fp32":
+            model = model.to(dev)
+            opt = torch.optim.AdamW(model.parameters(), lr=2e-5)
+            fwd = model
+        else:
+            fwd = NbdDDP(model.to(dev, torch.bfloat16), flat_params=True, grad_mode="bucket")
+            opt = FlatAdamW(fwd, lr=2e-5)
+        batches = [(ids[i * a.bs:(i + 1) * a.bs], mask[i * a.bs:(i + 1) * a.bs], labels[i * a.bs:(i + 1) * a.bs])
+                   for i in range(8)]
+
+        def step(x, m, y):
+            loss = fwd(input_ids=x, attention_mask=m, labels=y).loss
+            loss.backward()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            return loss.detach()
+
+        if mode == "graph":
+            from nbdistributed_amd.graphs import GraphedStep
+
+            runner = GraphedStep(step, batches[0], warmup=3)
+            call = runner
+        else:
+            call = step
+        for i in range(a.warm):
+            call(*batches[i % 8])
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for i in range(a.steps):
+            loss = call(*batches[i % 8])
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t) / a.steps * 1e3
+        print(f"{mode:9s} {ms:8.2f} ms/step  {a.bs / ms * 1e3:8.1f} samples/s  loss {float(loss):.4f}", flush=True)
+        del model, opt, fwd
+        torch.cuda.empty_cache()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -15,8 +15,9 @@ TORCH_LIBRARY(nbd, m) {
   m.def("ln_fwd(Tensor x, Tensor? delta, Tensor weight, Tensor bias, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("ln_bwd(Tensor x, Tensor dy, Tensor? dres, Tensor weight, Tensor mean, Tensor rstd) -> (Tensor, Tensor, Tensor)");
   m.def("colsum(Tensor x, ScalarType dtype) -> Tensor");
+  m.def("embedding_bwd(Tensor dy, Tensor idx, int V) -> Tensor");
   m.def("xent_fwd(Tensor logits, Tensor target, int ignore_index) -> (Tensor, Tensor)");
   m.def("xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor scale, int ignore_index, Tensor(a!) dlogits) -> ()");
   m.def("adamw_flat(Tensor grad, Tensor(a!) param, Tensor(b!) master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "
-        "float lr, float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, Tensor? grad_scale_t=None) -> ()");
+        "float lr, float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, Tensor? grad_scale_t=None, Tensor? step_t=None, Tensor? lr_t=None) -> ()");
 }

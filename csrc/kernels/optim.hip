@@ -31,15 +31,31 @@
 namespace nbd {
 
 struct AdamArgs {
-  float lr, beta1, beta2, eps, wd_factor, step_size, inv_sqrt_bc2, grad_scale;
+  float lr, beta1, beta2, eps, wd_factor, step_size, inv_sqrt_bc2, grad_scale, weight_decay;
 };
+
+// capturable mode (HIP graphs): step and lr come from device memory, so a replayed graph sees the
+// current values; the bias corrections are recomputed per thread (two powf per thread)
+__device__ __forceinline__ void device_hyper(AdamArgs& a, const float* dstep, const float* dlr) {
+  if (dlr != nullptr) {
+    a.lr = *dlr;
+    a.wd_factor = 1.f - a.lr * a.weight_decay;
+  }
+  if (dstep != nullptr) {
+    const float t = *dstep;
+    a.step_size = a.lr / (1.f - powf(a.beta1, t));
+    a.inv_sqrt_bc2 = rsqrtf(1.f - powf(a.beta2, t));
+  }
+}
 
 template <typename G, typename P>
 __global__ __launch_bounds__(256) void adamw_flat_kernel(const G* __restrict__ grad, P* __restrict__ param,
                                                          float* __restrict__ master, float* __restrict__ m,
                                                          float* __restrict__ v, const float* __restrict__ gscale,
-                                                         int64_t n, AdamArgs a) {
+                                                         const float* __restrict__ dstep,
+                                                         const float* __restrict__ dlr, int64_t n, AdamArgs a) {
   if (gscale != nullptr) a.grad_scale *= *gscale;  // device-side clip coefficient (no host sync)
+  device_hyper(a, dstep, dlr);
   const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t nth = (int64_t)gridDim.x * 256;
   const int64_t nv = n / 8;
@@ -79,24 +95,24 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(const G* __restrict__ g
 
 template <typename G, typename P>
 static void launch_adamw(const at::Tensor& grad, const at::Tensor& param, const at::Tensor& master,
-                         const at::Tensor& m, const at::Tensor& v, const float* gs, int64_t n, const AdamArgs& a,
-                         hipStream_t st) {
+                         const at::Tensor& m, const at::Tensor& v, const float* gs, const float* dstep,
+                         const float* dlr, int64_t n, const AdamArgs& a, hipStream_t st) {
   const int64_t work = (n + 7) / 8;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 256 * 8));
   hipLaunchKernelGGL((adamw_flat_kernel<G, P>), dim3((unsigned)blocks), dim3(256), 0, st,
                      static_cast<const G*>(grad.data_ptr()), static_cast<P*>(param.data_ptr()),
-                     master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), gs, n, a);
+                     master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), gs, dstep, dlr, n, a);
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
 template <typename G>
 static void dispatch_param(const at::Tensor& grad, const at::Tensor& param, const at::Tensor& master,
-                           const at::Tensor& m, const at::Tensor& v, const float* gs, int64_t n, const AdamArgs& a,
-                           hipStream_t st) {
+                           const at::Tensor& m, const at::Tensor& v, const float* gs, const float* dstep,
+                           const float* dlr, int64_t n, const AdamArgs& a, hipStream_t st) {
   switch (param.scalar_type()) {
-    case at::kFloat: launch_adamw<G, float>(grad, param, master, m, v, gs, n, a, st); break;
-    case at::kBFloat16: launch_adamw<G, bf16_t>(grad, param, master, m, v, gs, n, a, st); break;
-    case at::kHalf: launch_adamw<G, f16_t>(grad, param, master, m, v, gs, n, a, st); break;
+    case at::kFloat: launch_adamw<G, float>(grad, param, master, m, v, gs, dstep, dlr, n, a, st); break;
+    case at::kBFloat16: launch_adamw<G, bf16_t>(grad, param, master, m, v, gs, dstep, dlr, n, a, st); break;
+    case at::kHalf: launch_adamw<G, f16_t>(grad, param, master, m, v, gs, dstep, dlr, n, a, st); break;
     default: TORCH_CHECK(false, "adamw_flat: unsupported param dtype ", param.scalar_type());
   }
 }
@@ -104,7 +120,8 @@ static void dispatch_param(const at::Tensor& grad, const at::Tensor& param, cons
 void adamw_flat_hip(const at::Tensor& grad, const at::Tensor& param, const at::Tensor& master, const at::Tensor& exp_avg,
                     const at::Tensor& exp_avg_sq, double lr, double beta1, double beta2, double eps,
                     double weight_decay, int64_t step, double grad_scale,
-                    const c10::optional<at::Tensor>& grad_scale_t) {
+                    const c10::optional<at::Tensor>& grad_scale_t, const c10::optional<at::Tensor>& step_t,
+                    const c10::optional<at::Tensor>& lr_t) {
   TORCH_CHECK(grad.is_cuda() && param.is_cuda() && master.is_cuda() && exp_avg.is_cuda() && exp_avg_sq.is_cuda(),
               "adamw_flat: GPU tensors expected");
   TORCH_CHECK(grad.is_contiguous() && param.is_contiguous() && master.is_contiguous() && exp_avg.is_contiguous() &&
@@ -125,9 +142,19 @@ void adamw_flat_hip(const at::Tensor& grad, const at::Tensor& param, const at::T
                 "adamw_flat: grad_scale_t must be a 1-element float32 GPU tensor");
     gs = grad_scale_t->data_ptr<float>();
   }
+  auto dev_scalar = [&](const c10::optional<at::Tensor>& t, const char* name) -> const float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() == 1, "adamw_flat: ", name,
+                " must be a 1-element float32 GPU tensor");
+    return t->data_ptr<float>();
+  };
+  const float* dstep = dev_scalar(step_t, "step_t");
+  const float* dlr = dev_scalar(lr_t, "lr_t");
+  TORCH_CHECK((dstep == nullptr) == (dlr == nullptr), "adamw_flat: step_t and lr_t go together (capturable mode)");
   if (n == 0) return;
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(param.device());
   AdamArgs a;
+  a.weight_decay = (float)weight_decay;
   a.lr = (float)lr;
   a.beta1 = (float)beta1;
   a.beta2 = (float)beta2;
@@ -140,9 +167,9 @@ void adamw_flat_hip(const at::Tensor& grad, const at::Tensor& param, const at::T
   a.grad_scale = (float)grad_scale;
   hipStream_t stream = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   switch (grad.scalar_type()) {
-    case at::kFloat: dispatch_param<float>(grad, param, master, exp_avg, exp_avg_sq, gs, n, a, stream); break;
-    case at::kBFloat16: dispatch_param<bf16_t>(grad, param, master, exp_avg, exp_avg_sq, gs, n, a, stream); break;
-    case at::kHalf: dispatch_param<f16_t>(grad, param, master, exp_avg, exp_avg_sq, gs, n, a, stream); break;
+    case at::kFloat: dispatch_param<float>(grad, param, master, exp_avg, exp_avg_sq, gs, dstep, dlr, n, a, stream); break;
+    case at::kBFloat16: dispatch_param<bf16_t>(grad, param, master, exp_avg, exp_avg_sq, gs, dstep, dlr, n, a, stream); break;
+    case at::kHalf: dispatch_param<f16_t>(grad, param, master, exp_avg, exp_avg_sq, gs, dstep, dlr, n, a, stream); break;
     default: TORCH_CHECK(false, "adamw_flat: unsupported grad dtype ", grad.scalar_type());
   }
 }

@@ -1,0 +1,89 @@
+"""HIP graphs for whole training steps — the MI355X answer to launch-bound cells.
+
+A small-batch step of a deep model is thousands of short kernels (SmolLM2-135M at batch 16 x 128:
+≈4,600 launches, GPU busy 25 ms of a 40 ms eager step: ``profiles/notebook_prof_r1.md``).
+:class:`GraphedStep` records one step — forward, backward, the DDP bucket pipeline (flatten
+kernels, RCCL all-reduce on the side stream, stream joins) and the optimizer — into a HIP graph
+once, then replays it: one launch per step, no Python or per-kernel launch cost.
+
+Requirements (checked by construction, as for any CUDA/HIP graph):
+* static shapes; inputs are copied into the graph's static tensors on each call;
+* no host synchronisation inside the step (``.item()``, ``print(tensor)``, data-dependent
+  Python control flow);
+* optimizers that keep step/lr on the device: ``FlatAdamW(..., capturable=True)`` or
+  ``torch.optim.AdamW(..., capturable=True)``; ``sync_hyper()`` (FlatAdamW) is called before
+  each replay so LR schedulers keep working.
+"""
+from __future__ import annotations
+
+from typing import Any, Callable, Iterable, Sequence
+
+import torch
+
+
+def _clone_static(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach().clone()
+    return x
+
+
+def _copy_into(dst, src):
+    if isinstance(dst, torch.Tensor):
+        if src.shape != dst.shape or src.dtype != dst.dtype:
+            raise ValueError(f"GraphedStep: input {tuple(src.shape)}/{src.dtype} does not match the captured "
+                             f"{tuple(dst.shape)}/{dst.dtype}")
+        dst.copy_(src, non_blocking=True)
+    elif dst is not src and dst != src:
+        raise ValueError("GraphedStep: non-tensor arguments are baked into the graph and must not change")
+
+
+class GraphedStep:
+    """``step = GraphedStep(fn, example_args, optimizers=[opt])``; ``out = step(*args)``.
+
+    ``fn(*args)`` runs ``warmup`` times eagerly on a side stream (allocator and library
+    warm-up, DDP bucket state), is captured once, and every call replays the graph after
+    copying ``args`` into the static inputs.  Returns the captured output tensors (overwritten
+    by the next replay — clone what you keep).
+    """
+
+    def __init__(self, fn: Callable[..., Any], example_args: Sequence[Any], warmup: int = 3,
+                 optimizers: Iterable[Any] = (), pool=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("GraphedStep needs a GPU")
+        self.fn = fn
+        self.optimizers = list(optimizers)
+        self.static_args = [_clone_static(a) for a in example_args]
+        self.replays = 0
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                self._sync_hyper()
+                fn(*self.static_args)
+        cur.wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        self._sync_hyper()
+        with torch.cuda.graph(self.graph, pool=pool):
+            self.static_out = fn(*self.static_args)
+        torch.cuda.synchronize()
+
+    def _sync_hyper(self) -> None:
+        for o in self.optimizers:
+            sync = getattr(o, "sync_hyper", None)
+            if sync is not None:
+                sync()
+
+    def __call__(self, *args):
+        if len(args) != len(self.static_args):
+            raise ValueError(f"GraphedStep: expected {len(self.static_args)} arguments, got {len(args)}")
+        for dst, src in zip(self.static_args, args):
+            _copy_into(dst, src)
+        self._sync_hyper()
+        self.graph.replay()
+        self.replays += 1
+        return self.static_out
+
+
+__all__ = ["GraphedStep"]

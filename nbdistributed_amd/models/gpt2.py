@@ -139,6 +139,11 @@ class GPT2(nn.Module):
                 and x.dtype in (torch.bfloat16, torch.float16) and c.n_embd % 8 == 0 and c.n_embd <= 2048
                 and x.shape[1] % 128 == 0)
 
+    def _fast_ok(self, idx: torch.Tensor) -> bool:
+        c = self.config
+        return (c.fused_norm and idx.is_cuda and not torch.is_autocast_enabled()
+                and self.wte.weight.dtype in (torch.bfloat16, torch.float16))
+
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
@@ -147,7 +152,12 @@ class GPT2(nn.Module):
         not returned (None) and the fused loss writes its gradient over their storage."""
         B, T = idx.shape
         pos = torch.arange(T, device=idx.device)
-        x = self.wte(idx) + self.wpe(pos)
+        if self._fast_ok(idx):
+            from .. import ops
+
+            x = ops.embedding(idx, self.wte.weight) + ops.embedding(pos, self.wpe.weight)
+        else:
+            x = self.wte(idx) + self.wpe(pos)
         if self._fast(x):
             # residual stream through the HIP add+LayerNorm kernels: each block's two residual adds
             # are fused with the LayerNorm that follows them (ln_2, then the next block's ln_1 / ln_f)

@@ -16,6 +16,7 @@ flash_attention (K7)   QKᵀ→online softmax→PV fwd; FA2 dK/dV + dQ bwd    at
 add_layer_norm (K8)    residual add + LayerNorm fwd; LN bwd + residual   norm.hip
                        grad + dγ/dβ column partials
 colsum / linear (K9)   bias gradient column sums                        norm.hip
+embedding (K10)        counting-sort embedding backward (graph-safe)     embed.hip
 =====================  ==============================================  =========================
 
 GPU tensors always go to the HIP kernels; if ``libnbd_ops.so`` cannot be loaded on a GPU box the
@@ -190,9 +191,12 @@ def local_prereduce(inputs: Sequence, out=None, scale: float = 1.0, dtype=None):
     return out
 
 
-def _ref_adamw(grad, param, master, m, v, lr, beta1, beta2, eps, wd, step, grad_scale, grad_scale_t=None):
+def _ref_adamw(grad, param, master, m, v, lr, beta1, beta2, eps, wd, step, grad_scale, grad_scale_t=None,
+               step_t=None, lr_t=None):
     import math
 
+    if step_t is not None:
+        step, lr = float(step_t.reshape(())), float(lr_t.reshape(()))
     n = param.numel()
     g = grad.reshape(-1)[:n].float() * grad_scale
     if grad_scale_t is not None:
@@ -208,20 +212,23 @@ def _ref_adamw(grad, param, master, m, v, lr, beta1, beta2, eps, wd, step, grad_
 
 
 def adamw_flat(grad, param, master, exp_avg, exp_avg_sq, lr: float, beta1: float, beta2: float, eps: float,
-               weight_decay: float, step: int, grad_scale: float = 1.0, grad_scale_t=None) -> None:
+               weight_decay: float, step: int, grad_scale: float = 1.0, grad_scale_t=None, step_t=None,
+               lr_t=None) -> None:
     """One fused AdamW step over flat buffers (see csrc/kernels/optim.hip): fp32 master weights
     and moments, ``param`` (any float dtype) rewritten from the master copy.  The gradient is
     multiplied by ``grad_scale`` and, if given, by the 1-element device tensor ``grad_scale_t``
-    (a clip coefficient computed on the GPU — no host sync)."""
+    (a clip coefficient computed on the GPU — no host sync).  ``step_t``/``lr_t`` (1-element
+    float32 device tensors, together) override ``step``/``lr`` for HIP-graph replay."""
     import torch
 
     if param.is_cuda:
         _require()
         torch.ops.nbd.adamw_flat(grad, param, master, exp_avg, exp_avg_sq, float(lr), float(beta1), float(beta2),
-                                 float(eps), float(weight_decay), int(step), float(grad_scale), grad_scale_t)
+                                 float(eps), float(weight_decay), int(step), float(grad_scale), grad_scale_t,
+                                 step_t, lr_t)
     else:
         _ref_adamw(grad, param, master, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step, grad_scale,
-                   grad_scale_t)
+                   grad_scale_t, step_t, lr_t)
 
 
 _XentFn = None
@@ -452,6 +459,47 @@ def _norm_fns():
     return _NormFns
 
 
+_EmbFn = None
+
+
+def _emb_fn():
+    global _EmbFn
+    if _EmbFn is None:
+        import torch
+
+        class _Embedding(torch.autograd.Function):
+            @staticmethod
+            def forward(ctx, idx, weight):
+                ctx.save_for_backward(idx)
+                ctx.V = weight.shape[0]
+                return torch.nn.functional.embedding(idx, weight)
+
+            @staticmethod
+            def backward(ctx, dy):
+                (idx,) = ctx.saved_tensors
+                C = dy.shape[-1]
+                dy2 = dy.reshape(-1, C)
+                dy2 = dy2 if dy2.is_contiguous() else dy2.contiguous()
+                return None, torch.ops.nbd.embedding_bwd(dy2, idx.reshape(-1).contiguous(), ctx.V)
+
+        _EmbFn = _Embedding
+    return _EmbFn
+
+
+def embedding(idx, weight):
+    """``F.embedding`` whose weight gradient comes from the HIP counting-sort kernels
+    (``csrc/kernels/embed.hip``): deterministic launch shapes and caching-allocator memory only,
+    so a step containing it can be captured in a HIP graph (torch's sort/unique path cannot)."""
+    import torch
+
+    C = weight.shape[-1]
+    if (weight.is_cuda and idx.dtype == torch.int64 and C % 4 == 0 and C <= 4096 and weight.requires_grad
+            and weight.dtype in (torch.bfloat16, torch.float16, torch.float32)):
+        _require()
+        return _emb_fn().apply(idx, weight)
+    return torch.nn.functional.embedding(idx, weight)
+
+
 def _norm_ok(x, C: int) -> bool:
     import torch
 
@@ -550,5 +598,5 @@ def tensor_summary_text(x) -> str:
 
 __all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "cross_entropy",
            "flash_attention", "attention_qkv", "flash_supported", "layer_norm", "add_layer_norm", "linear",
-           "colsum", "tensor_summary", "tensor_summary_text",
+           "colsum", "embedding", "tensor_summary", "tensor_summary_text",
            "tensor_summary_raw", "plan_offsets", "native_available", "load_library", "SUMMARY_FIELDS"]

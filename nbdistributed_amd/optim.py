@@ -15,19 +15,31 @@ import torch
 from . import ops
 
 
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 class FlatAdamW(torch.optim.Optimizer):
     """A ``torch.optim.Optimizer`` (so LR schedulers and hooks work) whose state lives per DDP
     bucket: ``flat_state[i]`` = fp32 master / exp_avg / exp_avg_sq of bucket i.  One param group
     (the bucket kernels apply one lr / weight decay to the whole model)."""
 
     def __init__(self, ddp, lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 1e-2):
+                 weight_decay: float = 1e-2, capturable: bool = False):
+        """``capturable=True``: the step counter and lr live in device memory (``step_t``,
+        ``lr_t``) so the update can be captured in a HIP graph and replayed
+        (:class:`nbdistributed_amd.graphs.GraphedStep` calls :meth:`sync_hyper` before each
+        replay to push the current ``param_groups[0]['lr']``)."""
         if not getattr(ddp, "flat_params", False) or ddp.grad_mode != "bucket":
             raise ValueError("FlatAdamW needs DistributedDataParallel(..., flat_params=True, grad_mode='bucket')")
         super().__init__(list(ddp.params), dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.ddp = ddp
         self.step_count = 0
         self._clip_coef = None
+        self.capturable = capturable
+        dev = ddp.buckets[0].param_flat.device
+        self.step_t = torch.zeros(1, dtype=torch.float32, device=dev) if capturable else None
+        self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev) if capturable else None
         self.flat_state: List[Dict[str, torch.Tensor]] = []
         for b in ddp.buckets:
             master = b.param_flat.detach().float().clone()
@@ -40,11 +52,21 @@ class FlatAdamW(torch.optim.Optimizer):
         g = self.param_groups[0]
         self.step_count += 1
         b1, b2 = g["betas"]
+        if self.capturable:
+            self.step_t.add_(1.0)
+            if not _capturing():
+                self.lr_t.fill_(float(g["lr"]))
         for b, st in zip(self.ddp.buckets, self.flat_state):
             ops.adamw_flat(b.buffer, b.param_flat, st["master"], st["exp_avg"], st["exp_avg_sq"], g["lr"], b1, b2,
-                           g["eps"], g["weight_decay"], self.step_count, grad_scale_t=self._clip_coef)
+                           g["eps"], g["weight_decay"], max(self.step_count, 1), grad_scale_t=self._clip_coef,
+                           step_t=self.step_t, lr_t=self.lr_t)
         self._clip_coef = None
         return loss
+
+    def sync_hyper(self) -> None:
+        """Push the host-side lr (LR schedulers) into ``lr_t`` — call outside graph capture."""
+        if self.capturable:
+            self.lr_t.fill_(float(self.param_groups[0]["lr"]))
 
     @torch.no_grad()
     def clip_grad_norm_(self, max_norm: float, eps: float = 1e-6) -> torch.Tensor:
@@ -65,12 +87,15 @@ class FlatAdamW(torch.optim.Optimizer):
             p.grad = None
 
     def state_dict(self) -> Dict[str, Any]:
-        return {"step": self.step_count, "param_groups": [{k: v for k, v in self.param_groups[0].items() if k != "params"}],
+        step = int(self.step_t.item()) if self.capturable else self.step_count
+        return {"step": step, "param_groups": [{k: v for k, v in self.param_groups[0].items() if k != "params"}],
                 "buckets": [{k: v for k, v in st.items()} for st in self.flat_state]}
 
     @torch.no_grad()
     def load_state_dict(self, sd: Dict[str, Any]) -> None:
         self.step_count = int(sd["step"])
+        if self.capturable:
+            self.step_t.fill_(float(self.step_count))
         self.param_groups[0].update(sd["param_groups"][0])
         for st, src in zip(self.flat_state, sd["buckets"]):
             for k in st:

@@ -79,6 +79,8 @@ class DistributedDataParallel(torch.nn.Module):
         self.flat_params = flat_params
         self._require_sync = True
         self._in_backward = False
+        self._capturing = False
+        self._side = False
         self._next_launch = 0
         import os
 
@@ -162,6 +164,12 @@ class DistributedDataParallel(torch.nn.Module):
     def _start_backward(self) -> None:
         self._in_backward = True
         self._next_launch = 0
+        # Under HIP-graph capture the collectives are issued from the capturing stream itself
+        # (ProcessGroupNCCL's own stream becomes a parallel branch of the graph) and every wait
+        # is deferred to the end of backward: forking RCCL work off a second user stream inside
+        # a capture crashes hipStreamEndCapture on this stack (benchmarks/graph_probe.py "side").
+        self._capturing = self.cuda and torch.cuda.is_current_stream_capturing()
+        self._side = self.comm_stream is not None and not self._capturing
         for b in self.buckets:
             b.pending = len(b.params)
             b.ready = b.launched = False
@@ -197,12 +205,16 @@ class DistributedDataParallel(torch.nn.Module):
         b.grads = grads
         scale = 1.0 / self.world
         unflatten = self.grad_mode == "unflatten"
-        if self.cuda and self.comm_stream is None:
+        if self.cuda and self._capturing:
+            ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
+            b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)  # waited in _finalize
+        elif self.cuda and not self._side:
             ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
             b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)
             b.work.wait()
             if unflatten:
                 ops.bucket_unflatten(b.buffer, grads, b.offsets)
+            b.work = None
         elif self.cuda:
             cur = torch.cuda.current_stream(self.device)
             self.comm_stream.wait_stream(cur)  # the grads were produced on the compute stream
@@ -232,7 +244,7 @@ class DistributedDataParallel(torch.nn.Module):
             if not b.ready:
                 b.ready = True
         self._launch_ready()
-        if self.cuda and self.comm_stream is not None:
+        if self.cuda and self._side:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
         else:
             for b in self.buckets:

@@ -95,3 +95,18 @@ def test_gpt2_fused_path_matches_reference(dev):
     for n, p in m1.named_parameters():
         q = dict(m2.named_parameters())[n]
         assert _rel(p.grad, q.grad) < 6e-2, n
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("V,C,N", [(50257, 768, 8192), (1024, 256, 512), (7, 64, 1000), (33, 4096, 5)])
+def test_embedding_backward(dev, dt, V, C, N):
+    g = torch.Generator(device="cpu").manual_seed(V + N)
+    idx = torch.randint(0, V, (N,), generator=g)
+    idx[: N // 4] = idx[0]  # one heavily repeated id
+    w = torch.randn(V, C, generator=g).to(dev, dt).requires_grad_(True)
+    dy = torch.randn(N, C, generator=g).to(dev, dt)
+    ops.embedding(idx.to(dev), w).backward(dy)
+    ref = torch.zeros(V, C, dtype=torch.float32).index_add_(0, idx, dy.float().cpu())
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-5
+    assert w.grad.dtype == dt
+    assert torch.allclose(w.grad.float().cpu(), ref, atol=tol * (1 + float(ref.abs().max()) * 0.1), rtol=tol)
