@@ -4,9 +4,10 @@ in one process on one GPU, in several recipes, for profiling:
 
     python benchmarks/notebook_step.py [--modes fp32,bf16flat,graph] [--steps 20]
 
-fp32      : fp32 params, torch AdamW (the notebook's recipe, minus accelerate/DDP wrappers)
-bf16flat  : bf16 params in nbd DDP buckets (world 1) + FlatAdamW
-graph     : bf16flat captured once into a HIP graph (nbdistributed_amd.graphs) and replayed
+fp32      : HF model, fp32 params, torch AdamW (the notebook's recipe, minus accelerate/DDP wrappers)
+bf16flat  : HF model, bf16 params in nbd DDP buckets (world 1) + FlatAdamW
+nbd       : native Llama (models/llama.py, HIP kernels), bf16 flat DDP + FlatAdamW
+nbdgraph  : nbd captured once into a HIP graph (nbdistributed_amd.graphs) and replayed
 """
 from __future__ import annotations
 
@@ -44,29 +45,37 @@ def main():
     ids, mask, labels = ids.to(dev), mask.to(dev), labels.to(dev)
     for mode in a.modes.split(","):
         torch.manual_seed(42)
-        model = smollm2_135m_classifier()
+        native = mode in ("nbd", "nbdgraph")
+        if native:
+            from nbdistributed_amd.models.llama import LlamaConfig, LlamaForSequenceClassification
+
+            model = LlamaForSequenceClassification(LlamaConfig.smollm2_135m())
+        else:
+            model = smollm2_135m_classifier()
         if mode == "fp32":
             model = model.to(dev)
             opt = torch.optim.AdamW(model.parameters(), lr=2e-5)
             fwd = model
         else:
             fwd = NbdDDP(model.to(dev, torch.bfloat16), flat_params=True, grad_mode="bucket")
-            opt = FlatAdamW(fwd, lr=2e-5)
+            opt = FlatAdamW(fwd, lr=2e-5, capturable=mode == "nbdgraph")
         batches = [(ids[i * a.bs:(i + 1) * a.bs], mask[i * a.bs:(i + 1) * a.bs], labels[i * a.bs:(i + 1) * a.bs])
                    for i in range(8)]
 
         def step(x, m, y):
-            loss = fwd(input_ids=x, attention_mask=m, labels=y).loss
+            if native:
+                loss = fwd(x, m, y)[0]
+            else:
+                loss = fwd(input_ids=x, attention_mask=m, labels=y).loss
             loss.backward()
             opt.step()
             opt.zero_grad(set_to_none=True)
             return loss.detach()
 
-        if mode == "graph":
+        if mode == "nbdgraph":
             from nbdistributed_amd.graphs import GraphedStep
 
-            runner = GraphedStep(step, batches[0], warmup=3)
-            call = runner
+            call = GraphedStep(step, batches[0], warmup=3, optimizers=[opt])
         else:
             call = step
         for i in range(a.warm):
@@ -77,7 +86,8 @@ def main():
             loss = call(*batches[i % 8])
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t) / a.steps * 1e3
-        print(f"{mode:9s} {ms:8.2f} ms/step  {a.bs / ms * 1e3:8.1f} samples/s  loss {float(loss):.4f}", flush=True)
+        print(f"{mode:9s} {ms:8.2f} ms/step  {a.bs / ms * 1e3:8.1f} samples/s  loss {float(loss.detach()):.4f}",
+              flush=True)
         del model, opt, fwd
         torch.cuda.empty_cache()
     dist.destroy_process_group()

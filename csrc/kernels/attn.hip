@@ -23,6 +23,8 @@
 //   dq    one workgroup = 128 queries, wave = 32 queries on the lane; sweeps 64-key tiles:
 //         S^T = K·Q^T, dP^T = V·dO^T, dS^T = P^T(dP^T − δ), dQ^T += K^T·dS^T.
 // Causal: workgroups are launched heaviest-first; fully masked tiles are skipped per wave.
+// GQA: query head h reads key/value head h / group; dkdv runs per key/value head and sweeps its
+// group of query heads, accumulating dK/dV in the same registers (no atomics).
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -125,7 +127,7 @@ struct Stage2 {
 // ============================================================================ forward
 template <bool CAUSAL>
 __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MView o, float* __restrict__ lse,
-                                                     int H, int T, int nblk, float sc2) {
+                                                     int H, int T, int nblk, float sc2, int group) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[TILE * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[TILE * RSV];
   const int bh = blockIdx.x % (gridDim.x / nblk);
@@ -134,6 +136,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
   const int q0 = qb * BLK + w * 32;  // this wave's first query
   const int qi = q0 + r;             // this lane's query
+  const int kh = hh / group;         // GQA: the key/value head of this query head
   s8v qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qf[s] = ld16(q.row(b, hh, qi) + 16 * s + 8 * h);
@@ -141,15 +144,15 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
   float m = -INFINITY, l = 0.f;
   const int ntiles = CAUSAL ? (qb * BLK + BLK) / TILE : T / TILE;
   Stage2 sk, sv;
-  sk.load(k.row(b, hh, 0), k.st, tid);
-  sv.load(v.row(b, hh, 0), v.st, tid);
+  sk.load(k.row(b, kh, 0), k.st, tid);
+  sv.load(v.row(b, kh, 0), v.st, tid);
   sk.store(Ks, RS, tid);
   sv.store(Vs, RSV, tid);
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     if (t + 1 < ntiles) {  // issue the next tile's loads now, write them after this tile
-      sk.load(k.row(b, hh, (t + 1) * TILE), k.st, tid);
-      sv.load(v.row(b, hh, (t + 1) * TILE), v.st, tid);
+      sk.load(k.row(b, kh, (t + 1) * TILE), k.st, tid);
+      sv.load(v.row(b, kh, (t + 1) * TILE), v.st, tid);
     }
     const int k0 = t * TILE;
     if (!CAUSAL || k0 <= q0 + 31) {
@@ -243,7 +246,8 @@ template <bool CAUSAL>
 __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v, View dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta, MView dk, MView dv, int H,
-                                                          int T, int nblk, float sc2, float scale) {
+                                                          int T, int nblk, float sc2, float scale, int group) {
+  // H = key/value heads (the grid); query heads hq = kvh·group + g, g < group
   __shared__ __attribute__((aligned(16))) uint16_t Qs[TILE * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Os[TILE * RS];  // dO tile
   __shared__ __attribute__((aligned(16))) float Ls[TILE];           // lse * log2(e)
@@ -251,97 +255,102 @@ __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v,
   const int per = gridDim.x / nblk;
   const int bh = blockIdx.x % per;
   const int kb0 = blockIdx.x / per;  // key block; block 0 has the most query tiles under a causal mask
-  const int b = bh / H, hh = bh % H;
+  const int b = bh / H, kvh = bh % H;
+  const int Hq = H * group;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
   const int key0 = kb0 * BLK + w * 32;
   const int ki = key0 + r;  // this lane's key
   s8v kf[4], vf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    kf[s] = ld16(k.row(b, hh, ki) + 16 * s + 8 * h);
-    vf[s] = ld16(v.row(b, hh, ki) + 16 * s + 8 * h);
+    kf[s] = ld16(k.row(b, kvh, ki) + 16 * s + 8 * h);
+    vf[s] = ld16(v.row(b, kvh, ki) + 16 * s + 8 * h);
   }
   f16x dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
   const int t0 = CAUSAL ? (kb0 * BLK) / TILE : 0;
   const int nt = T / TILE;
-  const float* lse_bh = lse + (int64_t)bh * T;
-  const float* del_bh = delta + (int64_t)bh * T;
-  Stage2 sq, so;
-  float lv = 0.f, dlv = 0.f;
-  sq.load(q.row(b, hh, t0 * TILE), q.st, tid);
-  so.load(dout.row(b, hh, t0 * TILE), dout.st, tid);
-  if (tid < TILE) {
-    lv = lse_bh[t0 * TILE + tid] * kLog2e;
-    dlv = del_bh[t0 * TILE + tid];
-  }
-  sq.store(Qs, RS, tid);
-  so.store(Os, RS, tid);
-  if (tid < TILE) {
-    Ls[tid] = lv;
-    Ds[tid] = dlv;
-  }
-  __syncthreads();
-  for (int t = t0; t < nt; ++t) {
-    if (t + 1 < nt) {
-      sq.load(q.row(b, hh, (t + 1) * TILE), q.st, tid);
-      so.load(dout.row(b, hh, (t + 1) * TILE), dout.st, tid);
-      if (tid < TILE) {
-        lv = lse_bh[(t + 1) * TILE + tid] * kLog2e;
-        dlv = del_bh[(t + 1) * TILE + tid];
-      }
+  for (int g = 0; g < group; ++g) {
+    const int hq = kvh * group + g;
+    const float* lse_bh = lse + ((int64_t)b * Hq + hq) * T;
+    const float* del_bh = delta + ((int64_t)b * Hq + hq) * T;
+    Stage2 sq, so;
+    float lv = 0.f, dlv = 0.f;
+    sq.load(q.row(b, hq, t0 * TILE), q.st, tid);
+    so.load(dout.row(b, hq, t0 * TILE), dout.st, tid);
+    if (tid < TILE) {
+      lv = lse_bh[t0 * TILE + tid] * kLog2e;
+      dlv = del_bh[t0 * TILE + tid];
     }
-    const int qt0 = t * TILE;
-    if (!CAUSAL || qt0 + TILE - 1 >= key0) {
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        const int qr0 = qt0 + qb * 32;
-        if (CAUSAL && qr0 + 31 < key0) continue;  // this 32-query block sees none of our keys
-        // S[q][key] = Q . K^T (key on the lane)
-        f16x sacc = zero16(), dp = zero16();
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          sacc = mfma(ld16(Qs + (qb * 32 + r) * RS + 16 * s + 8 * h), kf[s], sacc);
-          dp = mfma(ld16(Os + (qb * 32 + r) * RS + 16 * s + 8 * h), vf[s], dp);
+    if (g > 0) __syncthreads();  // the previous head's last tile is still being read
+    sq.store(Qs, RS, tid);
+    so.store(Os, RS, tid);
+    if (tid < TILE) {
+      Ls[tid] = lv;
+      Ds[tid] = dlv;
+    }
+    __syncthreads();
+    for (int t = t0; t < nt; ++t) {
+      if (t + 1 < nt) {
+        sq.load(q.row(b, hq, (t + 1) * TILE), q.st, tid);
+        so.load(dout.row(b, hq, (t + 1) * TILE), dout.st, tid);
+        if (tid < TILE) {
+          lv = lse_bh[(t + 1) * TILE + tid] * kLog2e;
+          dlv = del_bh[(t + 1) * TILE + tid];
         }
-        const bool diag = CAUSAL && (qr0 < key0 + 31);
+      }
+      const int qt0 = t * TILE;
+      if (!CAUSAL || qt0 + TILE - 1 >= key0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int qrow = qb * 32 + crow(i, h);
-          float p = __builtin_amdgcn_exp2f(sacc[i] * sc2 - Ls[qrow]);
-          if (diag && ki > qt0 + qrow) p = 0.f;
-          sacc[i] = p;                      // P
-          dp[i] = p * (dp[i] - Ds[qrow]);   // dS
-        }
-        // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . dS[q][key]
+        for (int qb = 0; qb < 2; ++qb) {
+          const int qr0 = qt0 + qb * 32;
+          if (CAUSAL && qr0 + 31 < key0) continue;  // this 32-query block sees none of our keys
+          // S[q][key] = Q . K^T (key on the lane)
+          f16x sacc = zero16(), dp = zero16();
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const s8v pb = pack_half(sacc, s);
-          const s8v sb = pack_half(dp, s);
-          const int qrow = qb * 32 + 16 * s + 4 * h + (lane & 15) / 4;
+          for (int s = 0; s < 4; ++s) {
+            sacc = mfma(ld16(Qs + (qb * 32 + r) * RS + 16 * s + 8 * h), kf[s], sacc);
+            dp = mfma(ld16(Os + (qb * 32 + r) * RS + 16 * s + 8 * h), vf[s], dp);
+          }
+          const bool diag = CAUSAL && (qr0 < key0 + 31);
 #pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            const int col = db * 32 + (lane & 16) + 4 * (lane & 3);
-            const uint16_t* ob = Os + qrow * RS + col;
-            const uint16_t* qb_ = Qs + qrow * RS + col;
-            dvt[db] = mfma(cat(tr4(ob), tr4(ob + 8 * RS)), pb, dvt[db]);
-            dkt[db] = mfma(cat(tr4(qb_), tr4(qb_ + 8 * RS)), sb, dkt[db]);
+          for (int i = 0; i < 16; ++i) {
+            const int qrow = qb * 32 + crow(i, h);
+            float p = __builtin_amdgcn_exp2f(sacc[i] * sc2 - Ls[qrow]);
+            if (diag && ki > qt0 + qrow) p = 0.f;
+            sacc[i] = p;                      // P
+            dp[i] = p * (dp[i] - Ds[qrow]);   // dS
+          }
+          // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . dS[q][key]
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const s8v pb = pack_half(sacc, s);
+            const s8v sb = pack_half(dp, s);
+            const int qrow = qb * 32 + 16 * s + 4 * h + (lane & 15) / 4;
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+              const int col = db * 32 + (lane & 16) + 4 * (lane & 3);
+              const uint16_t* ob = Os + qrow * RS + col;
+              const uint16_t* qb_ = Qs + qrow * RS + col;
+              dvt[db] = mfma(cat(tr4(ob), tr4(ob + 8 * RS)), pb, dvt[db]);
+              dkt[db] = mfma(cat(tr4(qb_), tr4(qb_ + 8 * RS)), sb, dkt[db]);
+            }
           }
         }
       }
-    }
-    __syncthreads();
-    if (t + 1 < nt) {
-      sq.store(Qs, RS, tid);
-      so.store(Os, RS, tid);
-      if (tid < TILE) {
-        Ls[tid] = lv;
-        Ds[tid] = dlv;
-      }
       __syncthreads();
+      if (t + 1 < nt) {
+        sq.store(Qs, RS, tid);
+        so.store(Os, RS, tid);
+        if (tid < TILE) {
+          Ls[tid] = lv;
+          Ds[tid] = dlv;
+        }
+        __syncthreads();
+      }
     }
   }
-  uint16_t* dkr = dk.row(b, hh, ki);
-  uint16_t* dvr = dv.row(b, hh, ki);
+  uint16_t* dkr = dk.row(b, kvh, ki);
+  uint16_t* dvr = dv.row(b, kvh, ki);
   store_dT(dkr, dkt[0], 0, h, scale);
   store_dT(dkr, dkt[1], 1, h, scale);
   store_dT(dvr, dvt[0], 0, h, 1.f);
@@ -352,7 +361,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v,
 template <bool CAUSAL>
 __global__ __launch_bounds__(NT, 2) void bwd_dq_kernel(View q, View k, View v, View dout,
                                                         const float* __restrict__ lse, const float* __restrict__ delta,
-                                                        MView dq, int H, int T, int nblk, float sc2, float scale) {
+                                                        MView dq, int H, int T, int nblk, float sc2, float scale,
+                                                        int group) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[TILE * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[TILE * RS];
   const int per = gridDim.x / nblk;
@@ -362,6 +372,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_dq_kernel(View q, View k, View v, V
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
   const int q0 = qb * BLK + w * 32;
   const int qi = q0 + r;
+  const int kh = hh / group;
   s8v qf[4], of[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -373,15 +384,15 @@ __global__ __launch_bounds__(NT, 2) void bwd_dq_kernel(View q, View k, View v, V
   f16x dqt[2] = {zero16(), zero16()};
   const int ntiles = CAUSAL ? (qb * BLK + BLK) / TILE : T / TILE;
   Stage2 sk, sv;
-  sk.load(k.row(b, hh, 0), k.st, tid);
-  sv.load(v.row(b, hh, 0), v.st, tid);
+  sk.load(k.row(b, kh, 0), k.st, tid);
+  sv.load(v.row(b, kh, 0), v.st, tid);
   sk.store(Ks, RS, tid);
   sv.store(Vs, RS, tid);
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     if (t + 1 < ntiles) {
-      sk.load(k.row(b, hh, (t + 1) * TILE), k.st, tid);
-      sv.load(v.row(b, hh, (t + 1) * TILE), v.st, tid);
+      sk.load(k.row(b, kh, (t + 1) * TILE), k.st, tid);
+      sv.load(v.row(b, kh, (t + 1) * TILE), v.st, tid);
     }
     const int k0 = t * TILE;
     if (!CAUSAL || k0 <= q0 + 31) {
@@ -440,7 +451,9 @@ static MView mview_of(const at::Tensor& t, const char* name) {
   return MView{const_cast<uint16_t*>(v.p), v.sb, v.sh, v.st};
 }
 static void check_shapes(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
-  TORCH_CHECK(q.sizes() == k.sizes() && q.sizes() == v.sizes(), "attn: q, k, v shapes must match (no GQA yet)");
+  TORCH_CHECK(k.sizes() == v.sizes() && q.size(0) == k.size(0) && q.size(2) == k.size(2),
+              "attn: k and v must match, and share batch and length with q");
+  TORCH_CHECK(k.size(1) > 0 && q.size(1) % k.size(1) == 0, "attn: query heads must be a multiple of key/value heads");
   TORCH_CHECK(q.size(2) % BLK == 0 && q.size(2) >= BLK, "attn: sequence length must be a positive multiple of 128");
   TORCH_CHECK(q.size(0) * q.size(1) * (q.size(2) / BLK) < (1LL << 31), "attn: grid too large");
 }
@@ -459,12 +472,13 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::T
   const int nblk = T / BLK;
   const dim3 grid((unsigned)(B * H * nblk));
   const float sc2 = (float)scale * kLog2e;
+  const int group = H / (int)k.size(1);
   if (causal)
     hipLaunchKernelGGL((fwd_kernel<true>), grid, dim3(NT), 0, st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
-                       sc2);
+                       sc2, group);
   else
     hipLaunchKernelGGL((fwd_kernel<false>), grid, dim3(NT), 0, st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
-                       sc2);
+                       sc2, group);
   C10_HIP_KERNEL_LAUNCH_CHECK();
   return {o, lse};
 }
@@ -474,7 +488,7 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
                   const at::Tensor& dk, const at::Tensor& dv) {
   check_shapes(q, k, v);
   TORCH_CHECK(dout.sizes() == q.sizes() && out.sizes() == q.sizes() && dq.sizes() == q.sizes() &&
-                  dk.sizes() == q.sizes() && dv.sizes() == q.sizes(),
+                  dk.sizes() == k.sizes() && dv.sizes() == v.sizes(),
               "attn_bwd: shape mismatch");
   const int B = q.size(0), H = q.size(1), T = q.size(2);
   TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == (int64_t)B * H * T,
@@ -490,18 +504,19 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
                      delta.data_ptr<float>(), H, T, rows);
   C10_HIP_KERNEL_LAUNCH_CHECK();
   const int nblk = T / BLK;
-  const dim3 grid((unsigned)(B * H * nblk));
+  const int Hkv = (int)k.size(1), group = H / Hkv;
+  const dim3 grid((unsigned)(B * H * nblk)), kvgrid((unsigned)(B * Hkv * nblk));
   const float sc2 = (float)scale * kLog2e;
   if (causal) {
-    hipLaunchKernelGGL((bwd_dkdv_kernel<true>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dkv, dvv, H, T, nblk, sc2, (float)scale);
+    hipLaunchKernelGGL((bwd_dkdv_kernel<true>), kvgrid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), dkv, dvv, Hkv, T, nblk, sc2, (float)scale, group);
     hipLaunchKernelGGL((bwd_dq_kernel<true>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale);
+                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale, group);
   } else {
-    hipLaunchKernelGGL((bwd_dkdv_kernel<false>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dkv, dvv, H, T, nblk, sc2, (float)scale);
+    hipLaunchKernelGGL((bwd_dkdv_kernel<false>), kvgrid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), dkv, dvv, Hkv, T, nblk, sc2, (float)scale, group);
     hipLaunchKernelGGL((bwd_dq_kernel<false>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale);
+                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale, group);
   }
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }

@@ -15,7 +15,12 @@ TORCH_LIBRARY(nbd, m) {
   m.def("ln_fwd(Tensor x, Tensor? delta, Tensor weight, Tensor bias, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("ln_bwd(Tensor x, Tensor dy, Tensor? dres, Tensor weight, Tensor mean, Tensor rstd) -> (Tensor, Tensor, Tensor)");
   m.def("colsum(Tensor x, ScalarType dtype) -> Tensor");
+  m.def("rms_fwd(Tensor x, Tensor? delta, Tensor weight, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("rms_bwd(Tensor x, Tensor dy, Tensor? dres, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
   m.def("embedding_bwd(Tensor dy, Tensor idx, int V) -> Tensor");
+  m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, int n_rot, int head_dim, bool inverse) -> ()");
+  m.def("swiglu_fwd(Tensor gu) -> Tensor");
+  m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");
   m.def("xent_fwd(Tensor logits, Tensor target, int ignore_index) -> (Tensor, Tensor)");
   m.def("xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor scale, int ignore_index, Tensor(a!) dlogits) -> ()");
   m.def("adamw_flat(Tensor grad, Tensor(a!) param, Tensor(b!) master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "

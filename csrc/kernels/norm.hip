@@ -86,7 +86,7 @@ __device__ __forceinline__ float wsum(float v) {
 }
 
 // ============================================================================ forward
-template <typename T, typename W, bool RES, int NCH>
+template <typename T, typename W, bool RES, int NCH, bool RMS = false>
 __global__ __launch_bounds__(NT) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ delta,
                                                     T* __restrict__ xsum, const W* __restrict__ gamma,
                                                     const W* __restrict__ beta, T* __restrict__ y,
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const T* __restrict__ x, con
       s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
     }
   }
-  const float mean = wsum(s) / (float)C;
+  const float mean = RMS ? 0.f : wsum(s) / (float)C;  // RMSNorm: no centring
   float q = 0.f;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
@@ -133,9 +133,9 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const T* __restrict__ x, con
   for (int k = 0; k < NCH; ++k) {
     const int c = 4 * lane + 256 * k;
     if (c < C) {
-      float g[4], b[4], o[4];
+      float g[4], b[4] = {0.f, 0.f, 0.f, 0.f}, o[4];
       load4<W>(gamma + c, g);
-      load4<W>(beta + c, b);
+      if (!RMS) load4<W>(beta + c, b);
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = fmaf((v[k][e] - mean) * rstd, g[e], b[e]);
       store4<T>(y + base + c, o);
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const T* __restrict__ x, con
 constexpr int kBwdRows = 16;  // rows per workgroup (4 per wave, two at a time)
 constexpr int kRpi = 2;       // rows per wave iteration
 
-template <typename T, typename W, bool RES, int NCH>
+template <typename T, typename W, bool RES, int NCH, bool RMS = false>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                     const T* __restrict__ dres, const W* __restrict__ gamma,
                                                     const float* __restrict__ mean_in,
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, con
       const int64_t row = r0 + i + j;
       live[j] = row < rows;
       const int64_t rr = live[j] ? row : r0;  // dead rows re-read a live one; their results are dropped
-      mean[j] = mean_in[rr];
+      mean[j] = RMS ? 0.f : mean_in[rr];
       rstd[j] = rstd_in[rr];
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, con
           }
         }
       }
-      const float m1 = wsum(s1) / (float)C, m2 = wsum(s2) / (float)C;
+      const float m1 = RMS ? 0.f : wsum(s1) / (float)C, m2 = wsum(s2) / (float)C;
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
         const int c = 4 * lane + 256 * k;
@@ -465,6 +465,95 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_hip(const at::Tensor& x, c
   return {dx, dw, db};
 }
 
+// RMSNorm: y = x · rsqrt(mean(x²) + eps) · g  (optionally on x + delta, returned as xsum)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rms_fwd_hip(const at::Tensor& x, const c10::optional<at::Tensor>& delta,
+                                                           const at::Tensor& weight, double eps) {
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 4 == 0 && C <= 256 * kMaxCh && C > 0, "rms_fwd: C must be a multiple of 4 and <= 2048");
+  check_rows(x, C, "x");
+  TORCH_CHECK(weight.is_contiguous() && weight.numel() == C, "rms_fwd: weight must be [C]");
+  const bool res = delta.has_value() && delta->defined();
+  if (res) {
+    check_rows(*delta, C, "delta");
+    TORCH_CHECK(delta->sizes() == x.sizes() && delta->scalar_type() == x.scalar_type(), "rms_fwd: delta mismatch");
+  }
+  const int64_t rows = x.numel() / C;
+  at::Tensor y = at::empty_like(x);
+  at::Tensor xsum = res ? at::empty_like(x) : at::Tensor();
+  auto fo = x.options().dtype(at::kFloat);
+  at::Tensor mean = at::empty({rows}, fo), rstd = at::empty({rows}, fo);
+  if (rows == 0) return {y, xsum, rstd};
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  dispatch_tw(x.scalar_type(), weight.scalar_type(), [&](auto t, auto w) {
+   dispatch_nch(C, [&](auto nch) {
+    using T = decltype(t);
+    using W = decltype(w);
+    constexpr int N = decltype(nch)::value;
+    const T* dp = res ? static_cast<const T*>(delta->data_ptr()) : nullptr;
+    T* sp = res ? static_cast<T*>(xsum.data_ptr()) : nullptr;
+    if (res)
+      hipLaunchKernelGGL((ln_fwd_kernel<T, W, true, N, true>), grid, dim3(NT), 0, st,
+                         static_cast<const T*>(x.data_ptr()), dp, sp, static_cast<const W*>(weight.data_ptr()),
+                         nullptr, static_cast<T*>(y.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
+                         (int)C, (float)eps);
+    else
+      hipLaunchKernelGGL((ln_fwd_kernel<T, W, false, N, true>), grid, dim3(NT), 0, st,
+                         static_cast<const T*>(x.data_ptr()), dp, sp, static_cast<const W*>(weight.data_ptr()),
+                         nullptr, static_cast<T*>(y.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
+                         (int)C, (float)eps);
+   });
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return {y, xsum, rstd};
+}
+
+std::tuple<at::Tensor, at::Tensor> rms_bwd_hip(const at::Tensor& x, const at::Tensor& dy,
+                                               const c10::optional<at::Tensor>& dres, const at::Tensor& weight,
+                                               const at::Tensor& rstd) {
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 4 == 0 && C <= 256 * kMaxCh && C > 0, "rms_bwd: C must be a multiple of 4 and <= 2048");
+  check_rows(x, C, "x");
+  check_rows(dy, C, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "rms_bwd: dy mismatch");
+  const bool res = dres.has_value() && dres->defined();
+  if (res) {
+    check_rows(*dres, C, "dres");
+    TORCH_CHECK(dres->sizes() == x.sizes() && dres->scalar_type() == x.scalar_type(), "rms_bwd: dres mismatch");
+  }
+  const int64_t rows = x.numel() / C;
+  TORCH_CHECK(rstd.numel() == rows && rstd.scalar_type() == at::kFloat, "rms_bwd: rstd must be float32 [rows]");
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dw = at::empty({C}, weight.options()), db = at::empty({C}, weight.options());
+  const int nblk = (int)((rows + kBwdRows - 1) / kBwdRows);
+  if (rows == 0) return {dx, dw.zero_()};
+  at::Tensor pg = at::empty({nblk, 2 * C}, x.options().dtype(at::kFloat));
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  dispatch_tw(x.scalar_type(), weight.scalar_type(), [&](auto t, auto w) {
+   dispatch_nch(C, [&](auto nch) {
+    using T = decltype(t);
+    using W = decltype(w);
+    constexpr int N = decltype(nch)::value;
+    const T* dr = res ? static_cast<const T*>(dres->data_ptr()) : nullptr;
+    if (res)
+      hipLaunchKernelGGL((ln_bwd_kernel<T, W, true, N, true>), dim3(nblk), dim3(NT), 0, st,
+                         static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
+                         static_cast<const W*>(weight.data_ptr()), rstd.data_ptr<float>(), rstd.data_ptr<float>(),
+                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C);
+    else
+      hipLaunchKernelGGL((ln_bwd_kernel<T, W, false, N, true>), dim3(nblk), dim3(NT), 0, st,
+                         static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
+                         static_cast<const W*>(weight.data_ptr()), rstd.data_ptr<float>(), rstd.data_ptr<float>(),
+                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C);
+   });
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  reduce_into(pg, nblk, (int)(2 * C), (int)C, dw, db, st);
+  return {dx, dw};
+}
+
 // Σ over rows of a contiguous [..., C] tensor -> [C] in `dtype` (fp32 accumulation)
 at::Tensor colsum_hip(const at::Tensor& x, at::ScalarType dtype) {
   const int64_t C = x.size(-1);
@@ -505,4 +594,6 @@ TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
   m.impl("ln_fwd", &nbd::norm::ln_fwd_hip);
   m.impl("ln_bwd", &nbd::norm::ln_bwd_hip);
   m.impl("colsum", &nbd::norm::colsum_hip);
+  m.impl("rms_fwd", &nbd::norm::rms_fwd_hip);
+  m.impl("rms_bwd", &nbd::norm::rms_bwd_hip);
 }

@@ -1,0 +1,250 @@
+"""Llama-family models (SmolLM2, Llama 2/3-style) built on the framework's HIP kernels.
+
+The reference notebook fine-tunes SmolLM2-135M (``AutoModelForSequenceClassification``,
+``00_accelerate.ipynb`` exec 22) — a Llama with grouped-query attention.  Through HF modules its
+small-batch step is launch-bound (≈4,600 kernels, GPU busy 25 ms of a 40 ms step on MI355X:
+``profiles/notebook_prof_r1.md``).  This implementation keeps HF's weights and numerics
+(``from_hf`` / ``load_hf_state_dict``) but runs a block as:
+
+    x ─ rms_norm ─ qkv GEMM (fused q|k|v) ─ rope_ (in place) ─ flash attention (GQA) ─ o GEMM ─┐
+    └──────────────────────────── add_rms_norm (residual + norm in one pass) ◄───────────────┘
+      ─ gate|up GEMM (fused) ─ swiglu ─ down GEMM ─ add_rms_norm (into the next block's norm)
+
+i.e. ~12 kernels per block instead of ~70, nothing that synchronises with the host, and only
+caching-allocator memory — so the whole training step captures into a HIP graph
+(``nbdistributed_amd.graphs.GraphedStep``).  The GPU path needs bf16/f16, head_dim 64 and a
+sequence length that is a multiple of 128; anything else (CPU, fp32) runs the same math in
+plain PyTorch.  Attention is causal with right padding, like the notebook's tokenizer output:
+a non-pad query only ever sees non-pad keys, so no padding mask is needed (left padding is not
+supported).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Any, Dict, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+
+
+@dataclass
+class LlamaConfig:
+    vocab_size: int = 49152
+    hidden_size: int = 576
+    intermediate_size: int = 1536
+    num_hidden_layers: int = 30
+    num_attention_heads: int = 9
+    num_key_value_heads: int = 3
+    max_position_embeddings: int = 8192
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 100000.0
+    tie_word_embeddings: bool = True
+    num_labels: int = 2
+    pad_token_id: Optional[int] = 0
+    initializer_range: float = 0.02
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden_size // self.num_attention_heads
+
+    @classmethod
+    def smollm2_135m(cls, **kw) -> "LlamaConfig":
+        return cls(**kw)
+
+    @classmethod
+    def tiny(cls, **kw) -> "LlamaConfig":
+        d = dict(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+                 num_key_value_heads=2, max_position_embeddings=1024)
+        d.update(kw)
+        return cls(**d)
+
+    @classmethod
+    def from_hf(cls, hf) -> "LlamaConfig":
+        rope = getattr(hf, "rope_theta", None)
+        if rope is None:
+            rope = (getattr(hf, "rope_parameters", None) or {}).get("rope_theta", 10000.0)
+        return cls(vocab_size=hf.vocab_size, hidden_size=hf.hidden_size, intermediate_size=hf.intermediate_size,
+                   num_hidden_layers=hf.num_hidden_layers, num_attention_heads=hf.num_attention_heads,
+                   num_key_value_heads=hf.num_key_value_heads or hf.num_attention_heads,
+                   max_position_embeddings=hf.max_position_embeddings, rms_norm_eps=hf.rms_norm_eps,
+                   rope_theta=float(rope), tie_word_embeddings=bool(getattr(hf, "tie_word_embeddings", False)),
+                   num_labels=getattr(hf, "num_labels", 2), pad_token_id=getattr(hf, "pad_token_id", None))
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, n: int, eps: float):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(n))
+        self.eps = eps
+
+    def forward(self, x):
+        return ops.rms_norm(x, self.weight, self.eps)
+
+
+class LlamaAttention(nn.Module):
+    def __init__(self, c: LlamaConfig):
+        super().__init__()
+        self.H, self.Hkv, self.D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
+        self.qkv_proj = nn.Linear(c.hidden_size, (self.H + 2 * self.Hkv) * self.D, bias=False)
+        self.o_proj = nn.Linear(self.H * self.D, c.hidden_size, bias=False)
+
+    def forward(self, x, cos, sin):
+        qkv = ops.rope_(F.linear(x, self.qkv_proj.weight), cos, sin, self.H + self.Hkv, self.D)
+        return self.o_proj(ops.attention_qkv(qkv, self.H, causal=True, n_kv_head=self.Hkv))
+
+
+class LlamaMLP(nn.Module):
+    def __init__(self, c: LlamaConfig):
+        super().__init__()
+        self.gate_up_proj = nn.Linear(c.hidden_size, 2 * c.intermediate_size, bias=False)
+        self.down_proj = nn.Linear(c.intermediate_size, c.hidden_size, bias=False)
+
+    def forward(self, x):
+        return self.down_proj(ops.swiglu(self.gate_up_proj(x)))
+
+
+class LlamaDecoderLayer(nn.Module):
+    def __init__(self, c: LlamaConfig):
+        super().__init__()
+        self.input_layernorm = RMSNorm(c.hidden_size, c.rms_norm_eps)
+        self.self_attn = LlamaAttention(c)
+        self.post_attention_layernorm = RMSNorm(c.hidden_size, c.rms_norm_eps)
+        self.mlp = LlamaMLP(c)
+
+
+class LlamaModel(nn.Module):
+    """Decoder stack; ``forward`` returns the final-normed hidden states [B, T, C]."""
+
+    def __init__(self, c: LlamaConfig):
+        super().__init__()
+        self.config = c
+        self.embed_tokens = nn.Embedding(c.vocab_size, c.hidden_size)
+        self.layers = nn.ModuleList([LlamaDecoderLayer(c) for _ in range(c.num_hidden_layers)])
+        self.norm = RMSNorm(c.hidden_size, c.rms_norm_eps)
+        self._rope: Dict[Any, tuple] = {}
+
+    def rope(self, T: int, device) -> tuple:
+        key = (str(device), T)
+        if key not in self._rope:  # built once per (device, length), outside any graph capture
+            self._rope[key] = ops.rope_tables(T, self.config.head_dim, self.config.rope_theta, device)
+        return self._rope[key]
+
+    def forward(self, input_ids):
+        c = self.config
+        T = input_ids.shape[1]
+        cos, sin = self.rope(T, input_ids.device)
+        x = ops.embedding(input_ids, self.embed_tokens.weight)
+        # the residual stream: each block's two residual adds are fused with the RMSNorm after them
+        h = self.layers[0].input_layernorm(x)
+        for i, layer in enumerate(self.layers):
+            a = layer.self_attn(h, cos, sin)
+            x, h = ops.add_rms_norm(x, a, layer.post_attention_layernorm.weight, c.rms_norm_eps)
+            m = layer.mlp(h)
+            nxt = self.layers[i + 1].input_layernorm if i + 1 < len(self.layers) else self.norm
+            x, h = ops.add_rms_norm(x, m, nxt.weight, c.rms_norm_eps)
+        return h
+
+
+class _LlamaPreTrained(nn.Module):
+    def _init_weights(self) -> None:
+        std = self.config.initializer_range
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                nn.init.normal_(m.weight, mean=0.0, std=std)
+
+
+class LlamaForSequenceClassification(_LlamaPreTrained):
+    """HF ``LlamaForSequenceClassification`` semantics: score the rightmost non-pad token;
+    cross-entropy loss when ``labels`` are given.  Returns (loss, logits)."""
+
+    def __init__(self, c: LlamaConfig):
+        super().__init__()
+        self.config = c
+        self.model = LlamaModel(c)
+        self.score = nn.Linear(c.hidden_size, c.num_labels, bias=False)
+        self._init_weights()
+
+    def forward(self, input_ids, attention_mask=None, labels=None):
+        h = self.model(input_ids)
+        B, T, C = h.shape
+        if self.config.pad_token_id is None:
+            last = torch.full((B,), T - 1, dtype=torch.int64, device=h.device)
+        else:  # rightmost non-pad token (device-side, no host sync)
+            nonpad = (input_ids != self.config.pad_token_id).to(torch.int32)
+            last = (torch.arange(T, device=h.device, dtype=torch.int32) * nonpad).argmax(-1)
+        # gather (backward = scatter-add: no sort, graph-safe) instead of advanced indexing
+        pooled = torch.gather(h, 1, last.view(B, 1, 1).expand(B, 1, C)).squeeze(1)
+        logits = self.score(pooled)
+        loss = None
+        if labels is not None:
+            loss = F.cross_entropy(logits.float(), labels.view(-1))
+        return loss, logits
+
+
+class LlamaForCausalLM(_LlamaPreTrained):
+    """Causal LM head (tied to the embedding when ``tie_word_embeddings``); the loss runs
+    through the fused HIP cross-entropy on GPU.  Returns (loss, logits or None)."""
+
+    def __init__(self, c: LlamaConfig):
+        super().__init__()
+        self.config = c
+        self.model = LlamaModel(c)
+        self.lm_head = nn.Linear(c.hidden_size, c.vocab_size, bias=False)
+        self._init_weights()
+        if c.tie_word_embeddings:
+            self.lm_head.weight = self.model.embed_tokens.weight
+
+    def forward(self, input_ids, labels=None, return_logits: bool = True):
+        h = self.model(input_ids)
+        logits = self.lm_head(h)
+        loss = None
+        if labels is not None:  # next-token prediction
+            V = logits.shape[-1]
+            shift = logits[:, :-1].reshape(-1, V)
+            tgt = labels[:, 1:].reshape(-1)
+            loss = (ops.cross_entropy(shift, tgt) if logits.is_cuda
+                    else F.cross_entropy(shift.float(), tgt, ignore_index=-100))
+        return loss, (logits if return_logits else None)
+
+
+# ---------------------------------------------------------------------------- HF interop
+def hf_to_nbd_state_dict(sd: Dict[str, torch.Tensor], c: LlamaConfig) -> Dict[str, torch.Tensor]:
+    """Map an HF Llama state dict (q/k/v and gate/up as separate projections) onto this layout
+    (fused q|k|v and gate|up projections)."""
+    out: Dict[str, torch.Tensor] = {}
+    for k, v in sd.items():
+        if ".self_attn.q_proj." in k or ".self_attn.k_proj." in k or ".self_attn.v_proj." in k:
+            continue
+        if ".mlp.gate_proj." in k or ".mlp.up_proj." in k:
+            continue
+        if k.endswith("rotary_emb.inv_freq"):
+            continue
+        out[k] = v
+    for i in range(c.num_hidden_layers):
+        p = f"model.layers.{i}"
+        out[f"{p}.self_attn.qkv_proj.weight"] = torch.cat(
+            [sd[f"{p}.self_attn.q_proj.weight"], sd[f"{p}.self_attn.k_proj.weight"], sd[f"{p}.self_attn.v_proj.weight"]])
+        out[f"{p}.mlp.gate_up_proj.weight"] = torch.cat([sd[f"{p}.mlp.gate_proj.weight"], sd[f"{p}.mlp.up_proj.weight"]])
+    return out
+
+
+def from_hf(hf_model) -> nn.Module:
+    """Build the equivalent nbd model from an instantiated HF Llama sequence-classification or
+    causal-LM model (weights copied)."""
+    c = LlamaConfig.from_hf(hf_model.config)
+    cls = LlamaForSequenceClassification if hasattr(hf_model, "score") else LlamaForCausalLM
+    m = cls(c)
+    sd = hf_to_nbd_state_dict(hf_model.state_dict(), c)
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    missing = [k for k in missing if not (k == "lm_head.weight" and c.tie_word_embeddings)]
+    if missing or unexpected:
+        raise ValueError(f"from_hf: missing {missing}, unexpected {unexpected}")
+    return m.to(next(hf_model.parameters()).dtype)
+
+
+__all__ = ["LlamaConfig", "LlamaModel", "LlamaForSequenceClassification", "LlamaForCausalLM", "RMSNorm",
+           "from_hf", "hf_to_nbd_state_dict"]

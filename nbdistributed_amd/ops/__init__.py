@@ -17,6 +17,8 @@ add_layer_norm (K8)    residual add + LayerNorm fwd; LN bwd + residual   norm.hi
                        grad + dγ/dβ column partials
 colsum / linear (K9)   bias gradient column sums                        norm.hip
 embedding (K10)        counting-sort embedding backward (graph-safe)     embed.hip
+rms_norm / rope_ /     RMSNorm (+ residual), rotary in place on packed   norm.hip, act.hip
+swiglu (K11)           QKV, fused SwiGLU fwd/bwd (Llama family)
 =====================  ==============================================  =========================
 
 GPU tensors always go to the HIP kernels; if ``libnbd_ops.so`` cannot be loaded on a GPU box the
@@ -315,39 +317,45 @@ def _attn_fns():
         def backward(ctx, do):
             q, k, v, o, lse = ctx.saved_tensors
             B, H, T, D = q.shape
-            dqkv = torch.empty(B, T, 3, H, D, dtype=q.dtype, device=q.device)
-            dq, dk, dv = (dqkv[:, :, i].transpose(1, 2) for i in range(3))
+            Hkv = k.shape[1]
+            dq = torch.empty(B, T, H, D, dtype=q.dtype, device=q.device).transpose(1, 2)
+            dkv = torch.empty(B, T, 2, Hkv, D, dtype=q.dtype, device=q.device)
+            dk, dv = dkv[:, :, 0].transpose(1, 2), dkv[:, :, 1].transpose(1, 2)
             torch.ops.nbd.attn_bwd(_fix(do), q, k, v, o, lse, ctx.causal, ctx.scale, dq, dk, dv)
             return dq, dk, dv, None, None
 
+    def _split(qkv, H, Hkv):
+        B, T, W = qkv.shape
+        D = W // (H + 2 * Hkv)
+        q = qkv[:, :, : H * D].view(B, T, H, D).transpose(1, 2)
+        k = qkv[:, :, H * D:(H + Hkv) * D].view(B, T, Hkv, D).transpose(1, 2)
+        v = qkv[:, :, (H + Hkv) * D:].view(B, T, Hkv, D).transpose(1, 2)
+        return q, k, v
+
     class _FlashAttentionQKV(torch.autograd.Function):
-        """[B, T, 3·H·D] packed projection in, [B, T, H·D] out; the backward writes the packed
-        [B, T, 3·H·D] gradient directly (no split/cat, no transposes)."""
+        """[B, T, (H + 2·Hkv)·D] packed projection in, [B, T, H·D] out; the backward writes the
+        packed gradient directly (no split/cat, no transposes).  Hkv < H: grouped-query attention."""
 
         @staticmethod
-        def forward(ctx, qkv, n_head, causal, scale):
-            B, T, C3 = qkv.shape
-            C = C3 // 3
-            D = C // n_head
-            q, k, v = (qkv[:, :, i * C:(i + 1) * C].view(B, T, n_head, D).transpose(1, 2) for i in range(3))
+        def forward(ctx, qkv, n_head, n_kv, causal, scale):
+            B, T, _ = qkv.shape
+            q, k, v = _split(qkv, n_head, n_kv)
             o, lse = torch.ops.nbd.attn_fwd(q, k, v, causal, scale)
             ctx.save_for_backward(qkv, o, lse)
-            ctx.n_head, ctx.causal, ctx.scale = n_head, causal, scale
-            return o.transpose(1, 2).reshape(B, T, C)  # o is stored [B, T, H, D]: a view
+            ctx.n_head, ctx.n_kv, ctx.causal, ctx.scale = n_head, n_kv, causal, scale
+            return o.transpose(1, 2).reshape(B, T, -1)  # o is stored [B, T, H, D]: a view
 
         @staticmethod
         def backward(ctx, dy):
             qkv, o, lse = ctx.saved_tensors
-            B, T, C3 = qkv.shape
-            C, H = C3 // 3, ctx.n_head
-            D = C // H
-            q, k, v = (qkv[:, :, i * C:(i + 1) * C].view(B, T, H, D).transpose(1, 2) for i in range(3))
+            B, T, _ = qkv.shape
+            q, k, v = _split(qkv, ctx.n_head, ctx.n_kv)
             dy = dy if dy.is_contiguous() else dy.contiguous()
             dqkv = torch.empty_like(qkv, memory_format=torch.contiguous_format)
-            dq, dk, dv = (dqkv[:, :, i * C:(i + 1) * C].view(B, T, H, D).transpose(1, 2) for i in range(3))
-            do = dy.view(B, T, H, D).transpose(1, 2)
+            dq, dk, dv = _split(dqkv, ctx.n_head, ctx.n_kv)
+            do = dy.view(B, T, ctx.n_head, -1).transpose(1, 2)
             torch.ops.nbd.attn_bwd(do, q, k, v, o, lse, ctx.causal, ctx.scale, dq, dk, dv)
-            return dqkv, None, None, None
+            return dqkv, None, None, None, None
 
     _AttnFns = (_FlashAttention, _FlashAttentionQKV)
     return _AttnFns
@@ -367,29 +375,36 @@ def flash_attention(q, k, v, causal: bool = False, scale: Optional[float] = None
     import torch.nn.functional as F
 
     sc = float(scale) if scale is not None else q.shape[-1] ** -0.5
-    if flash_supported(q) and q.shape == k.shape == v.shape and k.dtype == v.dtype == q.dtype:
+    gqa = k.shape[1] != q.shape[1]
+    if (flash_supported(q) and k.shape == v.shape and q.shape[0] == k.shape[0] and q.shape[2:] == k.shape[2:]
+            and q.shape[1] % k.shape[1] == 0 and k.dtype == v.dtype == q.dtype):
         _require()
         return _attn_fns()[0].apply(q, k, v, bool(causal), sc)
-    return F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=sc)
+    return F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=sc, enable_gqa=gqa)
 
 
-def attention_qkv(qkv, n_head: int, causal: bool = True, scale: Optional[float] = None):
-    """Multi-head attention straight from a packed [B, T, 3·C] projection (GPT-2 ``c_attn``
-    output) to [B, T, C]."""
+def attention_qkv(qkv, n_head: int, causal: bool = True, scale: Optional[float] = None,
+                  n_kv_head: Optional[int] = None):
+    """Multi-head attention straight from a packed [B, T, (H + 2·Hkv)·D] projection (GPT-2's
+    ``c_attn`` output, or a fused Llama q|k|v projection) to [B, T, H·D].  ``n_kv_head`` < ``n_head``
+    is grouped-query attention."""
     import torch
     import torch.nn.functional as F
 
-    B, T, C3 = qkv.shape
-    C = C3 // 3
-    D = C // n_head
+    B, T, W = qkv.shape
+    Hkv = n_kv_head or n_head
+    D = W // (n_head + 2 * Hkv)
     sc = float(scale) if scale is not None else D ** -0.5
     if (qkv.is_cuda and qkv.dtype == torch.bfloat16 and D == 64 and T % 128 == 0 and qkv.stride(-1) == 1
-            and qkv.stride(1) % 8 == 0 and qkv.stride(0) % 8 == 0 and qkv.data_ptr() % 16 == 0):
+            and qkv.stride(1) % 8 == 0 and qkv.stride(0) % 8 == 0 and qkv.data_ptr() % 16 == 0
+            and n_head % Hkv == 0):
         _require()
-        return _attn_fns()[1].apply(qkv, int(n_head), bool(causal), sc)
-    q, k, v = (qkv[:, :, i * C:(i + 1) * C].view(B, T, n_head, D).transpose(1, 2) for i in range(3))
-    y = F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=sc)
-    return y.transpose(1, 2).reshape(B, T, C)
+        return _attn_fns()[1].apply(qkv, int(n_head), int(Hkv), bool(causal), sc)
+    q = qkv[:, :, : n_head * D].view(B, T, n_head, D).transpose(1, 2)
+    k = qkv[:, :, n_head * D:(n_head + Hkv) * D].view(B, T, Hkv, D).transpose(1, 2)
+    v = qkv[:, :, (n_head + Hkv) * D:].view(B, T, Hkv, D).transpose(1, 2)
+    y = F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=sc, enable_gqa=Hkv != n_head)
+    return y.transpose(1, 2).reshape(B, T, n_head * D)
 
 
 _NormFns = None
@@ -457,6 +472,145 @@ def _norm_fns():
 
     _NormFns = (_LayerNorm, _AddLayerNorm, _Linear)
     return _NormFns
+
+
+_LlamaFns = None
+
+
+def _llama_fns():
+    global _LlamaFns
+    if _LlamaFns is not None:
+        return _LlamaFns
+    import torch
+
+    def _c(t):
+        return t if t.is_contiguous() else t.contiguous()
+
+    class _RMSNorm(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w, eps):
+            y, _, rstd = torch.ops.nbd.rms_fwd(x, None, w, eps)
+            ctx.save_for_backward(x, w, rstd)
+            return y
+
+        @staticmethod
+        def backward(ctx, dy):
+            x, w, rstd = ctx.saved_tensors
+            dx, dw = torch.ops.nbd.rms_bwd(x, _c(dy), None, w, rstd)
+            return dx, dw, None
+
+    class _AddRMSNorm(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, delta, w, eps):
+            y, s, rstd = torch.ops.nbd.rms_fwd(x, delta, w, eps)
+            ctx.save_for_backward(s, w, rstd)
+            return s, y
+
+        @staticmethod
+        def backward(ctx, ds, dy):
+            s, w, rstd = ctx.saved_tensors
+            if dy is None:
+                return ds, ds, None, None
+            dx, dw = torch.ops.nbd.rms_bwd(s, _c(dy), None if ds is None else _c(ds), w, rstd)
+            return dx, dx, dw, None
+
+    class _Rope(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, cos, sin, n_rot, head_dim):
+            torch.ops.nbd.rope_(x, cos, sin, n_rot, head_dim, False)
+            ctx.mark_dirty(x)
+            ctx.save_for_backward(cos, sin)
+            ctx.n_rot, ctx.head_dim = n_rot, head_dim
+            return x
+
+        @staticmethod
+        def backward(ctx, g):
+            cos, sin = ctx.saved_tensors
+            g = g.contiguous().clone()  # never rotate a gradient buffer someone else may hold
+            torch.ops.nbd.rope_(g, cos, sin, ctx.n_rot, ctx.head_dim, True)
+            return g, None, None, None, None
+
+    class _SwiGLU(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, gu):
+            ctx.save_for_backward(gu)
+            return torch.ops.nbd.swiglu_fwd(gu)
+
+        @staticmethod
+        def backward(ctx, d):
+            (gu,) = ctx.saved_tensors
+            return torch.ops.nbd.swiglu_bwd(gu, _c(d))
+
+    _LlamaFns = (_RMSNorm, _AddRMSNorm, _Rope, _SwiGLU)
+    return _LlamaFns
+
+
+def _rms_ok(x, w) -> bool:
+    import torch
+
+    C = x.shape[-1]
+    return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32) and C % 8 == 0 and C <= 2048
+            and w.dtype == x.dtype and not torch.is_autocast_enabled())
+
+
+def rms_norm(x, weight, eps: float = 1e-6):
+    """RMSNorm over the last dim: ``x · rsqrt(mean(x²) + eps) · weight`` (HIP on GPU)."""
+    import torch
+
+    if _rms_ok(x, weight):
+        _require()
+        return _llama_fns()[0].apply(x if x.is_contiguous() else x.contiguous(), weight, float(eps))
+    xf = x.float()
+    return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype) * weight
+
+
+def add_rms_norm(x, delta, weight, eps: float = 1e-6):
+    """``s = x + delta; return s, RMSNorm(s)`` in one HIP pass (and one for the backward)."""
+    if _rms_ok(x, weight) and delta.dtype == x.dtype and delta.shape == x.shape:
+        _require()
+        return _llama_fns()[1].apply(x if x.is_contiguous() else x.contiguous(),
+                                     delta if delta.is_contiguous() else delta.contiguous(), weight, float(eps))
+    s = x + delta
+    return s, rms_norm(s, weight, eps)
+
+
+def rope_tables(T: int, head_dim: int, theta: float, device) -> tuple:
+    """cos/sin [T, head_dim/2] float32 for :func:`rope_` (HF default rope)."""
+    import torch
+
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float32, device=device) / head_dim))
+    f = torch.outer(torch.arange(T, dtype=torch.float32, device=device), inv)
+    return f.cos().contiguous(), f.sin().contiguous()
+
+
+def rope_(x, cos, sin, n_rot: int, head_dim: int):
+    """Rotary embedding in place on the first ``n_rot`` heads of each row of a packed
+    [B, T, H_total·head_dim] projection (HF rotate_half convention).  Returns ``x``."""
+    import torch
+
+    if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and head_dim % 8 == 0 and x.is_contiguous():
+        _require()
+        return _llama_fns()[2].apply(x, cos, sin, int(n_rot), int(head_dim))
+    B, T, W = x.shape
+    half = head_dim // 2
+    r = x[:, :, : n_rot * head_dim].view(B, T, n_rot, head_dim)
+    a, b = r[..., :half].float(), r[..., half:].float()
+    c, s_ = cos[:T, None, :], sin[:T, None, :]
+    rot = torch.cat([a * c - b * s_, b * c + a * s_], -1).to(x.dtype).view(B, T, n_rot * head_dim)
+    return torch.cat([rot, x[:, :, n_rot * head_dim:]], -1)
+
+
+def swiglu(gu):
+    """``silu(g) · u`` for a fused [..., 2I] gate|up projection (HIP fwd/bwd on GPU)."""
+    import torch
+    import torch.nn.functional as F
+
+    I2 = gu.shape[-1]
+    if gu.is_cuda and I2 % 16 == 0 and gu.dtype in (torch.bfloat16, torch.float16, torch.float32):
+        _require()
+        return _llama_fns()[3].apply(gu if gu.is_contiguous() else gu.contiguous())
+    g, u = gu[..., : I2 // 2], gu[..., I2 // 2:]
+    return F.silu(g) * u
 
 
 _EmbFn = None
@@ -598,5 +752,5 @@ def tensor_summary_text(x) -> str:
 
 __all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "cross_entropy",
            "flash_attention", "attention_qkv", "flash_supported", "layer_norm", "add_layer_norm", "linear",
-           "colsum", "embedding", "tensor_summary", "tensor_summary_text",
+           "colsum", "embedding", "rms_norm", "add_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary", "tensor_summary_text",
            "tensor_summary_raw", "plan_offsets", "native_available", "load_library", "SUMMARY_FIELDS"]

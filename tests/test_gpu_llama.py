@@ -1,0 +1,160 @@
+"""GPU: Llama-family kernels (RMSNorm, RoPE, SwiGLU, GQA flash attention) against fp32
+PyTorch references, the bf16 HIP model path against the fp32 math path, and a HIP-graph
+captured training step against eager."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from nbdistributed_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev(require_gpu):
+    assert ops.native_available(), ops._load_error
+    return torch.device("cuda", 0)
+
+
+def _rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("C", [576, 64, 2048])
+def test_rms_norm(dev, res, C):
+    x = torch.randn(257, C, device=dev, dtype=torch.bfloat16)
+    d = torch.randn(257, C, device=dev, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(C, device=dev)).to(torch.bfloat16)
+    dy = torch.randn(257, C, device=dev, dtype=torch.bfloat16)
+    xs, ds, ws = (t.clone().requires_grad_(True) for t in (x, d, w))
+    xr, dr, wr = (t.float().cpu().requires_grad_(True) for t in (x, d, w))
+    if res:
+        s, y = ops.add_rms_norm(xs, ds, ws, 1e-5)
+        sr = xr + dr
+    else:
+        y = ops.rms_norm(xs, ws, 1e-5)
+        sr = xr
+    yr = sr * torch.rsqrt(sr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    y.backward(dy)
+    yr.backward(dy.float().cpu())
+    assert _rel(y, yr) < 2e-2
+    assert _rel(xs.grad, xr.grad) < 3e-2 and _rel(ws.grad, wr.grad) < 3e-2
+    if res:
+        assert _rel(ds.grad, dr.grad) < 3e-2
+
+
+def test_rope_forward_backward(dev):
+    B, T, H, Hkv, D = 2, 128, 9, 3, 64
+    x = torch.randn(B, T, (H + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
+    cos, sin = ops.rope_tables(T, D, 100000.0, dev)
+    xr = x.float().cpu().requires_grad_(True)
+    ref = ops.rope_(xr, cos.cpu(), sin.cpu(), H + Hkv, D)  # CPU math path
+    xs = x.clone().requires_grad_(True)
+    y = ops.rope_(xs * 1, cos, sin, H + Hkv, D)
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref.backward(g.float().cpu())
+    assert _rel(y, ref) < 1e-2
+    assert _rel(xs.grad, xr.grad) < 1e-2
+
+
+def test_swiglu(dev):
+    gu = torch.randn(300, 2 * 1536, device=dev, dtype=torch.bfloat16)
+    d = torch.randn(300, 1536, device=dev, dtype=torch.bfloat16)
+    a = gu.clone().requires_grad_(True)
+    r = gu.float().cpu().requires_grad_(True)
+    y = ops.swiglu(a)
+    yr = F.silu(r[:, :1536]) * r[:, 1536:]
+    y.backward(d)
+    yr.backward(d.float().cpu())
+    assert _rel(y, yr) < 1e-2 and _rel(a.grad, r.grad) < 2e-2
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_gqa_flash_attention(dev, causal):
+    B, H, Hkv, T = 2, 9, 3, 256
+    q = torch.randn(B, H, T, 64, device=dev, dtype=torch.bfloat16)
+    k, v = (torch.randn(B, Hkv, T, 64, device=dev, dtype=torch.bfloat16) for _ in range(2))
+    do = torch.randn_like(q)
+    qs, ks, vs = (t.clone().requires_grad_(True) for t in (q, k, v))
+    out = ops.flash_attention(qs, ks, vs, causal=causal)
+    out.backward(do)
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    s = qr @ kr.repeat_interleave(H // Hkv, 1).transpose(-1, -2) * 0.125
+    if causal:
+        s = s.masked_fill(torch.ones(T, T, dtype=torch.bool, device=dev).triu(1), float("-inf"))
+    ref = torch.softmax(s, -1) @ vr.repeat_interleave(H // Hkv, 1)
+    ref.backward(do.float())
+    assert _rel(out, ref) < 2e-2
+    for a, b in ((qs.grad, qr.grad), (ks.grad, kr.grad), (vs.grad, vr.grad)):
+        assert _rel(a, b) < 3e-2
+
+
+def _smol_tiny():
+    from nbdistributed_amd.models.llama import LlamaConfig
+
+    # SmolLM2's head geometry (9 query heads, 3 kv heads, head_dim 64) with fewer layers
+    return LlamaConfig(vocab_size=4096, hidden_size=576, intermediate_size=1536, num_hidden_layers=3)
+
+
+def _batch(dev, B=4, T=128, V=4096):
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(1, V, (B, T), generator=g)
+    lens = torch.randint(T // 3, T + 1, (B,), generator=g)
+    mask = (torch.arange(T)[None] < lens[:, None]).long()
+    return (ids * mask).to(dev), mask.to(dev), torch.randint(0, 2, (B,), generator=g).to(dev)
+
+
+def test_llama_bf16_hip_path_matches_fp32_math(dev):
+    from nbdistributed_amd.models.llama import LlamaForSequenceClassification
+
+    torch.manual_seed(0)
+    ref = LlamaForSequenceClassification(_smol_tiny())
+    m = LlamaForSequenceClassification(_smol_tiny())
+    m.load_state_dict(ref.state_dict())
+    m = m.to(dev, torch.bfloat16)
+    ids, mask, labels = _batch(dev)
+    loss, logits = m(ids, mask, labels)
+    loss.backward()
+    lr_, logr = ref(ids.cpu(), mask.cpu(), labels.cpu())
+    lr_.backward()
+    assert _rel(logits, logr) < 5e-2, (logits, logr)
+    assert abs(float(loss.detach()) - float(lr_.detach())) < 3e-2
+    for name in ("model.layers.0.self_attn.qkv_proj.weight", "model.layers.2.mlp.gate_up_proj.weight",
+                 "model.embed_tokens.weight", "score.weight"):
+        a = dict(m.named_parameters())[name].grad
+        b = dict(ref.named_parameters())[name].grad
+        assert _rel(a, b) < 0.1, (name, _rel(a, b))
+
+
+def test_llama_training_step_graph_capture(dev):
+    from nbdistributed_amd.graphs import GraphedStep
+    from nbdistributed_amd.models.llama import LlamaForSequenceClassification
+
+    def build():
+        torch.manual_seed(3)
+        m = LlamaForSequenceClassification(_smol_tiny()).to(dev, torch.bfloat16)
+        return m, torch.optim.AdamW(m.parameters(), lr=1e-3, capturable=True)
+
+    batches = [_batch(dev, seed) if False else _batch(dev) for seed in range(1)]
+    ids, mask, labels = batches[0]
+
+    def make(m, o):
+        def step(i, mk, y):
+            loss, _ = m(i, mk, y)
+            loss.backward()
+            o.step()
+            o.zero_grad(set_to_none=False)
+            return loss.detach()
+        return step
+
+    m1, o1 = build()
+    s1 = make(m1, o1)
+    eager = [float(s1(ids, mask, labels)) for _ in range(6)]
+    m2, o2 = build()
+    gs = GraphedStep(make(m2, o2), (ids, mask, labels), warmup=3)
+    graphed = [float(gs(ids, mask, labels)) for _ in range(3)]
+    torch.cuda.synchronize()
+    assert max(abs(a - b) for a, b in zip(eager[3:], graphed)) < 2e-2, (eager, graphed)

@@ -1,0 +1,75 @@
+"""Native Llama family vs HF transformers (same random weights), CPU fp32 math path:
+sequence classification (the reference notebook's model type) and causal LM — logits, loss
+and gradients mapped back onto HF's separate q/k/v and gate/up projections."""
+import pytest
+import torch
+
+from nbdistributed_amd.models.llama import LlamaConfig, from_hf
+
+transformers = pytest.importorskip("transformers")
+
+
+def _hf_config(c: LlamaConfig, **kw):
+    hc = transformers.LlamaConfig(vocab_size=c.vocab_size, hidden_size=c.hidden_size,
+                                  intermediate_size=c.intermediate_size, num_hidden_layers=c.num_hidden_layers,
+                                  num_attention_heads=c.num_attention_heads,
+                                  num_key_value_heads=c.num_key_value_heads,
+                                  max_position_embeddings=c.max_position_embeddings, rms_norm_eps=c.rms_norm_eps,
+                                  rope_theta=c.rope_theta, tie_word_embeddings=True, pad_token_id=0, **kw)
+    hc._attn_implementation = "eager"
+    return hc
+
+
+def _batch(B=3, T=24, V=512, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(1, V, (B, T), generator=g)
+    lens = torch.tensor([T, T - 5, T // 2])[:B]
+    mask = (torch.arange(T)[None] < lens[:, None]).long()
+    return ids * mask, mask
+
+
+def test_sequence_classification_matches_hf():
+    torch.manual_seed(0)
+    c = LlamaConfig.tiny(rope_theta=100000.0)
+    hf = transformers.LlamaForSequenceClassification(_hf_config(c, num_labels=2)).eval()
+    ours = from_hf(hf).eval()
+    ids, mask = _batch()
+    labels = torch.tensor([0, 1, 1])
+    out = hf(input_ids=ids, attention_mask=mask, labels=labels)
+    loss, logits = ours(ids, mask, labels)
+    assert torch.allclose(logits, out.logits, atol=2e-5, rtol=1e-4), (logits, out.logits)
+    assert abs(float(loss) - float(out.loss)) < 1e-5
+    out.loss.backward()
+    loss.backward()
+    H, Hkv, D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
+    l0h, l0o = hf.model.layers[0], ours.model.layers[0]
+    gq = l0o.self_attn.qkv_proj.weight.grad
+    pairs = [(gq[: H * D], l0h.self_attn.q_proj.weight.grad),
+             (gq[H * D:(H + Hkv) * D], l0h.self_attn.k_proj.weight.grad),
+             (gq[(H + Hkv) * D:], l0h.self_attn.v_proj.weight.grad),
+             (l0o.mlp.gate_up_proj.weight.grad[: c.intermediate_size], l0h.mlp.gate_proj.weight.grad),
+             (ours.model.embed_tokens.weight.grad, hf.model.embed_tokens.weight.grad),
+             (ours.model.norm.weight.grad, hf.model.norm.weight.grad),
+             (ours.score.weight.grad, hf.score.weight.grad)]
+    for a, b in pairs:
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-3), float((a - b).abs().max())
+
+
+def test_causal_lm_matches_hf():
+    torch.manual_seed(1)
+    c = LlamaConfig.tiny(num_key_value_heads=4)
+    hf = transformers.LlamaForCausalLM(_hf_config(c)).eval()
+    ours = from_hf(hf).eval()
+    ids = torch.randint(1, 512, (2, 16))
+    out = hf(input_ids=ids, labels=ids)
+    loss, logits = ours(ids, labels=ids)
+    assert torch.allclose(logits, out.logits, atol=5e-5, rtol=1e-4)
+    assert abs(float(loss) - float(out.loss)) < 1e-5
+
+
+def test_tied_lm_head_and_param_count():
+    from nbdistributed_amd.models.llama import LlamaForCausalLM
+
+    m = LlamaForCausalLM(LlamaConfig.smollm2_135m())
+    assert m.lm_head.weight is m.model.embed_tokens.weight
+    assert sum(p.numel() for p in m.parameters()) == 134_515_008  # SmolLM2-135M
