@@ -38,7 +38,7 @@ def capture(name, fn):
     torch.cuda.synchronize()
     print(f"[{name}] capture", flush=True)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         out = fn()
     torch.cuda.synchronize()
     print(f"[{name}] replay", flush=True)

@@ -7,14 +7,18 @@
 // benchmarks/ddp_compare.py flatgraph).  This version only uses caching-allocator memory and
 // fixed launch shapes, so it captures and replays, and it is cheaper:
 //
-//   count   counts[v] = #tokens with id v                (int atomics)
-//   scan    offsets = exclusive_scan(counts), one 1024-thread workgroup (two passes over V)
-//   place   slot = offsets[v] + atomicAdd(cursor[v]) ; order[slot] = token position
-//   rows    one wave per vocabulary row: Σ dY[order[offsets[v] .. offsets[v+1])] in fp32, written
-//           once in the weight's dtype (zeros for rows no token touched) — the gradient is written
-//           exactly once, no zero-fill pass and no float atomics.
-// Summation order inside a row follows the atomic slot order (not bitwise run-to-run stable; DDP
-// ranks still agree after the all-reduce).
+//   count    counts[v] = #tokens with id v                (int atomics)
+//   scan     offsets = exclusive_scan(counts): per-1024 block scans + block sums, then each block
+//            adds the sum of the blocks before it (two fully parallel launches)
+//   place    slot = offsets[v] + atomicAdd(cursor[v]) ; order[slot] = token position
+//   partial  one wave per 16 consecutive sorted slots: runs of equal ids are summed in fp32 and
+//            flushed with float atomics into acc[offsets[v]] (a [N, C] scratch) — a frequent id
+//            (padding!) is spread over many waves instead of one wave looping over hundreds of
+//            occurrences (which took 550 µs per step on the notebook's right-padded batches)
+//   rows     one wave per vocabulary row: cast acc[offsets[v]] (or zeros) into the gradient —
+//            written exactly once, no separate zero-fill.
+// Float atomics make the summation order run-to-run dependent (DDP ranks still agree after the
+// all-reduce).
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -39,30 +43,38 @@ __global__ __launch_bounds__(NT) void count_kernel(const int64_t* __restrict__ i
   }
 }
 
-// exclusive scan of counts[0..V) into offsets[0..V]; one workgroup
-__global__ __launch_bounds__(kScanT) void scan_kernel(const int* __restrict__ counts, int V,
-                                                      int* __restrict__ offsets) {
+// exclusive scan of counts[0..V) into offsets[0..V], pass 1: block-local scans + block sums
+__global__ __launch_bounds__(kScanT) void scan_local_kernel(const int* __restrict__ counts, int V,
+                                                            int* __restrict__ offsets, int* __restrict__ bsum) {
   __shared__ int part[kScanT];
   const int t = threadIdx.x;
-  const int per = (V + kScanT - 1) / kScanT;
-  const int b = t * per, e = min(V, b + per);
-  int s = 0;
-  for (int i = b; i < e; ++i) s += counts[i];
-  part[t] = s;
+  const int i = blockIdx.x * kScanT + t;
+  const int c = i < V ? counts[i] : 0;
+  part[t] = c;
   __syncthreads();
-  // Hillis-Steele inclusive scan over the 1024 partial sums
-  for (int off = 1; off < kScanT; off <<= 1) {
+  for (int off = 1; off < kScanT; off <<= 1) {  // Hillis-Steele inclusive scan
     const int add = t >= off ? part[t - off] : 0;
     __syncthreads();
     part[t] += add;
     __syncthreads();
   }
-  int run = part[t] - s;  // exclusive prefix of this thread's range
-  for (int i = b; i < e; ++i) {
-    offsets[i] = run;
-    run += counts[i];
+  if (i < V) offsets[i] = part[t] - c;
+  if (t == kScanT - 1) bsum[blockIdx.x] = part[t];
+}
+
+// pass 2: add the sum of all earlier blocks; the last block also writes offsets[V]
+__global__ __launch_bounds__(kScanT) void scan_add_kernel(int* __restrict__ offsets, int V,
+                                                          const int* __restrict__ bsum, int nblk) {
+  __shared__ int base;
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int b = 0; b < (int)blockIdx.x; ++b) s += bsum[b];
+    base = s;
   }
-  if (t == kScanT - 1) offsets[V] = part[t];
+  __syncthreads();
+  const int i = blockIdx.x * kScanT + threadIdx.x;
+  if (i < V) offsets[i] += base;
+  if (blockIdx.x == nblk - 1 && threadIdx.x == 0) offsets[V] = base + bsum[nblk - 1];
 }
 
 __global__ __launch_bounds__(NT) void place_kernel(const int64_t* __restrict__ idx, int64_t n, int V,
@@ -100,36 +112,75 @@ __device__ __forceinline__ void st4(T* p, const float (&v)[4]) {
   }
 }
 
-// one wave per vocabulary row; a lane owns 4-column chunks c = 4·lane + 256·k, k < NCH
+// one wave per 16 sorted slots: sum runs of equal ids, flush each run into acc[offsets[id]]
+constexpr int kSlots = 16;
+
 template <typename T, int NCH>
-__global__ __launch_bounds__(NT) void rows_kernel(const T* __restrict__ dy, int C, const int* __restrict__ offsets,
-                                                  const int* __restrict__ order, int V, T* __restrict__ grad) {
+__global__ __launch_bounds__(NT) void partial_kernel(const T* __restrict__ dy, int C, const int64_t* __restrict__ idx,
+                                                     const int* __restrict__ offsets, const int* __restrict__ order,
+                                                     int V, float* __restrict__ acc) {
   const int lane = threadIdx.x & 63;
-  const int64_t v = (int64_t)blockIdx.x * (NT / kWave) + (threadIdx.x >> 6);
-  if (v >= V) return;
-  float acc[NCH][4];
+  const int64_t s0 = ((int64_t)blockIdx.x * (NT / kWave) + (threadIdx.x >> 6)) * kSlots;
+  const int n_valid = offsets[V];  // placed (in-range) tokens; never read unwritten slots of `order`
+  if (s0 >= n_valid) return;
+  const int s1 = (int)min<int64_t>(s0 + kSlots, n_valid);
+  float run[NCH][4];
+  int cur = -1;
+  auto flush = [&](int v) {
+    float* dst = acc + (int64_t)offsets[v] * C;
 #pragma unroll
-  for (int k = 0; k < NCH; ++k)
+    for (int k = 0; k < NCH; ++k) {
+      const int c = 4 * lane + 256 * k;
+      if (c < C)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) acc[k][e] = 0.f;
-  const int b = offsets[v], e = offsets[v + 1];
-  for (int j = b; j < e; ++j) {
-    const int64_t row = order[j];
+        for (int e = 0; e < 4; ++e) atomicAdd(dst + c + e, run[k][e]);
+    }
+  };
+  for (int s = (int)s0; s < s1; ++s) {
+    const int row = order[s];
+    const int v = (int)idx[row];
+    if (v != cur) {
+      if (cur >= 0) flush(cur);
+      cur = v;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) run[k][e] = 0.f;
+    }
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       const int c = 4 * lane + 256 * k;
       if (c < C) {
         float x[4];
-        ld4<T>(dy + row * C + c, x);
+        ld4<T>(dy + (int64_t)row * C + c, x);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[k][q] += x[q];
+        for (int e = 0; e < 4; ++e) run[k][e] += x[e];
       }
     }
   }
+  if (cur >= 0) flush(cur);
+}
+
+// one wave per vocabulary row; a lane owns 4-column chunks c = 4·lane + 256·k, k < NCH
+template <typename T, int NCH>
+__global__ __launch_bounds__(NT) void rows_kernel(const float* __restrict__ acc, int C, const int* __restrict__ offsets,
+                                                  int V, T* __restrict__ grad) {
+  const int lane = threadIdx.x & 63;
+  const int64_t v = (int64_t)blockIdx.x * (NT / kWave) + (threadIdx.x >> 6);
+  if (v >= V) return;
+  const int b = offsets[v];
+  const bool hit = offsets[v + 1] > b;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int c = 4 * lane + 256 * k;
-    if (c < C) st4<T>(grad + v * C + c, acc[k]);
+    if (c < C) {
+      float x[4] = {0.f, 0.f, 0.f, 0.f};
+      if (hit) {
+        const float4 a = *reinterpret_cast<const float4*>(acc + (int64_t)b * C + c);
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+      }
+      st4<T>(grad + v * C + c, x);
+    }
   }
 }
 
@@ -160,33 +211,39 @@ at::Tensor embedding_bwd_hip(const at::Tensor& dy, const at::Tensor& idx, int64_
   at::Tensor counts = at::zeros({V + 1}, io);  // [V] counts, [V] = out-of-range flag
   at::Tensor cursor = at::zeros({V}, io);
   at::Tensor offsets = at::empty({V + 1}, io);
+  const int nsb = (int)((V + kScanT - 1) / kScanT);
+  at::Tensor bsum = at::empty({nsb}, io);
   at::Tensor order = at::empty({std::max<int64_t>(N, 1)}, io);
+  at::Tensor acc = at::zeros({std::max<int64_t>(N, 1), C}, dy.options().dtype(at::kFloat));
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   const int blocks = (int)std::min<int64_t>((N + NT - 1) / NT + 1, 1024);
   int* cnt = counts.data_ptr<int>();
   hipLaunchKernelGGL(count_kernel, dim3(blocks), dim3(NT), 0, st, idx.data_ptr<int64_t>(), N, (int)V, cnt, cnt + V);
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(kScanT), 0, st, cnt, (int)V, offsets.data_ptr<int>());
+  hipLaunchKernelGGL(scan_local_kernel, dim3(nsb), dim3(kScanT), 0, st, cnt, (int)V, offsets.data_ptr<int>(),
+                     bsum.data_ptr<int>());
+  hipLaunchKernelGGL(scan_add_kernel, dim3(nsb), dim3(kScanT), 0, st, offsets.data_ptr<int>(), (int)V,
+                     bsum.data_ptr<int>(), nsb);
   hipLaunchKernelGGL(place_kernel, dim3(blocks), dim3(NT), 0, st, idx.data_ptr<int64_t>(), N, (int)V,
                      offsets.data_ptr<int>(), cursor.data_ptr<int>(), order.data_ptr<int>());
+  // slots [0, offsets[V]) hold every in-range token; out-of-range ids are flagged and never
+  // placed, and partial_kernel stops at offsets[V] (read on the device)
+  const dim3 pgrid((unsigned)((N + kSlots * 4 - 1) / (kSlots * 4)));
   const dim3 rgrid((unsigned)((V + 3) / 4));
   dispatch_nch(C, [&](auto nch) {
     constexpr int K = decltype(nch)::value;
+    auto launch = [&](auto tag) {
+      using T = decltype(tag);
+      hipLaunchKernelGGL((partial_kernel<T, K>), pgrid, dim3(NT), 0, st, static_cast<const T*>(dy.data_ptr()), (int)C,
+                         idx.data_ptr<int64_t>(), offsets.data_ptr<int>(), order.data_ptr<int>(), (int)V,
+                         acc.data_ptr<float>());
+      hipLaunchKernelGGL((rows_kernel<T, K>), rgrid, dim3(NT), 0, st, acc.data_ptr<float>(), (int)C,
+                         offsets.data_ptr<int>(), (int)V, static_cast<T*>(grad.data_ptr()));
+    };
     switch (dy.scalar_type()) {
-      case at::kFloat:
-        hipLaunchKernelGGL((rows_kernel<float, K>), rgrid, dim3(NT), 0, st, dy.data_ptr<float>(), (int)C,
-                           offsets.data_ptr<int>(), order.data_ptr<int>(), (int)V, grad.data_ptr<float>());
-        break;
-      case at::kBFloat16:
-        hipLaunchKernelGGL((rows_kernel<bf16_t, K>), rgrid, dim3(NT), 0, st,
-                           static_cast<const bf16_t*>(dy.data_ptr()), (int)C, offsets.data_ptr<int>(),
-                           order.data_ptr<int>(), (int)V, static_cast<bf16_t*>(grad.data_ptr()));
-        break;
-      case at::kHalf:
-        hipLaunchKernelGGL((rows_kernel<f16_t, K>), rgrid, dim3(NT), 0, st, static_cast<const f16_t*>(dy.data_ptr()),
-                           (int)C, offsets.data_ptr<int>(), order.data_ptr<int>(), (int)V,
-                           static_cast<f16_t*>(grad.data_ptr()));
-        break;
+      case at::kFloat: launch(float{}); break;
+      case at::kBFloat16: launch(bf16_t{}); break;
+      case at::kHalf: launch(f16_t{}); break;
       default: TORCH_CHECK(false, "embedding_bwd: unsupported dtype ", dy.scalar_type());
     }
   });

@@ -148,15 +148,23 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const T* __restrict__ x, con
 }
 
 // ============================================================================ backward
-constexpr int kBwdRows = 16;  // rows per workgroup (4 per wave, two at a time)
+constexpr int kBwdRows = 16;  // max rows per workgroup (4 per wave, two at a time)
 constexpr int kRpi = 2;       // rows per wave iteration
+
+// rows per workgroup: 16 for large inputs (GPT-2: 8192 rows -> 512 workgroups), fewer when that
+// would leave the chip under-filled (SmolLM2 at 16 x 128 tokens: 2048 rows -> 4 per workgroup)
+static int bwd_rows_per_block(int64_t rows) {
+  int r = kBwdRows;
+  while (r > 2 && (rows + r - 1) / r < 512) r /= 2;
+  return r;
+}
 
 template <typename T, typename W, bool RES, int NCH, bool RMS = false>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                     const T* __restrict__ dres, const W* __restrict__ gamma,
                                                     const float* __restrict__ mean_in,
                                                     const float* __restrict__ rstd_in, T* __restrict__ dx,
-                                                    float* __restrict__ part_g, int64_t rows, int C) {
+                                                    float* __restrict__ part_g, int64_t rows, int C, int rpb) {
   __shared__ float red[2][NT / kWave - 1][NCH * 256];  // waves 1..3 hand their column partials to wave 0
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float g[NCH][4], ag[NCH][4], ab[NCH][4];
@@ -167,16 +175,16 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, con
     for (int e = 0; e < 4; ++e) ag[k][e] = ab[k][e] = 0.f;
     if (c < C) load4<W>(gamma + c, g[k]);
   }
-  const int64_t r0 = (int64_t)blockIdx.x * kBwdRows;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
   // each wave takes kRpi rows at a time and issues all their loads before any arithmetic
-  for (int i = wave * kRpi; i < kBwdRows; i += (NT / kWave) * kRpi) {
+  for (int i = wave * kRpi; i < rpb; i += (NT / kWave) * kRpi) {
     float xv[kRpi][NCH][4], dv[kRpi][NCH][4], rv[kRpi][NCH][4];
     float mean[kRpi], rstd[kRpi];
     bool live[kRpi];
 #pragma unroll
     for (int j = 0; j < kRpi; ++j) {
       const int64_t row = r0 + i + j;
-      live[j] = row < rows;
+      live[j] = row < rows && i + j < rpb;
       const int64_t rr = live[j] ? row : r0;  // dead rows re-read a live one; their results are dropped
       mean[j] = RMS ? 0.f : mean_in[rr];
       rstd[j] = rstd_in[rr];
@@ -436,7 +444,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_hip(const at::Tensor& x, c
               "ln_bwd: mean/rstd must be float32 [rows]");
   at::Tensor dx = at::empty_like(x);
   at::Tensor dw = at::empty({C}, weight.options()), db = at::empty({C}, weight.options());
-  const int nblk = (int)((rows + kBwdRows - 1) / kBwdRows);
+  const int rpb = bwd_rows_per_block(rows);
+  const int nblk = (int)((rows + rpb - 1) / rpb);
   if (rows == 0) return {dx, dw.zero_(), db.zero_()};
   auto fo = x.options().dtype(at::kFloat);
   at::Tensor pg = at::empty({nblk, 2 * C}, fo);
@@ -452,12 +461,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_hip(const at::Tensor& x, c
       hipLaunchKernelGGL((ln_bwd_kernel<T, W, true, N>), dim3(nblk), dim3(NT), 0, st,
                          static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
                          static_cast<const W*>(weight.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C);
+                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C, rpb);
     else
       hipLaunchKernelGGL((ln_bwd_kernel<T, W, false, N>), dim3(nblk), dim3(NT), 0, st,
                          static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
                          static_cast<const W*>(weight.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C);
+                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C, rpb);
    });
   });
   C10_HIP_KERNEL_LAUNCH_CHECK();
@@ -526,7 +535,8 @@ std::tuple<at::Tensor, at::Tensor> rms_bwd_hip(const at::Tensor& x, const at::Te
   TORCH_CHECK(rstd.numel() == rows && rstd.scalar_type() == at::kFloat, "rms_bwd: rstd must be float32 [rows]");
   at::Tensor dx = at::empty_like(x);
   at::Tensor dw = at::empty({C}, weight.options()), db = at::empty({C}, weight.options());
-  const int nblk = (int)((rows + kBwdRows - 1) / kBwdRows);
+  const int rpb = bwd_rows_per_block(rows);
+  const int nblk = (int)((rows + rpb - 1) / rpb);
   if (rows == 0) return {dx, dw.zero_()};
   at::Tensor pg = at::empty({nblk, 2 * C}, x.options().dtype(at::kFloat));
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -541,12 +551,12 @@ std::tuple<at::Tensor, at::Tensor> rms_bwd_hip(const at::Tensor& x, const at::Te
       hipLaunchKernelGGL((ln_bwd_kernel<T, W, true, N, true>), dim3(nblk), dim3(NT), 0, st,
                          static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
                          static_cast<const W*>(weight.data_ptr()), rstd.data_ptr<float>(), rstd.data_ptr<float>(),
-                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C);
+                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C, rpb);
     else
       hipLaunchKernelGGL((ln_bwd_kernel<T, W, false, N, true>), dim3(nblk), dim3(NT), 0, st,
                          static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
                          static_cast<const W*>(weight.data_ptr()), rstd.data_ptr<float>(), rstd.data_ptr<float>(),
-                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C);
+                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C, rpb);
    });
   });
   C10_HIP_KERNEL_LAUNCH_CHECK();

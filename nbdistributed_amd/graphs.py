@@ -37,6 +37,22 @@ def _copy_into(dst, src):
         raise ValueError("GraphedStep: non-tensor arguments are baked into the graph and must not change")
 
 
+def _drain_collective_watchdog(poll_s: float = 0.35) -> None:
+    """ProcessGroupNCCL's watchdog thread polls the events of outstanding collectives (every
+    ~100 ms) and retires completed ones.  Warm-up collectives still on its list when capture
+    starts get their (recycled) events queried mid-capture, which aborts the process
+    ("operation not permitted when stream is capturing" / "... on an event last recorded in a
+    capturing stream").  After a device sync every warm-up collective is complete; give the
+    watchdog a few polling periods to drop them.  Collectives issued during capture are never
+    put on its list."""
+    import time
+
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        time.sleep(poll_s)
+
+
 class GraphedStep:
     """``step = GraphedStep(fn, example_args, optimizers=[opt])``; ``out = step(*args)``.
 
@@ -63,9 +79,13 @@ class GraphedStep:
                 fn(*self.static_args)
         cur.wait_stream(side)
         torch.cuda.synchronize()
+        _drain_collective_watchdog()
         self.graph = torch.cuda.CUDAGraph()
         self._sync_hyper()
-        with torch.cuda.graph(self.graph, pool=pool):
+        # thread_local: only this thread's calls are checked during capture — ProcessGroupNCCL's
+        # watchdog thread keeps querying its events meanwhile, which "global" mode turns into a
+        # hipErrorStreamCaptureUnsupported abort (seen intermittently on this stack)
+        with torch.cuda.graph(self.graph, pool=pool, capture_error_mode="thread_local"):
             self.static_out = fn(*self.static_args)
         torch.cuda.synchronize()
 
