@@ -1,0 +1,149 @@
+"""LayerNorm / RMSNorm with fused residual adds, bias-gradient column sums, Linear (K8, K9, K11)."""
+from __future__ import annotations
+
+from ._lib import _require
+from .llama import _llama_fns
+
+
+_NormFns = None
+
+def _norm_fns():
+    global _NormFns
+    if _NormFns is not None:
+        return _NormFns
+    import torch
+
+    def _c(t):
+        return t if t.is_contiguous() else t.contiguous()
+
+    class _LayerNorm(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w, b, eps):
+            y, _, mean, rstd = torch.ops.nbd.ln_fwd(x, None, w, b, eps)
+            ctx.save_for_backward(x, w, mean, rstd)
+            return y
+
+        @staticmethod
+        def backward(ctx, dy):
+            x, w, mean, rstd = ctx.saved_tensors
+            dx, dw, db = torch.ops.nbd.ln_bwd(x, _c(dy), None, w, mean, rstd)
+            return dx, dw, db, None
+
+    class _AddLayerNorm(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, delta, w, b, eps):
+            y, s, mean, rstd = torch.ops.nbd.ln_fwd(x, delta, w, b, eps)
+            ctx.save_for_backward(s, w, mean, rstd)
+            return s, y
+
+        @staticmethod
+        def backward(ctx, ds, dy):
+            s, w, mean, rstd = ctx.saved_tensors
+            if dy is None:
+                return ds, ds, None, None, None
+            dx, dw, db = torch.ops.nbd.ln_bwd(s, _c(dy), None if ds is None else _c(ds), w, mean, rstd)
+            return dx, dx, dw, db, None
+
+    class _Linear(torch.autograd.Function):
+        """F.linear forward (hipBLASLt, bias fused in the epilogue); backward with the two GEMMs
+        and the bias gradient from the HIP column-sum kernel."""
+
+        @staticmethod
+        def forward(ctx, x, w, b):
+            ctx.save_for_backward(x, w)
+            ctx.has_bias = b is not None
+            return torch.nn.functional.linear(x, w, b)
+
+        @staticmethod
+        def backward(ctx, dy):
+            x, w = ctx.saved_tensors
+            dy2 = _c(dy).view(-1, dy.shape[-1])
+            dx = dw = db = None
+            if ctx.needs_input_grad[0]:
+                dx = (dy2 @ w).view(x.shape)
+            if ctx.needs_input_grad[1]:
+                dw = dy2.t() @ _c(x).view(-1, x.shape[-1])
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                db = torch.ops.nbd.colsum(dy2, w.dtype)
+            return dx, dw, db
+
+    _NormFns = (_LayerNorm, _AddLayerNorm, _Linear)
+    return _NormFns
+
+def _norm_ok(x, C: int) -> bool:
+    import torch
+
+    return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32) and C % 8 == 0 and C <= 2048
+            and not torch.is_autocast_enabled())
+
+def layer_norm(x, weight, bias, eps: float = 1e-5):
+    """LayerNorm over the last dim (HIP kernels on GPU; ``F.layer_norm`` otherwise)."""
+    import torch.nn.functional as F
+
+    C = x.shape[-1]
+    if _norm_ok(x, C) and weight is not None and bias is not None and weight.dtype == x.dtype:
+        _require()
+        return _norm_fns()[0].apply(x if x.is_contiguous() else x.contiguous(), weight, bias, float(eps))
+    return F.layer_norm(x, (C,), weight, bias, eps)
+
+def add_layer_norm(x, delta, weight, bias, eps: float = 1e-5):
+    """``s = x + delta; return s, LayerNorm(s)`` — the residual add and the norm in one HIP pass
+    (and their backward in one pass: dx includes the residual stream's gradient)."""
+    import torch.nn.functional as F
+
+    C = x.shape[-1]
+    if (_norm_ok(x, C) and weight is not None and bias is not None and weight.dtype == x.dtype
+            and delta.dtype == x.dtype and delta.shape == x.shape):
+        _require()
+        return _norm_fns()[1].apply(x if x.is_contiguous() else x.contiguous(),
+                                    delta if delta.is_contiguous() else delta.contiguous(), weight, bias, float(eps))
+    s = x + delta
+    return s, F.layer_norm(s, (C,), weight, bias, eps)
+
+def linear(x, weight, bias=None):
+    """``F.linear`` whose backward computes the bias gradient with the HIP column-sum kernel."""
+    import torch.nn.functional as F
+
+    import torch
+
+    if (bias is not None and x.is_cuda and weight.shape[0] % 8 == 0 and x.dtype == weight.dtype == bias.dtype
+            and x.dtype in (torch.bfloat16, torch.float16, torch.float32) and not torch.is_autocast_enabled()):
+        _require()
+        return _norm_fns()[2].apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+def colsum(x, dtype=None):
+    """Σ over all rows of ``x`` [..., C] (fp32 accumulation), as ``dtype`` (default x.dtype)."""
+    import torch
+
+    C = x.shape[-1]
+    if x.is_cuda and C % 8 == 0:
+        _require()
+        return torch.ops.nbd.colsum(x if x.is_contiguous() else x.contiguous(), dtype or x.dtype)
+    return x.reshape(-1, C).float().sum(0).to(dtype or x.dtype)
+
+def _rms_ok(x, w) -> bool:
+    import torch
+
+    C = x.shape[-1]
+    return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32) and C % 8 == 0 and C <= 2048
+            and w.dtype == x.dtype and not torch.is_autocast_enabled())
+
+def rms_norm(x, weight, eps: float = 1e-6):
+    """RMSNorm over the last dim: ``x · rsqrt(mean(x²) + eps) · weight`` (HIP on GPU)."""
+    import torch
+
+    if _rms_ok(x, weight):
+        _require()
+        return _llama_fns()[0].apply(x if x.is_contiguous() else x.contiguous(), weight, float(eps))
+    xf = x.float()
+    return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype) * weight
+
+def add_rms_norm(x, delta, weight, eps: float = 1e-6):
+    """``s = x + delta; return s, RMSNorm(s)`` in one HIP pass (and one for the backward)."""
+    if _rms_ok(x, weight) and delta.dtype == x.dtype and delta.shape == x.shape:
+        _require()
+        return _llama_fns()[1].apply(x if x.is_contiguous() else x.contiguous(),
+                                     delta if delta.is_contiguous() else delta.contiguous(), weight, float(eps))
+    s = x + delta
+    return s, rms_norm(s, weight, eps)
