@@ -25,6 +25,10 @@
 // Causal: workgroups are launched heaviest-first; fully masked tiles are skipped per wave.
 // GQA: query head h reads key/value head h / group; dkdv runs per key/value head and sweeps its
 // group of query heads, accumulating dK/dV in the same registers (no atomics).
+// RoPE (optional, Llama family): q and k are rotated as they are loaded (Q/K fragments in
+// registers; K/Q tiles between the global load and the LDS store, one thread holding both halves
+// of a row chunk) and dQ/dK get the transpose rotation in the store epilogue — the packed
+// projection stays unrotated and no separate rotary kernels or gradient copies run.
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -105,6 +109,78 @@ __device__ __forceinline__ void store_dT(uint16_t* rowp, const f16x& c, int db, 
   }
 }
 
+// rotary embedding fused into the loads (HF rotate_half convention): dims d and d+32 of a row
+// rotate by the angle of (row position, d); cos/sin = [T_max, 32] fp32 tables, nullptr = no RoPE
+struct Rope {
+  const float* cos;
+  const float* sin;
+};
+
+// rotate 8 consecutive dims [d0, d0+8) of x (with their partners d+32 in y) for position t
+__device__ __forceinline__ void rope8(s8v& x, s8v& y, const Rope& rp, int t, int d0) {
+  const float4* c4 = reinterpret_cast<const float4*>(rp.cos + (int64_t)t * 32 + d0);
+  const float4* s4 = reinterpret_cast<const float4*>(rp.sin + (int64_t)t * 32 + d0);
+  const float4 ca = c4[0], cb = c4[1], sa = s4[0], sb = s4[1];
+  const float c[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
+  const float sn[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float a = bf16_to_f32((uint16_t)x[j]), b = bf16_to_f32((uint16_t)y[j]);
+    x[j] = (short)bf(a * c[j] - b * sn[j]);
+    y[j] = (short)bf(b * c[j] + a * sn[j]);
+  }
+}
+
+// Q or K fragments of one row held in registers (element s covers dims 16s + 8h + [0, 8)):
+// pairs (f[0], f[2]) and (f[1], f[3])
+__device__ __forceinline__ void rope_frag(s8v (&f)[4], const Rope& rp, int t, int h) {
+  rope8(f[0], f[2], rp, t, 8 * h);
+  rope8(f[1], f[3], rp, t, 16 + 8 * h);
+}
+
+// dQ/dK tiles: acc0 holds dims [0, 32), acc1 dims [32, 64) — a d/d+32 pair shares register i of
+// one lane, so the transpose rotation (gradient of the forward rotation) is applied right here
+__device__ __forceinline__ void store_dT_rope(uint16_t* rowp, const f16x& a0, const f16x& a1, int h, float mul,
+                                              const Rope& rp, int t) {
+  const float* cr = rp.cos + (int64_t)t * 32;
+  const float* sr = rp.sin + (int64_t)t * 32;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    uint16_t lo[4], hi[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int d = 8 * g + 4 * h + e;
+      const float x = a0[4 * g + e] * mul, y = a1[4 * g + e] * mul;
+      lo[e] = bf(x * cr[d] + y * sr[d]);
+      hi[e] = bf(y * cr[d] - x * sr[d]);
+    }
+    const int d = 8 * g + 4 * h;
+    *reinterpret_cast<uint2*>(rowp + d) =
+        make_uint2((uint32_t)lo[0] | ((uint32_t)lo[1] << 16), (uint32_t)lo[2] | ((uint32_t)lo[3] << 16));
+    *reinterpret_cast<uint2*>(rowp + 32 + d) =
+        make_uint2((uint32_t)hi[0] | ((uint32_t)hi[1] << 16), (uint32_t)hi[2] | ((uint32_t)hi[3] << 16));
+  }
+}
+
+// tile staging with the two halves of a row in one thread (row = tid/4, chunks q and q+4), so
+// the rotation can be applied between the global load and the LDS store
+struct StagePair {
+  s8v a, b;
+  __device__ __forceinline__ void load(const uint16_t* base, int64_t st, int tid) {
+    const uint16_t* p = base + (tid >> 2) * st + (tid & 3) * 8;
+    a = ld16(p);
+    b = ld16(p + 32);
+  }
+  __device__ __forceinline__ void rope(const Rope& rp, int t0, int tid) {
+    if (rp.cos != nullptr) rope8(a, b, rp, t0 + (tid >> 2), (tid & 3) * 8);
+  }
+  __device__ __forceinline__ void store(uint16_t* lds, int stride, int tid) const {
+    uint16_t* p = lds + (tid >> 2) * stride + (tid & 3) * 8;
+    st16(p, a);
+    st16(p + 32, b);
+  }
+};
+
 // cooperative tile staging: 64 rows x 64 d, 512 16-B chunks, 2 per thread
 struct Stage2 {
   s8v a[2];
@@ -127,7 +203,7 @@ struct Stage2 {
 // ============================================================================ forward
 template <bool CAUSAL>
 __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MView o, float* __restrict__ lse,
-                                                     int H, int T, int nblk, float sc2, int group) {
+                                                     int H, int T, int nblk, float sc2, int group, Rope rp) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[TILE * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[TILE * RSV];
   const int bh = blockIdx.x % (gridDim.x / nblk);
@@ -140,12 +216,15 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
   s8v qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qf[s] = ld16(q.row(b, hh, qi) + 16 * s + 8 * h);
+  if (rp.cos != nullptr) rope_frag(qf, rp, qi, h);
   f16x acc_o[2] = {zero16(), zero16()};
   float m = -INFINITY, l = 0.f;
   const int ntiles = CAUSAL ? (qb * BLK + BLK) / TILE : T / TILE;
-  Stage2 sk, sv;
+  StagePair sk;
+  Stage2 sv;
   sk.load(k.row(b, kh, 0), k.st, tid);
   sv.load(v.row(b, kh, 0), v.st, tid);
+  sk.rope(rp, 0, tid);
   sk.store(Ks, RS, tid);
   sv.store(Vs, RSV, tid);
   __syncthreads();
@@ -207,6 +286,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
     }
     __syncthreads();
     if (t + 1 < ntiles) {
+      sk.rope(rp, (t + 1) * TILE, tid);
       sk.store(Ks, RS, tid);
       sv.store(Vs, RSV, tid);
       __syncthreads();
@@ -246,7 +326,8 @@ template <bool CAUSAL>
 __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v, View dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta, MView dk, MView dv, int H,
-                                                          int T, int nblk, float sc2, float scale, int group) {
+                                                          int T, int nblk, float sc2, float scale, int group,
+                                                          Rope rp) {
   // H = key/value heads (the grid); query heads hq = kvh·group + g, g < group
   __shared__ __attribute__((aligned(16))) uint16_t Qs[TILE * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Os[TILE * RS];  // dO tile
@@ -266,6 +347,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v,
     kf[s] = ld16(k.row(b, kvh, ki) + 16 * s + 8 * h);
     vf[s] = ld16(v.row(b, kvh, ki) + 16 * s + 8 * h);
   }
+  if (rp.cos != nullptr) rope_frag(kf, rp, ki, h);
   f16x dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
   const int t0 = CAUSAL ? (kb0 * BLK) / TILE : 0;
   const int nt = T / TILE;
@@ -273,7 +355,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v,
     const int hq = kvh * group + g;
     const float* lse_bh = lse + ((int64_t)b * Hq + hq) * T;
     const float* del_bh = delta + ((int64_t)b * Hq + hq) * T;
-    Stage2 sq, so;
+    StagePair sq;
+    Stage2 so;
     float lv = 0.f, dlv = 0.f;
     sq.load(q.row(b, hq, t0 * TILE), q.st, tid);
     so.load(dout.row(b, hq, t0 * TILE), dout.st, tid);
@@ -282,6 +365,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v,
       dlv = del_bh[t0 * TILE + tid];
     }
     if (g > 0) __syncthreads();  // the previous head's last tile is still being read
+    sq.rope(rp, t0 * TILE, tid);
     sq.store(Qs, RS, tid);
     so.store(Os, RS, tid);
     if (tid < TILE) {
@@ -339,6 +423,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v,
       }
       __syncthreads();
       if (t + 1 < nt) {
+        sq.rope(rp, (t + 1) * TILE, tid);
         sq.store(Qs, RS, tid);
         so.store(Os, RS, tid);
         if (tid < TILE) {
@@ -351,8 +436,12 @@ __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v,
   }
   uint16_t* dkr = dk.row(b, kvh, ki);
   uint16_t* dvr = dv.row(b, kvh, ki);
-  store_dT(dkr, dkt[0], 0, h, scale);
-  store_dT(dkr, dkt[1], 1, h, scale);
+  if (rp.cos != nullptr) {
+    store_dT_rope(dkr, dkt[0], dkt[1], h, scale, rp, ki);
+  } else {
+    store_dT(dkr, dkt[0], 0, h, scale);
+    store_dT(dkr, dkt[1], 1, h, scale);
+  }
   store_dT(dvr, dvt[0], 0, h, 1.f);
   store_dT(dvr, dvt[1], 1, h, 1.f);
 }
@@ -362,7 +451,7 @@ template <bool CAUSAL>
 __global__ __launch_bounds__(NT, 2) void bwd_dq_kernel(View q, View k, View v, View dout,
                                                         const float* __restrict__ lse, const float* __restrict__ delta,
                                                         MView dq, int H, int T, int nblk, float sc2, float scale,
-                                                        int group) {
+                                                        int group, Rope rp) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[TILE * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[TILE * RS];
   const int per = gridDim.x / nblk;
@@ -379,13 +468,16 @@ __global__ __launch_bounds__(NT, 2) void bwd_dq_kernel(View q, View k, View v, V
     qf[s] = ld16(q.row(b, hh, qi) + 16 * s + 8 * h);
     of[s] = ld16(dout.row(b, hh, qi) + 16 * s + 8 * h);
   }
+  if (rp.cos != nullptr) rope_frag(qf, rp, qi, h);
   const float l2 = lse[(int64_t)bh * T + qi] * kLog2e;
   const float dl = delta[(int64_t)bh * T + qi];
   f16x dqt[2] = {zero16(), zero16()};
   const int ntiles = CAUSAL ? (qb * BLK + BLK) / TILE : T / TILE;
-  Stage2 sk, sv;
+  StagePair sk;
+  Stage2 sv;
   sk.load(k.row(b, kh, 0), k.st, tid);
   sv.load(v.row(b, kh, 0), v.st, tid);
+  sk.rope(rp, 0, tid);
   sk.store(Ks, RS, tid);
   sv.store(Vs, RS, tid);
   __syncthreads();
@@ -426,14 +518,19 @@ __global__ __launch_bounds__(NT, 2) void bwd_dq_kernel(View q, View k, View v, V
     }
     __syncthreads();
     if (t + 1 < ntiles) {
+      sk.rope(rp, (t + 1) * TILE, tid);
       sk.store(Ks, RS, tid);
       sv.store(Vs, RS, tid);
       __syncthreads();
     }
   }
   uint16_t* dqr = dq.row(b, hh, qi);
-  store_dT(dqr, dqt[0], 0, h, scale);
-  store_dT(dqr, dqt[1], 1, h, scale);
+  if (rp.cos != nullptr) {
+    store_dT_rope(dqr, dqt[0], dqt[1], h, scale, rp, qi);
+  } else {
+    store_dT(dqr, dqt[0], 0, h, scale);
+    store_dT(dqr, dqt[1], 1, h, scale);
+  }
 }
 
 // ============================================================================ host
@@ -458,9 +555,22 @@ static void check_shapes(const at::Tensor& q, const at::Tensor& k, const at::Ten
   TORCH_CHECK(q.size(0) * q.size(1) * (q.size(2) / BLK) < (1LL << 31), "attn: grid too large");
 }
 
+static Rope rope_of(const c10::optional<at::Tensor>& c, const c10::optional<at::Tensor>& s, int64_t T) {
+  const bool hc = c.has_value() && c->defined(), hs = s.has_value() && s->defined();
+  TORCH_CHECK(hc == hs, "attn: rope_cos and rope_sin go together");
+  if (!hc) return Rope{nullptr, nullptr};
+  TORCH_CHECK(c->is_cuda() && s->is_cuda() && c->scalar_type() == at::kFloat && s->scalar_type() == at::kFloat &&
+                  c->is_contiguous() && s->is_contiguous() && c->dim() == 2 && c->size(1) == D / 2 &&
+                  s->sizes() == c->sizes() && c->size(0) >= T,
+              "attn: rope tables must be contiguous float32 [>= T, 32]");
+  return Rope{c->data_ptr<float>(), s->data_ptr<float>()};
+}
+
 std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                                bool causal, double scale) {
+                                                bool causal, double scale, const c10::optional<at::Tensor>& rope_cos,
+                                                const c10::optional<at::Tensor>& rope_sin) {
   check_shapes(q, k, v);
+  const Rope rp = rope_of(rope_cos, rope_sin, q.size(2));
   const int B = q.size(0), H = q.size(1), T = q.size(2);
   View qv = view_of(q, "q"), kv = view_of(k, "k"), vv = view_of(v, "v");
   // output stored [B, T, H, D] (what the projection after attention reads), returned as [B, H, T, D]
@@ -475,18 +585,20 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::T
   const int group = H / (int)k.size(1);
   if (causal)
     hipLaunchKernelGGL((fwd_kernel<true>), grid, dim3(NT), 0, st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
-                       sc2, group);
+                       sc2, group, rp);
   else
     hipLaunchKernelGGL((fwd_kernel<false>), grid, dim3(NT), 0, st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
-                       sc2, group);
+                       sc2, group, rp);
   C10_HIP_KERNEL_LAUNCH_CHECK();
   return {o, lse};
 }
 
 void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                   const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
-                  const at::Tensor& dk, const at::Tensor& dv) {
+                  const at::Tensor& dk, const at::Tensor& dv, const c10::optional<at::Tensor>& rope_cos,
+                  const c10::optional<at::Tensor>& rope_sin) {
   check_shapes(q, k, v);
+  const Rope rp = rope_of(rope_cos, rope_sin, q.size(2));
   TORCH_CHECK(dout.sizes() == q.sizes() && out.sizes() == q.sizes() && dq.sizes() == q.sizes() &&
                   dk.sizes() == k.sizes() && dv.sizes() == v.sizes(),
               "attn_bwd: shape mismatch");
@@ -509,14 +621,14 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
   const float sc2 = (float)scale * kLog2e;
   if (causal) {
     hipLaunchKernelGGL((bwd_dkdv_kernel<true>), kvgrid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dkv, dvv, Hkv, T, nblk, sc2, (float)scale, group);
+                       delta.data_ptr<float>(), dkv, dvv, Hkv, T, nblk, sc2, (float)scale, group, rp);
     hipLaunchKernelGGL((bwd_dq_kernel<true>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale, group);
+                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale, group, rp);
   } else {
     hipLaunchKernelGGL((bwd_dkdv_kernel<false>), kvgrid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dkv, dvv, Hkv, T, nblk, sc2, (float)scale, group);
+                       delta.data_ptr<float>(), dkv, dvv, Hkv, T, nblk, sc2, (float)scale, group, rp);
     hipLaunchKernelGGL((bwd_dq_kernel<false>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale, group);
+                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale, group, rp);
   }
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }

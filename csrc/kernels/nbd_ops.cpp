@@ -9,9 +9,10 @@ TORCH_LIBRARY(nbd, m) {
   m.def("bucket_unflatten(Tensor bucket, Tensor(a!)[] tensors, int[] offsets, float scale, bool accumulate) -> ()");
   m.def("local_prereduce(Tensor[] inputs, Tensor(a!) out, float scale) -> ()");
   m.def("tensor_summary(Tensor x) -> Tensor");
-  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, Tensor? rope_cos=None, "
+        "Tensor? rope_sin=None) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale, "
-        "Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
+        "Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor? rope_cos=None, Tensor? rope_sin=None) -> ()");
   m.def("ln_fwd(Tensor x, Tensor? delta, Tensor weight, Tensor bias, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("ln_bwd(Tensor x, Tensor dy, Tensor? dres, Tensor weight, Tensor mean, Tensor rstd) -> (Tensor, Tensor, Tensor)");
   m.def("colsum(Tensor x, ScalarType dtype) -> Tensor");

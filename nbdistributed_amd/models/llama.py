@@ -6,7 +6,7 @@ small-batch step is launch-bound (≈4,600 kernels, GPU busy 25 ms of a 40 ms st
 ``profiles/notebook_prof_r1.md``).  This implementation keeps HF's weights and numerics
 (``from_hf`` / ``load_hf_state_dict``) but runs a block as:
 
-    x ─ rms_norm ─ qkv GEMM (fused q|k|v) ─ rope_ (in place) ─ flash attention (GQA) ─ o GEMM ─┐
+    x ─ rms_norm ─ qkv GEMM (fused q|k|v) ─ flash attention (GQA, RoPE fused into its loads) ─ o GEMM ─┐
     └──────────────────────────── add_rms_norm (residual + norm in one pass) ◄───────────────┘
       ─ gate|up GEMM (fused) ─ swiglu ─ down GEMM ─ add_rms_norm (into the next block's norm)
 
@@ -20,8 +20,7 @@ supported).
 """
 from __future__ import annotations
 
-import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Any, Dict, Optional
 
 import torch
@@ -93,8 +92,9 @@ class LlamaAttention(nn.Module):
         self.o_proj = nn.Linear(self.H * self.D, c.hidden_size, bias=False)
 
     def forward(self, x, cos, sin):
-        qkv = ops.rope_(F.linear(x, self.qkv_proj.weight), cos, sin, self.H + self.Hkv, self.D)
-        return self.o_proj(ops.attention_qkv(qkv, self.H, causal=True, n_kv_head=self.Hkv))
+        # RoPE is applied inside the attention kernels on the HIP path (rope_ + SDPA otherwise)
+        qkv = F.linear(x, self.qkv_proj.weight)
+        return self.o_proj(ops.attention_qkv(qkv, self.H, causal=True, n_kv_head=self.Hkv, rope=(cos, sin)))
 
 
 class LlamaMLP(nn.Module):

@@ -24,7 +24,7 @@ def _attn_fns():
         @staticmethod
         def forward(ctx, q, k, v, causal, scale):
             q, k, v = _fix(q), _fix(k), _fix(v)
-            o, lse = torch.ops.nbd.attn_fwd(q, k, v, causal, scale)
+            o, lse = torch.ops.nbd.attn_fwd(q, k, v, causal, scale, None, None)
             ctx.save_for_backward(q, k, v, o, lse)
             ctx.causal, ctx.scale = causal, scale
             return o
@@ -37,7 +37,7 @@ def _attn_fns():
             dq = torch.empty(B, T, H, D, dtype=q.dtype, device=q.device).transpose(1, 2)
             dkv = torch.empty(B, T, 2, Hkv, D, dtype=q.dtype, device=q.device)
             dk, dv = dkv[:, :, 0].transpose(1, 2), dkv[:, :, 1].transpose(1, 2)
-            torch.ops.nbd.attn_bwd(_fix(do), q, k, v, o, lse, ctx.causal, ctx.scale, dq, dk, dv)
+            torch.ops.nbd.attn_bwd(_fix(do), q, k, v, o, lse, ctx.causal, ctx.scale, dq, dk, dv, None, None)
             return dq, dk, dv, None, None
 
     def _split(qkv, H, Hkv):
@@ -53,25 +53,27 @@ def _attn_fns():
         packed gradient directly (no split/cat, no transposes).  Hkv < H: grouped-query attention."""
 
         @staticmethod
-        def forward(ctx, qkv, n_head, n_kv, causal, scale):
+        def forward(ctx, qkv, n_head, n_kv, causal, scale, cos, sin):
             B, T, _ = qkv.shape
             q, k, v = _split(qkv, n_head, n_kv)
-            o, lse = torch.ops.nbd.attn_fwd(q, k, v, causal, scale)
+            o, lse = torch.ops.nbd.attn_fwd(q, k, v, causal, scale, cos, sin)
             ctx.save_for_backward(qkv, o, lse)
             ctx.n_head, ctx.n_kv, ctx.causal, ctx.scale = n_head, n_kv, causal, scale
+            ctx.rope = (cos, sin)  # constant tables (no gradient), kept by reference
             return o.transpose(1, 2).reshape(B, T, -1)  # o is stored [B, T, H, D]: a view
 
         @staticmethod
         def backward(ctx, dy):
             qkv, o, lse = ctx.saved_tensors
+            cos, sin = ctx.rope
             B, T, _ = qkv.shape
             q, k, v = _split(qkv, ctx.n_head, ctx.n_kv)
             dy = dy if dy.is_contiguous() else dy.contiguous()
             dqkv = torch.empty_like(qkv, memory_format=torch.contiguous_format)
             dq, dk, dv = _split(dqkv, ctx.n_head, ctx.n_kv)
             do = dy.view(B, T, ctx.n_head, -1).transpose(1, 2)
-            torch.ops.nbd.attn_bwd(do, q, k, v, o, lse, ctx.causal, ctx.scale, dq, dk, dv)
-            return dqkv, None, None, None, None
+            torch.ops.nbd.attn_bwd(do, q, k, v, o, lse, ctx.causal, ctx.scale, dq, dk, dv, cos, sin)
+            return dqkv, None, None, None, None, None, None
 
     _AttnFns = (_FlashAttention, _FlashAttentionQKV)
     return _AttnFns
@@ -97,10 +99,11 @@ def flash_attention(q, k, v, causal: bool = False, scale: Optional[float] = None
     return F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=sc, enable_gqa=gqa)
 
 def attention_qkv(qkv, n_head: int, causal: bool = True, scale: Optional[float] = None,
-                  n_kv_head: Optional[int] = None):
+                  n_kv_head: Optional[int] = None, rope=None):
     """Multi-head attention straight from a packed [B, T, (H + 2·Hkv)·D] projection (GPT-2's
     ``c_attn`` output, or a fused Llama q|k|v projection) to [B, T, H·D].  ``n_kv_head`` < ``n_head``
-    is grouped-query attention."""
+    is grouped-query attention.  ``rope=(cos, sin)`` (tables from ``rope_tables``) applies rotary
+    embeddings to q and k — inside the attention kernels on the HIP path."""
     import torch
     import torch.nn.functional as F
 
@@ -112,7 +115,12 @@ def attention_qkv(qkv, n_head: int, causal: bool = True, scale: Optional[float] 
             and qkv.stride(1) % 8 == 0 and qkv.stride(0) % 8 == 0 and qkv.data_ptr() % 16 == 0
             and n_head % Hkv == 0):
         _require()
-        return _attn_fns()[1].apply(qkv, int(n_head), int(Hkv), bool(causal), sc)
+        cos, sin = rope if rope is not None else (None, None)
+        return _attn_fns()[1].apply(qkv, int(n_head), int(Hkv), bool(causal), sc, cos, sin)
+    if rope is not None:
+        from .llama import rope_
+
+        qkv = rope_(qkv if qkv.is_contiguous() else qkv.contiguous(), rope[0], rope[1], n_head + Hkv, D)
     q = qkv[:, :, : n_head * D].view(B, T, n_head, D).transpose(1, 2)
     k = qkv[:, :, n_head * D:(n_head + Hkv) * D].view(B, T, Hkv, D).transpose(1, 2)
     v = qkv[:, :, (n_head + Hkv) * D:].view(B, T, Hkv, D).transpose(1, 2)

@@ -158,3 +158,21 @@ def test_llama_training_step_graph_capture(dev):
     graphed = [float(gs(ids, mask, labels)) for _ in range(3)]
     torch.cuda.synchronize()
     assert max(abs(a - b) for a, b in zip(eager[3:], graphed)) < 2e-2, (eager, graphed)
+
+
+@pytest.mark.parametrize("Hkv", [3, 9])
+def test_attention_with_fused_rope_matches_separate_rope(dev, Hkv):
+    """RoPE inside the attention kernels == rope_ kernel + attention (fwd and packed dqkv)."""
+    B, T, H, D = 2, 256, 9, 64
+    qkv = torch.randn(B, T, (H + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
+    dy = torch.randn(B, T, H * D, device=dev, dtype=torch.bfloat16)
+    cos, sin = ops.rope_tables(T, D, 100000.0, dev)
+    a = qkv.clone().requires_grad_(True)
+    y1 = ops.attention_qkv(a, H, causal=True, n_kv_head=Hkv, rope=(cos, sin))
+    y1.backward(dy)
+    b = qkv.clone().requires_grad_(True)
+    y2 = ops.attention_qkv(ops.rope_(b * 1, cos, sin, H + Hkv, D), H, causal=True, n_kv_head=Hkv)
+    y2.backward(dy)
+    torch.cuda.synchronize()
+    assert _rel(y1, y2) < 1e-2, _rel(y1, y2)
+    assert _rel(a.grad, b.grad) < 2e-2, _rel(a.grad, b.grad)
