@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — headline benchmark of nbdistributed_amd (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--sweep]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-sweep]
 
 Single GPU (default): this process plays rank 0.  Multi-GPU: launched by the driver as
 ``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`` — every torchrun
@@ -35,7 +35,9 @@ def _args(argv=None):
     ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--sweep", action="store_true", help="also run the 1 KiB..1 GiB all_reduce sweep")
+    ap.add_argument("--sweep", action="store_true", default=True, help=argparse.SUPPRESS)  # the default now
+    ap.add_argument("--no-sweep", dest="sweep", action="store_false",
+                    help="skip the 1 KiB..1 GiB all_reduce bus-bandwidth sweep")
     ap.add_argument("--no-allreduce", action="store_true")
     ap.add_argument("--ar-bytes", type=int, default=1 << 30)
     ap.add_argument("--no-ddp", action="store_true", help="skip the DDP phases (configs 4 and 5)")
@@ -100,8 +102,8 @@ def main(argv=None) -> int:
         # started before this process touches the GPU; a child, never an exec
         cmd = [sys.executable, os.path.abspath(__file__), "--coordinator", "--endpoint", endpoint, "--world", str(world),
                "--steps", str(a.steps), "--warmup", str(a.warmup), "--out", out_path, "--ar-bytes", str(a.ar_bytes)]
-        if a.sweep:
-            cmd.append("--sweep")
+        if not a.sweep:
+            cmd.append("--no-sweep")
         if a.no_allreduce:
             cmd.append("--no-allreduce")
         if a.no_ddp:

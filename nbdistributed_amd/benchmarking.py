@@ -233,7 +233,8 @@ def bench_sweep(session, dtype: str = "bfloat16", max_bytes: int = 1 << 30, min_
     while b <= max_bytes:
         iters = 50 if b <= (16 << 20) else 20
         r = bench_allreduce(session, b, dtype, iters=iters, warm=5)
-        out.append({k: r[k] for k in ("bytes", "time_ms", "algbw_GBps", "busbw_GBps")})
+        out.append({"bytes": r["bytes"], "time_ms": round(r["time_ms"], 5), "algbw_GBps": round(r["algbw_GBps"], 2),
+                    "busbw_GBps": None if r["busbw_GBps"] is None else round(r["busbw_GBps"], 2)})
         b *= 4
     return out
 
@@ -486,8 +487,14 @@ def result_line(res: Dict[str, Any], n: int, steps: int, warmup: int) -> Dict[st
         line["allreduce_algbw_GBps"] = round(ar["algbw_GBps"], 2)
         line["allreduce_busbw_GBps"] = None if ar["busbw_GBps"] is None else round(ar["busbw_GBps"], 2)
         line["allreduce_correct"] = ar["correct"]
-    if res.get("sweep"):
-        line["allreduce_sweep"] = res["sweep"]
+    sw = res.get("sweep")
+    if isinstance(sw, list) and sw:
+        line["allreduce_sweep"] = sw
+        bus = [r["busbw_GBps"] for r in sw if r.get("busbw_GBps") is not None]
+        if bus:
+            line["allreduce_peak_busbw_GBps"] = round(max(bus), 2)
+    elif isinstance(sw, dict):
+        line["allreduce_sweep_error"] = sw.get("error") or sw.get("skipped")
     if res.get("aborted"):
         line["aborted_phase"] = res["aborted"]
     for k in ("ddp", "rank_broadcast", "notebook"):

@@ -34,6 +34,14 @@ def test_ddp_phase_multi_rank(sess):
     assert r["torch_ddp_ms_per_step"] > 0 and r["linear4096"]["ms_per_step"] > 0
 
 
+def test_allreduce_sweep_multi_rank(sess):
+    sw = B.bench_sweep(sess, max_bytes=1 << 14, min_bytes=1 << 10)
+    assert [r["bytes"] for r in sw] == [1024, 4096, 16384] and all(r["busbw_GBps"] is not None for r in sw)
+    cells = {"p50_ms": 1.0, "p90_ms": 1.0, "min_ms": 1.0, "mean_ms": 1.0}
+    line = B.result_line({"cell": cells, "sweep": sw}, 2, 1, 1)
+    assert line["allreduce_peak_busbw_GBps"] == max(r["busbw_GBps"] for r in sw)
+
+
 def test_notebook_phase_multi_rank(sess):
     r = B.bench_notebook(sess, steps=2, warmup=1, small=True)
     for mode in ("reference", "nbd"):
