@@ -1,0 +1,410 @@
+// gemm.hip — bf16 GEMM on the gfx950 matrix cores with fused epilogues, for the Linear layers of
+// the GPT-2 / Llama workloads (forward, input-gradient and weight-gradient products).
+//
+//   C[M,N] = Σ_k A[m,k]·B[k,n]   (fp32 accumulation, v_mfma_f32_16x16x32_bf16)
+//
+// Operand storage (row-major, unit stride innermost; `ld*` = row stride in elements):
+//   A: [M][K] ("row image": K-contiguous)    or  [K][M] (a_km: "transposed image")
+//   B: [N][K] ("row image")                  or  [K][N] (b_kn: "transposed image")
+// so the three products of a Linear y = x·Wᵀ are all direct, with no transposed copies:
+//   forward  y  = x·Wᵀ   A = x  [M][K],  B = W  [N][K]            (row, row)
+//   dgrad    dx = dy·W   A = dy [M][N],  B = W  [N][K] as [K][N]  (row, tr)
+//   wgrad    dW = dyᵀ·x  A = dy as [K][M], B = x as [K][N]        (tr, tr)
+//
+// Structure (cdna_hip_programming.md §5 "minimum 2-phase" + T1 + T2 + T10):
+//   * workgroup = 4 waves (2×2), tile BM×BN×64, each wave a (BM/2)×(BN/2) sub-tile of 16×16 MFMA
+//     fragments; two LDS buffers: the next K-tile streams global→LDS with 16-byte
+//     `global_load_lds_dwordx4` (no VGPR round trip) while the current one feeds the MFMAs.
+//   * LDS images are lane-linear (the DMA writes base + 16·lane), so the bank-conflict swizzles
+//     are applied to the per-lane *global source* address and undone on the LDS read:
+//       row image  [R][64] (128-B rows): 16-B chunk c of row r lives at chunk c ^ ((r>>1)&7) —
+//                  every 16-lane ds_read_b128 group of a 16x16x32 fragment hits 16 distinct slots;
+//       tr image   [64][R]: 8-B slot s of k-row k lives at s ^ h(k), h chosen so the 32 lanes of
+//                  each ds_read_b64_tr_b16 half (k rows {q, 8+q}, 4 column blocks) are distinct.
+//     The transposed image is read with ds_read_b64_tr_b16 (hardware transpose, T10): that is
+//     what lets dgrad / wgrad consume W, dy and x in their natural storage.
+//   * The MFMA is fed (B-fragment, A-fragment), i.e. it computes Cᵀ: each lane then holds 4
+//     consecutive output columns of one row → 8-byte stores, and bias / GELU operands are
+//     loaded 4-wide in the epilogue.
+//   * blockIdx → tile: bijective XCD remap (T1) then 8-row groups sweeping the column tiles, so
+//     the blocks sharing an A row panel run on the same XCD's L2.
+//   * split-K (grid.y) writes fp32 slabs; reduce_kernel sums them (weight gradients: K = tokens).
+// Epilogues: + bias[n]; GELU-tanh (stores the pre-activation for the backward too);
+// dGELU (multiplies by gelu'(pre-activation) — the MLP's activation backward fused into the
+// dgrad of its output projection); fp32 slab (split-K).
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include "nbd_common.h"
+
+namespace nbd {
+namespace gemm {
+
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4v lds_s4v;
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+enum Epi : int { EPI_NONE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3 };
+
+struct Args {
+  const uint16_t* a;
+  const uint16_t* b;
+  void* c;
+  const uint16_t* bias;    // [N] or nullptr
+  const uint16_t* aux_in;  // EPI_DGELU: pre-activation [M][ldc]
+  uint16_t* aux_out;       // EPI_GELU: pre-activation out [M][ldc]
+  int M, N, K;             // K = reduction length handled by one split
+  int64_t lda, ldb, ldc;
+  int tiles_m, tiles_n;
+};
+
+// ---- swizzles ---------------------------------------------------------------------------------
+__device__ __forceinline__ int row_swz(int r) { return (r >> 1) & 7; }  // 16-B chunk XOR, row image
+template <int R>
+__device__ __forceinline__ int tr_swz(int k) {  // 8-B slot XOR, tr image with R-element rows
+  if constexpr (R >= 128)
+    return ((k & 3) | (((k >> 3) & 1) << 2)) << 2;
+  else
+    return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 2;
+}
+
+__device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
+                                   (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
+}
+
+// Stage one 64-deep K-tile of an operand into its LDS image.  R = tile rows (BM or BN).
+// TR = false: global [rows][k] (row r0.., k0..), image [R][64]; TR = true: global [k][rows], image [64][R].
+template <int R, bool TR>
+__device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld, int r0, int k0, uint8_t* img,
+                                      int wave, int lane) {
+  constexpr int PER_WAVE = R / 32;  // (R*64*2 B) / (4 waves * 1 KiB)
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int wbase = (i * 4 + wave) * 1024;
+    const int byte = wbase + lane * 16;
+    const uint16_t* src;
+    if constexpr (!TR) {
+      const int r = byte >> 7, pc = (byte >> 4) & 7;
+      src = g + (int64_t)(r0 + r) * ld + k0 + 8 * (pc ^ row_swz(r));
+    } else {
+      constexpr int RB = 2 * R;
+      const int k = byte / RB, pc = (byte % RB) >> 4;
+      src = g + (int64_t)(k0 + k) * ld + r0 + 8 * (pc ^ (tr_swz<R>(k) >> 1));
+    }
+    glds16(src, img + wbase);
+  }
+}
+
+// 16x16x32 operand fragment (lane l: rows/cols r0 + (l&15), k = 32kk + 8(l>>4) + 0..7)
+template <int R, bool TR>
+__device__ __forceinline__ s8v frag(const uint8_t* img, int r0, int kk, int lane) {
+  if constexpr (!TR) {
+    const int r = r0 + (lane & 15), c = (lane >> 4) + 4 * kk;
+    return *reinterpret_cast<const s8v*>(img + r * 128 + ((c ^ row_swz(r)) << 4));
+  } else {
+    constexpr int RB = 2 * R;
+    const int i = lane & 15, g = lane >> 4;
+    const int k = 32 * kk + 8 * g + (i >> 2);
+    const int slot = ((r0 + 4 * (i & 3)) >> 2) ^ tr_swz<R>(k);
+    const uint8_t* p = img + k * RB + slot * 8;
+    const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p));
+    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p + 4 * RB));
+    s8v r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  }
+}
+
+constexpr float kBeta = 0.7978845608028654f;  // sqrt(2/pi)
+constexpr float kKappa = 0.044715f;
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float t = tanhf(kBeta * (x + kKappa * x * x * x));
+  return 0.5f * x * (1.f + t);
+}
+__device__ __forceinline__ float dgelu_tanh(float x) {  // d gelu / dx (torch's GeluBackward, tanh)
+  const float x2 = x * x;
+  const float t = tanhf(kBeta * (x + kKappa * x2 * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kBeta * (1.f + 3.f * kKappa * x2);
+}
+
+__device__ __forceinline__ void ld4(const uint16_t* p, float (&v)[4]) {
+  const uint2 w = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(w.x << 16);
+  v[1] = __uint_as_float(w.x & 0xffff0000u);
+  v[2] = __uint_as_float(w.y << 16);
+  v[3] = __uint_as_float(w.y & 0xffff0000u);
+}
+__device__ __forceinline__ void st4(uint16_t* p, const float (&v)[4]) {
+  uint2 w;
+  w.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+  w.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = w;
+}
+
+template <int BM, int BN, bool A_KM, bool B_KN, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
+  constexpr int FM = BM / 32, FN = BN / 32;  // 16-wide fragments per wave along m / n
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, BUF = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * BUF];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-aware bijective remap, then 8-row groups sweeping the column tiles
+  const int nwg = p.tiles_m * p.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  constexpr int G = 8;
+  const int per_group = G * p.tiles_n;
+  const int first_m = (bid / per_group) * G;
+  const int gsz = min(p.tiles_m - first_m, G);
+  const int local = bid % per_group;
+  const int tm = first_m + local % gsz, tn = local / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // split-K: grid.y selects the K range
+  const int64_t kz = (int64_t)blockIdx.y * p.K;
+  const uint16_t* A = p.a + (A_KM ? kz * p.lda : kz);
+  const uint16_t* B = p.b + (B_KN ? kz * p.ldb : kz);
+
+  f4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / BK;
+  stage<BM, A_KM>(A, p.lda, m0, 0, smem, wave, lane);
+  stage<BN, B_KN>(B, p.ldb, n0, 0, smem + A_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int t = 0; t < nk; ++t) {
+    uint8_t* cur = smem + (t & 1) * BUF;
+    if (t + 1 < nk) {
+      uint8_t* nxt = smem + ((t + 1) & 1) * BUF;
+      stage<BM, A_KM>(A, p.lda, m0, (t + 1) * BK, nxt, wave, lane);
+      stage<BN, B_KN>(B, p.ldb, n0, (t + 1) * BK, nxt + A_BYTES, wave, lane);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s8v af[FM], bf[FN];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) af[j] = frag<BM, A_KM>(cur, wm * (BM / 2) + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < FN; ++i) bf[i] = frag<BN, B_KN>(cur + A_BYTES, wn * (BN / 2) + 16 * i, kk, lane);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[i], af[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j] element e = C[m][n], m = .. + (lane&15), n = .. + 4(lane>>4) + e
+  const int mb = m0 + wm * (BM / 2) + (lane & 15);
+  const int nb = n0 + wn * (BN / 2) + 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int n = nb + 16 * i;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (EPI != EPI_F32 && EPI != EPI_DGELU && p.bias) ld4(p.bias + n, bias);
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int m = mb + 16 * j;
+      const int64_t off = (int64_t)m * p.ldc + n;
+      if constexpr (EPI == EPI_F32) {
+        float* c = static_cast<float*>(p.c) + (int64_t)blockIdx.y * p.M * p.ldc;
+        *reinterpret_cast<f4*>(c + off) = acc[i][j];
+      } else {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bias[e];
+        if constexpr (EPI == EPI_GELU) {
+          st4(p.aux_out + off, v);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+        } else if constexpr (EPI == EPI_DGELU) {
+          float h[4];
+          ld4(p.aux_in + off, h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= dgelu_tanh(h[e]);
+        }
+        st4(static_cast<uint16_t*>(p.c) + off, v);
+      }
+    }
+  }
+}
+
+// out[i] = Σ_s ws[s][i] as bf16; 8 elements per thread
+__global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ ws, int splits, int64_t n8, int64_t slab,
+                                                     uint16_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float v[8];
+    load8<float>(ws + 8 * i, v);
+    for (int s = 1; s < splits; ++s) {
+      float w[8];
+      load8<float>(ws + s * slab + 8 * i, w);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += w[e];
+    }
+    store8<bf16_t>(reinterpret_cast<bf16_t*>(out) + 8 * i, v);
+  }
+}
+
+// ---- host --------------------------------------------------------------------------------------
+struct Tile {
+  int bm, bn;
+};
+
+template <bool A_KM, bool B_KN, int EPI>
+static void launch_epi(const Tile& t, const Args& a, dim3 grid, hipStream_t st) {
+#define NBD_GEMM_CASE(BM_, BN_)                                                              \
+  if (t.bm == BM_ && t.bn == BN_) {                                                          \
+    hipLaunchKernelGGL((gemm_kernel<BM_, BN_, A_KM, B_KN, EPI>), grid, dim3(NT), 0, st, a); \
+    return;                                                                                  \
+  }
+  NBD_GEMM_CASE(128, 128)
+  NBD_GEMM_CASE(128, 64)
+  NBD_GEMM_CASE(64, 128)
+  NBD_GEMM_CASE(64, 64)
+#undef NBD_GEMM_CASE
+  TORCH_CHECK(false, "nbd::gemm: no kernel for tile ", t.bm, "x", t.bn);
+}
+
+template <bool A_KM, bool B_KN>
+static void launch_layout(int epi, const Tile& t, const Args& a, dim3 grid, hipStream_t st) {
+  switch (epi) {
+    case EPI_NONE: launch_epi<A_KM, B_KN, EPI_NONE>(t, a, grid, st); return;
+    case EPI_F32: launch_epi<A_KM, B_KN, EPI_F32>(t, a, grid, st); return;
+    case EPI_GELU:
+      if constexpr (!A_KM && !B_KN) {
+        launch_epi<false, false, EPI_GELU>(t, a, grid, st);
+        return;
+      }
+      break;
+    case EPI_DGELU:
+      if constexpr (!A_KM && B_KN) {
+        launch_epi<false, true, EPI_DGELU>(t, a, grid, st);
+        return;
+      }
+      break;
+    default: break;
+  }
+  TORCH_CHECK(false, "nbd::gemm: epilogue ", epi, " not built for this layout");
+}
+
+static bool tile_fits(const Tile& t, int M, int N) { return M % t.bm == 0 && N % t.bn == 0; }
+
+// The largest tile that still gives about one workgroup per CU (256 CUs); a hint (BM*1000+BN)
+// overrides it.
+static Tile pick_tile(int M, int N, int64_t tile_hint) {
+  if (tile_hint > 0) {
+    Tile t{(int)(tile_hint / 1000), (int)(tile_hint % 1000)};
+    TORCH_CHECK(tile_fits(t, M, N), "nbd::gemm: tile ", t.bm, "x", t.bn, " does not divide ", M, "x", N);
+    return t;
+  }
+  const Tile cands[4] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  int best = -1;
+  for (int i = 0; i < 4; ++i) {
+    if (!tile_fits(cands[i], M, N)) continue;
+    best = i;
+    if ((int64_t)(M / cands[i].bm) * (N / cands[i].bn) >= 256) break;
+  }
+  TORCH_CHECK(best >= 0, "nbd::gemm: M=", M, " N=", N, " not divisible by 64");
+  return cands[best];
+}
+
+// c = A·B with the layouts above; c is [M][N] bf16 (contiguous).
+void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_km, bool b_kn,
+              const c10::optional<at::Tensor>& bias, int64_t epi, const c10::optional<at::Tensor>& aux_in,
+              const c10::optional<at::Tensor>& aux_out, int64_t splits, int64_t tile_hint) {
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "nbd::gemm: 2-D operands");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kBFloat16,
+              "nbd::gemm: bf16 operands");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && c.is_contiguous(), "nbd::gemm: contiguous operands");
+  const int M = a_km ? a.size(1) : a.size(0);
+  const int K = a_km ? a.size(0) : a.size(1);
+  const int N = b_kn ? b.size(1) : b.size(0);
+  const int Kb = b_kn ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "nbd::gemm: K mismatch ", K, " vs ", Kb);
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "nbd::gemm: output shape");
+  TORCH_CHECK(K % BK == 0 && K > 0, "nbd::gemm: K % 64 != 0");
+  TORCH_CHECK(!(a_km && !b_kn), "nbd::gemm: layout (A [K][M], B [N][K]) not built");
+  for (const at::Tensor* x : {&a, &b, &c})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x->data_ptr()) % 16 == 0, "nbd::gemm: 16-byte aligned operands");
+  if (bias) {
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == N && bias->scalar_type() == at::kBFloat16, "nbd::gemm: bias");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0, "nbd::gemm: bias alignment");
+  }
+  if (epi == EPI_GELU)
+    TORCH_CHECK(aux_out && aux_out->sizes() == c.sizes() && aux_out->is_contiguous() &&
+                    aux_out->scalar_type() == at::kBFloat16, "nbd::gemm: aux_out");
+  if (epi == EPI_DGELU)
+    TORCH_CHECK(aux_in && aux_in->sizes() == c.sizes() && aux_in->is_contiguous() &&
+                    aux_in->scalar_type() == at::kBFloat16, "nbd::gemm: aux_in");
+  TORCH_CHECK(epi >= EPI_NONE && epi <= EPI_DGELU, "nbd::gemm: epilogue ", epi);
+  const Tile t = pick_tile(M, N, tile_hint);
+  const int tiles = (M / t.bm) * (N / t.bn);
+  const int S = splits > 0 ? (int)splits : 1;
+  TORCH_CHECK(S == 1 || (epi == EPI_NONE && !bias), "nbd::gemm: split-K only without an epilogue");
+  TORCH_CHECK(K % (BK * S) == 0, "nbd::gemm: K not divisible into ", S, " splits");
+
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  Args p;
+  p.a = static_cast<const uint16_t*>(a.data_ptr());
+  p.b = static_cast<const uint16_t*>(b.data_ptr());
+  p.bias = bias ? static_cast<const uint16_t*>(bias->data_ptr()) : nullptr;
+  p.aux_in = aux_in ? static_cast<const uint16_t*>(aux_in->data_ptr()) : nullptr;
+  p.aux_out = aux_out ? static_cast<uint16_t*>(aux_out->data_ptr()) : nullptr;
+  p.M = M;
+  p.N = N;
+  p.K = K / S;
+  p.lda = a.size(1);
+  p.ldb = b.size(1);
+  p.ldc = N;
+  p.tiles_m = M / t.bm;
+  p.tiles_n = N / t.bn;
+  const dim3 grid(tiles, S);
+  at::Tensor ws;
+  int e = (int)epi;
+  if (S > 1) {
+    ws = at::empty({S, M, N}, a.options().dtype(at::kFloat));
+    p.c = ws.data_ptr();
+    e = EPI_F32;
+  } else {
+    p.c = c.data_ptr();
+  }
+  if (!a_km && !b_kn)
+    launch_layout<false, false>(e, t, p, grid, st);
+  else if (!a_km && b_kn)
+    launch_layout<false, true>(e, t, p, grid, st);
+  else
+    launch_layout<true, true>(e, t, p, grid, st);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  if (S > 1) {
+    const int64_t n8 = (int64_t)M * N / 8;
+    const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 2048);
+    hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, static_cast<const float*>(ws.data_ptr()), S, n8,
+                       (int64_t)M * N, static_cast<uint16_t*>(c.data_ptr()));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+}
+
+}  // namespace gemm
+}  // namespace nbd
+
+TORCH_LIBRARY_IMPL(nbd, CUDA, m) { m.impl("gemm", &nbd::gemm::gemm_hip); }

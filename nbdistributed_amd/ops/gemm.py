@@ -1,0 +1,176 @@
+"""bf16 GEMM on the MI355X matrix cores with fused epilogues (K12, ``csrc/kernels/gemm.hip``).
+
+``matmul`` is the raw product with the three operand layouts of a Linear layer (forward
+``x·Wᵀ``, input gradient ``dy·W``, weight gradient ``dyᵀ·x`` — no transposed copies);
+``gemm_linear`` and ``mlp_gelu`` are autograd functions built on it.  ``mlp_gelu`` is GPT-2's
+MLP (``c_proj(gelu_tanh(c_fc(x)))``) with the activation fused into the GEMM epilogues: the
+forward GEMM writes both the pre-activation and GELU(pre), the backward dgrad of ``c_proj``
+multiplies by GELU'(pre) as it stores — no separate elementwise kernels either way.
+
+Shapes the kernel does not cover (a dimension not a multiple of 64, non-bf16, CPU) fall back
+to PyTorch (hipBLASLt on ROCm) with identical semantics.
+"""
+from __future__ import annotations
+
+from ._lib import _require
+
+EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
+
+
+def gemm_ok(M: int, N: int, K: int) -> bool:
+    return M > 0 and N > 0 and K > 0 and M % 64 == 0 and N % 64 == 0 and K % 64 == 0
+
+
+def _splits(M: int, N: int, K: int) -> int:
+    """split-K for long-reduction, few-tile products (weight gradients, K = tokens)."""
+    tiles = (M // 64) * (N // 64)
+    s = 1
+    while tiles * s < 512 and K % (64 * 2 * s) == 0 and K // (2 * s) >= 1024 and s < 8:
+        s *= 2
+    return s
+
+
+def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = EPI_NONE, aux=None, out=None,
+           splits: int = 0, tile: int = 0):
+    """C[M,N] = A·B.  ``a`` is [M,K] (or [K,M] with ``a_km``), ``b`` is [N,K] (or [K,N] with
+    ``b_kn``).  ``epi``: EPI_NONE (+bias), EPI_GELU (+bias, returns (gelu(pre), pre)),
+    EPI_DGELU (C · gelu'(aux)).  ``splits=0`` picks split-K automatically (no-epilogue only);
+    ``tile`` = BM*1000+BN forces a tile (benchmarks)."""
+    import torch
+
+    M = a.shape[1] if a_km else a.shape[0]
+    K = a.shape[0] if a_km else a.shape[1]
+    N = b.shape[1] if b_kn else b.shape[0]
+    if a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and gemm_ok(M, N, K):
+        _require()
+        a = a if a.is_contiguous() else a.contiguous()
+        b = b if b.is_contiguous() else b.contiguous()
+        c = out if out is not None else torch.empty(M, N, device=a.device, dtype=a.dtype)
+        pre = torch.empty_like(c) if epi == EPI_GELU else None
+        if splits == 0:
+            splits = _splits(M, N, K) if (epi == EPI_NONE and bias is None) else 1
+        torch.ops.nbd.gemm(a, b, c, a_km, b_kn, bias, epi, aux, pre, splits, tile)
+        return (c, pre) if epi == EPI_GELU else c
+    # reference path (CPU / uncovered shapes): same math through PyTorch
+    A = a.t() if a_km else a
+    B = b if b_kn else b.t()
+    c = A @ B
+    if bias is not None:
+        c = c + bias
+    if epi == EPI_GELU:
+        pre = c
+        c = torch.nn.functional.gelu(pre, approximate="tanh")
+        return c, pre
+    if epi == EPI_DGELU:
+        c = _dgelu_ref(c, aux)
+    if out is not None:
+        out.copy_(c)
+        return out
+    return c
+
+
+def _dgelu_ref(g, pre):
+    import torch
+
+    x = pre.float()
+    k = 0.7978845608028654
+    t = torch.tanh(k * (x + 0.044715 * x * x * x))
+    d = 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k * (1 + 3 * 0.044715 * x * x)
+    return (g.float() * d).to(g.dtype)
+
+
+_Fns = None
+
+
+def _fns():
+    global _Fns
+    if _Fns is not None:
+        return _Fns
+    import torch
+
+    def _c(t):
+        return t if t.is_contiguous() else t.contiguous()
+
+    def _colsum(x2, dtype):
+        return torch.ops.nbd.colsum(x2, dtype) if x2.is_cuda else x2.float().sum(0).to(dtype)
+
+    class _Linear(torch.autograd.Function):
+        """y = x·Wᵀ + b on the HIP GEMM; backward = dgrad + wgrad GEMMs + column-sum bias grad."""
+
+        @staticmethod
+        def forward(ctx, x, w, b):
+            x2 = _c(x).view(-1, x.shape[-1])
+            ctx.save_for_backward(x2, w)
+            ctx.xshape = x.shape
+            ctx.has_bias = b is not None
+            y = matmul(x2, w, bias=b)
+            return y.view(*x.shape[:-1], w.shape[0])
+
+        @staticmethod
+        def backward(ctx, dy):
+            x2, w = ctx.saved_tensors
+            dy2 = _c(dy).view(-1, dy.shape[-1])
+            dx = dw = db = None
+            if ctx.needs_input_grad[0]:
+                dx = matmul(dy2, w, b_kn=True).view(ctx.xshape)
+            if ctx.needs_input_grad[1]:
+                dw = matmul(dy2, x2, a_km=True, b_kn=True)
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                db = _colsum(dy2, w.dtype)
+            return dx, dw, db
+
+    class _MLPGelu(torch.autograd.Function):
+        """y = c_proj(gelu_tanh(c_fc(x))) with GELU / GELU' in the GEMM epilogues."""
+
+        @staticmethod
+        def forward(ctx, x, w1, b1, w2, b2):
+            x2 = _c(x).view(-1, x.shape[-1])
+            g, pre = matmul(x2, w1, bias=b1, epi=EPI_GELU)
+            y = matmul(g, w2, bias=b2)
+            ctx.save_for_backward(x2, w1, w2, pre, g)
+            ctx.xshape = x.shape
+            ctx.bias = (b1 is not None, b2 is not None)
+            return y.view(*x.shape[:-1], w2.shape[0])
+
+        @staticmethod
+        def backward(ctx, dy):
+            x2, w1, w2, pre, g = ctx.saved_tensors
+            dy2 = _c(dy).view(-1, dy.shape[-1])
+            dpre = matmul(dy2, w2, b_kn=True, epi=EPI_DGELU, aux=pre)
+            dw2 = matmul(dy2, g, a_km=True, b_kn=True)
+            db2 = _colsum(dy2, w2.dtype) if ctx.bias[1] else None
+            dx = matmul(dpre, w1, b_kn=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+            dw1 = matmul(dpre, x2, a_km=True, b_kn=True)
+            db1 = _colsum(dpre, w1.dtype) if ctx.bias[0] else None
+            return dx, dw1, db1, dw2, db2
+
+    _Fns = (_Linear, _MLPGelu)
+    return _Fns
+
+
+def _fast(x, *ws) -> bool:
+    import torch
+
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and not torch.is_autocast_enabled()):
+        return False
+    if (x.numel() // x.shape[-1]) % 64:
+        return False
+    return all(w.dtype == torch.bfloat16 and w.shape[-1] % 64 == 0 and w.shape[0] % 64 == 0 for w in ws)
+
+
+def gemm_linear(x, weight, bias=None):
+    """``F.linear`` on the HIP MFMA GEMM (bf16, dims multiple of 64); PyTorch otherwise."""
+    if _fast(x, weight):
+        return _fns()[0].apply(x, weight, bias)
+    import torch.nn.functional as F
+
+    return F.linear(x, weight, bias)
+
+
+def mlp_gelu(x, w1, b1, w2, b2):
+    """``F.linear(gelu_tanh(F.linear(x, w1, b1)), w2, b2)`` with the activation fused into the GEMMs."""
+    if _fast(x, w1, w2):
+        return _fns()[1].apply(x, w1, b1, w2, b2)
+    import torch.nn.functional as F
+
+    return F.linear(F.gelu(F.linear(x, w1, b1), approximate="tanh"), w2, b2)

@@ -58,6 +58,7 @@ same_init = all(torch.equal(p, q) for p, q in zip(ref.module.parameters(), ours.
 def sess():
     s = Session(writer=lambda t: None)
     s.start(2, backend="gloo")
+    s.execute(SETUP, render=False)  # every test can run alone (pytest -k / xdist splits the module)
     yield s
     s.shutdown()
 
