@@ -52,12 +52,17 @@ def main():
     for impl in a.impls.split(","):
         m = copy.deepcopy(base)
         amp = True
-        if impl in ("flat", "flatgraph"):
+        if impl.endswith("blas"):  # A/B: Linear layers on hipBLASLt instead of the HIP MFMA GEMM
+            for mod in m.modules():
+                if hasattr(mod, "hip_gemm"):
+                    mod.hip_gemm = False
+        kind = impl[:-4] if impl.endswith("blas") else impl
+        if kind in ("flat", "flatgraph"):
             # bf16 parameters re-homed into the DDP buckets, fp32 master/moments inside FlatAdamW,
             # one fused HIP AdamW kernel per bucket; no autocast casts in the forward
             m = m.to(torch.bfloat16)
             w = NbdDDP(m, flat_params=True, grad_mode="bucket")
-            models[impl] = (w, FlatAdamW(w, lr=3e-4, capturable=impl == "flatgraph"), False)
+            models[impl] = (w, FlatAdamW(w, lr=3e-4, capturable=kind == "flatgraph"), False)
             continue
         if impl == "torch":
             w = torch.nn.parallel.DistributedDataParallel(m, device_ids=[local])
@@ -85,11 +90,14 @@ def main():
         return loss.detach()
 
     graphs = {}
-    if "flatgraph" in models:
+    for gk in ("flatgraph", "flatgraphblas"):
+        if gk not in models:
+            continue
         from nbdistributed_amd.graphs import GraphedStep
 
-        w, opt, amp = models["flatgraph"]
-        graphs["flatgraph"] = GraphedStep(lambda xx: step(w, opt, amp, xx), (x,), warmup=3, optimizers=[opt])
+        w, opt, amp = models[gk]
+        graphs[gk] = GraphedStep(lambda xx, w=w, opt=opt, amp=amp: step(w, opt, amp, xx), (x,), warmup=3,
+                                 optimizers=[opt])
 
     def run(k, w, opt, amp):
         if k in graphs:

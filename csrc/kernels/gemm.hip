@@ -28,10 +28,12 @@
 //     loaded 4-wide in the epilogue.
 //   * blockIdx → tile: bijective XCD remap (T1) then 8-row groups sweeping the column tiles, so
 //     the blocks sharing an A row panel run on the same XCD's L2.
-//   * split-K (grid.y) writes fp32 slabs; reduce_kernel sums them (weight gradients: K = tokens).
+//   * split-K (grid.y) for long-K products (weight gradients, K = tokens): fp32 slabs, summed by
+//     reduce_kernel in a fixed order.
+//   * epilogue staged through LDS: each thread stores 8 consecutive bf16 of a row (16 B).
 // Epilogues: + bias[n]; GELU-tanh (stores the pre-activation for the backward too);
 // dGELU (multiplies by gelu'(pre-activation) — the MLP's activation backward fused into the
-// dgrad of its output projection); fp32 slab (split-K).
+// dgrad of its output projection).
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -50,12 +52,13 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int BK = 64;
 constexpr int NT = 256;
 
-enum Epi : int { EPI_NONE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3 };
+enum Epi : int { EPI_NONE = 0, EPI_GELU = 1, EPI_DGELU = 2 };
 
 struct Args {
   const uint16_t* a;
   const uint16_t* b;
-  void* c;
+  uint16_t* c;             // [M][ldc] bf16
+  float* ws;               // split-K: [splits][M][ldc] fp32 slabs
   const uint16_t* bias;    // [N] or nullptr
   const uint16_t* aux_in;  // EPI_DGELU: pre-activation [M][ldc]
   uint16_t* aux_out;       // EPI_GELU: pre-activation out [M][ldc]
@@ -125,35 +128,33 @@ __device__ __forceinline__ s8v frag(const uint8_t* img, int r0, int kk, int lane
 
 constexpr float kBeta = 0.7978845608028654f;  // sqrt(2/pi)
 constexpr float kKappa = 0.044715f;
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float t = tanhf(kBeta * (x + kKappa * x * x * x));
-  return 0.5f * x * (1.f + t);
+// tanh(u) = 2σ(2u) − 1 with σ from v_exp_f32 + one reciprocal (libm tanhf's branchy slow path
+// made the fused epilogue cost as much as a separate elementwise pass)
+__device__ __forceinline__ float sig2(float u) { return __fdividef(1.f, 1.f + __expf(-2.f * u)); }
+__device__ __forceinline__ float gelu_tanh(float x) {  // 0.5x(1 + tanh u) = x·σ(2u)
+  return x * sig2(kBeta * (x + kKappa * x * x * x));
 }
-__device__ __forceinline__ float dgelu_tanh(float x) {  // d gelu / dx (torch's GeluBackward, tanh)
+__device__ __forceinline__ float dgelu_tanh(float x) {  // d gelu / dx = s + 2x·s(1−s)·β(1 + 3κx²), s = σ(2u)
   const float x2 = x * x;
-  const float t = tanhf(kBeta * (x + kKappa * x2 * x));
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kBeta * (1.f + 3.f * kKappa * x2);
+  const float s = sig2(kBeta * (x + kKappa * x2 * x));
+  return s + 2.f * x * s * (1.f - s) * kBeta * (1.f + 3.f * kKappa * x2);
 }
 
-__device__ __forceinline__ void ld4(const uint16_t* p, float (&v)[4]) {
-  const uint2 w = *reinterpret_cast<const uint2*>(p);
-  v[0] = __uint_as_float(w.x << 16);
-  v[1] = __uint_as_float(w.x & 0xffff0000u);
-  v[2] = __uint_as_float(w.y << 16);
-  v[3] = __uint_as_float(w.y & 0xffff0000u);
-}
-__device__ __forceinline__ void st4(uint16_t* p, const float (&v)[4]) {
-  uint2 w;
-  w.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
-  w.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
-  *reinterpret_cast<uint2*>(p) = w;
-}
+template <int BM, int BN>
+struct Smem {
+  static constexpr int BUF = (BM + BN) * BK * 2;      // one A + B K-tile pair
+  static constexpr int LDC = BN + 4;                  // fp32 C-tile row stride (+16 B: rows hit distinct banks)
+  static constexpr int CT = BM * LDC * 4;             // fp32 C tile, reuses the operand buffers after the K loop
+  static constexpr int BYTES = 2 * BUF > CT ? 2 * BUF : CT;
+};
 
 template <int BM, int BN, bool A_KM, bool B_KN, int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
   constexpr int FM = BM / 32, FN = BN / 32;  // 16-wide fragments per wave along m / n
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, BUF = A_BYTES + B_BYTES;
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * BUF];
+  constexpr int A_BYTES = BM * BK * 2, BUF = Smem<BM, BN>::BUF, LDC = Smem<BM, BN>::LDC;
+  // one __shared__ array for everything (a second LDS object de-pipelines the glds loop:
+  // cdna_hip_programming.md §5 "Projection GEMM" item 4a)
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[Smem<BM, BN>::BYTES];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -213,42 +214,67 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
     __syncthreads();
   }
 
-  // epilogue: acc[i][j] element e = C[m][n], m = .. + (lane&15), n = .. + 4(lane>>4) + e
-  const int mb = m0 + wm * (BM / 2) + (lane & 15);
-  const int nb = n0 + wn * (BN / 2) + 4 * (lane >> 4);
+  // ---- epilogue ------------------------------------------------------------------------------
+  // The fp32 tile goes through LDS (the loop's last barrier retired every operand read) so the
+  // global traffic is row-contiguous: each thread then owns 8 consecutive columns of a row —
+  // 16-B bf16 stores / aux loads, 32-B fp32 slab stores.  acc[i][j] element e = C[m][n] with
+  // m = .. + (lane&15), n = .. + 4(lane>>4) + e.
+  float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int i = 0; i < FN; ++i) {
-    const int n = nb + 16 * i;
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
-    if (EPI != EPI_F32 && EPI != EPI_DGELU && p.bias) ld4(p.bias + n, bias);
+  for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int j = 0; j < FM; ++j) {
-      const int m = mb + 16 * j;
-      const int64_t off = (int64_t)m * p.ldc + n;
-      if constexpr (EPI == EPI_F32) {
-        float* c = static_cast<float*>(p.c) + (int64_t)blockIdx.y * p.M * p.ldc;
-        *reinterpret_cast<f4*>(c + off) = acc[i][j];
-      } else {
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bias[e];
-        if constexpr (EPI == EPI_GELU) {
-          st4(p.aux_out + off, v);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
-        } else if constexpr (EPI == EPI_DGELU) {
-          float h[4];
-          ld4(p.aux_in + off, h);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] *= dgelu_tanh(h[e]);
-        }
-        st4(static_cast<uint16_t*>(p.c) + off, v);
-      }
+    for (int j = 0; j < FM; ++j)
+      *reinterpret_cast<f4*>(ct + (wm * (BM / 2) + 16 * j + (lane & 15)) * LDC + wn * (BN / 2) + 16 * i +
+                             4 * (lane >> 4)) = acc[i][j];
+  __syncthreads();
+
+  constexpr int CPR = BN / 8;  // 8-column chunks per row
+  const int S = gridDim.y;
+  if (S > 1) {
+    // split-K: this split's fp32 slab; reduce_kernel sums the slabs.  (A last-arriver in-kernel
+    // reduction measured slower here: its serial read of S-1 slabs of 16-64 KiB per tile costs
+    // more than the extra launch — profiles/gemm_bench_r1.txt.)
+    float* slab = p.ws + (int64_t)blockIdx.y * p.M * p.ldc;
+    for (int c = threadIdx.x; c < BM * CPR; c += NT) {
+      const int r = c / CPR, cn = (c % CPR) * 8;
+      float* dst = slab + (int64_t)(m0 + r) * p.ldc + n0 + cn;
+      *reinterpret_cast<f4*>(dst) = *reinterpret_cast<const f4*>(ct + r * LDC + cn);
+      *reinterpret_cast<f4*>(dst + 4) = *reinterpret_cast<const f4*>(ct + r * LDC + cn + 4);
     }
+    return;
+  }
+
+  for (int c = threadIdx.x; c < BM * CPR; c += NT) {
+    const int r = c / CPR, cn = (c % CPR) * 8;
+    float v[8];
+    {
+      const f4 lo = *reinterpret_cast<const f4*>(ct + r * LDC + cn);
+      const f4 hi = *reinterpret_cast<const f4*>(ct + r * LDC + cn + 4);
+      v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+      v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+    }
+    const int64_t off = (int64_t)(m0 + r) * p.ldc + n0 + cn;
+    if (EPI != EPI_DGELU && p.bias) {
+      float b[8];
+      load8<bf16_t>(reinterpret_cast<const bf16_t*>(p.bias) + n0 + cn, b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += b[e];
+    }
+    if constexpr (EPI == EPI_GELU) {
+      store8<bf16_t>(reinterpret_cast<bf16_t*>(p.aux_out) + off, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+    } else if constexpr (EPI == EPI_DGELU) {
+      float h[8];
+      load8<bf16_t>(reinterpret_cast<const bf16_t*>(p.aux_in) + off, h);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= dgelu_tanh(h[e]);
+    }
+    store8<bf16_t>(reinterpret_cast<bf16_t*>(p.c) + off, v);
   }
 }
 
-// out[i] = Σ_s ws[s][i] as bf16; 8 elements per thread
+// out[i] = Σ_s ws[s][i] as bf16 (fixed order: deterministic); 8 elements per thread
 __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ ws, int splits, int64_t n8, int64_t slab,
                                                      uint16_t* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
@@ -288,7 +314,6 @@ template <bool A_KM, bool B_KN>
 static void launch_layout(int epi, const Tile& t, const Args& a, dim3 grid, hipStream_t st) {
   switch (epi) {
     case EPI_NONE: launch_epi<A_KM, B_KN, EPI_NONE>(t, a, grid, st); return;
-    case EPI_F32: launch_epi<A_KM, B_KN, EPI_F32>(t, a, grid, st); return;
     case EPI_GELU:
       if constexpr (!A_KM && !B_KN) {
         launch_epi<false, false, EPI_GELU>(t, a, grid, st);
@@ -359,8 +384,8 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   const Tile t = pick_tile(M, N, tile_hint);
   const int tiles = (M / t.bm) * (N / t.bn);
   const int S = splits > 0 ? (int)splits : 1;
-  TORCH_CHECK(S == 1 || (epi == EPI_NONE && !bias), "nbd::gemm: split-K only without an epilogue");
   TORCH_CHECK(K % (BK * S) == 0, "nbd::gemm: K not divisible into ", S, " splits");
+  TORCH_CHECK(S == 1 || (epi == EPI_NONE && !bias), "nbd::gemm: split-K only without an epilogue");
 
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
@@ -379,27 +404,24 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   p.tiles_m = M / t.bm;
   p.tiles_n = N / t.bn;
   const dim3 grid(tiles, S);
+  p.c = static_cast<uint16_t*>(c.data_ptr());
   at::Tensor ws;
-  int e = (int)epi;
+  p.ws = nullptr;
   if (S > 1) {
-    ws = at::empty({S, M, N}, a.options().dtype(at::kFloat));
-    p.c = ws.data_ptr();
-    e = EPI_F32;
-  } else {
-    p.c = c.data_ptr();
+    ws = at::empty({S, M, N}, a.options().dtype(at::kFloat));  // stream-ordered (caching allocator)
+    p.ws = ws.data_ptr<float>();
   }
   if (!a_km && !b_kn)
-    launch_layout<false, false>(e, t, p, grid, st);
+    launch_layout<false, false>((int)epi, t, p, grid, st);
   else if (!a_km && b_kn)
-    launch_layout<false, true>(e, t, p, grid, st);
+    launch_layout<false, true>((int)epi, t, p, grid, st);
   else
-    launch_layout<true, true>(e, t, p, grid, st);
+    launch_layout<true, true>((int)epi, t, p, grid, st);
   C10_HIP_KERNEL_LAUNCH_CHECK();
   if (S > 1) {
     const int64_t n8 = (int64_t)M * N / 8;
     const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 2048);
-    hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, static_cast<const float*>(ws.data_ptr()), S, n8,
-                       (int64_t)M * N, static_cast<uint16_t*>(c.data_ptr()));
+    hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, p.ws, S, n8, (int64_t)M * N, p.c);
     C10_HIP_KERNEL_LAUNCH_CHECK();
   }
 }

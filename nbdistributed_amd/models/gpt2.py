@@ -32,6 +32,7 @@ class GPT2Config:
     fused_ce: bool = True  # GPU: nbd.ops.cross_entropy (HIP) instead of F.cross_entropy(logits.float())
     fused_attn: bool = True  # GPU bf16: nbd.ops.attention_qkv (HIP flash fwd/bwd) instead of SDPA
     fused_norm: bool = True  # GPU, no autocast: HIP residual-add+LayerNorm and bias-grad kernels
+    hip_gemm: bool = True  # GPU bf16 fast path: Linear layers on the HIP MFMA GEMM (GELU fused in its epilogues)
 
     @classmethod
     def small(cls):
@@ -51,14 +52,16 @@ class CausalSelfAttention(nn.Module):
         self.c_attn = nn.Linear(c.n_embd, 3 * c.n_embd, bias=c.bias)
         self.c_proj = nn.Linear(c.n_embd, c.n_embd, bias=c.bias)
         self.dropout = c.dropout
+        self.hip_gemm = c.hip_gemm
 
     def forward(self, x: torch.Tensor, fast: bool = False) -> torch.Tensor:
         B, T, C = x.shape
         if fast:  # HIP path: bias grads by the column-sum kernel, flash attention on the packed QKV
             from .. import ops
 
-            qkv = ops.linear(x, self.c_attn.weight, self.c_attn.bias)
-            return ops.linear(ops.attention_qkv(qkv, self.n_head, causal=True), self.c_proj.weight, self.c_proj.bias)
+            lin = ops.gemm_linear if self.hip_gemm else ops.linear
+            qkv = lin(x, self.c_attn.weight, self.c_attn.bias)
+            return lin(ops.attention_qkv(qkv, self.n_head, causal=True), self.c_proj.weight, self.c_proj.bias)
         qkv = self.c_attn(x)
         if self.fused and qkv.is_cuda and (self.dropout == 0.0 or not self.training):
             from .. import ops
@@ -79,11 +82,14 @@ class MLP(nn.Module):
         super().__init__()
         self.c_fc = nn.Linear(c.n_embd, 4 * c.n_embd, bias=c.bias)
         self.c_proj = nn.Linear(4 * c.n_embd, c.n_embd, bias=c.bias)
+        self.hip_gemm = c.hip_gemm
 
     def forward(self, x: torch.Tensor, fast: bool = False) -> torch.Tensor:
         if fast:
             from .. import ops
 
+            if self.hip_gemm:  # GELU and GELU' ride in the GEMM epilogues
+                return ops.mlp_gelu(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias)
             h = F.gelu(ops.linear(x, self.c_fc.weight, self.c_fc.bias), approximate="tanh")
             return ops.linear(h, self.c_proj.weight, self.c_proj.bias)
         return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))

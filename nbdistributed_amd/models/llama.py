@@ -93,8 +93,9 @@ class LlamaAttention(nn.Module):
 
     def forward(self, x, cos, sin):
         # RoPE is applied inside the attention kernels on the HIP path (rope_ + SDPA otherwise)
-        qkv = F.linear(x, self.qkv_proj.weight)
-        return self.o_proj(ops.attention_qkv(qkv, self.H, causal=True, n_kv_head=self.Hkv, rope=(cos, sin)))
+        qkv = ops.gemm_linear(x, self.qkv_proj.weight)  # HIP MFMA GEMM on GPU bf16, F.linear otherwise
+        a = ops.attention_qkv(qkv, self.H, causal=True, n_kv_head=self.Hkv, rope=(cos, sin))
+        return ops.gemm_linear(a, self.o_proj.weight)
 
 
 class LlamaMLP(nn.Module):
@@ -104,7 +105,7 @@ class LlamaMLP(nn.Module):
         self.down_proj = nn.Linear(c.intermediate_size, c.hidden_size, bias=False)
 
     def forward(self, x):
-        return self.down_proj(ops.swiglu(self.gate_up_proj(x)))
+        return ops.gemm_linear(ops.swiglu(ops.gemm_linear(x, self.gate_up_proj.weight)), self.down_proj.weight)
 
 
 class LlamaDecoderLayer(nn.Module):

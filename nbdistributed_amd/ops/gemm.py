@@ -12,7 +12,12 @@ to PyTorch (hipBLASLt on ROCm) with identical semantics.
 """
 from __future__ import annotations
 
+import os
+
 from ._lib import _require
+
+# NBD_HIP_GEMM=0 routes gemm_linear / mlp_gelu to PyTorch (hipBLASLt) — for A/B measurements
+ENABLED = os.environ.get("NBD_HIP_GEMM", "1") != "0"
 
 EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
 
@@ -21,13 +26,60 @@ def gemm_ok(M: int, N: int, K: int) -> bool:
     return M > 0 and N > 0 and K > 0 and M % 64 == 0 and N % 64 == 0 and K % 64 == 0
 
 
-def _splits(M: int, N: int, K: int) -> int:
-    """split-K for long-reduction, few-tile products (weight gradients, K = tokens)."""
-    tiles = (M // 64) * (N // 64)
-    s = 1
-    while tiles * s < 512 and K % (64 * 2 * s) == 0 and K // (2 * s) >= 1024 and s < 8:
-        s *= 2
-    return s
+# Measured best (tile BM*1000+BN, split-K) per (a_km, b_kn, M, N, K) on MI355X for the bench
+# workloads' Linear products (benchmarks/gemm_bench.py --sweep, profiles/gemm_bench_r1.txt).
+_TUNED = {
+    # GPT-2 small, 8 x 1024 tokens: forward
+    (False, False, 8192, 2304, 768): (128128, 1), (False, False, 8192, 768, 768): (128064, 1),
+    (False, False, 8192, 3072, 768): (128128, 1), (False, False, 8192, 768, 3072): (128064, 1),
+    # dgrad
+    (False, True, 8192, 768, 2304): (128064, 1), (False, True, 8192, 768, 768): (128064, 1),
+    (False, True, 8192, 768, 3072): (128064, 1), (False, True, 8192, 3072, 768): (128128, 1),
+    # wgrad (K = tokens)
+    (True, True, 2304, 768, 8192): (128128, 4), (True, True, 768, 768, 8192): (64128, 8),
+    (True, True, 3072, 768, 8192): (64128, 2), (True, True, 768, 3072, 8192): (128064, 2),
+    # SmolLM2-135M, 16 x 128 tokens
+    (False, False, 2048, 960, 576): (64064, 1), (False, False, 2048, 576, 576): (64064, 1),
+    (False, False, 2048, 3072, 576): (128064, 1), (False, False, 2048, 576, 1536): (64064, 1),
+    (False, True, 2048, 576, 960): (64064, 1), (False, True, 2048, 576, 576): (64064, 1),
+    (False, True, 2048, 576, 3072): (64064, 2), (False, True, 2048, 1536, 576): (128064, 1),
+    (True, True, 960, 576, 2048): (64064, 4), (True, True, 576, 576, 2048): (64064, 4),
+    (True, True, 3072, 576, 2048): (64064, 1), (True, True, 576, 1536, 2048): (64128, 4),
+}
+
+_TILES = (128128, 128064, 64128, 64064)
+
+
+def _ntiles(tile: int, M: int, N: int) -> int:
+    bm, bn = tile // 1000, tile % 1000
+    return (M // bm) * (N // bn) if M % bm == 0 and N % bn == 0 else 0
+
+
+def config(a_km: bool, b_kn: bool, M: int, N: int, K: int, can_split: bool = True):
+    """(tile, splits) for a product: the tuned entry when there is one, else a heuristic —
+    the largest tile with >= 1024 workgroups (128x128), else >= 256 (128x64 / 64x128), else
+    64x64; long-K products with < 400 workgroups split K (the largest tile needing <= 8 splits,
+    each split >= 512 deep) — split-K (a second, reducing kernel) only without an epilogue."""
+    hit = _TUNED.get((a_km, b_kn, M, N, K))
+    if hit is not None and (can_split or hit[1] == 1):
+        return hit
+    fits = [t for t in _TILES if _ntiles(t, M, N)]
+    if not fits:
+        return 0, 1
+    tile = fits[-1]
+    for t in fits:
+        n = _ntiles(t, M, N)
+        if n >= (1024 if t == 128128 else 256):
+            tile = t
+            break
+    if can_split and _ntiles(tile, M, N) < 400 and K >= 2048:
+        for t in fits:
+            s = 1
+            while _ntiles(t, M, N) * s < 400 and s < 8 and K % (64 * 2 * s) == 0 and K // (2 * s) >= 512:
+                s *= 2
+            if _ntiles(t, M, N) * s >= 400:
+                return t, s
+    return tile, 1
 
 
 def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = EPI_NONE, aux=None, out=None,
@@ -41,14 +93,18 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
     M = a.shape[1] if a_km else a.shape[0]
     K = a.shape[0] if a_km else a.shape[1]
     N = b.shape[1] if b_kn else b.shape[0]
-    if a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and gemm_ok(M, N, K):
+    if (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and gemm_ok(M, N, K)
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and (out is None or out.data_ptr() % 16 == 0)
+            and (bias is None or (bias.data_ptr() % 8 == 0 and bias.dtype == torch.bfloat16))):
         _require()
         a = a if a.is_contiguous() else a.contiguous()
         b = b if b.is_contiguous() else b.contiguous()
         c = out if out is not None else torch.empty(M, N, device=a.device, dtype=a.dtype)
         pre = torch.empty_like(c) if epi == EPI_GELU else None
-        if splits == 0:
-            splits = _splits(M, N, K) if (epi == EPI_NONE and bias is None) else 1
+        if splits == 0 or tile == 0:
+            t, s = config(a_km, b_kn, M, N, K, can_split=(epi == EPI_NONE and bias is None))
+            tile = tile or t
+            splits = splits or s
         torch.ops.nbd.gemm(a, b, c, a_km, b_kn, bias, epi, aux, pre, splits, tile)
         return (c, pre) if epi == EPI_GELU else c
     # reference path (CPU / uncovered shapes): same math through PyTorch
@@ -151,7 +207,7 @@ def _fns():
 def _fast(x, *ws) -> bool:
     import torch
 
-    if not (x.is_cuda and x.dtype == torch.bfloat16 and not torch.is_autocast_enabled()):
+    if not (ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and not torch.is_autocast_enabled()):
         return False
     if (x.numel() // x.shape[-1]) % 64:
         return False

@@ -145,3 +145,9 @@ def test_gemm_rejects_bad_shapes_loudly():
     # the Python entry point routes uncovered shapes to PyTorch instead
     c = G.matmul(a, b)
     assert _err(c, a.float() @ b.float().t()) < 1e-2
+
+
+def test_gemm_split_k_is_deterministic():
+    a, b = _operands(768, 768, 8192, True, True, seed=7)
+    outs = [G.matmul(a, b, a_km=True, b_kn=True, splits=8) for _ in range(3)]
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
