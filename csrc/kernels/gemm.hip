@@ -39,6 +39,8 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
+#include <type_traits>
+
 #include "nbd_common.h"
 
 namespace nbd {
@@ -77,9 +79,20 @@ __device__ __forceinline__ int tr_swz(int k) {  // 8-B slot XOR, tr image with R
     return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 2;
 }
 
+// 16-B global -> LDS DMA (global_load_lds_dwordx4: lane l lands at lds_wave_base + 16 l).
+// Issued as inline asm on purpose: hipcc cannot prove that an in-flight DMA into one pipeline
+// buffer and the ds_reads of another do not alias, and drains vmcnt(0) before the reads â€” which
+// serialises a 3-stage pipeline.  Hidden from it, the DMA is counted by our own vmcnt(N) waits
+// (cdna_hip_programming.md Â§5.7 LDS-DMA recipe: M0 saved, written and restored in one statement).
 __device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
-                                   (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(lds_wave_base));
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
 }
 
 // Stage one 64-deep K-tile of an operand into its LDS image.  R = tile rows (BM or BN).
@@ -140,21 +153,37 @@ __device__ __forceinline__ float dgelu_tanh(float x) {  // d gelu / dx = s + 2xÂ
   return s + 2.f * x * s * (1.f - s) * kBeta * (1.f + 3.f * kKappa * x2);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int STAGES>
 struct Smem {
   static constexpr int BUF = (BM + BN) * BK * 2;      // one A + B K-tile pair
   static constexpr int LDC = BN + 4;                  // fp32 C-tile row stride (+16 B: rows hit distinct banks)
   static constexpr int CT = BM * LDC * 4;             // fp32 C tile, reuses the operand buffers after the K loop
-  static constexpr int BYTES = 2 * BUF > CT ? 2 * BUF : CT;
+  static constexpr int BYTES = STAGES * BUF > CT ? STAGES * BUF : CT;
 };
 
-template <int BM, int BN, bool A_KM, bool B_KN, int EPI>
+// Wait until at most N of this wave's vector-memory ops (here: glds) are outstanding, retire
+// its LDS reads, then a raw workgroup barrier â€” no vmcnt(0) drain, so a prefetched K-tile stays
+// in flight across it (cdna_hip_programming.md Â§5 "Pipelining across barriers").
+template <int N>
+__device__ __forceinline__ void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// STAGES = 2: load tile t+1 while computing t, drain + barrier per tile (fits 2 workgroups/CU at
+// 128x128).  STAGES = 3: tile t+2 is issued while t is computed and stays in flight across the
+// barrier (counted vmcnt) â€” the latency-bound regime of few, long-K tiles (weight gradients,
+// small token counts) where one workgroup per CU cannot hide a drained pipeline.
+template <int BM, int BN, bool A_KM, bool B_KN, int EPI, int STAGES>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
   constexpr int FM = BM / 32, FN = BN / 32;  // 16-wide fragments per wave along m / n
-  constexpr int A_BYTES = BM * BK * 2, BUF = Smem<BM, BN>::BUF, LDC = Smem<BM, BN>::LDC;
+  constexpr int A_BYTES = BM * BK * 2, BUF = Smem<BM, BN, STAGES>::BUF, LDC = Smem<BM, BN, STAGES>::LDC;
+  constexpr int NPT = BM / 32 + BN / 32;  // glds per thread per K-tile
   // one __shared__ array for everything (a second LDS object de-pipelines the glds loop:
   // cdna_hip_programming.md Â§5 "Projection GEMM" item 4a)
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[Smem<BM, BN>::BYTES];
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[Smem<BM, BN, STAGES>::BYTES];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -186,18 +215,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
     for (int j = 0; j < FM; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / BK;
-  stage<BM, A_KM>(A, p.lda, m0, 0, smem, wave, lane);
-  stage<BN, B_KN>(B, p.ldb, n0, 0, smem + A_BYTES, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int t = 0; t < nk; ++t) {
-    uint8_t* cur = smem + (t & 1) * BUF;
-    if (t + 1 < nk) {
-      uint8_t* nxt = smem + ((t + 1) & 1) * BUF;
-      stage<BM, A_KM>(A, p.lda, m0, (t + 1) * BK, nxt, wave, lane);
-      stage<BN, B_KN>(B, p.ldb, n0, (t + 1) * BK, nxt + A_BYTES, wave, lane);
-    }
+  auto compute = [&](const uint8_t* cur) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       s8v af[FM], bf[FN];
@@ -210,8 +228,51 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[i], af[j], acc[i][j], 0, 0, 0);
     }
+  };
+  auto stage_tile = [&](int t, uint8_t* buf) {
+    stage<BM, A_KM>(A, p.lda, m0, t * BK, buf, wave, lane);
+    stage<BN, B_KN>(B, p.ldb, n0, t * BK, buf + A_BYTES, wave, lane);
+  };
+
+  if constexpr (STAGES == 2) {
+    stage_tile(0, smem);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      uint8_t* cur = smem + (t & 1) * BUF;
+      if (t + 1 < nk) stage_tile(t + 1, smem + ((t + 1) & 1) * BUF);
+      compute(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // buffer t % 3 holds tile t.  Before the barrier that ends step t, tile t+1 must have landed
+    // (every wave: vmcnt leaves only tile t+2's NPT loads in flight); tile t+2 is written into
+    // the buffer tile t-1 occupied, which every wave finished reading before step t-1's barrier.
+    stage_tile(0, smem);
+    if (nk > 1) {
+      stage_tile(1, smem + BUF);
+      wait_barrier<NPT>();
+    } else {
+      wait_barrier<0>();
+    }
+    // unrolled by 3 so every buffer offset is a compile-time constant: the compiler can then
+    // prove the in-flight DMA (buffer t+2) and this step's ds_reads (buffer t) disjoint and does
+    // not drain vmcnt(0) before the reads (it did with a rotating runtime index)
+    auto step = [&](int t, auto cur_c) {
+      constexpr int CUR = decltype(cur_c)::value, NXT2 = (CUR + 2) % 3;
+      if (t + 2 < nk) stage_tile(t + 2, smem + NXT2 * BUF);
+      compute(smem + CUR * BUF);
+      if (t + 2 < nk)
+        wait_barrier<NPT>();
+      else
+        wait_barrier<0>();
+    };
+    for (int t = 0; t < nk; t += 3) {
+      step(t, std::integral_constant<int, 0>{});
+      if (t + 1 < nk) step(t + 1, std::integral_constant<int, 1>{});
+      if (t + 2 < nk) step(t + 2, std::integral_constant<int, 2>{});
+    }
   }
 
   // ---- epilogue ------------------------------------------------------------------------------
@@ -292,15 +353,18 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ w
 
 // ---- host --------------------------------------------------------------------------------------
 struct Tile {
-  int bm, bn;
+  int bm, bn, stages;
 };
 
 template <bool A_KM, bool B_KN, int EPI>
 static void launch_epi(const Tile& t, const Args& a, dim3 grid, hipStream_t st) {
-#define NBD_GEMM_CASE(BM_, BN_)                                                              \
-  if (t.bm == BM_ && t.bn == BN_) {                                                          \
-    hipLaunchKernelGGL((gemm_kernel<BM_, BN_, A_KM, B_KN, EPI>), grid, dim3(NT), 0, st, a); \
-    return;                                                                                  \
+#define NBD_GEMM_CASE(BM_, BN_)                                                                   \
+  if (t.bm == BM_ && t.bn == BN_) {                                                               \
+    if (t.stages == 3)                                                                            \
+      hipLaunchKernelGGL((gemm_kernel<BM_, BN_, A_KM, B_KN, EPI, 3>), grid, dim3(NT), 0, st, a); \
+    else                                                                                          \
+      hipLaunchKernelGGL((gemm_kernel<BM_, BN_, A_KM, B_KN, EPI, 2>), grid, dim3(NT), 0, st, a); \
+    return;                                                                                       \
   }
   NBD_GEMM_CASE(128, 128)
   NBD_GEMM_CASE(128, 64)
@@ -337,11 +401,13 @@ static bool tile_fits(const Tile& t, int M, int N) { return M % t.bm == 0 && N %
 // overrides it.
 static Tile pick_tile(int M, int N, int64_t tile_hint) {
   if (tile_hint > 0) {
-    Tile t{(int)(tile_hint / 1000), (int)(tile_hint % 1000)};
+    // hint = stages*1000000 + BM*1000 + BN (stages 0 -> 2)
+    const int stg = (int)(tile_hint / 1000000);
+    Tile t{(int)(tile_hint / 1000 % 1000), (int)(tile_hint % 1000), stg == 3 ? 3 : 2};
     TORCH_CHECK(tile_fits(t, M, N), "nbd::gemm: tile ", t.bm, "x", t.bn, " does not divide ", M, "x", N);
     return t;
   }
-  const Tile cands[4] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  const Tile cands[4] = {{128, 128, 2}, {128, 64, 2}, {64, 128, 2}, {64, 64, 2}};
   int best = -1;
   for (int i = 0; i < 4; ++i) {
     if (!tile_fits(cands[i], M, N)) continue;

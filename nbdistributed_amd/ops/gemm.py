@@ -26,40 +26,44 @@ def gemm_ok(M: int, N: int, K: int) -> bool:
     return M > 0 and N > 0 and K > 0 and M % 64 == 0 and N % 64 == 0 and K % 64 == 0
 
 
-# Measured best (tile BM*1000+BN, split-K) per (a_km, b_kn, M, N, K) on MI355X for the bench
-# workloads' Linear products (benchmarks/gemm_bench.py --sweep, profiles/gemm_bench_r1.txt).
+# Measured best (kernel, split-K) per (a_km, b_kn, M, N, K) on MI355X for the bench workloads'
+# Linear products — kernel = stages*1000000 + BM*1000 + BN; from benchmarks/gemm_bench.py --sweep
+# (profiles/gemm_bench_r1.txt; split-K only where it beats the best unsplit kernel by > 5 %).
 _TUNED = {
-    # GPT-2 small, 8 x 1024 tokens: forward
-    (False, False, 8192, 2304, 768): (128128, 1), (False, False, 8192, 768, 768): (128064, 1),
-    (False, False, 8192, 3072, 768): (128128, 1), (False, False, 8192, 768, 3072): (128064, 1),
-    # dgrad
-    (False, True, 8192, 768, 2304): (128064, 1), (False, True, 8192, 768, 768): (128064, 1),
-    (False, True, 8192, 768, 3072): (128064, 1), (False, True, 8192, 3072, 768): (128128, 1),
-    # wgrad (K = tokens)
-    (True, True, 2304, 768, 8192): (128128, 4), (True, True, 768, 768, 8192): (64128, 8),
-    (True, True, 3072, 768, 8192): (64128, 2), (True, True, 768, 3072, 8192): (128064, 2),
+    # GPT-2 small, 8 x 1024 tokens: forward, dgrad, wgrad (K = tokens)
+    (False, False, 8192, 2304, 768): (2064128, 1), (False, True, 8192, 768, 2304): (2128064, 1),
+    (True, True, 2304, 768, 8192): (3064128, 2),
+    (False, False, 8192, 768, 768): (2064128, 1), (False, True, 8192, 768, 768): (2128064, 1),
+    (True, True, 768, 768, 8192): (3064064, 8),
+    (False, False, 8192, 3072, 768): (2128128, 1), (False, True, 8192, 768, 3072): (2128128, 1),
+    (True, True, 3072, 768, 8192): (3064128, 4),
+    (False, False, 8192, 768, 3072): (2128128, 1), (False, True, 8192, 3072, 768): (2128128, 1),
+    (True, True, 768, 3072, 8192): (3128064, 1),
     # SmolLM2-135M, 16 x 128 tokens
-    (False, False, 2048, 960, 576): (64064, 1), (False, False, 2048, 576, 576): (64064, 1),
-    (False, False, 2048, 3072, 576): (128064, 1), (False, False, 2048, 576, 1536): (64064, 1),
-    (False, True, 2048, 576, 960): (64064, 1), (False, True, 2048, 576, 576): (64064, 1),
-    (False, True, 2048, 576, 3072): (64064, 2), (False, True, 2048, 1536, 576): (128064, 1),
-    (True, True, 960, 576, 2048): (64064, 4), (True, True, 576, 576, 2048): (64064, 4),
-    (True, True, 3072, 576, 2048): (64064, 1), (True, True, 576, 1536, 2048): (64128, 4),
+    (False, False, 2048, 960, 576): (3064064, 1), (False, True, 2048, 576, 960): (3064064, 1),
+    (True, True, 960, 576, 2048): (3064064, 1),
+    (False, False, 2048, 576, 576): (2064064, 1), (False, True, 2048, 576, 576): (3064064, 1),
+    (True, True, 576, 576, 2048): (3064064, 1),
+    (False, False, 2048, 3072, 576): (2064128, 1), (False, True, 2048, 576, 3072): (3064064, 1),
+    (True, True, 3072, 576, 2048): (3064064, 1),
+    (False, False, 2048, 576, 1536): (3064064, 1), (False, True, 2048, 1536, 576): (2064064, 1),
+    (True, True, 576, 1536, 2048): (3064064, 1),
 }
 
 _TILES = (128128, 128064, 64128, 64064)
 
 
 def _ntiles(tile: int, M: int, N: int) -> int:
-    bm, bn = tile // 1000, tile % 1000
+    bm, bn = tile // 1000 % 1000, tile % 1000
     return (M // bm) * (N // bn) if M % bm == 0 and N % bn == 0 else 0
 
 
 def config(a_km: bool, b_kn: bool, M: int, N: int, K: int, can_split: bool = True):
-    """(tile, splits) for a product: the tuned entry when there is one, else a heuristic —
+    """(kernel, splits) for a product: the tuned entry when there is one, else a heuristic —
     the largest tile with >= 1024 workgroups (128x128), else >= 256 (128x64 / 64x128), else
-    64x64; long-K products with < 400 workgroups split K (the largest tile needing <= 8 splits,
-    each split >= 512 deep) — split-K (a second, reducing kernel) only without an epilogue."""
+    64x64; the 3-stage pipeline when there are < 512 workgroups (one per CU cannot hide a
+    drained pipeline); long-K products with < 400 workgroups split K (the largest tile needing
+    <= 8 splits, each >= 512 deep) — split-K (a second, reducing kernel) only without an epilogue."""
     hit = _TUNED.get((a_km, b_kn, M, N, K))
     if hit is not None and (can_split or hit[1] == 1):
         return hit
@@ -78,8 +82,8 @@ def config(a_km: bool, b_kn: bool, M: int, N: int, K: int, can_split: bool = Tru
             while _ntiles(t, M, N) * s < 400 and s < 8 and K % (64 * 2 * s) == 0 and K // (2 * s) >= 512:
                 s *= 2
             if _ntiles(t, M, N) * s >= 400:
-                return t, s
-    return tile, 1
+                return (3 if _ntiles(t, M, N) * s < 512 else 2) * 1000000 + t, s
+    return (3 if _ntiles(tile, M, N) < 512 else 2) * 1000000 + tile, 1
 
 
 def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = EPI_NONE, aux=None, out=None,
@@ -87,7 +91,7 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
     """C[M,N] = A·B.  ``a`` is [M,K] (or [K,M] with ``a_km``), ``b`` is [N,K] (or [K,N] with
     ``b_kn``).  ``epi``: EPI_NONE (+bias), EPI_GELU (+bias, returns (gelu(pre), pre)),
     EPI_DGELU (C · gelu'(aux)).  ``splits=0`` picks split-K automatically (no-epilogue only);
-    ``tile`` = BM*1000+BN forces a tile (benchmarks)."""
+    ``tile`` = stages*1000000 + BM*1000 + BN forces a kernel (stages 2 or 3; benchmarks)."""
     import torch
 
     M = a.shape[1] if a_km else a.shape[0]

@@ -34,8 +34,8 @@ def _err(x, ref):
 
 
 @pytest.mark.parametrize("layout", LAYOUTS, ids=["fwd", "dgrad", "wgrad"])
-@pytest.mark.parametrize("tile", [128128, 128064, 64128, 64064])
-@pytest.mark.parametrize("shape", [(256, 256, 320), (384, 640, 192)])
+@pytest.mark.parametrize("tile", [128128, 128064, 64128, 64064, 3128128, 3128064, 3064128, 3064064])
+@pytest.mark.parametrize("shape", [(256, 256, 320), (384, 640, 192), (128, 128, 64), (128, 128, 128)])
 def test_gemm_layouts_and_tiles(layout, tile, shape):
     M, N, K = shape
     a_km, b_kn = layout
