@@ -54,7 +54,9 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int BK = 64;
 constexpr int NT = 256;
 
-enum Epi : int { EPI_NONE = 0, EPI_GELU = 1, EPI_DGELU = 2 };
+// EPI_ROWSUM (weight-gradient layout): also Σ_k A[m,k] -> aux_out[m] — the Linear's bias gradient
+// (Σ over tokens of dy) from the A fragments already in registers, one extra MFMA per fragment.
+enum Epi : int { EPI_NONE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_ROWSUM = 3 };
 
 struct Args {
   const uint16_t* a;
@@ -63,7 +65,7 @@ struct Args {
   float* ws;               // split-K: [splits][M][ldc] fp32 slabs
   const uint16_t* bias;    // [N] or nullptr
   const uint16_t* aux_in;  // EPI_DGELU: pre-activation [M][ldc]
-  uint16_t* aux_out;       // EPI_GELU: pre-activation out [M][ldc]
+  uint16_t* aux_out;       // EPI_GELU: pre-activation out [M][ldc]; EPI_ROWSUM: row sums [M]
   int M, N, K;             // K = reduction length handled by one split
   int64_t lda, ldb, ldc;
   int tiles_m, tiles_n;
@@ -214,6 +216,16 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
+  // EPI_ROWSUM: the waves of the first column of tiles (tn == 0, wn == 0) own the row sums
+  constexpr bool ROWSUM = EPI == EPI_ROWSUM;
+  const bool do_rs = ROWSUM && tn == 0 && wn == 0;  // uniform per wave
+  f4 accb[FM];
+#pragma unroll
+  for (int j = 0; j < FM; ++j) accb[j] = f4{0.f, 0.f, 0.f, 0.f};
+  s8v ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;  // bf16 1.0
+
   const int nk = p.K / BK;
   auto compute = [&](const uint8_t* cur) {
 #pragma unroll
@@ -227,6 +239,12 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
       for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[i], af[j], acc[i][j], 0, 0, 0);
+      if constexpr (ROWSUM) {
+        if (do_rs) {  // D[i][m] = Σ_k 1·A[m][k], identical in every row i
+#pragma unroll
+          for (int j = 0; j < FM; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[j], accb[j], 0, 0, 0);
+        }
+      }
     }
   };
   auto stage_tile = [&](int t, uint8_t* buf) {
@@ -291,6 +309,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
 
   constexpr int CPR = BN / 8;  // 8-column chunks per row
   const int S = gridDim.y;
+  if constexpr (ROWSUM) {
+    // lanes 0..15 hold row m = .. + lane in element 0 (all four elements are equal)
+    if (do_rs && lane < 16) {
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int m = m0 + wm * (BM / 2) + 16 * j + lane;
+        if (S > 1)
+          p.ws[(int64_t)S * p.M * p.ldc + (int64_t)blockIdx.y * p.M + m] = accb[j][0];
+        else
+          p.aux_out[m] = f32_to_bf16(accb[j][0]);
+      }
+    }
+  }
   if (S > 1) {
     // split-K: this split's fp32 slab; reduce_kernel sums the slabs.  (A last-arriver in-kernel
     // reduction measured slower here: its serial read of S-1 slabs of 16-64 KiB per tile costs
@@ -335,19 +366,24 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
   }
 }
 
-// out[i] = Σ_s ws[s][i] as bf16 (fixed order: deterministic); 8 elements per thread
+// out[i] = Σ_s ws[s][i] as bf16 (fixed order: deterministic); 8 elements per thread.  With
+// rs_out, the EPI_ROWSUM partials ws[S*slab + s*M + m] are summed into rs_out[m] the same way.
 __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ ws, int splits, int64_t n8, int64_t slab,
-                                                     uint16_t* __restrict__ out) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+                                                     uint16_t* __restrict__ out, int64_t m8,
+                                                     uint16_t* __restrict__ rs_out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8 + m8; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool rs = i >= n8;
+    const float* src = rs ? ws + splits * slab + 8 * (i - n8) : ws + 8 * i;
+    const int64_t stride = rs ? m8 * 8 : slab;
     float v[8];
-    load8<float>(ws + 8 * i, v);
+    load8<float>(src, v);
     for (int s = 1; s < splits; ++s) {
       float w[8];
-      load8<float>(ws + s * slab + 8 * i, w);
+      load8<float>(src + s * stride, w);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += w[e];
     }
-    store8<bf16_t>(reinterpret_cast<bf16_t*>(out) + 8 * i, v);
+    store8<bf16_t>(reinterpret_cast<bf16_t*>(rs ? rs_out : out) + 8 * (rs ? i - n8 : i), v);
   }
 }
 
@@ -387,6 +423,12 @@ static void launch_layout(int epi, const Tile& t, const Args& a, dim3 grid, hipS
     case EPI_DGELU:
       if constexpr (!A_KM && B_KN) {
         launch_epi<false, true, EPI_DGELU>(t, a, grid, st);
+        return;
+      }
+      break;
+    case EPI_ROWSUM:
+      if constexpr (A_KM && B_KN) {
+        launch_epi<true, true, EPI_ROWSUM>(t, a, grid, st);
         return;
       }
       break;
@@ -446,12 +488,17 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   if (epi == EPI_DGELU)
     TORCH_CHECK(aux_in && aux_in->sizes() == c.sizes() && aux_in->is_contiguous() &&
                     aux_in->scalar_type() == at::kBFloat16, "nbd::gemm: aux_in");
-  TORCH_CHECK(epi >= EPI_NONE && epi <= EPI_DGELU, "nbd::gemm: epilogue ", epi);
+  if (epi == EPI_ROWSUM)
+    TORCH_CHECK(aux_out && aux_out->numel() == M && aux_out->is_contiguous() &&
+                    aux_out->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(aux_out->data_ptr()) % 16 == 0,
+                "nbd::gemm: aux_out (row sums)");
+  TORCH_CHECK(epi >= EPI_NONE && epi <= EPI_ROWSUM, "nbd::gemm: epilogue ", epi);
   const Tile t = pick_tile(M, N, tile_hint);
   const int tiles = (M / t.bm) * (N / t.bn);
   const int S = splits > 0 ? (int)splits : 1;
   TORCH_CHECK(K % (BK * S) == 0, "nbd::gemm: K not divisible into ", S, " splits");
-  TORCH_CHECK(S == 1 || (epi == EPI_NONE && !bias), "nbd::gemm: split-K only without an epilogue");
+  TORCH_CHECK(S == 1 || ((epi == EPI_NONE || epi == EPI_ROWSUM) && !bias),
+              "nbd::gemm: split-K only without an elementwise epilogue");
 
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
@@ -474,7 +521,8 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   at::Tensor ws;
   p.ws = nullptr;
   if (S > 1) {
-    ws = at::empty({S, M, N}, a.options().dtype(at::kFloat));  // stream-ordered (caching allocator)
+    // stream-ordered (caching allocator): S slabs [M][N] (+ S row-sum partials [M])
+    ws = at::empty({(int64_t)S * M * N + (epi == EPI_ROWSUM ? (int64_t)S * M : 0)}, a.options().dtype(at::kFloat));
     p.ws = ws.data_ptr<float>();
   }
   if (!a_km && !b_kn)
@@ -485,9 +533,9 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
     launch_layout<true, true>((int)epi, t, p, grid, st);
   C10_HIP_KERNEL_LAUNCH_CHECK();
   if (S > 1) {
-    const int64_t n8 = (int64_t)M * N / 8;
-    const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 2048);
-    hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, p.ws, S, n8, (int64_t)M * N, p.c);
+    const int64_t n8 = (int64_t)M * N / 8, m8 = epi == EPI_ROWSUM ? M / 8 : 0;
+    const int blocks = (int)std::min<int64_t>((n8 + m8 + 255) / 256, 2048);
+    hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, p.ws, S, n8, (int64_t)M * N, p.c, m8, p.aux_out);
     C10_HIP_KERNEL_LAUNCH_CHECK();
   }
 }

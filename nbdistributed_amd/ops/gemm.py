@@ -19,7 +19,7 @@ from ._lib import _require
 # NBD_HIP_GEMM=0 routes gemm_linear / mlp_gelu to PyTorch (hipBLASLt) — for A/B measurements
 ENABLED = os.environ.get("NBD_HIP_GEMM", "1") != "0"
 
-EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
+EPI_NONE, EPI_GELU, EPI_DGELU, EPI_ROWSUM = 0, 1, 2, 3
 
 
 def gemm_ok(M: int, N: int, K: int) -> bool:
@@ -90,7 +90,8 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
            splits: int = 0, tile: int = 0):
     """C[M,N] = A·B.  ``a`` is [M,K] (or [K,M] with ``a_km``), ``b`` is [N,K] (or [K,N] with
     ``b_kn``).  ``epi``: EPI_NONE (+bias), EPI_GELU (+bias, returns (gelu(pre), pre)),
-    EPI_DGELU (C · gelu'(aux)).  ``splits=0`` picks split-K automatically (no-epilogue only);
+    EPI_DGELU (C · gelu'(aux)), EPI_ROWSUM (weight-gradient layout; returns (C, Σ_k A[m,k]) —
+    the bias gradient of the Linear whose weight gradient C is).  ``splits=0`` picks split-K automatically (no-epilogue only);
     ``tile`` = stages*1000000 + BM*1000 + BN forces a kernel (stages 2 or 3; benchmarks)."""
     import torch
 
@@ -105,12 +106,14 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
         b = b if b.is_contiguous() else b.contiguous()
         c = out if out is not None else torch.empty(M, N, device=a.device, dtype=a.dtype)
         pre = torch.empty_like(c) if epi == EPI_GELU else None
+        if epi == EPI_ROWSUM:
+            pre = torch.empty(M, device=a.device, dtype=a.dtype)
         if splits == 0 or tile == 0:
-            t, s = config(a_km, b_kn, M, N, K, can_split=(epi == EPI_NONE and bias is None))
+            t, s = config(a_km, b_kn, M, N, K, can_split=(epi in (EPI_NONE, EPI_ROWSUM) and bias is None))
             tile = tile or t
             splits = splits or s
         torch.ops.nbd.gemm(a, b, c, a_km, b_kn, bias, epi, aux, pre, splits, tile)
-        return (c, pre) if epi == EPI_GELU else c
+        return (c, pre) if epi in (EPI_GELU, EPI_ROWSUM) else c
     # reference path (CPU / uncovered shapes): same math through PyTorch
     A = a.t() if a_km else a
     B = b if b_kn else b.t()
@@ -123,6 +126,8 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
         return c, pre
     if epi == EPI_DGELU:
         c = _dgelu_ref(c, aux)
+    if epi == EPI_ROWSUM:
+        return c, A.float().sum(1).to(a.dtype)
     if out is not None:
         out.copy_(c)
         return out
@@ -173,9 +178,12 @@ def _fns():
             dx = dw = db = None
             if ctx.needs_input_grad[0]:
                 dx = matmul(dy2, w, b_kn=True).view(ctx.xshape)
-            if ctx.needs_input_grad[1]:
+            want_db = ctx.has_bias and ctx.needs_input_grad[2]
+            if ctx.needs_input_grad[1] and want_db:  # bias grad rides in the weight-grad GEMM
+                dw, db = matmul(dy2, x2, a_km=True, b_kn=True, epi=EPI_ROWSUM)
+            elif ctx.needs_input_grad[1]:
                 dw = matmul(dy2, x2, a_km=True, b_kn=True)
-            if ctx.has_bias and ctx.needs_input_grad[2]:
+            elif want_db:
                 db = _colsum(dy2, w.dtype)
             return dx, dw, db
 
@@ -197,11 +205,16 @@ def _fns():
             x2, w1, w2, pre, g = ctx.saved_tensors
             dy2 = _c(dy).view(-1, dy.shape[-1])
             dpre = matmul(dy2, w2, b_kn=True, epi=EPI_DGELU, aux=pre)
-            dw2 = matmul(dy2, g, a_km=True, b_kn=True)
-            db2 = _colsum(dy2, w2.dtype) if ctx.bias[1] else None
+            db1 = db2 = None
+            if ctx.bias[1]:
+                dw2, db2 = matmul(dy2, g, a_km=True, b_kn=True, epi=EPI_ROWSUM)
+            else:
+                dw2 = matmul(dy2, g, a_km=True, b_kn=True)
             dx = matmul(dpre, w1, b_kn=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-            dw1 = matmul(dpre, x2, a_km=True, b_kn=True)
-            db1 = _colsum(dpre, w1.dtype) if ctx.bias[0] else None
+            if ctx.bias[0]:
+                dw1, db1 = matmul(dpre, x2, a_km=True, b_kn=True, epi=EPI_ROWSUM)
+            else:
+                dw1 = matmul(dpre, x2, a_km=True, b_kn=True)
             return dx, dw1, db1, dw2, db2
 
     _Fns = (_Linear, _MLPGelu)

@@ -151,3 +151,15 @@ def test_gemm_split_k_is_deterministic():
     a, b = _operands(768, 768, 8192, True, True, seed=7)
     outs = [G.matmul(a, b, a_km=True, b_kn=True, splits=8) for _ in range(3)]
     assert all(torch.equal(outs[0], o) for o in outs[1:])
+
+
+@pytest.mark.parametrize("splits", [1, 2, 8])
+@pytest.mark.parametrize("tile", [2128128, 3064128, 2064064, 3128064])
+def test_gemm_rowsum_epilogue_is_the_bias_gradient(splits, tile):
+    # weight-gradient layout: dW = dyᵀ·x and db = Σ_tokens dy from the same kernel
+    M, N, K = 256, 384, 2048
+    a, b = _operands(M, N, K, True, True, seed=8)
+    c, rs = G.matmul(a, b, a_km=True, b_kn=True, epi=G.EPI_ROWSUM, splits=splits, tile=tile)
+    assert _err(c, _ref(a, b, True, True)) < 1e-2
+    assert rs.shape == (M,) and rs.dtype == torch.bfloat16
+    assert _err(rs, a.float().sum(0)) < 1e-2

@@ -221,7 +221,7 @@ def test_fd_capture_streams_python_and_c_output(tmp_path):
     """
     proc = subprocess.Popen([sys.executable, "-c", textwrap.dedent(code)], env=dict(os.environ, PYTHONPATH=ROOT))
     out, err = b"", b""
-    deadline = time.time() + 20
+    deadline = time.time() + 60  # a loaded host (pytest -n) can take many seconds to start the child
     while time.time() < deadline:
         m = r.recv(1)
         if m is None or m.is_event:
