@@ -90,24 +90,29 @@ def _nbd_wrap(m, impl, **kw):
 def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small"):
     torch.manual_seed(0)
     m = GPT2(getattr(GPT2Config, config)()).to(device)
-    amp = impl != "flat"
-    if impl == "flat":   # bf16 params in the DDP buckets + fp32 master/moments in FlatAdamW
+    amp = impl not in ("flat", "flatgraph")
+    if not amp:   # bf16 params in the DDP buckets + fp32 master/moments in FlatAdamW
         m = m.to(torch.bfloat16)
         model = _NbdDDP(m, flat_params=True, grad_mode="bucket")
-        opt = _FlatAdamW(model, lr=3e-4)
+        opt = _FlatAdamW(model, lr=3e-4, capturable=impl == "flatgraph")
     else:
         model = _nbd_wrap(m, impl, comm_dtype=torch.bfloat16)
         opt = torch.optim.AdamW(m.parameters(), lr=3e-4, fused=device.type == "cuda")
     x = torch.randint(0, m.config.vocab_size, (B, T), device=device)
-    def step():
+    def step(inp=x):
         with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
-            _, loss = model(x, x, return_logits=False)
+            _, loss = model(inp, inp, return_logits=False)
         loss.backward()
         opt.step()
         opt.zero_grad(set_to_none=True)
         return loss.detach()
-    ms, loss = _nbd_time_steps(step, steps, warm)
-    del model, opt, m, x
+    run = step
+    if impl == "flatgraph":   # the whole step (fwd, bwd, bucket all-reduces, AdamW) as one HIP graph
+        from nbdistributed_amd.graphs import GraphedStep
+        g = GraphedStep(step, (x,), warmup=3, optimizers=[opt])
+        run = lambda: g(x)
+    ms, loss = _nbd_time_steps(run, steps, warm)
+    del model, opt, m, x, run
     if device.type == "cuda":
         torch.cuda.empty_cache()
     return ms, loss
@@ -163,6 +168,11 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
                ms_per_step=ms, tokens_per_s=toks, tokens_per_s_per_gpu=toks / n)
     if config == "small":  # 6·N·tokens FLOPs over the 2.5 PFLOP/s dense bf16 peak per GPU
         out["mfu"] = 6 * 124_439_808 * toks / (2.5e15 * n)
+    if n == 1 or os.environ.get("NBD_BENCH_GRAPH_MULTI") == "1":  # see bench_notebook
+        r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flatgraph', {config!r})", render=False)
+        gms = _max_over_ranks(r)
+        out.update(graph_ms_per_step=gms, graph_tokens_per_s=n * B * T / (gms / 1e3),
+                   graph_recipe="as the primary recipe, whole step captured in one HIP graph (GraphedStep)")
     r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'nbd', {config!r})", render=False)
     ams = _max_over_ranks(r)
     out.update(amp_ms_per_step=ams, amp_tokens_per_s=n * B * T / (ams / 1e3))
