@@ -1086,6 +1086,28 @@ int nbd_send(nbd_socket* s, int nframes, const void* const* ptrs, const size_t* 
   return s->route(nullptr, nbd_socket::encode(nframes, ptrs, lens, 0), true);
 }
 
+int nbd_send_multi(nbd_socket* s, int nidents, const void* const* iptrs, const size_t* ilens, int nframes,
+                   const void* const* ptrs, const size_t* lens, int* status) {
+  Guard g(s);
+  if (!g.ok) return fail("ECLOSED");
+  if (s->type != NBD_ROUTER) return fail("EINVAL: nbd_send_multi needs a ROUTER socket");
+  if (nframes < 1) return fail("EINVAL: empty message");
+  // encode the frames once, route a copy to every identity (one call fans a cell out to N ranks)
+  const std::string body = nbd_socket::encode(nframes, ptrs, lens, 0);
+  int failed = 0;
+  for (int i = 0; i < nidents; ++i) {
+    std::string ident(static_cast<const char*>(iptrs[i]), ilens[i]);
+    const int rc = s->route(&ident, std::string(body), true);
+    int st = 0;
+    if (rc != 0) {
+      st = g_err.compare(0, 12, "EHOSTUNREACH") == 0 ? 1 : 2;
+      ++failed;
+    }
+    if (status) status[i] = st;
+  }
+  return failed;
+}
+
 int nbd_recv(nbd_socket* s, int timeout_ms, nbd_msg** out) {
   Guard g(s);
   if (!g.ok) return -1;
@@ -1104,6 +1126,49 @@ int nbd_recv(nbd_socket* s, int timeout_ms, nbd_msg** out) {
   delete m;
   *out = w;
   return 0;
+}
+
+int nbd_recv_batch(nbd_socket* s, int timeout_ms, void* buf, size_t cap, size_t* used, int max_msgs) {
+  Guard g(s);
+  if (!g.ok) return -1;
+  *used = 0;
+  std::unique_lock<std::mutex> lk(s->imu);
+  auto pred = [s] { return !s->inbox.empty() || s->inbox_closed; };
+  if (timeout_ms < 0) s->icv.wait(lk, pred);
+  else if (!s->icv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms), pred))
+    return 0;
+  if (s->inbox.empty()) return -1;
+  // serialise queued messages: u32 kind, u32 event, u32 nframes, then (u64 len, bytes) per frame
+  char* out = static_cast<char*>(buf);
+  size_t pos = 0;
+  int n = 0;
+  while (!s->inbox.empty() && n < max_msgs) {
+    Msg* m = s->inbox.front();
+    size_t need = 12;
+    for (const auto& f : m->frames) need += 8 + f.size();
+    if (pos + need > cap) {
+      if (n == 0) {  // the first message alone does not fit: report its size, keep it queued
+        *used = need;
+        return -2;
+      }
+      break;
+    }
+    const uint32_t hdr[3] = {(uint32_t)m->kind, (uint32_t)m->event, (uint32_t)m->frames.size()};
+    std::memcpy(out + pos, hdr, 12);
+    pos += 12;
+    for (const auto& f : m->frames) {
+      const uint64_t len = f.size();
+      std::memcpy(out + pos, &len, 8);
+      pos += 8;
+      if (len) std::memcpy(out + pos, f.data(), len);
+      pos += len;
+    }
+    s->inbox.pop_front();
+    delete m;
+    ++n;
+  }
+  *used = pos;
+  return n;
 }
 
 int nbd_msg_kind(const nbd_msg* m) { return m->m.kind; }

@@ -78,9 +78,21 @@ int nbd_connect(nbd_socket* s, const char* endpoint);
  * Returns 0, or -1 (errno-style code in nbd_last_error). */
 int nbd_send(nbd_socket* s, int nframes, const void* const* ptrs, const size_t* lens);
 
+/* ROUTER: send the same multipart body (frames, no identity) to each of nidents identities,
+ * encoding it once.  status[i] = 0 sent, 1 no such peer (EHOSTUNREACH, mandatory routing),
+ * 2 other error.  Returns the number of failed identities, or -1 if the call itself failed. */
+int nbd_send_multi(nbd_socket* s, int nidents, const void* const* iptrs, const size_t* ilens, int nframes,
+                   const void* const* ptrs, const size_t* lens, int* status);
+
 /* Wait up to timeout_ms (-1 = forever) for a message or event.
  * Returns 0 with *out set, 1 on timeout, -1 if the socket is closed. */
 int nbd_recv(nbd_socket* s, int timeout_ms, nbd_msg** out);
+/* Drain up to max_msgs queued messages (waiting up to timeout_ms, -1 = forever, for the first)
+ * into buf, serialised as: u32 kind, u32 event, u32 nframes, then per frame u64 length + bytes
+ * (native endianness).  Returns the number of messages (0 on timeout), -1 if the socket is
+ * closed, -2 if the first queued message needs more than cap bytes (*used = the size needed;
+ * it stays queued).  One call replaces recv + 5 accessor calls + free per message. */
+int nbd_recv_batch(nbd_socket* s, int timeout_ms, void* buf, size_t cap, size_t* used, int max_msgs);
 int nbd_msg_kind(const nbd_msg* m);
 int nbd_msg_event(const nbd_msg* m);
 int nbd_msg_nframes(const nbd_msg* m);

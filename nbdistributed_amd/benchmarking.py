@@ -88,6 +88,8 @@ def _nbd_wrap(m, impl, **kw):
     return _TorchDDP(m, device_ids=[device.index] if device.type == "cuda" else None, bucket_cap_mb=25)
 
 def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small"):
+    if impl == "flatgraph" and device.type != "cuda":
+        impl = "flat"   # HIP graphs need a GPU
     torch.manual_seed(0)
     m = GPT2(getattr(GPT2Config, config)()).to(device)
     amp = impl not in ("flat", "flatgraph")

@@ -223,15 +223,19 @@ class CommunicationManager:
             dead_now = {r: self.dead[r] for r in ranks if r in self.dead}
         for r, why in dead_now.items():
             req.on_dead(r, why)
-        for r in ranks:
-            if r in dead_now:
-                continue
-            try:
-                self.sock.send([P.worker_identity(r), header, body])
-            except HostUnreachable:
-                req.on_dead(r, "not connected")
-            except TransportError as ex:
+        live = [r for r in ranks if r not in dead_now]
+        try:  # one native call fans the request out (the body is encoded once)
+            status = self.sock.send_multi([P.worker_identity(r) for r in live], [header, body])
+        except TransportError as ex:
+            status = [2] * len(live)
+            for r in live:
                 req.on_dead(r, f"send failed: {ex}")
+            return req
+        for r, st in zip(live, status):
+            if st == 1:
+                req.on_dead(r, "not connected")
+            elif st:
+                req.on_dead(r, "send failed")
         return req
 
     def wait(self, req: PendingRequest, timeout: Optional[float] = None) -> PendingRequest:
@@ -310,28 +314,31 @@ class CommunicationManager:
     def _message_handler(self) -> None:
         while self.running:
             try:
-                m = self.sock.recv(timeout=None)
+                batch = self.sock.recv_batch(timeout=None)  # every queued reply in one native call
             except TransportError:
                 break
-            if m is None:
-                continue
+            for m in batch:
+                self._handle_message(m)
+
+    def _handle_message(self, m) -> None:
+        if True:
             if m.is_event:
                 self._on_event(m.event, P.rank_of_identity(m.identity))
-                continue
+                return
             if len(m.frames) < 2:
-                continue
+                return
             rank = P.rank_of_identity(m.frames[0])
             try:
                 h = P.unpack_header(m.frames[1])
             except ValueError:
-                continue
+                return
             body = m.frames[2] if len(m.frames) > 2 else b""
             if rank is None:
                 rank = h.rank
             if h.mtype == P.T_STREAM:
                 text = self._decode_stream(rank, h.stream, body)
                 if not text:
-                    continue
+                    return
                 stream = P.STREAM_NAMES.get(h.stream, "stdout")
                 with self._lock:
                     req = self.pending.get(h.seq)
@@ -346,7 +353,7 @@ class CommunicationManager:
                             pass
                     else:
                         self.background.put((rank, stream, text))
-                continue
+                return
             try:
                 data = P.decode_body(h.enc, body)
             except Exception as e:

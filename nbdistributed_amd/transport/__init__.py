@@ -11,6 +11,7 @@ Only standard library imports here: the coordinator may run on an interpreter wi
 from __future__ import annotations
 
 import ctypes
+import struct
 import os
 import threading
 from dataclasses import dataclass, field
@@ -82,7 +83,10 @@ def _load():
         lib.nbd_bind.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
         lib.nbd_connect.argtypes = [vp, ctypes.c_char_p]
         lib.nbd_send.argtypes = [vp, i, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz)]
+        lib.nbd_send_multi.argtypes = [vp, i, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), i,
+                                       ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), ctypes.POINTER(i)]
         lib.nbd_recv.argtypes = [vp, i, ctypes.POINTER(vp)]
+        lib.nbd_recv_batch.argtypes = [vp, i, vp, sz, ctypes.POINTER(sz), i]
         lib.nbd_msg_kind.argtypes = [vp]
         lib.nbd_msg_event.argtypes = [vp]
         lib.nbd_msg_nframes.argtypes = [vp]
@@ -107,6 +111,10 @@ def library_path() -> str:
 def _err(lib) -> str:
     e = lib.nbd_last_error()
     return e.decode(errors="replace") if e else "unknown error"
+
+
+_HDR3 = struct.Struct("=III")
+_LEN = struct.Struct("=Q")
 
 
 @dataclass
@@ -189,6 +197,58 @@ class Socket:
             if msg.startswith("EHOSTUNREACH"):
                 raise HostUnreachable(msg)
             raise TransportError(msg)
+
+    def send_multi(self, identities: Sequence[bytes], frames: Sequence[Union[bytes, bytearray, memoryview]]) -> List[int]:
+        """ROUTER: the same message to every identity in one native call (the body is encoded
+        once).  Returns a status per identity: 0 sent, 1 no such peer, 2 other error."""
+        k = len(identities)
+        if k == 0:
+            return []
+        n = len(frames)
+        fr = [f if isinstance(f, bytes) else bytes(f) for f in frames]
+        ptrs = (ctypes.c_char_p * n)(*fr)
+        lens = (ctypes.c_size_t * n)(*[len(f) for f in fr])
+        iptrs = (ctypes.c_char_p * k)(*identities)
+        ilens = (ctypes.c_size_t * k)(*[len(x) for x in identities])
+        status = (ctypes.c_int * k)()
+        if self._lib.nbd_send_multi(self._h, k, iptrs, ilens, n, ptrs, lens, status) < 0:
+            raise TransportError(_err(self._lib))
+        return list(status)
+
+    def recv_batch(self, timeout: Optional[float] = None, max_msgs: int = 256) -> List[Received]:
+        """Every queued message (up to ``max_msgs``) in one native call, waiting up to ``timeout``
+        seconds (None = forever) for the first; [] on timeout; raises TransportError once the
+        socket is closed."""
+        ms = -1 if timeout is None else max(0, int(timeout * 1000))
+        buf = getattr(self, "_rbuf", None)
+        if buf is None:
+            buf = self._rbuf = ctypes.create_string_buffer(1 << 16)
+        used = ctypes.c_size_t()
+        while True:
+            n = self._lib.nbd_recv_batch(self._h, ms, buf, len(buf), ctypes.byref(used), max_msgs)
+            if n == -2:  # a message larger than the buffer: grow and retry
+                buf = self._rbuf = ctypes.create_string_buffer(max(used.value, 2 * len(buf)))
+                continue
+            break
+        if n == 0:
+            return []
+        if n < 0:
+            raise TransportError("socket closed")
+        raw = ctypes.string_at(buf, used.value)
+        out: List[Received] = []
+        pos = 0
+        unpack3, unpack1 = _HDR3.unpack_from, _LEN.unpack_from
+        for _ in range(n):
+            kind, event, nf = unpack3(raw, pos)
+            pos += 12
+            frames = []
+            for _ in range(nf):
+                (ln,) = unpack1(raw, pos)
+                pos += 8
+                frames.append(raw[pos:pos + ln])
+                pos += ln
+            out.append(Received(kind, frames, event))
+        return out
 
     def recv(self, timeout: Optional[float] = None) -> Optional[Received]:
         """Block up to ``timeout`` seconds (None = forever).  Returns None on timeout; raises

@@ -468,7 +468,8 @@ class DistributedWorker:
         self._install_signal_handlers()
         while not self.stop:
             try:
-                m = self.sock.recv(timeout=0.5)
+                got = self.sock.recv_batch(timeout=0.5, max_msgs=1)  # one native call per message
+                m = got[0] if got else None
             except KeyboardInterrupt:
                 continue
             except TransportError:

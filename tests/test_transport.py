@@ -83,6 +83,41 @@ def test_fan_out_fan_in_8_peers():
     r.close()
 
 
+def test_send_multi_fans_out_once_and_reports_missing_peers():
+    r = T.Socket(T.ROUTER, mandatory=True)
+    ep = r.bind("tcp://127.0.0.1:0")
+    ds = [T.Socket(T.DEALER, identity=f"worker_{i}".encode()) for i in range(4)]
+    for d in ds:
+        d.connect(ep)
+    seen = set()
+    while len(seen) < 4:
+        seen.add(_drain_event(r).identity)
+    idents = [f"worker_{i}".encode() for i in range(4)] + [b"worker_9"]
+    for rnd in range(20):
+        status = r.send_multi(idents, [b"hdr", str(rnd).encode()])
+        assert status == [0, 0, 0, 0, 1]  # worker_9 never connected: EHOSTUNREACH
+        for d in ds:
+            m = d.recv(5)
+            while m.is_event:
+                m = d.recv(5)
+            assert m.frames == [b"hdr", str(rnd).encode()]
+    assert r.send_multi([], [b"x"]) == []
+    # batched receive: every queued reply in one call, in arrival order, frames intact
+    for i, d in enumerate(ds):
+        d.send([f"r{i}".encode(), b"", os.urandom(100_000) if i == 3 else b"small"])
+    got = []
+    deadline = time.time() + 10
+    while len(got) < 4 and time.time() < deadline:
+        got += [m for m in r.recv_batch(1) if not m.is_event]
+    assert sorted(m.frames[1] for m in got) == [b"r0", b"r1", b"r2", b"r3"]
+    assert all(m.frames[2] == b"" for m in got)
+    assert {len(m.frames[3]) for m in got} == {5, 100_000}  # > the 64 KiB batch buffer: grown
+    assert r.recv_batch(0.05) == []
+    for d in ds:
+        d.close()
+    r.close()
+
+
 def test_large_frame_64mib():
     r = T.Socket(T.ROUTER)
     ep = r.bind("ipc://" + tempfile.mkdtemp() + "/big.sock")
