@@ -88,12 +88,14 @@ def main():
                 for tile in (128128, 128064, 64128, 64064):
                     if M % (tile // 1000) or NN % (tile % 1000):
                         continue
-                    for stg in (2, 3):
+                    for wv, stg in ((4, 2), (4, 3), (8, 2), (8, 3)):
+                        if wv == 8 and tile != 128128:
+                            continue
                         for s in (1, 2, 4, 8):
                             if KK % (64 * s) or (s > 1 and KK // s < 256):
                                 continue
-                            hint = stg * 1000000 + tile
-                            var[f"{tile // 1000}x{tile % 1000}/p{stg}/s{s}"] = round(
+                            hint = wv * 10000000 + stg * 1000000 + tile
+                            var[f"{tile // 1000}x{tile % 1000}/w{wv}p{stg}/s{s}"] = round(
                                 timeit(lambda: G.matmul(A, B, a_km=a_km, b_kn=b_kn, splits=s, tile=hint)) * 1e3, 1)
                 row["variants_us"] = var
             rows.append(row)

@@ -99,13 +99,13 @@ __device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* lds_wave_ba
 
 // Stage one 64-deep K-tile of an operand into its LDS image.  R = tile rows (BM or BN).
 // TR = false: global [rows][k] (row r0.., k0..), image [R][64]; TR = true: global [k][rows], image [64][R].
-template <int R, bool TR>
+template <int R, bool TR, int W>
 __device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld, int r0, int k0, uint8_t* img,
                                       int wave, int lane) {
-  constexpr int PER_WAVE = R / 32;  // (R*64*2 B) / (4 waves * 1 KiB)
+  constexpr int PER_WAVE = R / (8 * W);  // (R*64*2 B) / (W waves * 1 KiB)
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
-    const int wbase = (i * 4 + wave) * 1024;
+    const int wbase = (i * W + wave) * 1024;
     const int byte = wbase + lane * 16;
     const uint16_t* src;
     if constexpr (!TR) {
@@ -178,17 +178,20 @@ __device__ __forceinline__ void wait_barrier() {
 // 128x128).  STAGES = 3: tile t+2 is issued while t is computed and stays in flight across the
 // barrier (counted vmcnt) — the latency-bound regime of few, long-K tiles (weight gradients,
 // small token counts) where one workgroup per CU cannot hide a drained pipeline.
-template <int BM, int BN, bool A_KM, bool B_KN, int EPI, int STAGES>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
-  constexpr int FM = BM / 32, FN = BN / 32;  // 16-wide fragments per wave along m / n
+// W = waves per workgroup: 4 (2x2, each wave (BM/2)x(BN/2)) or 8 (2x4, each (BM/2)x(BN/4): twice
+// the waves per SIMD to hide the barrier / DMA latency, at more LDS reads per MFMA).
+template <int BM, int BN, bool A_KM, bool B_KN, int EPI, int STAGES, int W>
+__global__ __launch_bounds__(64 * W, 2) void gemm_kernel(Args p) {
+  constexpr int NTW = 64 * W, WM = 2, WN = W / 2;
+  constexpr int FM = BM / (16 * WM), FN = BN / (16 * WN);  // 16-wide fragments per wave along m / n
   constexpr int A_BYTES = BM * BK * 2, BUF = Smem<BM, BN, STAGES>::BUF, LDC = Smem<BM, BN, STAGES>::LDC;
-  constexpr int NPT = BM / 32 + BN / 32;  // glds per thread per K-tile
+  constexpr int NPT = (BM + BN) / (8 * W);  // glds per thread per K-tile
   // one __shared__ array for everything (a second LDS object de-pipelines the glds loop:
   // cdna_hip_programming.md §5 "Projection GEMM" item 4a)
   __shared__ __attribute__((aligned(1024))) uint8_t smem[Smem<BM, BN, STAGES>::BYTES];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
 
   // XCD-aware bijective remap, then 8-row groups sweeping the column tiles
   const int nwg = p.tiles_m * p.tiles_n;
@@ -232,9 +235,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
     for (int kk = 0; kk < 2; ++kk) {
       s8v af[FM], bf[FN];
 #pragma unroll
-      for (int j = 0; j < FM; ++j) af[j] = frag<BM, A_KM>(cur, wm * (BM / 2) + 16 * j, kk, lane);
+      for (int j = 0; j < FM; ++j) af[j] = frag<BM, A_KM>(cur, wm * (BM / WM) + 16 * j, kk, lane);
 #pragma unroll
-      for (int i = 0; i < FN; ++i) bf[i] = frag<BN, B_KN>(cur + A_BYTES, wn * (BN / 2) + 16 * i, kk, lane);
+      for (int i = 0; i < FN; ++i) bf[i] = frag<BN, B_KN>(cur + A_BYTES, wn * (BN / WN) + 16 * i, kk, lane);
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -248,8 +251,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
     }
   };
   auto stage_tile = [&](int t, uint8_t* buf) {
-    stage<BM, A_KM>(A, p.lda, m0, t * BK, buf, wave, lane);
-    stage<BN, B_KN>(B, p.ldb, n0, t * BK, buf + A_BYTES, wave, lane);
+    stage<BM, A_KM, W>(A, p.lda, m0, t * BK, buf, wave, lane);
+    stage<BN, B_KN, W>(B, p.ldb, n0, t * BK, buf + A_BYTES, wave, lane);
   };
 
   if constexpr (STAGES == 2) {
@@ -303,7 +306,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
   for (int i = 0; i < FN; ++i)
 #pragma unroll
     for (int j = 0; j < FM; ++j)
-      *reinterpret_cast<f4*>(ct + (wm * (BM / 2) + 16 * j + (lane & 15)) * LDC + wn * (BN / 2) + 16 * i +
+      *reinterpret_cast<f4*>(ct + (wm * (BM / WM) + 16 * j + (lane & 15)) * LDC + wn * (BN / WN) + 16 * i +
                              4 * (lane >> 4)) = acc[i][j];
   __syncthreads();
 
@@ -314,7 +317,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
     if (do_rs && lane < 16) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
-        const int m = m0 + wm * (BM / 2) + 16 * j + lane;
+        const int m = m0 + wm * (BM / WM) + 16 * j + lane;
         if (S > 1)
           p.ws[(int64_t)S * p.M * p.ldc + (int64_t)blockIdx.y * p.M + m] = accb[j][0];
         else
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
     // reduction measured slower here: its serial read of S-1 slabs of 16-64 KiB per tile costs
     // more than the extra launch — profiles/gemm_bench_r1.txt.)
     float* slab = p.ws + (int64_t)blockIdx.y * p.M * p.ldc;
-    for (int c = threadIdx.x; c < BM * CPR; c += NT) {
+    for (int c = threadIdx.x; c < BM * CPR; c += NTW) {
       const int r = c / CPR, cn = (c % CPR) * 8;
       float* dst = slab + (int64_t)(m0 + r) * p.ldc + n0 + cn;
       *reinterpret_cast<f4*>(dst) = *reinterpret_cast<const f4*>(ct + r * LDC + cn);
@@ -336,7 +339,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args p) {
     return;
   }
 
-  for (int c = threadIdx.x; c < BM * CPR; c += NT) {
+  for (int c = threadIdx.x; c < BM * CPR; c += NTW) {
     const int r = c / CPR, cn = (c % CPR) * 8;
     float v[8];
     {
@@ -389,25 +392,31 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ w
 
 // ---- host --------------------------------------------------------------------------------------
 struct Tile {
-  int bm, bn, stages;
+  int bm, bn, stages, waves;
 };
 
 template <bool A_KM, bool B_KN, int EPI>
 static void launch_epi(const Tile& t, const Args& a, dim3 grid, hipStream_t st) {
-#define NBD_GEMM_CASE(BM_, BN_)                                                                   \
-  if (t.bm == BM_ && t.bn == BN_) {                                                               \
-    if (t.stages == 3)                                                                            \
-      hipLaunchKernelGGL((gemm_kernel<BM_, BN_, A_KM, B_KN, EPI, 3>), grid, dim3(NT), 0, st, a); \
-    else                                                                                          \
-      hipLaunchKernelGGL((gemm_kernel<BM_, BN_, A_KM, B_KN, EPI, 2>), grid, dim3(NT), 0, st, a); \
-    return;                                                                                       \
+#define NBD_GEMM_K(BM_, BN_, S_, W_) \
+  hipLaunchKernelGGL((gemm_kernel<BM_, BN_, A_KM, B_KN, EPI, S_, W_>), grid, dim3(64 * W_), 0, st, a)
+#define NBD_GEMM_CASE(BM_, BN_)                         \
+  if (t.bm == BM_ && t.bn == BN_ && t.waves == 4) {     \
+    if (t.stages == 3) NBD_GEMM_K(BM_, BN_, 3, 4);      \
+    else NBD_GEMM_K(BM_, BN_, 2, 4);                    \
+    return;                                             \
   }
   NBD_GEMM_CASE(128, 128)
   NBD_GEMM_CASE(128, 64)
   NBD_GEMM_CASE(64, 128)
   NBD_GEMM_CASE(64, 64)
+  if (t.bm == 128 && t.bn == 128 && t.waves == 8) {  // 8 waves: 128x128 only
+    if (t.stages == 3) NBD_GEMM_K(128, 128, 3, 8);
+    else NBD_GEMM_K(128, 128, 2, 8);
+    return;
+  }
 #undef NBD_GEMM_CASE
-  TORCH_CHECK(false, "nbd::gemm: no kernel for tile ", t.bm, "x", t.bn);
+#undef NBD_GEMM_K
+  TORCH_CHECK(false, "nbd::gemm: no kernel for tile ", t.bm, "x", t.bn, " with ", t.waves, " waves");
 }
 
 template <bool A_KM, bool B_KN>
@@ -443,13 +452,13 @@ static bool tile_fits(const Tile& t, int M, int N) { return M % t.bm == 0 && N %
 // overrides it.
 static Tile pick_tile(int M, int N, int64_t tile_hint) {
   if (tile_hint > 0) {
-    // hint = stages*1000000 + BM*1000 + BN (stages 0 -> 2)
-    const int stg = (int)(tile_hint / 1000000);
-    Tile t{(int)(tile_hint / 1000 % 1000), (int)(tile_hint % 1000), stg == 3 ? 3 : 2};
+    // hint = waves*10000000 + stages*1000000 + BM*1000 + BN (waves 0 -> 4, stages 0 -> 2)
+    const int stg = (int)(tile_hint / 1000000 % 10), wv = (int)(tile_hint / 10000000);
+    Tile t{(int)(tile_hint / 1000 % 1000), (int)(tile_hint % 1000), stg == 3 ? 3 : 2, wv == 8 ? 8 : 4};
     TORCH_CHECK(tile_fits(t, M, N), "nbd::gemm: tile ", t.bm, "x", t.bn, " does not divide ", M, "x", N);
     return t;
   }
-  const Tile cands[4] = {{128, 128, 2}, {128, 64, 2}, {64, 128, 2}, {64, 64, 2}};
+  const Tile cands[4] = {{128, 128, 2, 4}, {128, 64, 2, 4}, {64, 128, 2, 4}, {64, 64, 2, 4}};
   int best = -1;
   for (int i = 0; i < 4; ++i) {
     if (!tile_fits(cands[i], M, N)) continue;

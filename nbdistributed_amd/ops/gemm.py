@@ -27,27 +27,34 @@ def gemm_ok(M: int, N: int, K: int) -> bool:
 
 
 # Measured best (kernel, split-K) per (a_km, b_kn, M, N, K) on MI355X for the bench workloads'
-# Linear products — kernel = stages*1000000 + BM*1000 + BN; from benchmarks/gemm_bench.py --sweep
+# Linear products — kernel = waves*10^7 (8 waves; 4 if absent) + stages*10^6 + BM*1000 + BN; from
+# benchmarks/gemm_bench.py --sweep
 # (profiles/gemm_bench_r1.txt; split-K only where it beats the best unsplit kernel by > 5 %).
 _TUNED = {
-    # GPT-2 small, 8 x 1024 tokens: forward, dgrad, wgrad (K = tokens)
-    (False, False, 8192, 2304, 768): (2064128, 1), (False, True, 8192, 768, 2304): (2128064, 1),
-    (True, True, 2304, 768, 8192): (3064128, 2),
-    (False, False, 8192, 768, 768): (2064128, 1), (False, True, 8192, 768, 768): (2128064, 1),
-    (True, True, 768, 768, 8192): (3064064, 8),
-    (False, False, 8192, 3072, 768): (2128128, 1), (False, True, 8192, 768, 3072): (2128128, 1),
-    (True, True, 3072, 768, 8192): (3064128, 4),
-    (False, False, 8192, 768, 3072): (2128128, 1), (False, True, 8192, 3072, 768): (2128128, 1),
-    (True, True, 768, 3072, 8192): (3128064, 1),
-    # SmolLM2-135M, 16 x 128 tokens
-    (False, False, 2048, 960, 576): (3064064, 1), (False, True, 2048, 576, 960): (3064064, 1),
-    (True, True, 960, 576, 2048): (3064064, 1),
-    (False, False, 2048, 576, 576): (2064064, 1), (False, True, 2048, 576, 576): (3064064, 1),
-    (True, True, 576, 576, 2048): (3064064, 1),
-    (False, False, 2048, 3072, 576): (2064128, 1), (False, True, 2048, 576, 3072): (3064064, 1),
-    (True, True, 3072, 576, 2048): (3064064, 1),
-    (False, False, 2048, 576, 1536): (3064064, 1), (False, True, 2048, 1536, 576): (2064064, 1),
-    (True, True, 576, 1536, 2048): (3064064, 1),
+    (False, False, 8192, 2304, 768): (82128128, 1),  # gpt2.c_attn fwd 44.5 us
+    (False, True, 8192, 768, 2304): (82128128, 1),  # gpt2.c_attn dgrad 42.3 us
+    (True, True, 2304, 768, 8192): (3064128, 2),  # gpt2.c_attn wgrad 52.5 us
+    (False, False, 8192, 768, 768): (82128128, 1),  # gpt2.attn.c_proj fwd 21.0 us
+    (False, True, 8192, 768, 768): (2128064, 1),  # gpt2.attn.c_proj dgrad 21.8 us
+    (True, True, 768, 768, 8192): (3064064, 8),  # gpt2.attn.c_proj wgrad 32.7 us
+    (False, False, 8192, 3072, 768): (82128128, 1),  # gpt2.c_fc fwd 49.7 us
+    (False, True, 8192, 768, 3072): (2128128, 1),  # gpt2.c_fc dgrad 50.9 us
+    (True, True, 3072, 768, 8192): (3064128, 4),  # gpt2.c_fc wgrad 72.6 us
+    (False, False, 8192, 768, 3072): (2128128, 1),  # gpt2.mlp.c_proj fwd 50.5 us
+    (False, True, 8192, 3072, 768): (82128128, 1),  # gpt2.mlp.c_proj dgrad 50.9 us
+    (True, True, 768, 3072, 8192): (82128128, 2),  # gpt2.mlp.c_proj wgrad 68.9 us
+    (False, False, 2048, 960, 576): (3064064, 1),  # smollm2.qkv fwd 13.5 us
+    (False, True, 2048, 576, 960): (3064064, 1),  # smollm2.qkv dgrad 14.9 us
+    (True, True, 960, 576, 2048): (3064064, 1),  # smollm2.qkv wgrad 18.1 us
+    (False, False, 2048, 576, 576): (2064064, 1),  # smollm2.o_proj fwd 12.6 us
+    (False, True, 2048, 576, 576): (2064064, 1),  # smollm2.o_proj dgrad 13.0 us
+    (True, True, 576, 576, 2048): (3064064, 1),  # smollm2.o_proj wgrad 17.9 us
+    (False, False, 2048, 3072, 576): (2064128, 1),  # smollm2.gate_up fwd 19.4 us
+    (False, True, 2048, 576, 3072): (3064064, 1),  # smollm2.gate_up dgrad 26.1 us
+    (True, True, 3072, 576, 2048): (3064064, 1),  # smollm2.gate_up wgrad 22.0 us
+    (False, False, 2048, 576, 1536): (3064064, 1),  # smollm2.down fwd 18.0 us
+    (False, True, 2048, 1536, 576): (2064064, 1),  # smollm2.down dgrad 15.3 us
+    (True, True, 576, 1536, 2048): (3064064, 1),  # smollm2.down wgrad 18.3 us
 }
 
 _TILES = (128128, 128064, 64128, 64064)
@@ -92,7 +99,8 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
     ``b_kn``).  ``epi``: EPI_NONE (+bias), EPI_GELU (+bias, returns (gelu(pre), pre)),
     EPI_DGELU (C · gelu'(aux)), EPI_ROWSUM (weight-gradient layout; returns (C, Σ_k A[m,k]) —
     the bias gradient of the Linear whose weight gradient C is).  ``splits=0`` picks split-K automatically (no-epilogue only);
-    ``tile`` = stages*1000000 + BM*1000 + BN forces a kernel (stages 2 or 3; benchmarks)."""
+    ``tile`` = waves*10^7 + stages*10^6 + BM*1000 + BN forces a kernel (waves 4 or 8, 8 only at
+    128x128; stages 2 or 3; benchmarks)."""
     import torch
 
     M = a.shape[1] if a_km else a.shape[0]

@@ -34,7 +34,7 @@ def _err(x, ref):
 
 
 @pytest.mark.parametrize("layout", LAYOUTS, ids=["fwd", "dgrad", "wgrad"])
-@pytest.mark.parametrize("tile", [128128, 128064, 64128, 64064, 3128128, 3128064, 3064128, 3064064])
+@pytest.mark.parametrize("tile", [128128, 128064, 64128, 64064, 3128128, 3128064, 3064128, 3064064, 82128128, 83128128])
 @pytest.mark.parametrize("shape", [(256, 256, 320), (384, 640, 192), (128, 128, 64), (128, 128, 128)])
 def test_gemm_layouts_and_tiles(layout, tile, shape):
     M, N, K = shape
@@ -154,7 +154,7 @@ def test_gemm_split_k_is_deterministic():
 
 
 @pytest.mark.parametrize("splits", [1, 2, 8])
-@pytest.mark.parametrize("tile", [2128128, 3064128, 2064064, 3128064])
+@pytest.mark.parametrize("tile", [2128128, 3064128, 2064064, 3128064, 82128128, 83128128])
 def test_gemm_rowsum_epilogue_is_the_bias_gradient(splits, tile):
     # weight-gradient layout: dW = dyᵀ·x and db = Σ_tokens dy from the same kernel
     M, N, K = 256, 384, 2048
