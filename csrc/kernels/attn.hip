@@ -322,21 +322,26 @@ __global__ __launch_bounds__(NT) void bwd_pre_kernel(View dout, View out, float*
 }
 
 // ============================================================================ backward: dK, dV
+// Block `blk` of `nblocks` (= B·H·gsplit·nblk).  gsplit > 1 (GQA with few key/value heads):
+// the `group` query heads of a key/value head are split over gsplit workgroups, each writing a
+// partial dK/dV (split index s at dk/dv + s·split_stride) that gqa_reduce_kernel sums — 3x the
+// workgroups for SmolLM2 (9 query / 3 kv heads) instead of one workgroup sweeping all 3 heads.
 template <bool CAUSAL>
-__global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v, View dout,
-                                                          const float* __restrict__ lse,
-                                                          const float* __restrict__ delta, MView dk, MView dv, int H,
-                                                          int T, int nblk, float sc2, float scale, int group,
-                                                          Rope rp) {
-  // H = key/value heads (the grid); query heads hq = kvh·group + g, g < group
+__device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, View v, View dout,
+                                          const float* __restrict__ lse, const float* __restrict__ delta, MView dk,
+                                          MView dv, int H, int T, int nblk, float sc2, float scale, int group,
+                                          Rope rp, int gsplit, int64_t split_stride) {
+  // H = key/value heads; query heads hq = kvh·group + g, g < group
   __shared__ __attribute__((aligned(16))) uint16_t Qs[TILE * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Os[TILE * RS];  // dO tile
   __shared__ __attribute__((aligned(16))) float Ls[TILE];           // lse * log2(e)
   __shared__ __attribute__((aligned(16))) float Ds[TILE];           // delta
-  const int per = gridDim.x / nblk;
-  const int bh = blockIdx.x % per;
-  const int kb0 = blockIdx.x / per;  // key block; block 0 has the most query tiles under a causal mask
+  const int per = nblocks / nblk;
+  const int bhs = blk % per;
+  const int kb0 = blk / per;  // key block; block 0 has the most query tiles under a causal mask
+  const int split = bhs % gsplit, bh = bhs / gsplit;
   const int b = bh / H, kvh = bh % H;
+  const int gpw = group / gsplit;
   const int Hq = H * group;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
   const int key0 = kb0 * BLK + w * 32;
@@ -351,7 +356,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v,
   f16x dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
   const int t0 = CAUSAL ? (kb0 * BLK) / TILE : 0;
   const int nt = T / TILE;
-  for (int g = 0; g < group; ++g) {
+  for (int g = split * gpw; g < (split + 1) * gpw; ++g) {
     const int hq = kvh * group + g;
     const float* lse_bh = lse + ((int64_t)b * Hq + hq) * T;
     const float* del_bh = delta + ((int64_t)b * Hq + hq) * T;
@@ -364,7 +369,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v,
       lv = lse_bh[t0 * TILE + tid] * kLog2e;
       dlv = del_bh[t0 * TILE + tid];
     }
-    if (g > 0) __syncthreads();  // the previous head's last tile is still being read
+    if (g > split * gpw) __syncthreads();  // the previous head's last tile is still being read
     sq.rope(rp, t0 * TILE, tid);
     sq.store(Qs, RS, tid);
     so.store(Os, RS, tid);
@@ -434,8 +439,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v,
       }
     }
   }
-  uint16_t* dkr = dk.row(b, kvh, ki);
-  uint16_t* dvr = dv.row(b, kvh, ki);
+  uint16_t* dkr = dk.row(b, kvh, ki) + split * split_stride;
+  uint16_t* dvr = dv.row(b, kvh, ki) + split * split_stride;
   if (rp.cos != nullptr) {
     store_dT_rope(dkr, dkt[0], dkt[1], h, scale, rp, ki);
   } else {
@@ -448,15 +453,14 @@ __global__ __launch_bounds__(NT, 2) void bwd_dkdv_kernel(View q, View k, View v,
 
 // ============================================================================ backward: dQ
 template <bool CAUSAL>
-__global__ __launch_bounds__(NT, 2) void bwd_dq_kernel(View q, View k, View v, View dout,
-                                                        const float* __restrict__ lse, const float* __restrict__ delta,
-                                                        MView dq, int H, int T, int nblk, float sc2, float scale,
-                                                        int group, Rope rp) {
+__device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, View v, View dout,
+                                        const float* __restrict__ lse, const float* __restrict__ delta, MView dq,
+                                        int H, int T, int nblk, float sc2, float scale, int group, Rope rp) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[TILE * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[TILE * RS];
-  const int per = gridDim.x / nblk;
-  const int bh = blockIdx.x % per;
-  const int qb = CAUSAL ? nblk - 1 - blockIdx.x / per : blockIdx.x / per;
+  const int per = nblocks / nblk;
+  const int bh = blk % per;
+  const int qb = CAUSAL ? nblk - 1 - blk / per : blk / per;
   const int b = bh / H, hh = bh % H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
   const int q0 = qb * BLK + w * 32;
@@ -530,6 +534,44 @@ __global__ __launch_bounds__(NT, 2) void bwd_dq_kernel(View q, View k, View v, V
   } else {
     store_dT(dqr, dqt[0], 0, h, scale);
     store_dT(dqr, dqt[1], 1, h, scale);
+  }
+}
+
+// One launch for both backward passes: blocks [0, nkv) compute dK/dV, the rest dQ — the two
+// are independent, and for short sequences (SmolLM2: T = 128) neither fills the chip alone.
+template <bool CAUSAL>
+__global__ __launch_bounds__(NT, 2) void bwd_kernel(View q, View k, View v, View dout, const float* __restrict__ lse,
+                                                     const float* __restrict__ delta, MView dq, MView dk, MView dv,
+                                                     int Hq, int Hkv, int T, int nblk, float sc2, float scale,
+                                                     int group, Rope rp, int nkv, int gsplit, int64_t split_stride) {
+  if ((int)blockIdx.x < nkv)
+    dkdv_body<CAUSAL>(blockIdx.x, nkv, q, k, v, dout, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale, group, rp,
+                      gsplit, split_stride);
+  else
+    dq_body<CAUSAL>(blockIdx.x - nkv, gridDim.x - nkv, q, k, v, dout, lse, delta, dq, Hq, T, nblk, sc2, scale,
+                    group, rp);
+}
+
+// dk/dv[b, h, t, :] = Σ_s part[s][b][h][t][:] (fp32 sum of the gsplit partials); 8 elements per thread
+__global__ __launch_bounds__(NT) void gqa_reduce_kernel(const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pv,
+                                                         MView dk, MView dv, int Hkv, int T, int gsplit,
+                                                         int64_t split_stride, int64_t n8) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < 2 * n8; i += (int64_t)gridDim.x * NT) {
+    const bool isv = i >= n8;
+    const int64_t j = isv ? i - n8 : i;
+    const int d8 = (int)(j % (D / 8));
+    const int64_t row = j / (D / 8);  // (b, h, t) row of the contiguous partial
+    const int t = (int)(row % T), hh = (int)(row / T % Hkv), b = (int)(row / T / Hkv);
+    const uint16_t* src = (isv ? pv : pk) + row * D + d8 * 8;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < gsplit; ++sp) {
+      float x[8];
+      load8<bf16_t>(reinterpret_cast<const bf16_t*>(src + sp * split_stride), x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += x[e];
+    }
+    uint16_t* dst = (isv ? dv : dk).row(b, hh, t) + d8 * 8;
+    store8<bf16_t>(reinterpret_cast<bf16_t*>(dst), acc);
   }
 }
 
@@ -617,20 +659,36 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
   C10_HIP_KERNEL_LAUNCH_CHECK();
   const int nblk = T / BLK;
   const int Hkv = (int)k.size(1), group = H / Hkv;
-  const dim3 grid((unsigned)(B * H * nblk)), kvgrid((unsigned)(B * Hkv * nblk));
   const float sc2 = (float)scale * kLog2e;
-  if (causal) {
-    hipLaunchKernelGGL((bwd_dkdv_kernel<true>), kvgrid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dkv, dvv, Hkv, T, nblk, sc2, (float)scale, group, rp);
-    hipLaunchKernelGGL((bwd_dq_kernel<true>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale, group, rp);
-  } else {
-    hipLaunchKernelGGL((bwd_dkdv_kernel<false>), kvgrid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dkv, dvv, Hkv, T, nblk, sc2, (float)scale, group, rp);
-    hipLaunchKernelGGL((bwd_dq_kernel<false>), grid, dim3(NT), 0, st, qv, kv, vv, dov, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), dqv, H, T, nblk, sc2, (float)scale, group, rp);
+  // GQA with few key/value workgroups: split each kv head's query-head group over workgroups
+  const int gsplit = (group > 1 && B * Hkv * nblk < 256) ? group : 1;
+  const int nkv = B * Hkv * nblk * gsplit, nq = B * H * nblk;
+  MView dkw = dkv, dvw = dvv;
+  at::Tensor pk, pv;
+  int64_t split_stride = 0;
+  if (gsplit > 1) {  // contiguous partials [gsplit][B][Hkv][T][D]
+    pk = at::empty({gsplit, B, Hkv, T, D}, q.options());
+    pv = at::empty({gsplit, B, Hkv, T, D}, q.options());
+    split_stride = (int64_t)B * Hkv * T * D;
+    dkw = MView{static_cast<uint16_t*>(pk.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
+    dvw = MView{static_cast<uint16_t*>(pv.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
   }
+  if (causal)
+    hipLaunchKernelGGL((bwd_kernel<true>), dim3((unsigned)(nkv + nq)), dim3(NT), 0, st, qv, kv, vv, dov,
+                       lse.data_ptr<float>(), delta.data_ptr<float>(), dqv, dkw, dvw, H, Hkv, T, nblk, sc2,
+                       (float)scale, group, rp, nkv, gsplit, split_stride);
+  else
+    hipLaunchKernelGGL((bwd_kernel<false>), dim3((unsigned)(nkv + nq)), dim3(NT), 0, st, qv, kv, vv, dov,
+                       lse.data_ptr<float>(), delta.data_ptr<float>(), dqv, dkw, dvw, H, Hkv, T, nblk, sc2,
+                       (float)scale, group, rp, nkv, gsplit, split_stride);
   C10_HIP_KERNEL_LAUNCH_CHECK();
+  if (gsplit > 1) {
+    const int64_t n8 = (int64_t)B * Hkv * T * (D / 8);
+    const int blocks = (int)std::min<int64_t>((2 * n8 + NT - 1) / NT, 1024);
+    hipLaunchKernelGGL(gqa_reduce_kernel, dim3(blocks), dim3(NT), 0, st, static_cast<const uint16_t*>(pk.data_ptr()),
+                       static_cast<const uint16_t*>(pv.data_ptr()), dkv, dvv, Hkv, T, gsplit, split_stride, n8);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
 }
 
 }  // namespace attn
