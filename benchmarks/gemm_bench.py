@@ -88,14 +88,16 @@ def main():
                 for tile in (128128, 128064, 64128, 64064):
                     if M % (tile // 1000) or NN % (tile % 1000):
                         continue
-                    for wv, stg in ((4, 2), (4, 3), (8, 2), (8, 3)):
+                    for wv, stg, ks in ((4, 2, 1), (4, 3, 1), (8, 2, 1), (8, 3, 1), (4, 2, 2), (4, 3, 2)):
+                        if ks == 2 and tile == 128128:
+                            continue
                         if wv == 8 and tile != 128128:
                             continue
                         for s in (1, 2, 4, 8):
-                            if KK % (64 * s) or (s > 1 and KK // s < 256):
+                            if KK % (64 * s * ks) or (s > 1 and KK // s < 256):
                                 continue
-                            hint = wv * 10000000 + stg * 1000000 + tile
-                            var[f"{tile // 1000}x{tile % 1000}/w{wv}p{stg}/s{s}"] = round(
+                            hint = ks * 100000000 + wv * 10000000 + stg * 1000000 + tile
+                            var[f"{tile // 1000}x{tile % 1000}/w{wv}p{stg}k{ks}/s{s}"] = round(
                                 timeit(lambda: G.matmul(A, B, a_km=a_km, b_kn=b_kn, splits=s, tile=hint)) * 1e3, 1)
                 row["variants_us"] = var
             rows.append(row)

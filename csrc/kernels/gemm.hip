@@ -155,12 +155,13 @@ __device__ __forceinline__ float dgelu_tanh(float x) {  // d gelu / dx = s + 2xÂ
   return s + 2.f * x * s * (1.f - s) * kBeta * (1.f + 3.f * kKappa * x2);
 }
 
-template <int BM, int BN, int STAGES>
+template <int BM, int BN, int STAGES, int KS = 1>
 struct Smem {
   static constexpr int BUF = (BM + BN) * BK * 2;      // one A + B K-tile pair
   static constexpr int LDC = BN + 4;                  // fp32 C-tile row stride (+16 B: rows hit distinct banks)
-  static constexpr int CT = BM * LDC * 4;             // fp32 C tile, reuses the operand buffers after the K loop
-  static constexpr int BYTES = STAGES * BUF > CT ? STAGES * BUF : CT;
+  static constexpr int CT = BM * LDC * 4 + BM * 4;    // fp32 C tile (+ row-sum scratch), reuses the operand buffers
+  static constexpr int PIPE = KS * STAGES * BUF;      // one pipeline per K-split group
+  static constexpr int BYTES = PIPE > CT ? PIPE : CT;
 };
 
 // Wait until at most N of this wave's vector-memory ops (here: glds) are outstanding, retire
@@ -178,20 +179,27 @@ __device__ __forceinline__ void wait_barrier() {
 // 128x128).  STAGES = 3: tile t+2 is issued while t is computed and stays in flight across the
 // barrier (counted vmcnt) â€” the latency-bound regime of few, long-K tiles (weight gradients,
 // small token counts) where one workgroup per CU cannot hide a drained pipeline.
-// W = waves per workgroup: 4 (2x2, each wave (BM/2)x(BN/2)) or 8 (2x4, each (BM/2)x(BN/4): twice
+// W = waves per K-group: 4 (2x2, each wave (BM/2)x(BN/2)) or 8 (2x4, each (BM/2)x(BN/4): twice
 // the waves per SIMD to hide the barrier / DMA latency, at more LDS reads per MFMA).
-template <int BM, int BN, bool A_KM, bool B_KN, int EPI, int STAGES, int W>
-__global__ __launch_bounds__(64 * W, 2) void gemm_kernel(Args p) {
-  constexpr int NTW = 64 * W, WM = 2, WN = W / 2;
+// KS = K-split groups inside the workgroup: group g runs its own pipeline over K-tiles g, g+KS, â€¦
+// and the groups' fp32 tiles are summed in LDS before the epilogue â€” twice the independent work
+// per CU for small, latency-bound products (few tiles, one workgroup per CU), with no extra
+// global traffic or second kernel (unlike split-K across workgroups).
+template <int BM, int BN, bool A_KM, bool B_KN, int EPI, int STAGES, int W, int KS>
+__global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args p) {
+  constexpr int NTW = 64 * W * KS, WM = 2, WN = W / 2;
   constexpr int FM = BM / (16 * WM), FN = BN / (16 * WN);  // 16-wide fragments per wave along m / n
-  constexpr int A_BYTES = BM * BK * 2, BUF = Smem<BM, BN, STAGES>::BUF, LDC = Smem<BM, BN, STAGES>::LDC;
+  using SM = Smem<BM, BN, STAGES, KS>;
+  constexpr int A_BYTES = BM * BK * 2, BUF = SM::BUF, LDC = SM::LDC;
   constexpr int NPT = (BM + BN) / (8 * W);  // glds per thread per K-tile
   // one __shared__ array for everything (a second LDS object de-pipelines the glds loop:
   // cdna_hip_programming.md Â§5 "Projection GEMM" item 4a)
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[Smem<BM, BN, STAGES>::BYTES];
+  __shared__ __attribute__((aligned(1024))) uint8_t smem_all[SM::BYTES];
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave_all = threadIdx.x >> 6;
+  const int kg = wave_all / W, wave = wave_all % W;  // K-split group, wave within the group
   const int wm = wave / WN, wn = wave % WN;
+  uint8_t* smem = smem_all + kg * (STAGES * BUF);   // this group's pipeline buffers
 
   // XCD-aware bijective remap, then 8-row groups sweeping the column tiles
   const int nwg = p.tiles_m * p.tiles_n;
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(64 * W, 2) void gemm_kernel(Args p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;  // bf16 1.0
 
-  const int nk = p.K / BK;
+  const int nk = p.K / BK / KS;  // K-tiles of this group: t_global = t * KS + kg
   auto compute = [&](const uint8_t* cur) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -251,8 +259,8 @@ __global__ __launch_bounds__(64 * W, 2) void gemm_kernel(Args p) {
     }
   };
   auto stage_tile = [&](int t, uint8_t* buf) {
-    stage<BM, A_KM, W>(A, p.lda, m0, t * BK, buf, wave, lane);
-    stage<BN, B_KN, W>(B, p.ldb, n0, t * BK, buf + A_BYTES, wave, lane);
+    stage<BM, A_KM, W>(A, p.lda, m0, (t * KS + kg) * BK, buf, wave, lane);
+    stage<BN, B_KN, W>(B, p.ldb, n0, (t * KS + kg) * BK, buf + A_BYTES, wave, lane);
   };
 
   if constexpr (STAGES == 2) {
@@ -301,20 +309,47 @@ __global__ __launch_bounds__(64 * W, 2) void gemm_kernel(Args p) {
   // global traffic is row-contiguous: each thread then owns 8 consecutive columns of a row â€”
   // 16-B bf16 stores / aux loads, 32-B fp32 slab stores.  acc[i][j] element e = C[m][n] with
   // m = .. + (lane&15), n = .. + 4(lane>>4) + e.
-  float* ct = reinterpret_cast<float*>(smem);
+  float* ct = reinterpret_cast<float*>(smem_all);
+  float* rsb = ct + BM * LDC;  // K-split row-sum scratch
+  auto cslot = [&](int i, int j) -> f4* {
+    return reinterpret_cast<f4*>(ct + (wm * (BM / WM) + 16 * j + (lane & 15)) * LDC + wn * (BN / WN) + 16 * i +
+                                 4 * (lane >> 4));
+  };
+  if (kg == 0) {
 #pragma unroll
-  for (int i = 0; i < FN; ++i)
+    for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int j = 0; j < FM; ++j)
-      *reinterpret_cast<f4*>(ct + (wm * (BM / WM) + 16 * j + (lane & 15)) * LDC + wn * (BN / WN) + 16 * i +
-                             4 * (lane >> 4)) = acc[i][j];
+      for (int j = 0; j < FM; ++j) *cslot(i, j) = acc[i][j];
+  } else if constexpr (ROWSUM) {
+    if (do_rs && lane < 16)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) rsb[wm * (BM / WM) + 16 * j + lane] = accb[j][0];
+  }
   __syncthreads();
+  if constexpr (KS > 1) {  // the second group adds its partial tile (and row sums)
+    if (kg == 1) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          f4 v = *cslot(i, j);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += acc[i][j][e];
+          *cslot(i, j) = v;
+        }
+    } else if constexpr (ROWSUM) {
+      if (do_rs && lane < 16)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) accb[j][0] += rsb[wm * (BM / WM) + 16 * j + lane];
+    }
+    __syncthreads();
+  }
 
   constexpr int CPR = BN / 8;  // 8-column chunks per row
   const int S = gridDim.y;
   if constexpr (ROWSUM) {
     // lanes 0..15 hold row m = .. + lane in element 0 (all four elements are equal)
-    if (do_rs && lane < 16) {
+    if (do_rs && kg == 0 && lane < 16) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
         const int m = m0 + wm * (BM / WM) + 16 * j + lane;
@@ -392,31 +427,34 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ w
 
 // ---- host --------------------------------------------------------------------------------------
 struct Tile {
-  int bm, bn, stages, waves;
+  int bm, bn, stages, waves, ks;
 };
 
 template <bool A_KM, bool B_KN, int EPI>
 static void launch_epi(const Tile& t, const Args& a, dim3 grid, hipStream_t st) {
-#define NBD_GEMM_K(BM_, BN_, S_, W_) \
-  hipLaunchKernelGGL((gemm_kernel<BM_, BN_, A_KM, B_KN, EPI, S_, W_>), grid, dim3(64 * W_), 0, st, a)
-#define NBD_GEMM_CASE(BM_, BN_)                         \
-  if (t.bm == BM_ && t.bn == BN_ && t.waves == 4) {     \
-    if (t.stages == 3) NBD_GEMM_K(BM_, BN_, 3, 4);      \
-    else NBD_GEMM_K(BM_, BN_, 2, 4);                    \
-    return;                                             \
+#define NBD_GEMM_K(BM_, BN_, S_, W_, KS_)                                                              \
+  hipLaunchKernelGGL((gemm_kernel<BM_, BN_, A_KM, B_KN, EPI, S_, W_, KS_>), grid, dim3(64 * W_ * KS_), 0, st, a)
+#define NBD_GEMM_CASE(BM_, BN_, KS_)                                   \
+  if (t.bm == BM_ && t.bn == BN_ && t.waves == 4 && t.ks == KS_) {     \
+    if (t.stages == 3) NBD_GEMM_K(BM_, BN_, 3, 4, KS_);                \
+    else NBD_GEMM_K(BM_, BN_, 2, 4, KS_);                              \
+    return;                                                            \
   }
-  NBD_GEMM_CASE(128, 128)
-  NBD_GEMM_CASE(128, 64)
-  NBD_GEMM_CASE(64, 128)
-  NBD_GEMM_CASE(64, 64)
-  if (t.bm == 128 && t.bn == 128 && t.waves == 8) {  // 8 waves: 128x128 only
-    if (t.stages == 3) NBD_GEMM_K(128, 128, 3, 8);
-    else NBD_GEMM_K(128, 128, 2, 8);
+  NBD_GEMM_CASE(128, 128, 1)
+  NBD_GEMM_CASE(128, 64, 1)
+  NBD_GEMM_CASE(64, 128, 1)
+  NBD_GEMM_CASE(64, 64, 1)
+  NBD_GEMM_CASE(128, 64, 2)  // intra-workgroup K-split: small, latency-bound products
+  NBD_GEMM_CASE(64, 128, 2)
+  NBD_GEMM_CASE(64, 64, 2)
+  if (t.bm == 128 && t.bn == 128 && t.waves == 8 && t.ks == 1) {  // 8 waves: 128x128 only
+    if (t.stages == 3) NBD_GEMM_K(128, 128, 3, 8, 1);
+    else NBD_GEMM_K(128, 128, 2, 8, 1);
     return;
   }
 #undef NBD_GEMM_CASE
 #undef NBD_GEMM_K
-  TORCH_CHECK(false, "nbd::gemm: no kernel for tile ", t.bm, "x", t.bn, " with ", t.waves, " waves");
+  TORCH_CHECK(false, "nbd::gemm: no kernel for tile ", t.bm, "x", t.bn, " with ", t.waves, " waves, K-split ", t.ks);
 }
 
 template <bool A_KM, bool B_KN>
@@ -452,13 +490,14 @@ static bool tile_fits(const Tile& t, int M, int N) { return M % t.bm == 0 && N %
 // overrides it.
 static Tile pick_tile(int M, int N, int64_t tile_hint) {
   if (tile_hint > 0) {
-    // hint = waves*10000000 + stages*1000000 + BM*1000 + BN (waves 0 -> 4, stages 0 -> 2)
-    const int stg = (int)(tile_hint / 1000000 % 10), wv = (int)(tile_hint / 10000000);
-    Tile t{(int)(tile_hint / 1000 % 1000), (int)(tile_hint % 1000), stg == 3 ? 3 : 2, wv == 8 ? 8 : 4};
+    // hint = ks*10^8 + waves*10^7 + stages*10^6 + BM*1000 + BN (ks 0 -> 1, waves 0 -> 4, stages 0 -> 2)
+    const int stg = (int)(tile_hint / 1000000 % 10), wv = (int)(tile_hint / 10000000 % 10);
+    const int ks = (int)(tile_hint / 100000000);
+    Tile t{(int)(tile_hint / 1000 % 1000), (int)(tile_hint % 1000), stg == 3 ? 3 : 2, wv == 8 ? 8 : 4, ks == 2 ? 2 : 1};
     TORCH_CHECK(tile_fits(t, M, N), "nbd::gemm: tile ", t.bm, "x", t.bn, " does not divide ", M, "x", N);
     return t;
   }
-  const Tile cands[4] = {{128, 128, 2, 4}, {128, 64, 2, 4}, {64, 128, 2, 4}, {64, 64, 2, 4}};
+  const Tile cands[4] = {{128, 128, 2, 4, 1}, {128, 64, 2, 4, 1}, {64, 128, 2, 4, 1}, {64, 64, 2, 4, 1}};
   int best = -1;
   for (int i = 0; i < 4; ++i) {
     if (!tile_fits(cands[i], M, N)) continue;
@@ -505,7 +544,7 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   const Tile t = pick_tile(M, N, tile_hint);
   const int tiles = (M / t.bm) * (N / t.bn);
   const int S = splits > 0 ? (int)splits : 1;
-  TORCH_CHECK(K % (BK * S) == 0, "nbd::gemm: K not divisible into ", S, " splits");
+  TORCH_CHECK(K % (BK * S * t.ks) == 0, "nbd::gemm: K not divisible into ", S, " splits x ", t.ks, " K-groups");
   TORCH_CHECK(S == 1 || ((epi == EPI_NONE || epi == EPI_ROWSUM) && !bias),
               "nbd::gemm: split-K only without an elementwise epilogue");
 

@@ -18,6 +18,7 @@ from ._lib import _require
 
 # NBD_HIP_GEMM=0 routes gemm_linear / mlp_gelu to PyTorch (hipBLASLt) — for A/B measurements
 ENABLED = os.environ.get("NBD_HIP_GEMM", "1") != "0"
+KSPLIT = os.environ.get("NBD_GEMM_KSPLIT", "1") != "0"  # 0: tuned K-split kernels run as one K-group (A/B)
 
 EPI_NONE, EPI_GELU, EPI_DGELU, EPI_ROWSUM = 0, 1, 2, 3
 
@@ -27,16 +28,17 @@ def gemm_ok(M: int, N: int, K: int) -> bool:
 
 
 # Measured best (kernel, split-K) per (a_km, b_kn, M, N, K) on MI355X for the bench workloads'
-# Linear products — kernel = waves*10^7 (8 waves; 4 if absent) + stages*10^6 + BM*1000 + BN; from
+# Linear products — kernel = ks*10^8 (2 K-groups in the workgroup; 1 if absent) + waves*10^7
+# (8 waves; 4 if absent) + stages*10^6 + BM*1000 + BN; from
 # benchmarks/gemm_bench.py --sweep
 # (profiles/gemm_bench_r1.txt; split-K only where it beats the best unsplit kernel by > 5 %).
 _TUNED = {
     (False, False, 8192, 2304, 768): (82128128, 1),  # gpt2.c_attn fwd 44.5 us
     (False, True, 8192, 768, 2304): (82128128, 1),  # gpt2.c_attn dgrad 42.3 us
-    (True, True, 2304, 768, 8192): (3064128, 2),  # gpt2.c_attn wgrad 52.5 us
+    (True, True, 2304, 768, 8192): (203128064, 1),  # gpt2.c_attn wgrad 49.7 us (K-split groups)
     (False, False, 8192, 768, 768): (82128128, 1),  # gpt2.attn.c_proj fwd 21.0 us
     (False, True, 8192, 768, 768): (2128064, 1),  # gpt2.attn.c_proj dgrad 21.8 us
-    (True, True, 768, 768, 8192): (3064064, 8),  # gpt2.attn.c_proj wgrad 32.7 us
+    (True, True, 768, 768, 8192): (203064064, 1),  # gpt2.attn.c_proj wgrad 32.7 us (no reduce kernel)
     (False, False, 8192, 3072, 768): (82128128, 1),  # gpt2.c_fc fwd 49.7 us
     (False, True, 8192, 768, 3072): (2128128, 1),  # gpt2.c_fc dgrad 50.9 us
     (True, True, 3072, 768, 8192): (3064128, 4),  # gpt2.c_fc wgrad 72.6 us
@@ -45,16 +47,16 @@ _TUNED = {
     (True, True, 768, 3072, 8192): (82128128, 2),  # gpt2.mlp.c_proj wgrad 68.9 us
     (False, False, 2048, 960, 576): (3064064, 1),  # smollm2.qkv fwd 13.5 us
     (False, True, 2048, 576, 960): (3064064, 1),  # smollm2.qkv dgrad 14.9 us
-    (True, True, 960, 576, 2048): (3064064, 1),  # smollm2.qkv wgrad 18.1 us
+    (True, True, 960, 576, 2048): (203064064, 1),  # smollm2.qkv wgrad 13.2 us (15.3 one K-group)
     (False, False, 2048, 576, 576): (2064064, 1),  # smollm2.o_proj fwd 12.6 us
     (False, True, 2048, 576, 576): (2064064, 1),  # smollm2.o_proj dgrad 13.0 us
-    (True, True, 576, 576, 2048): (3064064, 1),  # smollm2.o_proj wgrad 17.9 us
+    (True, True, 576, 576, 2048): (203064064, 1),  # smollm2.o_proj wgrad 13.2 us (15.0)
     (False, False, 2048, 3072, 576): (2064128, 1),  # smollm2.gate_up fwd 19.4 us
-    (False, True, 2048, 576, 3072): (3064064, 1),  # smollm2.gate_up dgrad 26.1 us
+    (False, True, 2048, 576, 3072): (202064064, 1),  # smollm2.gate_up dgrad 22.3 us
     (True, True, 3072, 576, 2048): (3064064, 1),  # smollm2.gate_up wgrad 22.0 us
-    (False, False, 2048, 576, 1536): (3064064, 1),  # smollm2.down fwd 18.0 us
+    (False, False, 2048, 576, 1536): (202064064, 1),  # smollm2.down fwd 13.6 us (14.5)
     (False, True, 2048, 1536, 576): (2064064, 1),  # smollm2.down dgrad 15.3 us
-    (True, True, 576, 1536, 2048): (3064064, 1),  # smollm2.down wgrad 18.3 us
+    (True, True, 576, 1536, 2048): (203064064, 1),  # smollm2.down wgrad 13.7 us (15.6)
 }
 
 _TILES = (128128, 128064, 64128, 64064)
@@ -73,7 +75,7 @@ def config(a_km: bool, b_kn: bool, M: int, N: int, K: int, can_split: bool = Tru
     <= 8 splits, each >= 512 deep) — split-K (a second, reducing kernel) only without an epilogue."""
     hit = _TUNED.get((a_km, b_kn, M, N, K))
     if hit is not None and (can_split or hit[1] == 1):
-        return hit
+        return hit if KSPLIT else (hit[0] % 100000000, hit[1])
     fits = [t for t in _TILES if _ntiles(t, M, N)]
     if not fits:
         return 0, 1
@@ -99,8 +101,9 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
     ``b_kn``).  ``epi``: EPI_NONE (+bias), EPI_GELU (+bias, returns (gelu(pre), pre)),
     EPI_DGELU (C · gelu'(aux)), EPI_ROWSUM (weight-gradient layout; returns (C, Σ_k A[m,k]) —
     the bias gradient of the Linear whose weight gradient C is).  ``splits=0`` picks split-K automatically (no-epilogue only);
-    ``tile`` = waves*10^7 + stages*10^6 + BM*1000 + BN forces a kernel (waves 4 or 8, 8 only at
-    128x128; stages 2 or 3; benchmarks)."""
+    ``tile`` = ks*10^8 + waves*10^7 + stages*10^6 + BM*1000 + BN forces a kernel (waves 4 or 8,
+    8 only at 128x128; stages 2 or 3; ks = 2 runs two K-groups of 4 waves inside the workgroup,
+    tiles other than 128x128, K a multiple of 128; benchmarks)."""
     import torch
 
     M = a.shape[1] if a_km else a.shape[0]

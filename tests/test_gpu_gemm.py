@@ -34,10 +34,13 @@ def _err(x, ref):
 
 
 @pytest.mark.parametrize("layout", LAYOUTS, ids=["fwd", "dgrad", "wgrad"])
-@pytest.mark.parametrize("tile", [128128, 128064, 64128, 64064, 3128128, 3128064, 3064128, 3064064, 82128128, 83128128])
+@pytest.mark.parametrize("tile", [128128, 128064, 64128, 64064, 3128128, 3128064, 3064128, 3064064, 82128128, 83128128,
+                                  202064064, 203064064, 202128064, 203064128])
 @pytest.mark.parametrize("shape", [(256, 256, 320), (384, 640, 192), (128, 128, 64), (128, 128, 128)])
 def test_gemm_layouts_and_tiles(layout, tile, shape):
     M, N, K = shape
+    if tile >= 100000000:  # intra-workgroup K-split: K in multiples of 2 x 64
+        K = 2 * K if K % 128 else K
     a_km, b_kn = layout
     a, b = _operands(M, N, K, a_km, b_kn)
     c = G.matmul(a, b, a_km=a_km, b_kn=b_kn, tile=tile, splits=1)
@@ -154,7 +157,7 @@ def test_gemm_split_k_is_deterministic():
 
 
 @pytest.mark.parametrize("splits", [1, 2, 8])
-@pytest.mark.parametrize("tile", [2128128, 3064128, 2064064, 3128064, 82128128, 83128128])
+@pytest.mark.parametrize("tile", [2128128, 3064128, 2064064, 3128064, 82128128, 83128128, 202064064, 203064128])
 def test_gemm_rowsum_epilogue_is_the_bias_gradient(splits, tile):
     # weight-gradient layout: dW = dyᵀ·x and db = Σ_tokens dy from the same kernel
     M, N, K = 256, 384, 2048
