@@ -48,6 +48,8 @@ class Config:
     # timeline ring buffer
     timeline_capacity: int = field(default_factory=lambda: _env("NBD_TIMELINE_CAPACITY", 2000, int))
     log_level: str = field(default_factory=lambda: _env("NBD_LOG_LEVEL", "WARNING"))
+    # fault injection armed at worker start (faults.py grammar, e.g. "crash:7@1#3")
+    faults: str = field(default_factory=lambda: _env("NBD_FAULTS", ""))
 
     def as_dict(self):
         return {f.name: getattr(self, f.name) for f in fields(self)}

@@ -82,12 +82,17 @@ class CellExecutor:
             return _run_coroutine(coro)
         return eval(code_obj, self.ns)
 
-    def run(self, code: str, echo: bool = True) -> ExecResult:
+    def run(self, code: str, echo: bool = True, pre=None) -> ExecResult:
+        """Execute one cell.  ``pre`` (optional callable) runs first, inside the same error
+        handling as the cell (used by fault injection: an injected hang is interruptible and an
+        injected exception is reported like the cell's own)."""
         t0 = time.time()
         p0 = time.perf_counter()
         filename = self._register_source(code)
         res = ExecResult(status="ok", t_start=t0, filename=filename)
         try:
+            if pre is not None:
+                pre()
             try:
                 tree = ast.parse(code, filename=filename, mode="exec")
             except SyntaxError as e:

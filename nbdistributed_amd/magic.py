@@ -445,6 +445,41 @@ class MagicCore:
         what = "Killed" if args.kill else "Interrupt sent to"
         self.p(f"⚡ {what} ranks {format_ranks(ranks or s.all_ranks())}")
 
+    def dist_fault(self, line: str = "") -> None:
+        """%dist_fault SPEC [SPEC ...] | --clear | --list — inject failures for testing the recovery
+        paths.  SPEC = kind[:arg][@ranks][#cell], kind in crash/abort/hang/delay/raise/flood
+        (see nbdistributed_amd/faults.py); e.g. ``%dist_fault crash:7@1#2``."""
+        p = _parser("%dist_fault")
+        p.add_argument("specs", nargs="*")
+        p.add_argument("--clear", action="store_true")
+        p.add_argument("--list", action="store_true")
+        args = p.parse_args(shlex.split(line))
+        s = self.session
+        if not s.active:
+            self.p("No distributed workers running")
+            return
+        if args.clear or args.list:
+            res = s.fault("clear" if args.clear else "list")
+        elif args.specs:
+            try:
+                res = s.fault("arm", ";".join(args.specs))
+            except ValueError as e:
+                self.p(f"❌ {e}")
+                return
+        else:
+            self.p("Usage: %dist_fault kind[:arg][@ranks][#cell] ... | --clear | --list")
+            return
+        for r in sorted(res):
+            v = res[r]
+            if isinstance(v, dict) and "error" in v:
+                self.p(f"Rank {r}: ❌ {v['error']}")
+            elif args.clear:
+                self.p(f"Rank {r}: cleared {v.get('cleared', 0)}")
+            else:
+                pend = ", ".join(v.get("pending") or []) or "none armed"
+                fired = v.get("fired")
+                self.p(f"Rank {r}: {pend}" + (f"; fired: {', '.join(fired)}" if fired else ""))
+
     def dist_recover(self, line: str = "") -> None:
         s = self.session
         if not s.active:
@@ -565,7 +600,8 @@ class MagicCore:
 
 LINE_MAGICS = ["dist_init", "sync", "dist_status", "dist_mode", "dist_shutdown", "dist_reset", "dist_debug",
                "dist_sync_ide", "timeline_save", "timeline_debug", "timeline_clear", "dist_interrupt",
-               "dist_recover", "dist_pull", "dist_push", "dist_profile", "dist_checkpoint", "dist_topology"]
+               "dist_recover", "dist_pull", "dist_push", "dist_profile", "dist_checkpoint", "dist_topology",
+               "dist_fault"]
 CELL_MAGICS = ["distributed", "rank"]
 
 

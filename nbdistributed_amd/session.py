@@ -432,6 +432,22 @@ class Session:
         data.update(kw)
         return comm.send_to_ranks(self.alive_ranks(), "profile", data, timeout=timeout)
 
+    def call(self, name: str, args: Optional[Dict[str, Any]] = None, ranks: Optional[List[int]] = None,
+             timeout: float = 30.0) -> Dict[int, Any]:
+        """Invoke the worker-side call handler ``name`` (``DistributedWorker.calls``) on ``ranks``
+        (default: every live rank)."""
+        comm = self._require()
+        return comm.send_to_ranks(ranks or self.alive_ranks(), "call", {"name": name, "args": args or {}},
+                                  timeout=timeout)
+
+    def fault(self, action: str = "arm", spec: str = "", timeout: float = 30.0) -> Dict[int, Any]:
+        """Arm (``spec`` in the faults.py grammar), clear or list injected faults on every live rank."""
+        from . import faults
+
+        if action == "arm":
+            faults.parse(spec)  # validate here: a bad spec fails in the notebook, not on the ranks
+        return self.call("fault", {"action": action, "spec": spec}, timeout=timeout)
+
     def ping(self, timeout: float = 5.0) -> Dict[int, float]:
         """Control-plane round trip per rank (seconds)."""
         comm = self._require()

@@ -38,6 +38,7 @@ import time
 import traceback
 from typing import Any, Dict, Optional
 
+from . import faults
 from . import protocol as P
 from .config import get_config
 from .executor import CellExecutor
@@ -100,6 +101,9 @@ class DistributedWorker:
         self.tracker = NamespaceTracker()
         self.guard = CollectiveGuard()
         self.executor = CellExecutor(tag=f"cell-r{rank}")
+        self.faults = faults.FaultPlan(rank, faults.parse(self.cfg.faults))
+        # T_CALL handlers by name (extensibility hook; data = {"name": ..., "args": {...}})
+        self.calls: Dict[str, Any] = {"fault": self.call_fault}
         self.ns = self.executor.ns
         self.sock: Optional[Socket] = None
         self.console_err = sys.__stderr__
@@ -310,7 +314,8 @@ class DistributedWorker:
         self.cell_seq = seq
         self.in_cell = True
         try:
-            res = self.executor.run(code, echo=not (flags & P.F_NO_ECHO))
+            res = self.executor.run(code, echo=not (flags & P.F_NO_ECHO),
+                                    pre=self.faults.before_cell if self.faults.pending else None)
         finally:
             self.in_cell = False
             self.guard.exit()
@@ -428,6 +433,18 @@ class DistributedWorker:
             return {"status": "stopped", "rank": self.rank, "trace": os.path.abspath(path), "table": table}
         raise ValueError(f"unknown profile action {action!r}")
 
+    def call_fault(self, args: Dict[str, Any]) -> Dict[str, Any]:
+        """Arm / clear / list injected faults (``%dist_fault``; grammar in faults.py)."""
+        action = args.get("action", "arm")
+        if action == "arm":
+            armed = [f.spec() for f in faults.parse(args.get("spec", "")) if self.faults.arm(f)]
+            return {"rank": self.rank, "armed": armed, "pending": self.faults.armed()}
+        if action == "clear":
+            return {"rank": self.rank, "cleared": self.faults.clear(), "pending": []}
+        if action == "list":
+            return {"rank": self.rank, "pending": self.faults.armed(), "fired": list(self.faults.fired)}
+        raise ValueError(f"unknown fault action {action!r}")
+
     def dispatch(self, h: P.Header, data: Any) -> Any:
         t = h.mtype
         if t == P.T_EXECUTE:
@@ -450,6 +467,11 @@ class DistributedWorker:
             return self.handle_recover(data)
         if t == P.T_PROFILE:
             return self.handle_profile(data)
+        if t == P.T_CALL:
+            fn = self.calls.get(data.get("name")) if isinstance(data, dict) else None
+            if fn is None:
+                raise ValueError(f"no worker call handler {data.get('name') if isinstance(data, dict) else data!r}")
+            return fn(data.get("args") or {})
         if t == P.T_INTERRUPT:
             return None  # the signal already did the work; nothing to answer
         raise ValueError(f"unknown message type {h.mtype}")

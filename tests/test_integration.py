@@ -242,6 +242,9 @@ def test_rank_crash_mid_cell_fails_fast_with_partial_results():
         r2 = s.execute("rank", raise_on_error=False)
         assert 1 in r2.dead and time.time() - t < 2
         assert r2.results[0]["output"] == "0"
+        deadline = time.time() + 5  # the socket EOF can beat the process waiter
+        while s.status()[1]["returncode"] is None and time.time() < deadline:
+            time.sleep(0.05)
         st = s.status()
         assert st[1]["running"] is False and st[1]["returncode"] == 7
     finally:

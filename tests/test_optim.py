@@ -105,6 +105,8 @@ opt2.load_state_dict(sd)
 def sess():
     s = Session(writer=lambda t: None)
     s.start(2, backend="gloo")
+    # every test can run alone (pytest-xdist spreads a module's tests over processes)
+    assert s.execute(SETUP, render=False).ok
     yield s
     s.shutdown()
 
