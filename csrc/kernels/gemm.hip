@@ -33,7 +33,9 @@
 //   * epilogue staged through LDS: each thread stores 8 consecutive bf16 of a row (16 B).
 // Epilogues: + bias[n]; GELU-tanh (stores the pre-activation for the backward too);
 // dGELU (multiplies by gelu'(pre-activation) — the MLP's activation backward fused into the
-// dgrad of its output projection).
+// dgrad of its output projection); SwiGLU (Llama: the gate|up projection's workgroup takes
+// matching gate and up columns, writes silu(g)·u and the pre-activations) and its backward
+// (the down projection's dgrad writes d[g|u] from dact and the saved pre-activations).
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -56,7 +58,12 @@ constexpr int NT = 256;
 
 // EPI_ROWSUM (weight-gradient layout): also Σ_k A[m,k] -> aux_out[m] — the Linear's bias gradient
 // (Σ over tokens of dy) from the A fragments already in registers, one extra MFMA per fragment.
-enum Epi : int { EPI_NONE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_ROWSUM = 3 };
+// EPI_SWIGLU (forward layout, B = [gate; up] weights [2I][K]): tile column block tn stages gate
+// rows tn·BN/2.. and up rows I + tn·BN/2.. side by side, so the epilogue has g and u of the same
+// feature: c = silu(g)·u [M][I], aux_out = [g|u] pre-activations [M][2I].
+// EPI_DSWIGLU (dgrad layout, C = dact [M][I] never stored): aux_in = [g|u] [M][2I];
+// c = d[g|u] [M][2I] = [dact·u·σ(g)(1 + g(1−σ(g))) | dact·silu(g)].
+enum Epi : int { EPI_NONE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_ROWSUM = 3, EPI_SWIGLU = 4, EPI_DSWIGLU = 5 };
 
 struct Args {
   const uint16_t* a;
@@ -64,8 +71,9 @@ struct Args {
   uint16_t* c;             // [M][ldc] bf16
   float* ws;               // split-K: [splits][M][ldc] fp32 slabs
   const uint16_t* bias;    // [N] or nullptr
-  const uint16_t* aux_in;  // EPI_DGELU: pre-activation [M][ldc]
-  uint16_t* aux_out;       // EPI_GELU: pre-activation out [M][ldc]; EPI_ROWSUM: row sums [M]
+  const uint16_t* aux_in;  // EPI_DGELU: pre-activation [M][ldc]; EPI_DSWIGLU: [g|u] [M][2N]
+  uint16_t* aux_out;       // EPI_GELU: pre-activation out [M][ldc]; EPI_ROWSUM: row sums [M];
+                           // EPI_SWIGLU: [g|u] out [M][N]
   int M, N, K;             // K = reduction length handled by one split
   int64_t lda, ldb, ldc;
   int tiles_m, tiles_n;
@@ -99,9 +107,11 @@ __device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* lds_wave_ba
 
 // Stage one 64-deep K-tile of an operand into its LDS image.  R = tile rows (BM or BN).
 // TR = false: global [rows][k] (row r0.., k0..), image [R][64]; TR = true: global [k][rows], image [64][R].
+// r1 = first global row of the tile's second half (r0 + R/2 for a contiguous tile; EPI_SWIGLU
+// gives the up rows there; row images only).
 template <int R, bool TR, int W>
 __device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld, int r0, int k0, uint8_t* img,
-                                      int wave, int lane) {
+                                      int wave, int lane, int r1 = -1) {
   constexpr int PER_WAVE = R / (8 * W);  // (R*64*2 B) / (W waves * 1 KiB)
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
@@ -110,7 +120,8 @@ __device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld
     const uint16_t* src;
     if constexpr (!TR) {
       const int r = byte >> 7, pc = (byte >> 4) & 7;
-      src = g + (int64_t)(r0 + r) * ld + k0 + 8 * (pc ^ row_swz(r));
+      const int row = (r1 >= 0 && r >= R / 2) ? r1 + r - R / 2 : r0 + r;
+      src = g + (int64_t)row * ld + k0 + 8 * (pc ^ row_swz(r));
     } else {
       constexpr int RB = 2 * R;
       const int k = byte / RB, pc = (byte % RB) >> 4;
@@ -146,6 +157,7 @@ constexpr float kKappa = 0.044715f;
 // tanh(u) = 2σ(2u) − 1 with σ from v_exp_f32 + one reciprocal (libm tanhf's branchy slow path
 // made the fused epilogue cost as much as a separate elementwise pass)
 __device__ __forceinline__ float sig2(float u) { return __fdividef(1.f, 1.f + __expf(-2.f * u)); }
+__device__ __forceinline__ float sigm(float x) { return __fdividef(1.f, 1.f + __expf(-x)); }
 __device__ __forceinline__ float gelu_tanh(float x) {  // 0.5x(1 + tanh u) = x·σ(2u)
   return x * sig2(kBeta * (x + kKappa * x * x * x));
 }
@@ -260,7 +272,10 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
   };
   auto stage_tile = [&](int t, uint8_t* buf) {
     stage<BM, A_KM, W>(A, p.lda, m0, (t * KS + kg) * BK, buf, wave, lane);
-    stage<BN, B_KN, W>(B, p.ldb, n0, (t * KS + kg) * BK, buf + A_BYTES, wave, lane);
+    if constexpr (EPI == EPI_SWIGLU)
+      stage<BN, B_KN, W>(B, p.ldb, n0 / 2, (t * KS + kg) * BK, buf + A_BYTES, wave, lane, p.N / 2 + n0 / 2);
+    else
+      stage<BN, B_KN, W>(B, p.ldb, n0, (t * KS + kg) * BK, buf + A_BYTES, wave, lane);
   };
 
   if constexpr (STAGES == 2) {
@@ -374,6 +389,60 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
     return;
   }
 
+  if constexpr (EPI == EPI_SWIGLU) {
+    // tile columns [0, BN/2) = gate features n0/2.., [BN/2, BN) = up features of the same indices
+    constexpr int HPR = BN / 16;  // 8-column chunks per half row
+    const int I = p.N / 2;
+    for (int c = threadIdx.x; c < BM * HPR; c += NTW) {
+      const int r = c / HPR, cn = (c % HPR) * 8;
+      float g[8], u[8];
+      {
+        const f4 g0 = *reinterpret_cast<const f4*>(ct + r * LDC + cn);
+        const f4 g1 = *reinterpret_cast<const f4*>(ct + r * LDC + cn + 4);
+        const f4 u0 = *reinterpret_cast<const f4*>(ct + r * LDC + BN / 2 + cn);
+        const f4 u1 = *reinterpret_cast<const f4*>(ct + r * LDC + BN / 2 + cn + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          g[e] = g0[e]; g[e + 4] = g1[e]; u[e] = u0[e]; u[e + 4] = u1[e];
+        }
+      }
+      const int64_t m = m0 + r, j = n0 / 2 + cn;
+      store8<bf16_t>(reinterpret_cast<bf16_t*>(p.aux_out) + m * p.N + j, g);
+      store8<bf16_t>(reinterpret_cast<bf16_t*>(p.aux_out) + m * p.N + I + j, u);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = g[e] * sigm(g[e]) * u[e];
+      store8<bf16_t>(reinterpret_cast<bf16_t*>(p.c) + m * p.ldc + j, g);
+    }
+    return;
+  }
+  if constexpr (EPI == EPI_DSWIGLU) {
+    // v = dact[m][j]; pre-activations [g|u] and the output d[g|u] are [M][2N]
+    for (int c = threadIdx.x; c < BM * CPR; c += NTW) {
+      const int r = c / CPR, cn = (c % CPR) * 8;
+      float d[8], g[8], u[8];
+      {
+        const f4 lo = *reinterpret_cast<const f4*>(ct + r * LDC + cn);
+        const f4 hi = *reinterpret_cast<const f4*>(ct + r * LDC + cn + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          d[e] = lo[e]; d[e + 4] = hi[e];
+        }
+      }
+      const int64_t off = (int64_t)(m0 + r) * 2 * p.N + n0 + cn;
+      load8<bf16_t>(reinterpret_cast<const bf16_t*>(p.aux_in) + off, g);
+      load8<bf16_t>(reinterpret_cast<const bf16_t*>(p.aux_in) + off + p.N, u);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sg = sigm(g[e]);
+        const float du = d[e] * g[e] * sg;
+        d[e] = d[e] * u[e] * sg * (1.f + g[e] * (1.f - sg));
+        u[e] = du;
+      }
+      store8<bf16_t>(reinterpret_cast<bf16_t*>(p.c) + off, d);
+      store8<bf16_t>(reinterpret_cast<bf16_t*>(p.c) + off + p.N, u);
+    }
+    return;
+  }
   for (int c = threadIdx.x; c < BM * CPR; c += NTW) {
     const int r = c / CPR, cn = (c % CPR) * 8;
     float v[8];
@@ -473,6 +542,18 @@ static void launch_layout(int epi, const Tile& t, const Args& a, dim3 grid, hipS
         return;
       }
       break;
+    case EPI_SWIGLU:
+      if constexpr (!A_KM && !B_KN) {
+        launch_epi<false, false, EPI_SWIGLU>(t, a, grid, st);
+        return;
+      }
+      break;
+    case EPI_DSWIGLU:
+      if constexpr (!A_KM && B_KN) {
+        launch_epi<false, true, EPI_DSWIGLU>(t, a, grid, st);
+        return;
+      }
+      break;
     case EPI_ROWSUM:
       if constexpr (A_KM && B_KN) {
         launch_epi<true, true, EPI_ROWSUM>(t, a, grid, st);
@@ -521,7 +602,9 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   const int N = b_kn ? b.size(1) : b.size(0);
   const int Kb = b_kn ? b.size(0) : b.size(1);
   TORCH_CHECK(K == Kb, "nbd::gemm: K mismatch ", K, " vs ", Kb);
-  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "nbd::gemm: output shape");
+  // EPI_SWIGLU writes silu(g)·u: [M][N/2]; EPI_DSWIGLU writes d[g|u]: [M][2N]
+  const int64_t cN = epi == EPI_SWIGLU ? N / 2 : epi == EPI_DSWIGLU ? 2 * (int64_t)N : N;
+  TORCH_CHECK(c.size(0) == M && c.size(1) == cN, "nbd::gemm: output shape");
   TORCH_CHECK(K % BK == 0 && K > 0, "nbd::gemm: K % 64 != 0");
   TORCH_CHECK(!(a_km && !b_kn), "nbd::gemm: layout (A [K][M], B [N][K]) not built");
   for (const at::Tensor* x : {&a, &b, &c})
@@ -540,7 +623,19 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
     TORCH_CHECK(aux_out && aux_out->numel() == M && aux_out->is_contiguous() &&
                     aux_out->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(aux_out->data_ptr()) % 16 == 0,
                 "nbd::gemm: aux_out (row sums)");
-  TORCH_CHECK(epi >= EPI_NONE && epi <= EPI_ROWSUM, "nbd::gemm: epilogue ", epi);
+  if (epi == EPI_SWIGLU) {
+    TORCH_CHECK(!a_km && !b_kn && !bias, "nbd::gemm: SwiGLU epilogue: forward layout, no bias");
+    TORCH_CHECK(aux_out && aux_out->size(0) == M && aux_out->size(1) == N && aux_out->is_contiguous() &&
+                    aux_out->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(aux_out->data_ptr()) % 16 == 0,
+                "nbd::gemm: aux_out ([g|u] pre-activations)");
+  }
+  if (epi == EPI_DSWIGLU) {
+    TORCH_CHECK(!a_km && b_kn && !bias, "nbd::gemm: SwiGLU backward epilogue: dgrad layout, no bias");
+    TORCH_CHECK(aux_in && aux_in->size(0) == M && aux_in->size(1) == 2 * (int64_t)N && aux_in->is_contiguous() &&
+                    aux_in->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(aux_in->data_ptr()) % 16 == 0,
+                "nbd::gemm: aux_in ([g|u] pre-activations)");
+  }
+  TORCH_CHECK(epi >= EPI_NONE && epi <= EPI_DSWIGLU, "nbd::gemm: epilogue ", epi);
   const Tile t = pick_tile(M, N, tile_hint);
   const int tiles = (M / t.bm) * (N / t.bn);
   const int S = splits > 0 ? (int)splits : 1;
@@ -561,7 +656,7 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   p.K = K / S;
   p.lda = a.size(1);
   p.ldb = b.size(1);
-  p.ldc = N;
+  p.ldc = cN;
   p.tiles_m = M / t.bm;
   p.tiles_n = N / t.bn;
   const dim3 grid(tiles, S);

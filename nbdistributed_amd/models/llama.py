@@ -8,7 +8,7 @@ small-batch step is launch-bound (≈4,600 kernels, GPU busy 25 ms of a 40 ms st
 
     x ─ rms_norm ─ qkv GEMM (fused q|k|v) ─ flash attention (GQA, RoPE fused into its loads) ─ o GEMM ─┐
     └──────────────────────────── add_rms_norm (residual + norm in one pass) ◄───────────────┘
-      ─ gate|up GEMM (fused) ─ swiglu ─ down GEMM ─ add_rms_norm (into the next block's norm)
+      ─ gate|up GEMM (fused, SwiGLU in its epilogue) ─ down GEMM ─ add_rms_norm (into the next block's norm)
 
 i.e. ~12 kernels per block instead of ~70, nothing that synchronises with the host, and only
 caching-allocator memory — so the whole training step captures into a HIP graph
@@ -105,7 +105,8 @@ class LlamaMLP(nn.Module):
         self.down_proj = nn.Linear(c.intermediate_size, c.hidden_size, bias=False)
 
     def forward(self, x):
-        return ops.gemm_linear(ops.swiglu(ops.gemm_linear(x, self.gate_up_proj.weight)), self.down_proj.weight)
+        # SwiGLU (and its backward) run in the gate|up GEMM's (the down dgrad's) epilogue
+        return ops.mlp_swiglu(x, self.gate_up_proj.weight, self.down_proj.weight)
 
 
 class LlamaDecoderLayer(nn.Module):

@@ -20,7 +20,8 @@ embedding (K10)        counting-sort embedding backward (graph-safe)     embed.h
 rms_norm / rope_ /     RMSNorm (+ residual), rotary in place on packed   norm.hip, act.hip
 swiglu (K11)           QKV, fused SwiGLU fwd/bwd (Llama family)
 gemm_linear /          bf16 GEMM on MFMA 16x16x32: x·Wᵀ, dy·W, dyᵀ·x     gemm.hip (glds + LDS
-mlp_gelu (K12)         + bias / GELU / GELU' epilogues, split-K          swizzles, tr-reads)
+mlp_gelu /             + bias / GELU / GELU' / SwiGLU / SwiGLU'          swizzles, tr-reads)
+mlp_swiglu (K12)       epilogues, split-K, K-groups
 =====================  ==============================================  =========================
 
 GPU tensors always go to the HIP kernels; if ``libnbd_ops.so`` cannot be loaded on a GPU box the
@@ -35,7 +36,7 @@ from .attention import attention_qkv, flash_attention, flash_supported
 from .bucket import (_ref_flatten, _ref_prereduce, _ref_unflatten, bucket_flatten, bucket_unflatten, local_prereduce,
                      plan_offsets)
 from .embedding import embedding
-from .gemm import gemm_linear, mlp_gelu
+from .gemm import gemm_linear, mlp_gelu, mlp_swiglu
 from .llama import rope_, rope_tables, swiglu
 from .loss import cross_entropy
 from .norm import add_layer_norm, add_rms_norm, colsum, layer_norm, linear, rms_norm
@@ -51,6 +52,6 @@ def __getattr__(name):
 
 __all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "cross_entropy",
            "flash_attention", "attention_qkv", "flash_supported", "layer_norm", "add_layer_norm", "linear",
-           "colsum", "embedding", "gemm_linear", "mlp_gelu", "rms_norm", "add_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary",
+           "colsum", "embedding", "gemm_linear", "mlp_gelu", "mlp_swiglu", "rms_norm", "add_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary",
            "tensor_summary_text", "tensor_summary_raw", "plan_offsets", "native_available", "load_library",
            "SUMMARY_FIELDS"]

@@ -18,9 +18,10 @@ from ._lib import _require
 
 # NBD_HIP_GEMM=0 routes gemm_linear / mlp_gelu to PyTorch (hipBLASLt) — for A/B measurements
 ENABLED = os.environ.get("NBD_HIP_GEMM", "1") != "0"
-KSPLIT = os.environ.get("NBD_GEMM_KSPLIT", "1") != "0"  # 0: tuned K-split kernels run as one K-group (A/B)
+KSPLIT = os.environ.get("NBD_GEMM_KSPLIT", "1") != "0"
+FUSED_SWIGLU = os.environ.get("NBD_FUSED_SWIGLU", "1") != "0"  # 0: separate swiglu kernels (A/B)  # 0: tuned K-split kernels run as one K-group (A/B)
 
-EPI_NONE, EPI_GELU, EPI_DGELU, EPI_ROWSUM = 0, 1, 2, 3
+EPI_NONE, EPI_GELU, EPI_DGELU, EPI_ROWSUM, EPI_SWIGLU, EPI_DSWIGLU = 0, 1, 2, 3, 4, 5
 
 
 def gemm_ok(M: int, N: int, K: int) -> bool:
@@ -100,7 +101,10 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
     """C[M,N] = A·B.  ``a`` is [M,K] (or [K,M] with ``a_km``), ``b`` is [N,K] (or [K,N] with
     ``b_kn``).  ``epi``: EPI_NONE (+bias), EPI_GELU (+bias, returns (gelu(pre), pre)),
     EPI_DGELU (C · gelu'(aux)), EPI_ROWSUM (weight-gradient layout; returns (C, Σ_k A[m,k]) —
-    the bias gradient of the Linear whose weight gradient C is).  ``splits=0`` picks split-K automatically (no-epilogue only);
+    the bias gradient of the Linear whose weight gradient C is), EPI_SWIGLU (``b`` = [gate; up]
+    weights [2I, K]; returns (silu(g)·u [M, I], [g|u] [M, 2I])), EPI_DSWIGLU (dgrad layout,
+    ``aux`` = [g|u] [M, 2N]; returns d[g|u] [M, 2N] from dact = A·B).  ``splits=0`` picks split-K
+    automatically (no-epilogue only);
     ``tile`` = ks*10^8 + waves*10^7 + stages*10^6 + BM*1000 + BN forces a kernel (waves 4 or 8,
     8 only at 128x128; stages 2 or 3; ks = 2 runs two K-groups of 4 waves inside the workgroup,
     tiles other than 128x128, K a multiple of 128; benchmarks)."""
@@ -115,16 +119,21 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
         _require()
         a = a if a.is_contiguous() else a.contiguous()
         b = b if b.is_contiguous() else b.contiguous()
-        c = out if out is not None else torch.empty(M, N, device=a.device, dtype=a.dtype)
+        cN = N // 2 if epi == EPI_SWIGLU else 2 * N if epi == EPI_DSWIGLU else N
+        c = out if out is not None else torch.empty(M, cN, device=a.device, dtype=a.dtype)
         pre = torch.empty_like(c) if epi == EPI_GELU else None
         if epi == EPI_ROWSUM:
             pre = torch.empty(M, device=a.device, dtype=a.dtype)
+        if epi == EPI_SWIGLU:
+            pre = torch.empty(M, N, device=a.device, dtype=a.dtype)
+        if epi == EPI_DSWIGLU and not aux.is_contiguous():
+            aux = aux.contiguous()
         if splits == 0 or tile == 0:
             t, s = config(a_km, b_kn, M, N, K, can_split=(epi in (EPI_NONE, EPI_ROWSUM) and bias is None))
             tile = tile or t
             splits = splits or s
         torch.ops.nbd.gemm(a, b, c, a_km, b_kn, bias, epi, aux, pre, splits, tile)
-        return (c, pre) if epi in (EPI_GELU, EPI_ROWSUM) else c
+        return (c, pre) if epi in (EPI_GELU, EPI_ROWSUM, EPI_SWIGLU) else c
     # reference path (CPU / uncovered shapes): same math through PyTorch
     A = a.t() if a_km else a
     B = b if b_kn else b.t()
@@ -137,6 +146,11 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
         return c, pre
     if epi == EPI_DGELU:
         c = _dgelu_ref(c, aux)
+    if epi == EPI_SWIGLU:
+        g, u = c.float().chunk(2, dim=1)
+        return (torch.nn.functional.silu(g) * u).to(c.dtype), c
+    if epi == EPI_DSWIGLU:
+        c = _dswiglu_ref(c, aux)
     if epi == EPI_ROWSUM:
         return c, A.float().sum(1).to(a.dtype)
     if out is not None:
@@ -153,6 +167,15 @@ def _dgelu_ref(g, pre):
     t = torch.tanh(k * (x + 0.044715 * x * x * x))
     d = 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k * (1 + 3 * 0.044715 * x * x)
     return (g.float() * d).to(g.dtype)
+
+
+def _dswiglu_ref(dact, pre):
+    import torch
+
+    g, u = pre.float().chunk(2, dim=-1)
+    d = dact.float()
+    sg = torch.sigmoid(g)
+    return torch.cat([d * u * sg * (1 + g * (1 - sg)), d * g * sg], dim=-1).to(dact.dtype)
 
 
 _Fns = None
@@ -228,7 +251,30 @@ def _fns():
                 dw1 = matmul(dpre, x2, a_km=True, b_kn=True)
             return dx, dw1, db1, dw2, db2
 
-    _Fns = (_Linear, _MLPGelu)
+    class _MLPSwiGLU(torch.autograd.Function):
+        """y = down(silu(g)·u), [g|u] = x·W_guᵀ (Llama MLP) with SwiGLU / its backward in the GEMM
+        epilogues: two GEMMs forward, four backward, no elementwise kernels."""
+
+        @staticmethod
+        def forward(ctx, x, w_gu, w_down):
+            x2 = _c(x).view(-1, x.shape[-1])
+            act, pre = matmul(x2, w_gu, epi=EPI_SWIGLU)
+            y = matmul(act, w_down)
+            ctx.save_for_backward(x2, w_gu, w_down, pre, act)
+            ctx.xshape = x.shape
+            return y.view(*x.shape[:-1], w_down.shape[0])
+
+        @staticmethod
+        def backward(ctx, dy):
+            x2, w_gu, w_down, pre, act = ctx.saved_tensors
+            dy2 = _c(dy).view(-1, dy.shape[-1])
+            dgu = matmul(dy2, w_down, b_kn=True, epi=EPI_DSWIGLU, aux=pre)
+            dw_down = matmul(dy2, act, a_km=True, b_kn=True)
+            dx = matmul(dgu, w_gu, b_kn=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+            dw_gu = matmul(dgu, x2, a_km=True, b_kn=True)
+            return dx, dw_gu, dw_down
+
+    _Fns = (_Linear, _MLPGelu, _MLPSwiGLU)
     return _Fns
 
 
@@ -258,3 +304,21 @@ def mlp_gelu(x, w1, b1, w2, b2):
     import torch.nn.functional as F
 
     return F.linear(F.gelu(F.linear(x, w1, b1), approximate="tanh"), w2, b2)
+
+
+def mlp_swiglu(x, w_gu, w_down):
+    """Llama MLP ``down(silu(g)·u)`` with ``[g|u] = F.linear(x, w_gu)`` (``w_gu`` = [gate; up],
+    [2I, H]) — SwiGLU and its backward fused into the GEMM epilogues on the GPU path."""
+    if FUSED_SWIGLU and _fast(x, w_gu, w_down):
+        return _fns()[2].apply(x, w_gu, w_down)
+    if not FUSED_SWIGLU:
+        return gemm_linear(_swiglu(gemm_linear(x, w_gu)), w_down)
+    import torch.nn.functional as F
+
+    return F.linear(_swiglu(F.linear(x, w_gu)), w_down)
+
+
+def _swiglu(gu):
+    from .llama import swiglu
+
+    return swiglu(gu)

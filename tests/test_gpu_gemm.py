@@ -139,6 +139,53 @@ def test_mlp_gelu_autograd_matches_fp32():
         assert _err(t.grad, r.grad) < 2e-2
 
 
+@pytest.mark.parametrize("tile", [64064, 3064128, 128128, 82128128, 203064064, 202128064])
+def test_swiglu_epilogue(tile):
+    # [g|u] = x·[W_gate; W_up]ᵀ: the workgroup of column block tn takes gate AND up rows
+    M, I, K = 256, 384, 256
+    x, w = _operands(M, 2 * I, K, False, False, seed=21)
+    act, pre = G.matmul(x, w, epi=G.EPI_SWIGLU, tile=tile, splits=1)
+    ref = _ref(x, w, False, False)
+    assert act.shape == (M, I) and pre.shape == (M, 2 * I)
+    assert _err(pre, ref) < 1e-2
+    g, u = ref[:, :I], ref[:, I:]
+    assert _err(act, torch.nn.functional.silu(g) * u) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [64064, 2064064, 128128, 82128128, 202064064])
+def test_dswiglu_epilogue(tile):
+    # d[g|u] from dact = dy·W_down, written straight into the [M, 2I] gradient of the projection
+    M, H, I = 256, 256, 384
+    dy, wd = _operands(M, I, H, False, True, seed=22)  # dy [M, H], W_down [H, I]
+    pre = torch.randn(M, 2 * I, device="cuda").to(torch.bfloat16)
+    dgu = G.matmul(dy, wd, b_kn=True, epi=G.EPI_DSWIGLU, aux=pre, tile=tile, splits=1)
+    assert dgu.shape == (M, 2 * I)
+    dact = _ref(dy, wd, False, True)
+    g, u = pre.float()[:, :I], pre.float()[:, I:]
+    s = torch.sigmoid(g)
+    ref = torch.cat([dact * u * s * (1 + g * (1 - s)), dact * g * s], dim=1)
+    assert _err(dgu, ref) < 1e-2
+
+
+def test_mlp_swiglu_autograd_matches_fp32():
+    torch.manual_seed(2)
+    H, I = 576, 1536  # SmolLM2-135M
+    x = torch.randn(2, 128, H, device="cuda").to(torch.bfloat16).requires_grad_()
+    wgu = (torch.randn(2 * I, H, device="cuda") * 0.04).to(torch.bfloat16).requires_grad_()
+    wd = (torch.randn(H, I, device="cuda") * 0.03).to(torch.bfloat16).requires_grad_()
+    y = G.mlp_swiglu(x, wgu, wd)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    ref = [t.detach().float().requires_grad_() for t in (x, wgu, wd)]
+    F = torch.nn.functional
+    g, u = F.linear(ref[0], ref[1]).chunk(2, dim=-1)
+    yr = F.linear(F.silu(g) * u, ref[2])
+    yr.backward(dy.float())
+    assert _err(y, yr) < 2e-2
+    for t, r in zip((x, wgu, wd), ref):
+        assert _err(t.grad, r.grad) < 2e-2
+
+
 def test_gemm_rejects_bad_shapes_loudly():
     a = torch.randn(100, 64, device="cuda").to(torch.bfloat16)
     b = torch.randn(64, 64, device="cuda").to(torch.bfloat16)
