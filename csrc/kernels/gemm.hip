@@ -290,33 +290,47 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
       __syncthreads();
     }
   } else {
-    // buffer t % 3 holds tile t.  Before the barrier that ends step t, tile t+1 must have landed
-    // (every wave: vmcnt leaves only tile t+2's NPT loads in flight); tile t+2 is written into
-    // the buffer tile t-1 occupied, which every wave finished reading before step t-1's barrier.
-    stage_tile(0, smem);
-    if (nk > 1) {
-      stage_tile(1, smem + BUF);
-      wait_barrier<NPT>();
-    } else {
-      wait_barrier<0>();
-    }
-    // unrolled by 3 so every buffer offset is a compile-time constant: the compiler can then
-    // prove the in-flight DMA (buffer t+2) and this step's ds_reads (buffer t) disjoint and does
-    // not drain vmcnt(0) before the reads (it did with a rotating runtime index)
-    auto step = [&](int t, auto cur_c) {
-      constexpr int CUR = decltype(cur_c)::value, NXT2 = (CUR + 2) % 3;
-      if (t + 2 < nk) stage_tile(t + 2, smem + NXT2 * BUF);
-      compute(smem + CUR * BUF);
-      if (t + 2 < nk)
-        wait_barrier<NPT>();
-      else
-        wait_barrier<0>();
+    // S-stage ring (S = STAGES >= 3): buffer t % S holds tile t; tiles t+1 .. t+S-2 are in flight
+    // while tile t is computed, and tile t+S-1 is issued into the buffer tile t-1 occupied (every
+    // wave finished reading it before step t-1's barrier).  The barrier that ends step t waits
+    // for tile t+1 only (counted vmcnt: the younger tiles' NPT loads each stay in flight).  Deep
+    // rings are for latency-bound products: with K ≤ (S-1)·64 every K-tile is requested at once.
+    constexpr int S = STAGES;
+    // wait until at most n younger tiles are outstanding (n ≤ S-2, runtime only at the tail)
+    static_assert(S <= 9 && (S - 2) * NPT <= 63, "vmcnt range");
+    auto wait_tiles = [&](int n) {
+      switch (n) {
+        case 0: wait_barrier<0>(); break;
+        case 1: wait_barrier<NPT>(); break;
+        case 2: wait_barrier<2 * NPT>(); break;
+        case 3: wait_barrier<3 * NPT>(); break;
+        case 4: wait_barrier<4 * NPT>(); break;
+        case 5: wait_barrier<5 * NPT>(); break;
+        case 6: wait_barrier<6 * NPT>(); break;
+        default: wait_barrier<(S - 2) * NPT>(); break;
+      }
     };
-    for (int t = 0; t < nk; t += 3) {
-      step(t, std::integral_constant<int, 0>{});
-      if (t + 1 < nk) step(t + 1, std::integral_constant<int, 1>{});
-      if (t + 2 < nk) step(t + 2, std::integral_constant<int, 2>{});
+    const int pro = nk < S - 1 ? nk : S - 1;
+    for (int t = 0; t < pro; ++t) stage_tile(t, smem + t * BUF);
+    wait_tiles(pro - 1);
+    // unrolled by S so every buffer offset is a compile-time constant: the compiler can then
+    // prove the in-flight DMA and this step's ds_reads disjoint and does not drain vmcnt(0)
+    // before the reads (it did with a rotating runtime index)
+    auto step = [&](int t, auto cur_c) {
+      constexpr int CUR = decltype(cur_c)::value, PREV = (CUR + S - 1) % S;
+      const bool issue = t + S - 1 < nk;
+      if (issue) stage_tile(t + S - 1, smem + PREV * BUF);
+      compute(smem + CUR * BUF);
+      // tiles t+2 .. min(t+S-1, nk-1) may stay outstanding
+      const int last = issue ? t + S - 1 : nk - 1;
+      wait_tiles(last - (t + 1) > 0 ? last - (t + 1) : 0);
+    };
+#define NBD_STEP(J) \
+  if constexpr (J < S) { if (t + J < nk) step(t + J, std::integral_constant<int, J>{}); }
+    for (int t = 0; t < nk; t += S) {
+      NBD_STEP(0) NBD_STEP(1) NBD_STEP(2) NBD_STEP(3) NBD_STEP(4) NBD_STEP(5) NBD_STEP(6) NBD_STEP(7) NBD_STEP(8)
     }
+#undef NBD_STEP
   }
 
   // ---- epilogue ------------------------------------------------------------------------------
@@ -506,16 +520,22 @@ static void launch_epi(const Tile& t, const Args& a, dim3 grid, hipStream_t st) 
 #define NBD_GEMM_CASE(BM_, BN_, KS_)                                   \
   if (t.bm == BM_ && t.bn == BN_ && t.waves == 4 && t.ks == KS_) {     \
     if (t.stages == 3) NBD_GEMM_K(BM_, BN_, 3, 4, KS_);                \
-    else NBD_GEMM_K(BM_, BN_, 2, 4, KS_);                              \
+    else if (t.stages == 2) NBD_GEMM_K(BM_, BN_, 2, 4, KS_);           \
+    else break;                                                        \
     return;                                                            \
   }
-  NBD_GEMM_CASE(128, 128, 1)
-  NBD_GEMM_CASE(128, 64, 1)
-  NBD_GEMM_CASE(64, 128, 1)
-  NBD_GEMM_CASE(64, 64, 1)
-  NBD_GEMM_CASE(128, 64, 2)  // intra-workgroup K-split: small, latency-bound products
-  NBD_GEMM_CASE(64, 128, 2)
-  NBD_GEMM_CASE(64, 64, 2)
+  // (deeper rings — 4, 6 and 8 stages, most K-tiles of a small product in flight at once —
+  // measured slower on every workload shape: one workgroup per CU then leaves the tail round
+  // serial; profiles/gemm_bench_r1.txt history)
+  do {
+    NBD_GEMM_CASE(128, 128, 1)
+    NBD_GEMM_CASE(128, 64, 1)
+    NBD_GEMM_CASE(64, 128, 1)
+    NBD_GEMM_CASE(64, 64, 1)
+    NBD_GEMM_CASE(128, 64, 2)  // intra-workgroup K-split: small, latency-bound products
+    NBD_GEMM_CASE(64, 128, 2)
+    NBD_GEMM_CASE(64, 64, 2)
+  } while (0);
   if (t.bm == 128 && t.bn == 128 && t.waves == 8 && t.ks == 1) {  // 8 waves: 128x128 only
     if (t.stages == 3) NBD_GEMM_K(128, 128, 3, 8, 1);
     else NBD_GEMM_K(128, 128, 2, 8, 1);
@@ -523,7 +543,8 @@ static void launch_epi(const Tile& t, const Args& a, dim3 grid, hipStream_t st) 
   }
 #undef NBD_GEMM_CASE
 #undef NBD_GEMM_K
-  TORCH_CHECK(false, "nbd::gemm: no kernel for tile ", t.bm, "x", t.bn, " with ", t.waves, " waves, K-split ", t.ks);
+  TORCH_CHECK(false, "nbd::gemm: no kernel for tile ", t.bm, "x", t.bn, " with ", t.waves, " waves, ", t.stages,
+              " stages, K-split ", t.ks);
 }
 
 template <bool A_KM, bool B_KN>
@@ -574,7 +595,7 @@ static Tile pick_tile(int M, int N, int64_t tile_hint) {
     // hint = ks*10^8 + waves*10^7 + stages*10^6 + BM*1000 + BN (ks 0 -> 1, waves 0 -> 4, stages 0 -> 2)
     const int stg = (int)(tile_hint / 1000000 % 10), wv = (int)(tile_hint / 10000000 % 10);
     const int ks = (int)(tile_hint / 100000000);
-    Tile t{(int)(tile_hint / 1000 % 1000), (int)(tile_hint % 1000), stg == 3 ? 3 : 2, wv == 8 ? 8 : 4, ks == 2 ? 2 : 1};
+    Tile t{(int)(tile_hint / 1000 % 1000), (int)(tile_hint % 1000), stg < 2 ? 2 : stg, wv == 8 ? 8 : 4, ks == 2 ? 2 : 1};
     TORCH_CHECK(tile_fits(t, M, N), "nbd::gemm: tile ", t.bm, "x", t.bn, " does not divide ", M, "x", N);
     return t;
   }

@@ -48,6 +48,18 @@ def test_gemm_layouts_and_tiles(layout, tile, shape):
     assert _err(c, _ref(a, b, a_km, b_kn)) < 1e-2
 
 
+@pytest.mark.parametrize("layout", LAYOUTS, ids=["fwd", "dgrad", "wgrad"])
+@pytest.mark.parametrize("tile,K", [(3064064, 1216), (3128128, 704), (203064064, 1280), (203128064, 1408),
+                                    (83128128, 1216)])
+def test_gemm_deep_ring_wraps(layout, tile, K):
+    # K-tile counts that wrap the S-stage ring several times and end mid-ring
+    M, N = 256, 384
+    a_km, b_kn = layout
+    a, b = _operands(M, N, K, a_km, b_kn, seed=5)
+    c = G.matmul(a, b, a_km=a_km, b_kn=b_kn, tile=tile, splits=1)
+    assert _err(c, _ref(a, b, a_km, b_kn)) < 1e-2
+
+
 def test_gemm_identity_with_asymmetric_b():
     # A = I catches a row/column swap in the C write (cdna_hip_programming.md §3)
     M = N = K = 128
@@ -152,7 +164,7 @@ def test_swiglu_epilogue(tile):
     assert _err(act, torch.nn.functional.silu(g) * u) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [64064, 2064064, 128128, 82128128, 202064064])
+@pytest.mark.parametrize("tile", [64064, 2064064, 128128, 82128128, 202064064, 203064128])
 def test_dswiglu_epilogue(tile):
     # d[g|u] from dact = dy·W_down, written straight into the [M, 2I] gradient of the projection
     M, H, I = 256, 256, 384
