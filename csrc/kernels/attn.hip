@@ -36,6 +36,7 @@
 
 #include <cmath>
 #include <tuple>
+#include <type_traits>
 
 #include "nbd_common.h"
 
@@ -234,35 +235,42 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
       sv.load(v.row(b, kh, (t + 1) * TILE), v.st, tid);
     }
     const int k0 = t * TILE;
-    if (!CAUSAL || k0 <= q0 + 31) {
+    // one tile; DIAG = the causal mask cuts through it (only those tiles pay for the compares)
+    auto tile_body = [&](auto diag_c) {
+      constexpr bool DIAG = decltype(diag_c)::value;
       f16x sacc[2] = {zero16(), zero16()};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int s = 0; s < 4; ++s) sacc[kb] = mfma(ld16(Ks + (kb * 32 + r) * RS + 16 * s + 8 * h), qf[s], sacc[kb]);
-      const bool diag = CAUSAL && (k0 + TILE - 1 > q0);
+      // running max on the raw scores (sc2 > 0), scaled once; p = exp2(s·sc2 − m) as one FMA + exp
       float mt = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float x = sacc[kb][i] * sc2;
-          if (diag && k0 + kb * 32 + crow(i, h) > qi) x = -INFINITY;
-          sacc[kb][i] = x;
-          mt = fmaxf(mt, x);
+          if constexpr (DIAG) {
+            if (k0 + kb * 32 + crow(i, h) > qi) sacc[kb][i] = -INFINITY;
+          }
+          mt = fmaxf(mt, sacc[kb][i]);
         }
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mn = fmaxf(m, mt);
+      const float mn = fmaxf(m, mt * sc2);
       const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      float rs = 0.f;
+      const float nmn = -mn;
+      float rs0 = 0.f, rs1 = 0.f;  // two chains; scalar adds (no v_pk_add_f32: -fno-slp-vectorize)
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(sacc[kb][i] - mn);
-          sacc[kb][i] = p;
-          rs += p;
+        for (int i = 0; i < 16; i += 2) {
+          const float p0 = __builtin_amdgcn_exp2f(fmaf(sacc[kb][i], sc2, nmn));
+          const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[kb][i + 1], sc2, nmn));
+          sacc[kb][i] = p0;
+          sacc[kb][i + 1] = p1;
+          rs0 += p0;
+          rs1 += p1;
         }
+      float rs = rs0 + rs1;
       rs += __shfl_xor(rs, 32, 64);
       l = l * alpha + rs;
       m = mn;
@@ -283,6 +291,12 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
             acc_o[db] = mfma(cat(tr4(base), tr4(base + 8 * RSV)), pb, acc_o[db]);
           }
         }
+    };
+    if (!CAUSAL || k0 <= q0 + 31) {
+      if (CAUSAL && k0 + TILE - 1 > q0)
+        tile_body(std::true_type{});
+      else
+        tile_body(std::false_type{});
     }
     __syncthreads();
     if (t + 1 < ntiles) {
@@ -404,7 +418,7 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int qrow = qb * 32 + crow(i, h);
-            float p = __builtin_amdgcn_exp2f(sacc[i] * sc2 - Ls[qrow]);
+            float p = __builtin_amdgcn_exp2f(fmaf(sacc[i], sc2, -Ls[qrow]));
             if (diag && ki > qt0 + qrow) p = 0.f;
             sacc[i] = p;                      // P
             dp[i] = p * (dp[i] - Ds[qrow]);   // dS
@@ -492,6 +506,8 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
     }
     const int k0 = t * TILE;
     if (!CAUSAL || k0 <= q0 + 31) {
+      // (a diagonal-only masked copy of this body, as in the forward, pushes the combined
+      // backward kernel past 256 VGPRs into scratch; the per-element mask stays here)
       const bool diag = CAUSAL && (k0 + TILE - 1 > q0);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -503,7 +519,7 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float p = __builtin_amdgcn_exp2f(sacc[i] * sc2 - l2);
+          float p = __builtin_amdgcn_exp2f(fmaf(sacc[i], sc2, -l2));
           if (diag && k0 + kb * 32 + crow(i, h) > qi) p = 0.f;
           dp[i] = p * (dp[i] - dl);  // dS^T[key][q]
         }

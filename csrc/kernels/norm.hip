@@ -152,10 +152,12 @@ constexpr int kBwdRows = 16;  // max rows per workgroup (4 per wave, two at a ti
 constexpr int kRpi = 2;       // rows per wave iteration
 
 // rows per workgroup: 16 for large inputs (GPT-2: 8192 rows -> 512 workgroups), fewer when that
-// would leave the chip under-filled (SmolLM2 at 16 x 128 tokens: 2048 rows -> 4 per workgroup)
+// would leave the chip under-filled, but at least 8 so all four waves hold rows (SmolLM2 at
+// 16 x 128 tokens: 2048 rows -> 8 per workgroup; with 4, two of the four waves idled and the
+// weight-gradient partial rows doubled)
 static int bwd_rows_per_block(int64_t rows) {
   int r = kBwdRows;
-  while (r > 2 && (rows + r - 1) / r < 512) r /= 2;
+  while (r > 8 && (rows + r - 1) / r < 512) r /= 2;
   return r;
 }
 
