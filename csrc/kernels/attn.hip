@@ -340,8 +340,27 @@ __global__ __launch_bounds__(NT) void bwd_pre_kernel(View dout, View out, float*
 // the `group` query heads of a key/value head are split over gsplit workgroups, each writing a
 // partial dK/dV (split index s at dk/dv + s·split_stride) that gqa_reduce_kernel sums — 3x the
 // workgroups for SmolLM2 (9 query / 3 kv heads) instead of one workgroup sweeping all 3 heads.
-template <bool CAUSAL>
-__device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, View v, View dout,
+// δ of a 64-row tile from register-staged dO and O chunks (Stage2 mapping: chunk c = tid + i·NT
+// is row c/8, dims 8(c%8)..+8): 8-element partial dot, summed over the row's 8 consecutive lanes
+__device__ __forceinline__ void tile_delta(const Stage2& dO, const Stage2& O, float* Ds, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    float acc = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      acc = fmaf(bf16_to_f32((uint16_t)dO.a[i][e]), bf16_to_f32((uint16_t)O.a[i][e]), acc);
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if ((tid & 7) == 0) Ds[(tid + i * NT) >> 3] = acc;
+  }
+}
+
+// FD (fused δ, short sequences): δ = Σ_d dO·O is computed from the staged dO tile and an O tile
+// loaded beside it, instead of by bwd_pre_kernel — one launch less where each (query head, tile)
+// is swept by one key block anyway (T ≤ 256).
+template <bool CAUSAL, bool FD>
+__device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, View v, View dout, View out,
                                           const float* __restrict__ lse, const float* __restrict__ delta, MView dk,
                                           MView dv, int H, int T, int nblk, float sc2, float scale, int group,
                                           Rope rp, int gsplit, int64_t split_stride) {
@@ -373,15 +392,16 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
   for (int g = split * gpw; g < (split + 1) * gpw; ++g) {
     const int hq = kvh * group + g;
     const float* lse_bh = lse + ((int64_t)b * Hq + hq) * T;
-    const float* del_bh = delta + ((int64_t)b * Hq + hq) * T;
+    const float* del_bh = FD ? nullptr : delta + ((int64_t)b * Hq + hq) * T;
     StagePair sq;
-    Stage2 so;
+    Stage2 so, sov;  // dO tile; O tile (FD only)
     float lv = 0.f, dlv = 0.f;
     sq.load(q.row(b, hq, t0 * TILE), q.st, tid);
     so.load(dout.row(b, hq, t0 * TILE), dout.st, tid);
+    if constexpr (FD) sov.load(out.row(b, hq, t0 * TILE), out.st, tid);
     if (tid < TILE) {
       lv = lse_bh[t0 * TILE + tid] * kLog2e;
-      dlv = del_bh[t0 * TILE + tid];
+      if constexpr (!FD) dlv = del_bh[t0 * TILE + tid];
     }
     if (g > split * gpw) __syncthreads();  // the previous head's last tile is still being read
     sq.rope(rp, t0 * TILE, tid);
@@ -389,16 +409,18 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
     so.store(Os, RS, tid);
     if (tid < TILE) {
       Ls[tid] = lv;
-      Ds[tid] = dlv;
+      if constexpr (!FD) Ds[tid] = dlv;
     }
+    if constexpr (FD) tile_delta(so, sov, Ds, tid);
     __syncthreads();
     for (int t = t0; t < nt; ++t) {
       if (t + 1 < nt) {
         sq.load(q.row(b, hq, (t + 1) * TILE), q.st, tid);
         so.load(dout.row(b, hq, (t + 1) * TILE), dout.st, tid);
+        if constexpr (FD) sov.load(out.row(b, hq, (t + 1) * TILE), out.st, tid);
         if (tid < TILE) {
           lv = lse_bh[(t + 1) * TILE + tid] * kLog2e;
-          dlv = del_bh[(t + 1) * TILE + tid];
+          if constexpr (!FD) dlv = del_bh[(t + 1) * TILE + tid];
         }
       }
       const int qt0 = t * TILE;
@@ -447,8 +469,9 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
         so.store(Os, RS, tid);
         if (tid < TILE) {
           Ls[tid] = lv;
-          Ds[tid] = dlv;
+          if constexpr (!FD) Ds[tid] = dlv;
         }
+        if constexpr (FD) tile_delta(so, sov, Ds, tid);
         __syncthreads();
       }
     }
@@ -466,8 +489,8 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
 }
 
 // ============================================================================ backward: dQ
-template <bool CAUSAL>
-__device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, View v, View dout,
+template <bool CAUSAL, bool FD>
+__device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, View v, View dout, View out,
                                         const float* __restrict__ lse, const float* __restrict__ delta, MView dq,
                                         int H, int T, int nblk, float sc2, float scale, int group, Rope rp) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[TILE * RS];
@@ -488,7 +511,19 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
   }
   if (rp.cos != nullptr) rope_frag(qf, rp, qi, h);
   const float l2 = lse[(int64_t)bh * T + qi] * kLog2e;
-  const float dl = delta[(int64_t)bh * T + qi];
+  float dl;
+  if constexpr (FD) {  // δ of this lane's query row: its 32 dims of dO·O + the partner lane's 32
+    float acc = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const s8v ov = ld16(out.row(b, hh, qi) + 16 * s + 8 * h);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc = fmaf(bf16_to_f32((uint16_t)of[s][e]), bf16_to_f32((uint16_t)ov[e]), acc);
+    }
+    dl = acc + __shfl_xor(acc, 32, 64);
+  } else {
+    dl = delta[(int64_t)bh * T + qi];
+  }
   f16x dqt[2] = {zero16(), zero16()};
   const int ntiles = CAUSAL ? (qb * BLK + BLK) / TILE : T / TILE;
   StagePair sk;
@@ -555,16 +590,17 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
 
 // One launch for both backward passes: blocks [0, nkv) compute dK/dV, the rest dQ — the two
 // are independent, and for short sequences (SmolLM2: T = 128) neither fills the chip alone.
-template <bool CAUSAL>
-__global__ __launch_bounds__(NT, 2) void bwd_kernel(View q, View k, View v, View dout, const float* __restrict__ lse,
+template <bool CAUSAL, bool FD>
+__global__ __launch_bounds__(NT, 2) void bwd_kernel(View q, View k, View v, View dout, View out,
+                                                     const float* __restrict__ lse,
                                                      const float* __restrict__ delta, MView dq, MView dk, MView dv,
                                                      int Hq, int Hkv, int T, int nblk, float sc2, float scale,
                                                      int group, Rope rp, int nkv, int gsplit, int64_t split_stride) {
   if ((int)blockIdx.x < nkv)
-    dkdv_body<CAUSAL>(blockIdx.x, nkv, q, k, v, dout, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale, group, rp,
+    dkdv_body<CAUSAL, FD>(blockIdx.x, nkv, q, k, v, dout, out, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale, group, rp,
                       gsplit, split_stride);
   else
-    dq_body<CAUSAL>(blockIdx.x - nkv, gridDim.x - nkv, q, k, v, dout, lse, delta, dq, Hq, T, nblk, sc2, scale,
+    dq_body<CAUSAL, FD>(blockIdx.x - nkv, gridDim.x - nkv, q, k, v, dout, out, lse, delta, dq, Hq, T, nblk, sc2, scale,
                     group, rp);
 }
 
@@ -668,12 +704,18 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
   MView dqv = mview_of(dq, "dq"), dkv = mview_of(dk, "dk"), dvv = mview_of(dv, "dv");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-  at::Tensor delta = at::empty({B, H, T}, lse.options());
-  const int64_t rows = (int64_t)B * H * T;
-  hipLaunchKernelGGL(bwd_pre_kernel, dim3((unsigned)((rows + NT - 1) / NT)), dim3(NT), 0, st, dov, ov,
-                     delta.data_ptr<float>(), H, T, rows);
-  C10_HIP_KERNEL_LAUNCH_CHECK();
   const int nblk = T / BLK;
+  // short sequences: δ inside the main kernel (each (query head, tile) is swept by <= 2 key blocks)
+  const bool fd = nblk <= 2;
+  at::Tensor delta;
+  if (!fd) {
+    delta = at::empty({B, H, T}, lse.options());
+    const int64_t rows = (int64_t)B * H * T;
+    hipLaunchKernelGGL(bwd_pre_kernel, dim3((unsigned)((rows + NT - 1) / NT)), dim3(NT), 0, st, dov, ov,
+                       delta.data_ptr<float>(), H, T, rows);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+  float* dptr = fd ? nullptr : delta.data_ptr<float>();
   const int Hkv = (int)k.size(1), group = H / Hkv;
   const float sc2 = (float)scale * kLog2e;
   // GQA with few key/value workgroups: split each kv head's query-head group over workgroups
@@ -689,14 +731,18 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     dkw = MView{static_cast<uint16_t*>(pk.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
     dvw = MView{static_cast<uint16_t*>(pv.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
   }
-  if (causal)
-    hipLaunchKernelGGL((bwd_kernel<true>), dim3((unsigned)(nkv + nq)), dim3(NT), 0, st, qv, kv, vv, dov,
-                       lse.data_ptr<float>(), delta.data_ptr<float>(), dqv, dkw, dvw, H, Hkv, T, nblk, sc2,
-                       (float)scale, group, rp, nkv, gsplit, split_stride);
-  else
-    hipLaunchKernelGGL((bwd_kernel<false>), dim3((unsigned)(nkv + nq)), dim3(NT), 0, st, qv, kv, vv, dov,
-                       lse.data_ptr<float>(), delta.data_ptr<float>(), dqv, dkw, dvw, H, Hkv, T, nblk, sc2,
-                       (float)scale, group, rp, nkv, gsplit, split_stride);
+#define NBD_BWD(C_, F_)                                                                                      \
+  hipLaunchKernelGGL((bwd_kernel<C_, F_>), dim3((unsigned)(nkv + nq)), dim3(NT), 0, st, qv, kv, vv, dov, ov,   \
+                     lse.data_ptr<float>(), dptr, dqv, dkw, dvw, H, Hkv, T, nblk, sc2, (float)scale, group, rp, nkv, \
+                     gsplit, split_stride)
+  if (causal) {
+    if (fd) NBD_BWD(true, true);
+    else NBD_BWD(true, false);
+  } else {
+    if (fd) NBD_BWD(false, true);
+    else NBD_BWD(false, false);
+  }
+#undef NBD_BWD
   C10_HIP_KERNEL_LAUNCH_CHECK();
   if (gsplit > 1) {
     const int64_t n8 = (int64_t)B * Hkv * T * (D / 8);
