@@ -1,8 +1,10 @@
-"""Data-plane helpers: the ``rccl`` backend, DDP with fused HIP bucket kernels, collectives."""
+"""Data-plane helpers: the ``rccl`` backend, DDP with fused HIP bucket kernels, tensor parallelism
+(``parallel.tensor``), Ulysses sequence parallelism (``parallel.sequence``)."""
 from .backend import abort_process_group, init_data_plane, rccl_version, register_rccl_backend, resolve_backend
 
 __all__ = ["abort_process_group", "init_data_plane", "rccl_version", "register_rccl_backend", "resolve_backend",
-           "DistributedDataParallel", "bf16_compress_hook", "allreduce_hook", "broadcast_params", "broadcast_tensors"]
+           "DistributedDataParallel", "bf16_compress_hook", "allreduce_hook", "broadcast_params", "broadcast_tensors",
+           "tensor", "sequence", "parallelize_gpt2", "ColumnParallelLinear", "RowParallelLinear", "ulysses_attention"]
 
 
 def __getattr__(name):
@@ -11,4 +13,16 @@ def __getattr__(name):
         from . import ddp
 
         return getattr(ddp, name)
+    if name in ("tensor", "sequence"):
+        import importlib
+
+        return importlib.import_module(f".{name}", __name__)
+    if name in ("parallelize_gpt2", "ColumnParallelLinear", "RowParallelLinear"):
+        from . import tensor
+
+        return getattr(tensor, name)
+    if name == "ulysses_attention":
+        from . import sequence
+
+        return sequence.ulysses_attention
     raise AttributeError(name)

@@ -101,3 +101,58 @@ def test_gpt2_hip_path_two_ranks_stay_in_sync(sess):
     r = sess.execute(GPT2, render=False)
     for rank in (0, 1):
         assert r.results[rank]["echo"] == "(True, True)", r.results[rank]
+
+
+TP_GPT2 = """
+from nbdistributed_amd.models import GPT2, GPT2Config
+from nbdistributed_amd.parallel.tensor import parallelize_gpt2
+torch.manual_seed(5)                      # same init on both ranks: TP shards one replicated model
+cfg = GPT2Config(vocab_size=512, n_positions=128, n_embd=256, n_layer=2, n_head=4)
+ref = GPT2(cfg).to(device, torch.bfloat16)
+tp = GPT2(cfg).to(device, torch.bfloat16)
+tp.load_state_dict(ref.state_dict())
+parallelize_gpt2(tp)
+idx = torch.randint(0, 512, (2, 128), generator=torch.Generator().manual_seed(9)).to(device)
+l_ref = ref(idx, idx)[1]; l_tp = tp(idx, idx)[1]
+l_ref.backward(); l_tp.backward()
+hid = slice(rank * 512, (rank + 1) * 512)
+g_ref = ref.h[1].mlp.c_fc.weight.grad[hid].float(); g_tp = tp.h[1].mlp.c_fc.weight.grad.float()
+gerr = ((g_tp - g_ref).abs().max() / g_ref.abs().max()).item()
+w_err = ((tp.wte.weight.grad.float() - ref.wte.weight.grad.float()).abs().max()
+         / ref.wte.weight.grad.float().abs().max()).item()
+(abs(float(l_tp) - float(l_ref)) < 2e-2 * abs(float(l_ref)), gerr < 5e-2, w_err < 5e-2, tp.h[0].attn.n_head)
+"""
+
+
+def test_tensor_parallel_gpt2_hip_path_two_ranks(sess):
+    """parallel.tensor: GPT-2 heads / MLP features split over 2 ranks (HIP GEMM + flash attention
+    on the shards) = the unsharded bf16 model on the same rank."""
+    r = sess.execute(TP_GPT2, render=False)
+    for rank in (0, 1):
+        assert r.results[rank]["echo"] == "(True, True, True, 2)", r.results[rank]
+
+
+ULYSSES = """
+from nbdistributed_amd.parallel.sequence import ulysses_attention, shard_sequence
+torch.manual_seed(6)
+q = torch.randn(1, 4, 256, 64, device=device, dtype=torch.bfloat16, requires_grad=True)
+k = torch.randn(1, 4, 256, 64, device=device, dtype=torch.bfloat16, requires_grad=True)
+v = torch.randn(1, 4, 256, 64, device=device, dtype=torch.bfloat16, requires_grad=True)
+w = torch.randn(1, 4, 256, 64, device=device, dtype=torch.bfloat16)
+ref = nbd.ops.flash_attention(q, k, v, causal=True)
+(ref.float() * w.float()).sum().backward()
+ql, kl, vl = (shard_sequence(t.detach(), dim=2).clone().requires_grad_() for t in (q, k, v))
+out = ulysses_attention(ql, kl, vl, causal=True)
+(out.float() * shard_sequence(w, dim=2).float()).sum().backward()
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max()).item()
+(_rel(out, shard_sequence(ref.detach(), dim=2)) < 2e-2, _rel(kl.grad, shard_sequence(k.grad, dim=2)) < 5e-2)
+"""
+
+
+def test_ulysses_attention_hip_path_two_ranks(sess):
+    """parallel.sequence: sequence split over 2 ranks, all-to-all to heads, HIP flash attention on the
+    full sequence (T = 256), all-to-all back = flash attention on the unsplit sequence."""
+    r = sess.execute(ULYSSES, render=False)
+    for rank in (0, 1):
+        assert r.results[rank]["echo"] == "(True, True)", r.results[rank]

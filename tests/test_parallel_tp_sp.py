@@ -1,0 +1,143 @@
+"""Tensor and sequence parallelism (parallel/tensor.py, parallel/sequence.py) vs the unsharded
+single-process computation — CPU/gloo, 2 ranks (world 1 for the degenerate path)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn(fn, n):
+    port = _port()
+    mp.spawn(_entry, args=(fn, n, port), nprocs=n, join=True)
+
+
+def _entry(rank, fn, n, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=n)
+    try:
+        fn(rank, n)
+    finally:
+        dist.destroy_process_group()
+
+
+def _close(a, b, tol=2e-5):
+    assert a.shape == b.shape, (a.shape, b.shape)
+    err = (a - b).abs().max().item()
+    assert err <= tol * max(1.0, b.abs().max().item()), err
+
+
+def _tp_linear_case(rank, n):
+    from nbdistributed_amd.parallel.tensor import ColumnParallelLinear, RowParallelLinear
+
+    torch.manual_seed(0)
+    l1, l2 = torch.nn.Linear(16, 32), torch.nn.Linear(32, 8)
+    x = torch.randn(4, 5, 16, requires_grad=True)
+    ref = l2(torch.relu(l1(x)))
+    ref.square().sum().backward()
+    c = ColumnParallelLinear.from_linear(l1)
+    r = RowParallelLinear.from_linear(l2)
+    xs = x.detach().clone().requires_grad_()
+    y = r(torch.relu(c(xs)))
+    _close(y, ref)
+    y.square().sum().backward()
+    _close(xs.grad, x.grad)
+    sl = slice(rank * 32 // n, (rank + 1) * 32 // n)
+    _close(c.weight.grad, l1.weight.grad[sl])
+    _close(c.bias.grad, l1.bias.grad[sl])
+    _close(r.weight.grad, l2.weight.grad[:, sl])
+    _close(r.bias.grad, l2.bias.grad)
+    # gather_output / input_is_parallel=False round trip
+    c2 = ColumnParallelLinear.from_linear(l1, gather_output=True)
+    r2 = RowParallelLinear.from_linear(l2, input_is_parallel=False)
+    xs2 = x.detach().clone().requires_grad_()
+    y2 = r2(torch.relu(c2(xs2)))
+    _close(y2, ref)
+    y2.square().sum().backward()
+    _close(xs2.grad, x.grad)
+
+
+def _tp_gpt2_case(rank, n):
+    from nbdistributed_amd.models import GPT2, GPT2Config
+    from nbdistributed_amd.parallel.tensor import parallelize_gpt2
+
+    torch.manual_seed(0)
+    cfg = GPT2Config(vocab_size=96, n_positions=32, n_embd=32, n_layer=2, n_head=4)
+    ref = GPT2(cfg)
+    tp = GPT2(cfg)
+    tp.load_state_dict(ref.state_dict())
+    parallelize_gpt2(tp)
+    idx = torch.randint(0, 96, (2, 16), generator=torch.Generator().manual_seed(1))
+    _, l_ref = ref(idx, idx)
+    _, l_tp = tp(idx, idx)
+    _close(l_tp, l_ref, 1e-5)
+    l_ref.backward()
+    l_tp.backward()
+    C, H = 32, 4
+    D, Hl = C // H, H // n
+    heads = torch.arange(rank * Hl * D, (rank + 1) * Hl * D)
+    rows = torch.cat([heads + i * C for i in range(3)])
+    hid = slice(rank * 4 * C // n, (rank + 1) * 4 * C // n)
+    for b_ref, b_tp in zip(ref.h, tp.h):
+        _close(b_tp.attn.c_attn.weight.grad, b_ref.attn.c_attn.weight.grad[rows], 1e-4)
+        _close(b_tp.attn.c_attn.bias.grad, b_ref.attn.c_attn.bias.grad[rows], 1e-4)
+        _close(b_tp.attn.c_proj.weight.grad, b_ref.attn.c_proj.weight.grad[:, heads], 1e-4)
+        _close(b_tp.attn.c_proj.bias.grad, b_ref.attn.c_proj.bias.grad, 1e-4)
+        _close(b_tp.mlp.c_fc.weight.grad, b_ref.mlp.c_fc.weight.grad[hid], 1e-4)
+        _close(b_tp.mlp.c_proj.weight.grad, b_ref.mlp.c_proj.weight.grad[:, hid], 1e-4)
+        _close(b_tp.ln_1.weight.grad, b_ref.ln_1.weight.grad, 1e-4)
+    _close(tp.wte.weight.grad, ref.wte.weight.grad, 1e-4)
+
+
+def _ulysses_case(rank, n):
+    import torch.nn.functional as F
+
+    from nbdistributed_amd.parallel.sequence import (gather_sequence, head_to_seq, seq_to_head, shard_sequence,
+                                                     ulysses_attention)
+
+    torch.manual_seed(0)
+    B, H, Hkv, T, D = 2, 4, 2, 16, 8
+    q = torch.randn(B, H, T, D, requires_grad=True)
+    k = torch.randn(B, Hkv, T, D, requires_grad=True)
+    v = torch.randn(B, Hkv, T, D, requires_grad=True)
+    w = torch.randn(B, H, T, D)
+    for causal in (True, False):
+        for t in (q, k, v):
+            t.grad = None
+        ref = F.scaled_dot_product_attention(q, k, v, is_causal=causal, enable_gqa=True)
+        (ref * w).sum().backward()
+        ql, kl, vl = (shard_sequence(t.detach(), dim=2).clone().requires_grad_() for t in (q, k, v))
+        out = ulysses_attention(ql, kl, vl, causal=causal)
+        _close(out, shard_sequence(ref.detach(), dim=2), 1e-5)
+        (out * shard_sequence(w, dim=2)).sum().backward()
+        _close(ql.grad, shard_sequence(q.grad, dim=2), 1e-5)
+        _close(kl.grad, shard_sequence(k.grad, dim=2), 1e-5)
+        _close(vl.grad, shard_sequence(v.grad, dim=2), 1e-5)
+        _close(gather_sequence(out, dim=2), ref.detach(), 1e-5)
+    # the two all-to-alls are inverses
+    x = torch.randn(B, H, T // n, D)
+    _close(head_to_seq(seq_to_head(x)), x, 0)
+
+
+@pytest.mark.parametrize("case", [_tp_linear_case, _tp_gpt2_case, _ulysses_case],
+                         ids=["tp_linear", "tp_gpt2", "ulysses"])
+def test_two_ranks(case):
+    _spawn(case, 2)
+
+
+def test_single_process_is_identity():
+    """Without an initialised process group every wrapper degenerates to the plain op."""
+    assert not dist.is_initialized()
+    _tp_linear_case(0, 1)
+    _ulysses_case(0, 1)
