@@ -1,5 +1,5 @@
-"""Tensor and sequence parallelism (parallel/tensor.py, parallel/sequence.py) vs the unsharded
-single-process computation — CPU/gloo, 2 ranks (world 1 for the degenerate path)."""
+"""Tensor, sequence and expert parallelism (parallel/tensor.py, sequence.py, expert.py) vs the
+unsharded single-process computation — CPU/gloo, 2 ranks (world 1 for the degenerate path)."""
 import os
 import socket
 
@@ -141,3 +141,59 @@ def test_single_process_is_identity():
     assert not dist.is_initialized()
     _tp_linear_case(0, 1)
     _ulysses_case(0, 1)
+
+
+def _moe_case(rank, n):
+    import torch.nn.functional as F
+
+    from nbdistributed_amd.parallel.expert import MoE
+
+    C, Hd, E, k, N = 16, 32, 4, 2, 24
+    torch.manual_seed(0)
+    moe = MoE(C, Hd, E, top_k=k)
+    g = torch.Generator().manual_seed(7)
+    X = torch.randn(n, N, C, generator=g)       # every rank's tokens, identical everywhere
+    W = torch.randn(n, N, C, generator=g)
+    x = X[rank].clone().requires_grad_()
+    out = moe(x)
+    (out * W[rank]).sum().backward()
+    assert moe.aux_loss is not None and torch.isfinite(moe.aux_loss)
+
+    # dense single-process reference over all ranks' tokens with the full expert set
+    def full(p):
+        if n == 1:
+            return p.detach().clone()
+        parts = [torch.empty_like(p) for _ in range(n)]
+        dist.all_gather(parts, p.detach().contiguous())
+        return torch.cat(parts)
+    w1 = full(moe.w1).requires_grad_()
+    w2 = full(moe.w2).requires_grad_()
+    router = moe.router.weight.detach().clone().requires_grad_()
+    Xr = X.reshape(-1, C).clone().requires_grad_()
+    probs = F.softmax(Xr @ router.t(), -1)
+    gates, idx = probs.topk(k, -1)
+    gates = gates / gates.sum(-1, keepdim=True)
+    ref = torch.zeros_like(Xr)
+    for j in range(k):
+        for e in range(E):
+            m = idx[:, j] == e
+            h = F.gelu(Xr[m] @ w1[e].t(), approximate="tanh") @ w2[e].t()
+            ref = ref.index_add(0, m.nonzero().squeeze(1), h * gates[m, j:j + 1])
+    (ref * W.reshape(-1, C)).sum().backward()
+    _close(out, ref.detach().view(n, N, C)[rank], 1e-5)
+    _close(x.grad, Xr.grad.view(n, N, C)[rank], 1e-5)
+    sl = slice(rank * E // n, (rank + 1) * E // n)
+    _close(moe.w1.grad, w1.grad[sl], 1e-5)
+    _close(moe.w2.grad, w2.grad[sl], 1e-5)
+    rg = moe.router.weight.grad.clone()
+    if n > 1:
+        dist.all_reduce(rg)
+    _close(rg, router.grad, 1e-5)
+
+
+def test_moe_two_ranks():
+    _spawn(_moe_case, 2)
+
+
+def test_moe_single_process():
+    _moe_case(0, 1)
