@@ -1,10 +1,11 @@
 """Data-plane helpers: the ``rccl`` backend, DDP with fused HIP bucket kernels, tensor parallelism
-(``parallel.tensor``), Ulysses sequence parallelism (``parallel.sequence``), expert parallelism (``parallel.expert``)."""
+(``parallel.tensor``), Ulysses sequence parallelism (``parallel.sequence``), expert parallelism (``parallel.expert``),
+pipeline parallelism (``parallel.pipeline``)."""
 from .backend import abort_process_group, init_data_plane, rccl_version, register_rccl_backend, resolve_backend
 
 __all__ = ["abort_process_group", "init_data_plane", "rccl_version", "register_rccl_backend", "resolve_backend",
            "DistributedDataParallel", "bf16_compress_hook", "allreduce_hook", "broadcast_params", "broadcast_tensors",
-           "tensor", "sequence", "expert", "MoE", "parallelize_gpt2", "ColumnParallelLinear", "RowParallelLinear", "ulysses_attention"]
+           "tensor", "sequence", "expert", "pipeline", "pipeline_step", "MoE", "parallelize_gpt2", "ColumnParallelLinear", "RowParallelLinear", "ulysses_attention"]
 
 
 def __getattr__(name):
@@ -13,7 +14,7 @@ def __getattr__(name):
         from . import ddp
 
         return getattr(ddp, name)
-    if name in ("tensor", "sequence", "expert"):
+    if name in ("tensor", "sequence", "expert", "pipeline"):
         import importlib
 
         return importlib.import_module(f".{name}", __name__)
@@ -21,6 +22,10 @@ def __getattr__(name):
         from . import tensor
 
         return getattr(tensor, name)
+    if name == "pipeline_step":
+        from . import pipeline
+
+        return pipeline.pipeline_step
     if name == "MoE":
         from . import expert
 

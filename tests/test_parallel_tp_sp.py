@@ -1,5 +1,6 @@
-"""Tensor, sequence and expert parallelism (parallel/tensor.py, sequence.py, expert.py) vs the
-unsharded single-process computation — CPU/gloo, 2 ranks (world 1 for the degenerate path)."""
+"""Tensor, sequence, expert and pipeline parallelism (parallel/tensor.py, sequence.py, expert.py,
+pipeline.py) vs the unsharded single-process computation — CPU/gloo, 2 and 4 ranks (world 1 for
+the degenerate path)."""
 import os
 import socket
 
@@ -197,3 +198,61 @@ def test_moe_two_ranks():
 
 def test_moe_single_process():
     _moe_case(0, 1)
+
+
+def _pipe_model():
+    torch.manual_seed(0)
+    layers = []
+    for _ in range(4):
+        layers += [torch.nn.Linear(12, 12), torch.nn.Tanh()]
+    return torch.nn.Sequential(*layers)
+
+
+def _pipeline_case(rank, n, schedule="1f1b"):
+    from nbdistributed_amd.parallel.pipeline import pipeline_step, split_sequential
+
+    M, mb = 6, 3
+    full = _pipe_model()
+    g = torch.Generator().manual_seed(3)
+    X, Y = torch.randn(M * mb, 12, generator=g), torch.randn(M * mb, 12, generator=g)
+    torch.nn.functional.mse_loss(full(X), Y).backward()
+    stage = split_sequential(_pipe_model(), n, rank)
+    xs, ys = list(X.chunk(M)), list(Y.chunk(M))
+    loss = pipeline_step(stage, xs if rank == 0 else None, ys if rank == n - 1 else None,
+                         torch.nn.functional.mse_loss, M, (mb, 12), schedule=schedule)
+    if rank == n - 1:
+        _close(loss, torch.nn.functional.mse_loss(full(X), Y).detach(), 1e-5)
+    else:
+        assert loss is None
+    # the stage holds copies of a contiguous run of layers: match them by position
+    full_layers = list(full)
+    stage_layers = list(stage)
+    for k0 in range(len(full_layers) - len(stage_layers) + 1):
+        if all(type(a) is type(b) and all(torch.equal(pa, pb) for pa, pb in zip(a.parameters(), b.parameters()))
+               for a, b in zip(full_layers[k0:], stage_layers)):
+            break
+    else:
+        raise AssertionError("stage layers not found in the full model")
+    for a, b in zip(full_layers[k0:], stage_layers):
+        for pa, pb in zip(a.parameters(), b.parameters()):
+            _close(pb.grad, pa.grad, 1e-5)
+
+
+def _pipeline_gpipe_case(rank, n):
+    _pipeline_case(rank, n, "gpipe")
+
+
+@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("case", [_pipeline_case, _pipeline_gpipe_case], ids=["1f1b", "gpipe"])
+def test_pipeline_schedules(case, n):
+    _spawn(case, n)
+
+
+def test_split_sequential_balanced():
+    from nbdistributed_amd.parallel.pipeline import split_sequential
+
+    m = _pipe_model()
+    parts = [split_sequential(m, 4, s) for s in range(4)]
+    assert sum(len(p) for p in parts) == len(m)
+    assert all(len(p) == 2 for p in parts)
+    assert len(split_sequential(m, 1, 0)) == len(m)
