@@ -175,6 +175,123 @@ __global__ __launch_bounds__(kXentThreads) void xent_bwd_kernel(const T* __restr
   }
 }
 
+// ---- forward and backward in one pass (the LM-head + loss path: logits are dead after the loss) --
+// One read and one in-place write of each row: the row is held in registers between the two (NV
+// 16-B chunks per lane, 256 lanes: V <= 256·8·NV), so the separate forward read of the two-kernel
+// path disappears.  dx = (softmax(x) - onehot(t)) * scale with scale = 1/n_valid (or 1) read from
+// device memory; grad_out is folded into the LM-head GEMMs' small operands by the caller.
+template <typename T>
+__device__ __forceinline__ void unpack8(const u32x4& w, float (&v)[8]);
+template <>
+__device__ __forceinline__ void unpack8<bf16_t>(const u32x4& w, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
+}
+template <>
+__device__ __forceinline__ void unpack8<f16_t>(const u32x4& w, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = f16_to_f32((uint16_t)(w[j] & 0xffffu));
+    v[2 * j + 1] = f16_to_f32((uint16_t)(w[j] >> 16));
+  }
+}
+
+constexpr int kFusedChunks = 32;  // at most 256 lanes x 32 x 8 = 65,536 columns (instances: 8, 16, 25, 32)
+
+template <typename T, int NV>
+__global__ __launch_bounds__(kXentThreads) void xent_fused_kernel(T* logits, int64_t ld,
+                                                                  const int64_t* __restrict__ target, int64_t V,
+                                                                  int64_t ignore_index,
+                                                                  const float* __restrict__ scale,
+                                                                  float* __restrict__ loss,
+                                                                  float* __restrict__ lse_out) {
+  const int64_t row = blockIdx.x;
+  T* x = logits + row * ld;
+  const int tid = threadIdx.x;
+  const int64_t t = target[row];
+  const bool valid = t != ignore_index && t >= 0 && t < V;
+  float xt = 0.f;
+  if (tid == 0 && valid) xt = Elem<T>::load(x, t);
+  const int64_t head = head_elems(x, V);
+  T* xv = x + head;
+  const int64_t nv = (V - head) / 8;
+  const int64_t tail0 = head + nv * 8;
+  // lanes 0..7 own the unaligned head elements, lanes 8..15 the tail (each < 8)
+  int64_t is = -1;
+  if (tid < head) is = tid;
+  else if (tid >= 8 && tid < 16 && tid - 8 < V - tail0) is = tail0 + tid - 8;
+  const float xs = is >= 0 ? Elem<T>::load(x, is) : 0.f;
+  u32x4 r[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int64_t k = tid + (int64_t)c * kXentThreads;
+    if (k < nv) r[c] = *reinterpret_cast<const u32x4*>(xv + k * 8);
+  }
+  OnlineLse acc;
+  if (is >= 0) acc.add(xs * kLog2e);
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int64_t k = tid + (int64_t)c * kXentThreads;
+    if (k < nv) {
+      float v[8];
+      unpack8<T>(r[c], v);
+      acc.add8(v);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float m2 = __shfl_xor(acc.m, off, kWave);
+    const float s2 = __shfl_xor(acc.s, off, kWave);
+    acc.merge(m2, s2);
+  }
+  __shared__ float sm[kXentThreads / kWave], ss[kXentThreads / kWave];
+  const int wave = tid / kWave;
+  if ((tid & (kWave - 1)) == 0) {
+    sm[wave] = acc.m;
+    ss[wave] = acc.s;
+  }
+  __syncthreads();  // every read of the row (registers, xs, xt) happened before any write below
+  // keep the row packed between the passes: without this the compiler holds 8 unpacked floats per
+  // chunk (306 VGPRs at NV = 32) instead of re-unpacking (a shift and a mask per pair)
+#pragma unroll
+  for (int c = 0; c < NV; ++c) asm volatile("" : "+v"(r[c]));
+  OnlineLse tot;
+#pragma unroll
+  for (int w = 0; w < kXentThreads / kWave; ++w) tot.merge(sm[w], ss[w]);
+  const float lse = (tot.m + log2f(tot.s)) * kLn2;
+  if (tid == 0) {
+    lse_out[row] = lse;
+    loss[row] = valid ? lse - xt : (t == ignore_index ? 0.f : NAN);
+  }
+  const float sc = valid ? *scale : 0.f;
+  const float l2 = lse * kLog2e;
+  if (is >= 0) {
+    float g = __builtin_amdgcn_exp2f(xs * kLog2e - l2) * sc;
+    if (is == t) g -= sc;
+    Elem<T>::store(x, is, g);
+  }
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int64_t k = tid + (int64_t)c * kXentThreads;
+    if (k < nv) {
+      float v[8];
+      unpack8<T>(r[c], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = __builtin_amdgcn_exp2f(v[j] * kLog2e - l2) * sc;
+      const int64_t d = t - (head + k * 8);
+      if (d >= 0 && d < 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j == d) v[j] -= sc;
+      }
+      store8_nt<T>(xv + k * 8, v);
+    }
+  }
+}
+
 static void check_logits(const at::Tensor& logits, const at::Tensor& target) {
   TORCH_CHECK(logits.is_cuda() && target.is_cuda(), "xent: GPU tensors expected");
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "xent: logits must be [N, V] with unit column stride");
@@ -252,9 +369,51 @@ void xent_bwd_hip(const at::Tensor& logits, const at::Tensor& target, const at::
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
+std::tuple<at::Tensor, at::Tensor> xent_fused_hip(const at::Tensor& logits, const at::Tensor& target,
+                                                  int64_t ignore_index, const at::Tensor& scale) {
+  check_logits(logits, target);
+  const int64_t N = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kHalf,
+              "xent_fused: bf16 / fp16 logits expected");
+  TORCH_CHECK(V > 0 && V <= (int64_t)kXentThreads * 8 * kFusedChunks + 14, "xent_fused: vocabulary too large");
+  TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() == 1,
+              "xent_fused: scale must be a 1-element float32 GPU tensor");
+  auto opts = logits.options().dtype(at::kFloat);
+  at::Tensor loss = at::empty({N}, opts), lse = at::empty({N}, opts);
+  if (N == 0) return {loss, lse};
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  const int64_t ld = logits.stride(0);
+  // registers per lane scale with the chunk count: use the smallest instance covering the row
+  const int64_t need = (V + (int64_t)kXentThreads * 8 - 1) / ((int64_t)kXentThreads * 8);
+  const bool bf = logits.scalar_type() == at::kBFloat16;
+#define NBD_XFU(NV)                                                                                              \
+  if (bf)                                                                                                        \
+    hipLaunchKernelGGL((xent_fused_kernel<bf16_t, NV>), dim3((unsigned)N), dim3(kXentThreads), 0, st,           \
+                       static_cast<bf16_t*>(logits.data_ptr()), ld, target.data_ptr<int64_t>(), V, ignore_index, \
+                       scale.data_ptr<float>(), loss.data_ptr<float>(), lse.data_ptr<float>());                 \
+  else                                                                                                           \
+    hipLaunchKernelGGL((xent_fused_kernel<f16_t, NV>), dim3((unsigned)N), dim3(kXentThreads), 0, st,            \
+                       static_cast<f16_t*>(logits.data_ptr()), ld, target.data_ptr<int64_t>(), V, ignore_index,  \
+                       scale.data_ptr<float>(), loss.data_ptr<float>(), lse.data_ptr<float>());
+  if (need <= 8) {
+    NBD_XFU(8)
+  } else if (need <= 16) {
+    NBD_XFU(16)
+  } else if (need <= 25) {
+    NBD_XFU(25)
+  } else {
+    NBD_XFU(32)
+  }
+#undef NBD_XFU
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return {loss, lse};
+}
+
 }  // namespace nbd
 
 TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
   m.impl("xent_fwd", &nbd::xent_fwd_hip);
   m.impl("xent_bwd", &nbd::xent_bwd_hip);
+  m.impl("xent_fused", &nbd::xent_fused_hip);
 }

@@ -177,6 +177,9 @@ class GPT2(nn.Module):
                                           blk.ln_2.eps)
                 nxt = self.h[i + 1].ln_1 if i + 1 < c.n_layer else self.ln_f
                 x, h = ops.add_layer_norm(x, blk.mlp(h, fast=True), nxt.weight, nxt.bias, nxt.eps)
+            if targets is not None and not return_logits and c.fused_ce and ops.loss.FUSED_XENT:
+                # LM head + loss: one pass over the logits for the loss forward and backward
+                return None, ops.linear_cross_entropy(h, self.lm_head.weight, targets)
             logits = self.lm_head(h)
         else:
             for blk in self.h:

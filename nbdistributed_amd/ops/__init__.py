@@ -38,7 +38,7 @@ from .bucket import (_ref_flatten, _ref_prereduce, _ref_unflatten, bucket_flatte
 from .embedding import embedding
 from .gemm import gemm_linear, mlp_gelu, mlp_swiglu
 from .llama import rope_, rope_tables, swiglu
-from .loss import cross_entropy
+from .loss import cross_entropy, linear_cross_entropy
 from .norm import add_layer_norm, add_rms_norm, colsum, layer_norm, linear, rms_norm
 from .optim import _ref_adamw, adamw_flat
 from .summary import SUMMARY_FIELDS, _ref_summary, tensor_summary, tensor_summary_raw, tensor_summary_text
@@ -50,7 +50,7 @@ def __getattr__(name):
     raise AttributeError(name)
 
 
-__all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "cross_entropy",
+__all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "cross_entropy", "linear_cross_entropy",
            "flash_attention", "attention_qkv", "flash_supported", "layer_norm", "add_layer_norm", "linear",
            "colsum", "embedding", "gemm_linear", "mlp_gelu", "mlp_swiglu", "rms_norm", "add_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary",
            "tensor_summary_text", "tensor_summary_raw", "plan_offsets", "native_available", "load_library",

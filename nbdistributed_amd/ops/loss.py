@@ -1,7 +1,12 @@
 """Fused large-vocabulary softmax cross-entropy (K6)."""
 from __future__ import annotations
 
+import os
+
 from ._lib import _require
+
+# GPT-2's return_logits=False path through linear_cross_entropy (A/B switch: NBD_FUSED_XENT=0)
+FUSED_XENT = os.environ.get("NBD_FUSED_XENT", "1") != "0"
 
 
 _XentFn = None
@@ -35,7 +40,32 @@ def _xent_fn():
             torch.ops.nbd.xent_bwd(logits, target, lse, scale, ctx.ignore_index, dlogits)
             return dlogits, None, None, None, None
 
-    _XentFn = _FusedCrossEntropy
+    class _LinearCrossEntropy(torch.autograd.Function):
+        """loss(h·Wᵀ, target) with the loss forward and backward in ONE pass over the logits
+        (``nbd::xent_fused``: the row stays in registers between the logsumexp and the in-place
+        gradient write).  grad_out is applied to the two small GEMM operands in backward, never to
+        the [N, V] gradient."""
+
+        @staticmethod
+        def forward(ctx, h2, w, target, ignore_index, reduction):
+            logits = torch.mm(h2, w.t())
+            if reduction == "mean":
+                scale = (1.0 / (target != ignore_index).sum().float()).reshape(1)  # inf (-> nan loss) if none
+            else:
+                scale = torch.ones(1, dtype=torch.float32, device=h2.device)
+            loss_rows, _ = torch.ops.nbd.xent_fused(logits, target, ignore_index, scale)
+            ctx.save_for_backward(h2, w, logits)  # logits now hold d(loss)/d(logits) for grad_out = 1
+            return loss_rows.sum() * scale[0]
+
+        @staticmethod
+        def backward(ctx, grad):
+            h2, w, dlogits = ctx.saved_tensors
+            g = grad.to(h2.dtype)
+            dh = torch.mm(dlogits, w).mul_(g) if ctx.needs_input_grad[0] else None
+            dw = torch.mm(dlogits.t(), h2 * g) if ctx.needs_input_grad[1] else None
+            return dh, dw, None, None, None
+
+    _XentFn = (_FusedCrossEntropy, _LinearCrossEntropy)
     return _XentFn
 
 def cross_entropy(logits, target, ignore_index: int = -100, reduction: str = "mean", inplace_backward: bool = False):
@@ -55,4 +85,27 @@ def cross_entropy(logits, target, ignore_index: int = -100, reduction: str = "me
     _require()
     if logits.stride(-1) != 1:
         logits = logits.contiguous()
-    return _xent_fn().apply(logits, target.contiguous().long(), int(ignore_index), reduction, bool(inplace_backward))
+    return _xent_fn()[0].apply(logits, target.contiguous().long(), int(ignore_index), reduction, bool(inplace_backward))
+
+
+FUSED_MAX_VOCAB = 256 * 8 * 32  # xent_fused keeps a row in registers: 256 lanes x 32 chunks x 8
+
+
+def linear_cross_entropy(h, weight, target, ignore_index: int = -100, reduction: str = "mean"):
+    """``cross_entropy(h @ weight.T, target)`` for an LM head (``h`` [..., C], ``weight`` [V, C]) —
+    the loss's forward and backward fused into one pass over the logits on the GPU path (bf16/fp16,
+    V ≤ 65,536: one read and one in-place write of the [N, V] logits instead of two reads and a
+    write), the GEMMs on hipBLASLt.  The logits are not returned."""
+    import torch
+    import torch.nn.functional as F
+
+    if reduction not in ("mean", "sum"):
+        raise ValueError("linear_cross_entropy: reduction must be 'mean' or 'sum'")
+    h2 = h.reshape(-1, h.shape[-1])
+    tgt = target.reshape(-1)
+    if not (h.is_cuda and h.dtype in (torch.bfloat16, torch.float16) and weight.dtype == h.dtype
+            and weight.shape[0] <= FUSED_MAX_VOCAB and not torch.is_autocast_enabled()):
+        return F.cross_entropy(F.linear(h2, weight).float(), tgt, ignore_index=ignore_index, reduction=reduction)
+    _require()
+    return _xent_fn()[1].apply(h2 if h2.is_contiguous() else h2.contiguous(), weight, tgt.contiguous().long(),
+                               int(ignore_index), reduction)
