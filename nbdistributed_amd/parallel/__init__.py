@@ -1,11 +1,12 @@
 """Data-plane helpers: the ``rccl`` backend, DDP with fused HIP bucket kernels, tensor parallelism
 (``parallel.tensor``), Ulysses sequence parallelism (``parallel.sequence``), expert parallelism (``parallel.expert``),
-pipeline parallelism (``parallel.pipeline``)."""
+pipeline parallelism (``parallel.pipeline``),
+ring-attention context parallelism (``parallel.context``)."""
 from .backend import abort_process_group, init_data_plane, rccl_version, register_rccl_backend, resolve_backend
 
 __all__ = ["abort_process_group", "init_data_plane", "rccl_version", "register_rccl_backend", "resolve_backend",
            "DistributedDataParallel", "bf16_compress_hook", "allreduce_hook", "broadcast_params", "broadcast_tensors",
-           "tensor", "sequence", "expert", "pipeline", "pipeline_step", "MoE", "parallelize_gpt2", "ColumnParallelLinear", "RowParallelLinear", "ulysses_attention"]
+           "tensor", "sequence", "expert", "pipeline", "pipeline_step", "MoE", "parallelize_gpt2", "ColumnParallelLinear", "RowParallelLinear", "ulysses_attention", "context", "ring_attention"]
 
 
 def __getattr__(name):
@@ -14,7 +15,7 @@ def __getattr__(name):
         from . import ddp
 
         return getattr(ddp, name)
-    if name in ("tensor", "sequence", "expert", "pipeline"):
+    if name in ("tensor", "sequence", "expert", "pipeline", "context"):
         import importlib
 
         return importlib.import_module(f".{name}", __name__)
@@ -34,4 +35,8 @@ def __getattr__(name):
         from . import sequence
 
         return sequence.ulysses_attention
+    if name == "ring_attention":
+        from . import context
+
+        return context.ring_attention
     raise AttributeError(name)

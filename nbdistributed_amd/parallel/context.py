@@ -1,0 +1,282 @@
+"""Context parallelism: ring attention over a CP group.
+
+The reference has no long-context support (SP/CP "would be user code calling
+``dist.all_to_all`` … inside cells").  ``parallel.sequence`` covers Ulysses (all-to-all, needs
+``H % n == 0``); this module is the other standard scheme, for sequences whose activations do not
+fit one GPU even after head sharding or whose head count is smaller than the group:
+
+* every rank keeps its own query chunk(s); key/value chunks travel round the ring (one
+  ``batch_isend_irecv`` per step, posted *before* the step's attention so the xGMI transfer of
+  the next K/V block overlaps the HIP flash-attention kernels on the current one);
+* each block is one call of the gfx950 flash kernels (``nbd::attn_fwd``), which return the
+  block's log-sum-exp; blocks are merged exactly with the usual LSE rescaling (fp32 accumulator);
+* backward replays the ring: ``nbd::attn_bwd`` is given the *merged* output and LSE, so each
+  block's dQ/dK/dV is the exact slice of the full gradient; dQ accumulates locally and dK/dV
+  accumulators travel with their K/V block and take one extra hop home at the end.
+
+Causal load balance: with the contiguous layout rank r only needs kv chunks ≤ r (rank n-1 does n
+blocks, rank 0 one).  ``layout="zigzag"`` splits the sequence into 2n chunks and gives rank r chunks
+r and 2n-1-r, so every rank does the same number of (sub-)blocks at every step.
+
+A ring (not one all-gather) is the right shape on MI355X: each step moves one K/V chunk over a
+single point-to-point xGMI link, peak extra HBM is two K/V chunks instead of the whole sequence,
+and the transfer hides behind attention compute once chunks are ≥ a few thousand tokens.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .sequence import _rank, _size
+
+
+def _global(group, r: int) -> int:
+    return dist.get_global_rank(group, r) if group is not None else r
+
+
+def _chunk_ids(r: int, n: int, layout: str) -> List[int]:
+    if layout == "contiguous":
+        return [r]
+    if layout == "zigzag":
+        return [r, 2 * n - 1 - r]
+    raise ValueError(f"unknown context-parallel layout {layout!r} (contiguous | zigzag)")
+
+
+def shard_context(x, group=None, dim: int = 2, layout: str = "contiguous"):
+    """This rank's part of ``x`` along ``dim`` for ``layout`` (contiguous: chunk r of n; zigzag:
+    chunks r and 2n-1-r of 2n, concatenated)."""
+    n, r = _size(group), _rank(group)
+    parts = 1 if layout == "contiguous" else 2
+    if x.shape[dim] % (n * parts):
+        raise ValueError(f"length {x.shape[dim]} is not divisible into {n * parts} context chunks")
+    chunks = x.chunk(n * parts, dim=dim)
+    return torch.cat([chunks[c] for c in _chunk_ids(r, n, layout)], dim=dim)
+
+
+def gather_context(x, group=None, dim: int = 2, layout: str = "contiguous"):
+    """Inverse of :func:`shard_context`: the full sequence on every rank (forward only)."""
+    n = _size(group)
+    if n == 1:
+        return x
+    parts = [torch.empty_like(x) for _ in range(n)]
+    dist.all_gather(parts, x.contiguous(), group=group)
+    if layout == "contiguous":
+        return torch.cat(parts, dim=dim)
+    chunks = [None] * (2 * n)
+    for r, p in enumerate(parts):
+        a, b = p.chunk(2, dim=dim)
+        chunks[r], chunks[2 * n - 1 - r] = a, b
+    return torch.cat(chunks, dim=dim)
+
+
+# ---------------------------------------------------------------------------------------------
+# one attention block: HIP flash kernels where they apply, an fp32 reference otherwise
+# ---------------------------------------------------------------------------------------------
+
+def _hip_ok(q, k) -> bool:
+    from ..ops.attention import flash_supported
+
+    return (flash_supported(q) and k.shape[2] == q.shape[2] and k.dtype == q.dtype
+            and q.shape[1] % k.shape[1] == 0)
+
+
+def _fix(t):
+    """``t`` itself when the HIP attention kernels can read it as a strided view, else a copy."""
+    ok = t.stride(-1) == 1 and all(st % 8 == 0 for st in t.stride()[:-1]) and t.data_ptr() % 16 == 0
+    return t if ok else t.contiguous()
+
+
+def _rep(x, g: int):
+    return x if g == 1 else x.repeat_interleave(g, dim=1)
+
+
+def _blk_fwd(q, k, v, causal: bool, scale: float):
+    """(o [B, H, Tq, D], lse [B, H, Tq] fp32) of softmax(q·kᵀ·scale)·v; o is bf16 from the HIP
+    kernels, fp32 from the reference path."""
+    if _hip_ok(q, k):
+        from ..ops._lib import _require
+
+        _require()
+        return torch.ops.nbd.attn_fwd(_fix(q), _fix(k), _fix(v), causal, scale, None, None)
+    g = q.shape[1] // k.shape[1]
+    s = torch.matmul(q.float(), _rep(k, g).float().transpose(-1, -2)) * scale
+    if causal:
+        Tq, Tk = s.shape[-2:]
+        s = s.masked_fill(torch.ones(Tq, Tk, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    lse = torch.logsumexp(s, dim=-1)
+    return torch.matmul(torch.exp(s - lse.unsqueeze(-1)), _rep(v, g).float()), lse
+
+
+def _blk_bwd(do, q, k, v, o, lse, causal: bool, scale: float):
+    """This block's (dq, dk, dv) given the merged output ``o`` and merged ``lse`` of the rows."""
+    if _hip_ok(q, k):
+        B, H, T, D = q.shape
+        Hkv = k.shape[1]
+        dq = torch.empty(B, T, H, D, dtype=q.dtype, device=q.device).transpose(1, 2)
+        dkv = torch.empty(B, T, 2, Hkv, D, dtype=q.dtype, device=q.device)
+        dk, dv = dkv[:, :, 0].transpose(1, 2), dkv[:, :, 1].transpose(1, 2)
+        torch.ops.nbd.attn_bwd(_fix(do), _fix(q), _fix(k), _fix(v), _fix(o), lse, causal, scale, dq, dk, dv,
+                               None, None)
+        return dq, dk, dv
+    g = q.shape[1] // k.shape[1]
+    qf, kf, vf, dof = q.float(), _rep(k, g).float(), _rep(v, g).float(), do.float()
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        Tq, Tk = s.shape[-2:]
+        s = s.masked_fill(torch.ones(Tq, Tk, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    p = torch.exp(s - lse.unsqueeze(-1))
+    dv = torch.matmul(p.transpose(-1, -2), dof)
+    dp = torch.matmul(dof, vf.transpose(-1, -2))
+    delta = (dof * o.float()).sum(-1, keepdim=True)
+    ds = p * (dp - delta) * scale
+    dq = torch.matmul(ds, kf)
+    dk = torch.matmul(ds.transpose(-1, -2), qf)
+    if g > 1:
+        B, H, Tk, D = dk.shape
+        dk = dk.view(B, H // g, g, Tk, D).sum(2)
+        dv = dv.view(B, H // g, g, Tk, D).sum(2)
+    return dq, dk, dv
+
+
+def _merge(o_acc, lse_acc, o_b, l_b, out=None):
+    """Fold block (o_b, l_b) into the running (o_acc fp32, lse_acc) in place; with ``out`` (the
+    rows' last block) the merged rows go to ``out`` instead of ``o_acc``.  One HIP pass
+    (``nbd::attn_merge_``, csrc/kernels/ring.hip) for bf16 blocks, PyTorch otherwise."""
+    if o_b.is_cuda and o_b.dtype == torch.bfloat16 and o_b.shape[-1] == 64:
+        torch.ops.nbd.attn_merge_(o_acc, lse_acc, _fix(o_b), l_b, out)
+        return
+    l_new = torch.logaddexp(lse_acc, l_b)
+    merged = (o_acc * torch.exp(lse_acc - l_new).unsqueeze(-1) + o_b.float() * torch.exp(l_b - l_new).unsqueeze(-1))
+    lse_acc.copy_(l_new)
+    (out if out is not None else o_acc).copy_(merged)
+
+
+# ---------------------------------------------------------------------------------------------
+# ring plumbing
+# ---------------------------------------------------------------------------------------------
+
+class _Ring:
+    """Send to rank r+1 / receive from rank r-1 of ``group``, both posted in one batch.  Gloo has
+    no device-memory point-to-point path, so CUDA tensors are staged through host memory there."""
+
+    def __init__(self, group):
+        self.group = group
+        self.n, self.r = _size(group), _rank(group)
+        self.nxt = _global(group, (self.r + 1) % self.n)
+        self.prv = _global(group, (self.r - 1) % self.n)
+        self.stage = dist.is_initialized() and dist.get_backend(group) == "gloo"
+
+    def start(self, send: torch.Tensor):
+        """Post the exchange; returns a handle for :meth:`finish` (the received tensor)."""
+        dev = send.device
+        if self.stage and dev.type != "cpu":
+            send = send.cpu()
+        recv = torch.empty_like(send)
+        reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, send, self.nxt, self.group),
+                                       dist.P2POp(dist.irecv, recv, self.prv, self.group)])
+        return reqs, recv, dev, send
+
+    @staticmethod
+    def finish(handle) -> torch.Tensor:
+        reqs, recv, dev, _send = handle
+        for w in reqs:
+            w.wait()
+        return recv.to(dev, non_blocking=True) if recv.device != dev else recv
+
+
+def _blocks(r_q: int, r_kv: int, n: int, layout: str):
+    """(q sub-chunk, kv sub-chunk, causal) triples rank ``r_q`` computes against rank ``r_kv``'s
+    K/V for a causal mask (sub-chunks index into the rank's local concatenation)."""
+    out = []
+    for iq, cq in enumerate(_chunk_ids(r_q, n, layout)):
+        for ik, ck in enumerate(_chunk_ids(r_kv, n, layout)):
+            if ck < cq:
+                out.append((iq, ik, False))
+            elif ck == cq:
+                out.append((iq, ik, True))
+    return out
+
+
+class _RingAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale, group, layout):
+        ring = _Ring(group)
+        n, r = ring.n, ring.r
+        parts = 1 if layout == "contiguous" else 2
+        qs = q.chunk(parts, dim=2)
+        sched = [(_blocks(r, (r - s) % n, n, layout) if causal
+                  else [(iq, ik, False) for iq in range(parts) for ik in range(parts)]) for s in range(n)]
+        left = [sum(b[0] == iq for step in sched for b in step) for iq in range(parts)]
+        out = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+        outs = out.chunk(parts, dim=2)
+        o_acc, lse_acc = [None] * parts, [None] * parts
+        kv = torch.stack([k, v])
+        for s in range(n):
+            h = ring.start(kv) if s < n - 1 else None
+            ks, vs = kv[0].chunk(parts, dim=2), kv[1].chunk(parts, dim=2)
+            for iq, ik, diag in sched[s]:
+                o_b, l_b = _blk_fwd(qs[iq], ks[ik], vs[ik], diag, scale)
+                left[iq] -= 1
+                if lse_acc[iq] is None:
+                    lse_acc[iq] = l_b.contiguous()
+                    if left[iq] == 0:
+                        outs[iq].copy_(o_b)
+                    else:
+                        o_acc[iq] = o_b.to(torch.float32, memory_format=torch.contiguous_format)
+                else:
+                    _merge(o_acc[iq], lse_acc[iq], o_b, l_b, outs[iq] if left[iq] == 0 else None)
+            if h is not None:
+                kv = ring.finish(h)
+        ctx.save_for_backward(q, k, v, out, *lse_acc)
+        ctx.causal, ctx.scale, ctx.group, ctx.layout = causal, scale, group, layout
+        return out
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, *ls = ctx.saved_tensors
+        causal, scale, layout = ctx.causal, ctx.scale, ctx.layout
+        ring = _Ring(ctx.group)
+        n, r = ring.n, ring.r
+        parts = 1 if layout == "contiguous" else 2
+        do = do.contiguous()
+        qs, os_, dos = (t.chunk(parts, dim=2) for t in (q, o, do))
+        dq = [torch.zeros(c.shape, dtype=torch.float32, device=q.device) for c in qs]
+        kv = torch.stack([k, v])
+        dkv = torch.zeros(kv.shape, dtype=torch.float32, device=q.device)
+        for s in range(n):
+            h = ring.start(kv) if s < n - 1 else None
+            src = (r - s) % n
+            ks, vs = kv[0].chunk(parts, dim=2), kv[1].chunk(parts, dim=2)
+            dks, dvs = dkv[0].chunk(parts, dim=2), dkv[1].chunk(parts, dim=2)
+            blocks = (_blocks(r, src, n, layout) if causal
+                      else [(iq, ik, False) for iq in range(parts) for ik in range(parts)])
+            for iq, ik, diag in blocks:
+                dq_b, dk_b, dv_b = _blk_bwd(dos[iq], qs[iq], ks[ik], vs[ik], os_[iq], ls[iq], diag, scale)
+                dq[iq].add_(dq_b)
+                dks[ik].add_(dk_b)
+                dvs[ik].add_(dv_b)
+            # the dK/dV accumulator follows its K/V block (one extra hop home after the last step)
+            dkv = ring.finish(ring.start(dkv)) if n > 1 else dkv
+            if h is not None:
+                kv = ring.finish(h)
+        dq = torch.cat(dq, dim=2).to(q.dtype)
+        return dq, dkv[0].to(k.dtype), dkv[1].to(v.dtype), None, None, None, None
+
+
+def ring_attention(q, k, v, causal: bool = True, scale: Optional[float] = None, group=None,
+                   layout: str = "contiguous"):
+    """Attention over a sequence split across ``group`` by :func:`shard_context`: q [B, H, Tl, D],
+    k/v [B, Hkv, Tl, D] (``Hkv`` divides ``H``: grouped-query) → this rank's [B, H, Tl, D] output.
+    Exact (same result as attention on the gathered sequence); HIP flash kernels per block for bf16,
+    head dim 64 and chunks of a multiple of 128 tokens, an fp32 reference otherwise."""
+    sc = float(scale) if scale is not None else q.shape[-1] ** -0.5
+    if _size(group) == 1 and layout == "contiguous":
+        from .. import ops
+
+        return ops.flash_attention(q, k, v, causal=causal, scale=sc)
+    return _RingAttention.apply(q, k, v, bool(causal), sc, group, layout)
+
+
+__all__ = ["ring_attention", "shard_context", "gather_context"]

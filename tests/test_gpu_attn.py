@@ -94,3 +94,51 @@ def test_gpt2_small_step_fused_matches_sdpa(dev):
     g1 = m1.h[0].attn.c_attn.weight.grad
     g2 = m2.h[0].attn.c_attn.weight.grad
     assert _rel(g1, g2) < 5e-2
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("H,Hkv", [(4, 4), (4, 2)])
+def test_ring_attention_zigzag_single_rank_hip_blocks(dev, causal, H, Hkv):
+    """parallel.context on one rank with the zigzag layout: two 128-token HIP flash blocks per
+    query chunk merged through their log-sum-exps, and the backward given the merged output/LSE —
+    vs the fp32 reference on the whole sequence."""
+    from nbdistributed_amd.parallel.context import ring_attention
+
+    g = torch.Generator(device="cpu").manual_seed(H * 7 + Hkv)
+    B, T = 2, 256
+    q, do = (torch.randn(B, H, T, 64, generator=g).to(dev, torch.bfloat16) for _ in range(2))
+    k, v = (torch.randn(B, Hkv, T, 64, generator=g).to(dev, torch.bfloat16) for _ in range(2))
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    rep = H // Hkv
+    ref = ref_attn(qr, kr.repeat_interleave(rep, 1), vr.repeat_interleave(rep, 1), causal, 0.125)
+    ref.backward(do.float())
+    qh, kh, vh = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
+    out = ring_attention(qh, kh, vh, causal=causal, scale=0.125, layout="zigzag")
+    out.backward(do)
+    assert _rel(out, ref) < 2e-2
+    assert _rel(qh.grad, qr.grad) < 3e-2
+    assert _rel(kh.grad, kr.grad) < 3e-2
+    assert _rel(vh.grad, vr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("last", [False, True])
+def test_attn_merge_kernel(dev, last):
+    """nbd::attn_merge_ (csrc/kernels/ring.hip) vs the fp32 log-sum-exp merge, on a strided bf16
+    block (the [B, T, H, D]-stored output of attn_fwd)."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    B, H, T = 2, 3, 256
+    acc = torch.randn(B, H, T, 64, generator=g).to(dev)
+    la = (torch.randn(B, H, T, generator=g) * 3).to(dev)
+    ob = torch.randn(B, T, H, 64, generator=g).to(dev, torch.bfloat16).transpose(1, 2)
+    lb = (torch.randn(B, H, T, generator=g) * 3).to(dev)
+    l_ref = torch.logaddexp(la, lb)
+    o_ref = acc * torch.exp(la - l_ref).unsqueeze(-1) + ob.float() * torch.exp(lb - l_ref).unsqueeze(-1)
+    out = torch.empty(B, H, T, 64, device=dev, dtype=torch.bfloat16) if last else None
+    acc0 = acc.clone()
+    torch.ops.nbd.attn_merge_(acc, la, ob, lb, out)
+    assert (la - l_ref).abs().max().item() < 1e-4
+    if last:
+        assert _rel(out, o_ref) < 1e-2
+        assert torch.equal(acc, acc0)
+    else:
+        assert _rel(acc, o_ref) < 1e-5

@@ -256,3 +256,42 @@ def test_split_sequential_balanced():
     assert sum(len(p) for p in parts) == len(m)
     assert all(len(p) == 2 for p in parts)
     assert len(split_sequential(m, 1, 0)) == len(m)
+
+
+def _ring_case(rank, n):
+    import torch.nn.functional as F
+
+    from nbdistributed_amd.parallel.context import gather_context, ring_attention, shard_context
+
+    torch.manual_seed(0)
+    B, H, Hkv, T, D = 2, 4, 2, 16, 8
+    q = torch.randn(B, H, T, D, requires_grad=True)
+    k = torch.randn(B, Hkv, T, D, requires_grad=True)
+    v = torch.randn(B, Hkv, T, D, requires_grad=True)
+    w = torch.randn(B, H, T, D)
+    for layout in ("contiguous", "zigzag"):
+        for causal in (True, False):
+            for t in (q, k, v):
+                t.grad = None
+            ref = F.scaled_dot_product_attention(q, k, v, is_causal=causal, enable_gqa=True)
+            (ref * w).sum().backward()
+            sh = lambda t: shard_context(t, dim=2, layout=layout)  # noqa: E731
+            ql, kl, vl = (sh(t.detach()).clone().requires_grad_() for t in (q, k, v))
+            out = ring_attention(ql, kl, vl, causal=causal, layout=layout)
+            _close(out, sh(ref.detach()), 1e-5)
+            (out * sh(w)).sum().backward()
+            _close(ql.grad, sh(q.grad), 1e-5)
+            _close(kl.grad, sh(k.grad), 1e-5)
+            _close(vl.grad, sh(v.grad), 1e-5)
+            _close(gather_context(out, dim=2, layout=layout), ref.detach(), 1e-5)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_ring_attention(n):
+    """parallel.context: ring attention (contiguous and zigzag layouts, causal and full, GQA) —
+    outputs and q/k/v gradients = attention on the gathered sequence."""
+    _spawn(_ring_case, n)
+
+
+def test_ring_attention_single_process():
+    _ring_case(0, 1)
