@@ -157,7 +157,8 @@ class GPT2(nn.Module):
         """Returns (logits, loss).  With ``targets`` and ``return_logits=False`` the logits are
         not returned (None) and the fused loss writes its gradient over their storage."""
         B, T = idx.shape
-        pos = torch.arange(T, device=idx.device)
+        pos_fn = getattr(self, "position_ids", None)  # set by parallel.context (global positions)
+        pos = pos_fn(T, idx.device) if pos_fn is not None else torch.arange(T, device=idx.device)
         if self._fast_ok(idx):
             from .. import ops
 

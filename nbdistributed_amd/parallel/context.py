@@ -279,4 +279,47 @@ def ring_attention(q, k, v, causal: bool = True, scale: Optional[float] = None, 
     return _RingAttention.apply(q, k, v, bool(causal), sc, group, layout)
 
 
-__all__ = ["ring_attention", "shard_context", "gather_context"]
+def context_positions(t_local: int, group=None, layout: str = "contiguous", device=None):
+    """Global token positions of this rank's ``t_local`` tokens under ``layout``."""
+    n, r = _size(group), _rank(group)
+    parts = 1 if layout == "contiguous" else 2
+    tc = t_local // parts
+    return torch.cat([torch.arange(c * tc, (c + 1) * tc, device=device) for c in _chunk_ids(r, n, layout)])
+
+
+class CPCausalSelfAttention(torch.nn.Module):
+    """GPT-2 attention over a context-parallel group: this rank's tokens' packed q|k|v projection,
+    ring attention across the group, output projection — the wrapped module's own parameters."""
+
+    def __init__(self, attn, group=None, layout: str = "contiguous"):
+        super().__init__()
+        self.c_attn, self.c_proj, self.n_head = attn.c_attn, attn.c_proj, attn.n_head
+        self.hip_gemm = getattr(attn, "hip_gemm", False)
+        self.group, self.layout = group, layout
+
+    def forward(self, x, fast: bool = False):
+        from .. import ops
+
+        B, T, C = x.shape
+        lin = ops.gemm_linear if (fast and self.hip_gemm) else ops.linear
+        qkv = lin(x, self.c_attn.weight, self.c_attn.bias)
+        H, D = self.n_head, C // self.n_head
+        q, k, v = (t.view(B, T, H, D).transpose(1, 2) for t in qkv.split(C, dim=2))
+        y = ring_attention(q, k, v, causal=True, group=self.group, layout=self.layout)
+        return lin(y.transpose(1, 2).reshape(B, T, C), self.c_proj.weight, self.c_proj.bias)
+
+
+def parallelize_gpt2_context(model, group=None, layout: str = "contiguous"):
+    """Context parallelism for a (replicated) ``models.GPT2`` in place: every rank feeds its
+    :func:`shard_context` part of each sequence (``idx``/``targets`` [B, T/n]); positions are the
+    global ones, attention is :func:`ring_attention` over ``group``.  Each rank's loss is the mean
+    over its tokens, so averaging losses and gradients over ``group`` (e.g. DDP over a group that
+    contains it) gives exactly the full-sequence loss and gradients.  Returns the model."""
+    for blk in model.h:
+        blk.attn = CPCausalSelfAttention(blk.attn, group, layout)
+    model.position_ids = lambda T, device: context_positions(T, group, layout, device)
+    return model
+
+
+__all__ = ["ring_attention", "shard_context", "gather_context", "context_positions", "CPCausalSelfAttention",
+           "parallelize_gpt2_context"]

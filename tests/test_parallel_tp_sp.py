@@ -295,3 +295,36 @@ def test_ring_attention(n):
 
 def test_ring_attention_single_process():
     _ring_case(0, 1)
+
+
+def _cp_gpt2_case(rank, n):
+    from nbdistributed_amd.models import GPT2, GPT2Config
+    from nbdistributed_amd.parallel.context import parallelize_gpt2_context, shard_context
+
+    for layout in ("contiguous", "zigzag"):
+        torch.manual_seed(0)
+        c = GPT2Config(vocab_size=128, n_positions=32, n_embd=32, n_layer=2, n_head=4)
+        ref = GPT2(c)
+        cp = GPT2(c)
+        cp.load_state_dict(ref.state_dict())
+        parallelize_gpt2_context(cp, layout=layout)
+        idx = torch.randint(0, 128, (2, 32), generator=torch.Generator().manual_seed(1))
+        tgt = torch.randint(0, 128, (2, 32), generator=torch.Generator().manual_seed(2))
+        _, loss_ref = ref(idx, tgt)
+        loss_ref.backward()
+        _, loss = cp(shard_context(idx, dim=1, layout=layout), shard_context(tgt, dim=1, layout=layout))
+        loss.backward()
+        tot = loss.detach().clone()
+        dist.all_reduce(tot)
+        _close(tot / n, loss_ref.detach(), 1e-5)
+        for (name, p), (_, pr) in zip(cp.named_parameters(), ref.named_parameters()):
+            g = p.grad.clone()
+            dist.all_reduce(g)
+            _close(g / n, pr.grad, 1e-4)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_context_parallel_gpt2(n):
+    """parallel.context.parallelize_gpt2_context: every rank trains on its shard of each sequence
+    (global positions, ring attention); averaged losses and gradients = the unsplit model's."""
+    _spawn(_cp_gpt2_case, n)
