@@ -168,22 +168,24 @@ class _Ring:
         self.prv = _global(group, (self.r - 1) % self.n)
         self.stage = dist.is_initialized() and dist.get_backend(group) == "gloo"
 
-    def start(self, send: torch.Tensor):
-        """Post the exchange; returns a handle for :meth:`finish` (the received tensor)."""
-        dev = send.device
+    def start(self, *send: torch.Tensor):
+        """Post the exchange of every tensor in ``send``; returns a handle for :meth:`finish`."""
+        dev = send[0].device
         if self.stage and dev.type != "cpu":
-            send = send.cpu()
-        recv = torch.empty_like(send)
-        reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, send, self.nxt, self.group),
-                                       dist.P2POp(dist.irecv, recv, self.prv, self.group)])
-        return reqs, recv, dev, send
+            send = tuple(t.cpu() for t in send)
+        recv = tuple(torch.empty_like(t) for t in send)
+        ops = []
+        for a, b in zip(send, recv):
+            ops += [dist.P2POp(dist.isend, a, self.nxt, self.group), dist.P2POp(dist.irecv, b, self.prv, self.group)]
+        return dist.batch_isend_irecv(ops), recv, dev, send
 
     @staticmethod
-    def finish(handle) -> torch.Tensor:
+    def finish(handle):
+        """The received tensors (a tuple, in the order sent), on the sender's device."""
         reqs, recv, dev, _send = handle
         for w in reqs:
             w.wait()
-        return recv.to(dev, non_blocking=True) if recv.device != dev else recv
+        return tuple(t.to(dev, non_blocking=True) if t.device != dev else t for t in recv)
 
 
 def _blocks(r_q: int, r_kv: int, n: int, layout: str):
@@ -212,10 +214,10 @@ class _RingAttention(torch.autograd.Function):
         out = torch.empty(q.shape, dtype=q.dtype, device=q.device)
         outs = out.chunk(parts, dim=2)
         o_acc, lse_acc = [None] * parts, [None] * parts
-        kv = torch.stack([k, v])
+        kc, vc = (k.contiguous(), v.contiguous()) if n > 1 else (k, v)  # only sent tensors need packing
         for s in range(n):
-            h = ring.start(kv) if s < n - 1 else None
-            ks, vs = kv[0].chunk(parts, dim=2), kv[1].chunk(parts, dim=2)
+            h = ring.start(kc, vc) if s < n - 1 else None
+            ks, vs = kc.chunk(parts, dim=2), vc.chunk(parts, dim=2)
             for iq, ik, diag in sched[s]:
                 o_b, l_b = _blk_fwd(qs[iq], ks[ik], vs[ik], diag, scale)
                 left[iq] -= 1
@@ -228,7 +230,7 @@ class _RingAttention(torch.autograd.Function):
                 else:
                     _merge(o_acc[iq], lse_acc[iq], o_b, l_b, outs[iq] if left[iq] == 0 else None)
             if h is not None:
-                kv = ring.finish(h)
+                kc, vc = ring.finish(h)
         ctx.save_for_backward(q, k, v, out, *lse_acc)
         ctx.causal, ctx.scale, ctx.group, ctx.layout = causal, scale, group, layout
         return out
@@ -242,27 +244,32 @@ class _RingAttention(torch.autograd.Function):
         parts = 1 if layout == "contiguous" else 2
         do = do.contiguous()
         qs, os_, dos = (t.chunk(parts, dim=2) for t in (q, o, do))
-        dq = [torch.zeros(c.shape, dtype=torch.float32, device=q.device) for c in qs]
-        kv = torch.stack([k, v])
-        dkv = torch.zeros(kv.shape, dtype=torch.float32, device=q.device)
+        dq = [None] * parts
+        kc, vc = (k.contiguous(), v.contiguous()) if n > 1 else (k, v)  # only sent tensors need packing
+        dk = torch.zeros(k.shape, dtype=torch.float32, device=q.device)
+        dv = torch.zeros(v.shape, dtype=torch.float32, device=q.device)
         for s in range(n):
-            h = ring.start(kv) if s < n - 1 else None
+            h = ring.start(kc, vc) if s < n - 1 else None
             src = (r - s) % n
-            ks, vs = kv[0].chunk(parts, dim=2), kv[1].chunk(parts, dim=2)
-            dks, dvs = dkv[0].chunk(parts, dim=2), dkv[1].chunk(parts, dim=2)
+            ks, vs = kc.chunk(parts, dim=2), vc.chunk(parts, dim=2)
+            dks, dvs = dk.chunk(parts, dim=2), dv.chunk(parts, dim=2)
             blocks = (_blocks(r, src, n, layout) if causal
                       else [(iq, ik, False) for iq in range(parts) for ik in range(parts)])
             for iq, ik, diag in blocks:
                 dq_b, dk_b, dv_b = _blk_bwd(dos[iq], qs[iq], ks[ik], vs[ik], os_[iq], ls[iq], diag, scale)
-                dq[iq].add_(dq_b)
+                if dq[iq] is None:
+                    dq[iq] = dq_b.to(torch.float32, memory_format=torch.contiguous_format)
+                else:
+                    dq[iq].add_(dq_b)
                 dks[ik].add_(dk_b)
                 dvs[ik].add_(dv_b)
-            # the dK/dV accumulator follows its K/V block (one extra hop home after the last step)
-            dkv = ring.finish(ring.start(dkv)) if n > 1 else dkv
+            # the dK/dV accumulators follow their K/V block (one extra hop home after the last step)
+            if n > 1:
+                dk, dv = ring.finish(ring.start(dk, dv))
             if h is not None:
-                kv = ring.finish(h)
+                kc, vc = ring.finish(h)
         dq = torch.cat(dq, dim=2).to(q.dtype)
-        return dq, dkv[0].to(k.dtype), dkv[1].to(v.dtype), None, None, None, None
+        return dq, dk.to(k.dtype), dv.to(v.dtype), None, None, None, None
 
 
 def ring_attention(q, k, v, causal: bool = True, scale: Optional[float] = None, group=None,
