@@ -328,5 +328,59 @@ def parallelize_gpt2_context(model, group=None, layout: str = "contiguous"):
     return model
 
 
+class CPLlamaAttention(torch.nn.Module):
+    """Llama attention over a context-parallel group: fused q|k|v projection, RoPE at this rank's
+    global positions (``nbd::rope_`` in place on the projection — the fused-in-attention rotation
+    assumes q and k share positions, which ring blocks do not), grouped-query ring attention,
+    output projection; the wrapped module's own parameters."""
+
+    def __init__(self, attn, group=None, layout: str = "contiguous"):
+        super().__init__()
+        self.qkv_proj, self.o_proj = attn.qkv_proj, attn.o_proj
+        self.H, self.Hkv, self.D = attn.H, attn.Hkv, attn.D
+        self.group, self.layout = group, layout
+
+    def forward(self, x, cos, sin):
+        from .. import ops
+
+        B, T, _ = x.shape
+        H, Hkv, D = self.H, self.Hkv, self.D
+        qkv = ops.gemm_linear(x, self.qkv_proj.weight)
+        if qkv._base is not None:  # the GEMM's output is a view of its autograd output: no in-place on it
+            qkv = qkv.clone()
+        qkv = ops.rope_(qkv, cos, sin, H + Hkv, D)
+        q = qkv[:, :, : H * D].view(B, T, H, D).transpose(1, 2)
+        k = qkv[:, :, H * D:(H + Hkv) * D].view(B, T, Hkv, D).transpose(1, 2)
+        v = qkv[:, :, (H + Hkv) * D:].view(B, T, Hkv, D).transpose(1, 2)
+        y = ring_attention(q, k, v, causal=True, group=self.group, layout=self.layout)
+        return ops.gemm_linear(y.transpose(1, 2).reshape(B, T, H * D), self.o_proj.weight)
+
+
+def parallelize_llama_context(model, group=None, layout: str = "contiguous"):
+    """Context parallelism for a native ``models.llama`` model (``LlamaModel`` or a wrapper with
+    ``.model``) in place: every rank feeds its :func:`shard_context` part of each sequence; RoPE
+    tables are taken at the rank's global positions and attention is :func:`ring_attention` over
+    ``group``.  Returns the model."""
+    from .. import ops
+
+    base = model.model if hasattr(model, "model") else model
+    c = base.config
+    cache = {}
+
+    def rope(T, device):
+        key = (str(device), T)
+        if key not in cache:
+            n = _size(group)
+            cos, sin = ops.rope_tables(T * n, c.head_dim, c.rope_theta, device)
+            pos = context_positions(T, group, layout, device)
+            cache[key] = (cos[pos].contiguous(), sin[pos].contiguous())
+        return cache[key]
+
+    base.rope = rope
+    for layer in base.layers:
+        layer.self_attn = CPLlamaAttention(layer.self_attn, group, layout)
+    return model
+
+
 __all__ = ["ring_attention", "shard_context", "gather_context", "context_positions", "CPCausalSelfAttention",
-           "parallelize_gpt2_context"]
+           "parallelize_gpt2_context", "CPLlamaAttention", "parallelize_llama_context"]

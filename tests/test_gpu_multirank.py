@@ -251,3 +251,35 @@ def test_context_parallel_gpt2_hip_path_two_ranks(sess):
     r = sess.execute(CP_GPT2, render=False)
     for rank in (0, 1):
         assert r.results[rank]["echo"] == "(True, True)", r.results[rank]
+
+
+CP_LLAMA = """
+from nbdistributed_amd.models.llama import LlamaConfig, LlamaModel
+from nbdistributed_amd.parallel.context import parallelize_llama_context, shard_context
+torch.manual_seed(5)
+c = LlamaConfig.tiny()
+ref = LlamaModel(c).to(device, torch.bfloat16)
+cp = LlamaModel(c).to(device, torch.bfloat16)
+cp.load_state_dict(ref.state_dict())
+parallelize_llama_context(cp, layout="zigzag")
+g = torch.Generator().manual_seed(6)
+ids = torch.randint(0, 512, (2, 512), generator=g).to(device)
+w = torch.randn(2, 512, 256, generator=g).to(device, torch.bfloat16)
+h_ref = ref(ids)
+(h_ref.float() * w.float()).sum().backward()
+h = cp(shard_context(ids, dim=1, layout="zigzag"))
+(h.float() * shard_context(w, dim=1, layout="zigzag").float()).sum().backward()
+hs = shard_context(h_ref.detach(), dim=1, layout="zigzag")
+gq = cp.layers[0].self_attn.qkv_proj.weight.grad.float().clone(); dist.all_reduce(gq)
+gr = ref.layers[0].self_attn.qkv_proj.weight.grad.float()
+(((h.float() - hs.float()).abs().max() / hs.float().abs().max()).item() < 3e-2,
+ ((gq - gr).abs().max() / gr.abs().max()).item() < 5e-2)
+"""
+
+
+def test_context_parallel_llama_hip_path_two_ranks(sess):
+    """parallel.context: bf16 native Llama (GQA, RoPE at global positions by nbd::rope_) with each
+    512-token sequence zigzag-split over 2 ranks = the unsplit model (hidden states, qkv grad)."""
+    r = sess.execute(CP_LLAMA, render=False)
+    for rank in (0, 1):
+        assert r.results[rank]["echo"] == "(True, True)", r.results[rank]

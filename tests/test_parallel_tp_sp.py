@@ -328,3 +328,35 @@ def test_context_parallel_gpt2(n):
     """parallel.context.parallelize_gpt2_context: every rank trains on its shard of each sequence
     (global positions, ring attention); averaged losses and gradients = the unsplit model's."""
     _spawn(_cp_gpt2_case, n)
+
+
+def _cp_llama_case(rank, n):
+    from nbdistributed_amd.models.llama import LlamaConfig, LlamaModel
+    from nbdistributed_amd.parallel.context import parallelize_llama_context, shard_context
+
+    for layout in ("contiguous", "zigzag"):
+        torch.manual_seed(0)
+        c = LlamaConfig.tiny(vocab_size=64, hidden_size=64, intermediate_size=128, num_attention_heads=4,
+                             num_key_value_heads=2)
+        ref = LlamaModel(c)
+        cp = LlamaModel(c)
+        cp.load_state_dict(ref.state_dict())
+        parallelize_llama_context(cp, layout=layout)
+        ids = torch.randint(0, 64, (2, 32), generator=torch.Generator().manual_seed(1))
+        w = torch.randn(2, 32, 64, generator=torch.Generator().manual_seed(2))
+        h_ref = ref(ids)
+        (h_ref * w).sum().backward()
+        h = cp(shard_context(ids, dim=1, layout=layout))
+        _close(h, shard_context(h_ref.detach(), dim=1, layout=layout), 1e-4)
+        (h * shard_context(w, dim=1, layout=layout)).sum().backward()
+        for (name, p), (_, pr) in zip(cp.named_parameters(), ref.named_parameters()):
+            g = p.grad.clone()
+            dist.all_reduce(g)
+            _close(g, pr.grad, 1e-4)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_context_parallel_llama(n):
+    """parallel.context.parallelize_llama_context: RoPE at global positions + GQA ring attention;
+    hidden states = the shard of the unsplit model's, summed gradients = its gradients."""
+    _spawn(_cp_llama_case, n)
