@@ -12,7 +12,8 @@ fit one GPU even after head sharding or whose head count is smaller than the gro
   block's log-sum-exp; blocks are merged exactly with the usual LSE rescaling (fp32 accumulator);
 * backward replays the ring: ``nbd::attn_bwd`` is given the *merged* output and LSE, so each
   block's dQ/dK/dV is the exact slice of the full gradient; dQ accumulates locally and dK/dV
-  accumulators travel with their K/V block and take one extra hop home at the end.
+  accumulators travel with their K/V block (their transfer overlaps the next step's attention
+  backward) and take one extra hop home at the end.
 
 Causal load balance: with the contiguous layout rank r only needs kv chunks ≤ r (rank n-1 does n
 blocks, rank 0 one).  ``layout="zigzag"`` splits the sequence into 2n chunks and gives rank r chunks
@@ -248,26 +249,35 @@ class _RingAttention(torch.autograd.Function):
         kc, vc = (k.contiguous(), v.contiguous()) if n > 1 else (k, v)  # only sent tensors need packing
         dk = torch.zeros(k.shape, dtype=torch.float32, device=q.device)
         dv = torch.zeros(v.shape, dtype=torch.float32, device=q.device)
+        pending = None  # the dK/dV accumulators in flight from the previous step
         for s in range(n):
             h = ring.start(kc, vc) if s < n - 1 else None
             src = (r - s) % n
             ks, vs = kc.chunk(parts, dim=2), vc.chunk(parts, dim=2)
-            dks, dvs = dk.chunk(parts, dim=2), dv.chunk(parts, dim=2)
             blocks = (_blocks(r, src, n, layout) if causal
                       else [(iq, ik, False) for iq in range(parts) for ik in range(parts)])
+            contrib = []
             for iq, ik, diag in blocks:
                 dq_b, dk_b, dv_b = _blk_bwd(dos[iq], qs[iq], ks[ik], vs[ik], os_[iq], ls[iq], diag, scale)
                 if dq[iq] is None:
                     dq[iq] = dq_b.to(torch.float32, memory_format=torch.contiguous_format)
                 else:
                     dq[iq].add_(dq_b)
+                contrib.append((ik, dk_b, dv_b))
+            # the accumulators of this step's K/V block arrive while its attention backward ran
+            if pending is not None:
+                dk, dv = ring.finish(pending)
+            dks, dvs = dk.chunk(parts, dim=2), dv.chunk(parts, dim=2)
+            for ik, dk_b, dv_b in contrib:
                 dks[ik].add_(dk_b)
                 dvs[ik].add_(dv_b)
-            # the dK/dV accumulators follow their K/V block (one extra hop home after the last step)
+            # ... and follow it to the next rank (after the last step: one extra hop home)
             if n > 1:
-                dk, dv = ring.finish(ring.start(dk, dv))
+                pending = ring.start(dk, dv)
             if h is not None:
                 kc, vc = ring.finish(h)
+        if pending is not None:
+            dk, dv = ring.finish(pending)
         dq = torch.cat(dq, dim=2).to(q.dtype)
         return dq, dk.to(k.dtype), dv.to(v.dtype), None, None, None, None
 
