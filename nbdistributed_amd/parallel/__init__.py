@@ -6,7 +6,7 @@ from .backend import abort_process_group, init_data_plane, rccl_version, registe
 
 __all__ = ["abort_process_group", "init_data_plane", "rccl_version", "register_rccl_backend", "resolve_backend",
            "DistributedDataParallel", "bf16_compress_hook", "allreduce_hook", "broadcast_params", "broadcast_tensors",
-           "tensor", "sequence", "expert", "pipeline", "pipeline_step", "MoE", "parallelize_gpt2", "ColumnParallelLinear", "RowParallelLinear", "ulysses_attention", "context", "ring_attention"]
+           "tensor", "sequence", "expert", "pipeline", "pipeline_step", "MoE", "parallelize_gpt2", "ColumnParallelLinear", "RowParallelLinear", "ulysses_attention", "context", "ring_attention", "mesh", "ParallelMesh"]
 
 
 def __getattr__(name):
@@ -15,7 +15,7 @@ def __getattr__(name):
         from . import ddp
 
         return getattr(ddp, name)
-    if name in ("tensor", "sequence", "expert", "pipeline", "context"):
+    if name in ("tensor", "sequence", "expert", "pipeline", "context", "mesh"):
         import importlib
 
         return importlib.import_module(f".{name}", __name__)
@@ -35,6 +35,10 @@ def __getattr__(name):
         from . import sequence
 
         return sequence.ulysses_attention
+    if name == "ParallelMesh":
+        from . import mesh
+
+        return mesh.ParallelMesh
     if name == "ring_attention":
         from . import context
 

@@ -360,3 +360,38 @@ def test_context_parallel_llama(n):
     """parallel.context.parallelize_llama_context: RoPE at global positions + GQA ring attention;
     hidden states = the shard of the unsplit model's, summed gradients = its gradients."""
     _spawn(_cp_llama_case, n)
+
+
+def _mesh_dp_cp_case(rank, n):
+    from nbdistributed_amd.models import GPT2, GPT2Config
+    from nbdistributed_amd.parallel import ParallelMesh
+    from nbdistributed_amd.parallel.context import parallelize_gpt2_context, shard_context
+
+    mesh = ParallelMesh(dp=2, cp=2)
+    assert mesh.members("cp") == [2 * (rank // 2), 2 * (rank // 2) + 1]
+    assert mesh.members("dp") == [rank % 2, rank % 2 + 2]
+    assert mesh.coord("cp") == rank % 2 and mesh.coord("dp") == rank // 2
+    torch.manual_seed(0)
+    c = GPT2Config(vocab_size=128, n_positions=32, n_embd=32, n_layer=2, n_head=4)
+    ref = GPT2(c)
+    cp = GPT2(c)
+    cp.load_state_dict(ref.state_dict())
+    parallelize_gpt2_context(cp, group=mesh.group("cp"), layout="zigzag")
+    idx = torch.randint(0, 128, (4, 32), generator=torch.Generator().manual_seed(1))
+    tgt = torch.randint(0, 128, (4, 32), generator=torch.Generator().manual_seed(2))
+    _, loss_ref = ref(idx, tgt)  # the global batch, full sequences
+    loss_ref.backward()
+    d = mesh.coord("dp")
+    mine = lambda t: shard_context(t[2 * d:2 * d + 2], group=mesh.group("cp"), dim=1, layout="zigzag")  # noqa: E731
+    _, loss = cp(mine(idx), mine(tgt))
+    loss.backward()
+    for (_, p), (_, pr) in zip(cp.named_parameters(), ref.named_parameters()):
+        g = p.grad.clone()
+        dist.all_reduce(g)  # DP x CP: average over all four ranks
+        _close(g / 4, pr.grad, 1e-4)
+
+
+def test_mesh_dp_x_cp_gpt2():
+    """parallel.mesh.ParallelMesh(dp=2, cp=2) on 4 ranks: group membership, and GPT-2 with the batch
+    split over dp and each sequence ring-attended over cp = the single-process model's gradients."""
+    _spawn(_mesh_dp_cp_case, 4)
