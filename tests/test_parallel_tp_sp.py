@@ -395,3 +395,14 @@ def test_mesh_dp_x_cp_gpt2():
     """parallel.mesh.ParallelMesh(dp=2, cp=2) on 4 ranks: group membership, and GPT-2 with the batch
     split over dp and each sequence ring-attended over cp = the single-process model's gradients."""
     _spawn(_mesh_dp_cp_case, 4)
+
+
+def test_mesh_single_process_and_shape_check():
+    from nbdistributed_amd.parallel import ParallelMesh
+
+    m = ParallelMesh(dp=1, tp=1)
+    assert m.coord("dp") == 0 and m.size("tp") == 1 and m.members("tp") == [0]
+    with pytest.raises(ValueError):
+        ParallelMesh(dp=3)
+    with pytest.raises(ValueError):
+        ParallelMesh()
