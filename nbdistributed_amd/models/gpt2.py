@@ -157,6 +157,7 @@ class GPT2(nn.Module):
         """Returns (logits, loss).  With ``targets`` and ``return_logits=False`` the logits are
         not returned (None) and the fused loss writes its gradient over their storage."""
         B, T = idx.shape
+        cp = getattr(self, "context_group", None)  # set by parallel.context: (group,)
         pos_fn = getattr(self, "position_ids", None)  # set by parallel.context (global positions)
         pos = pos_fn(T, idx.device) if pos_fn is not None else torch.arange(T, device=idx.device)
         if self._fast_ok(idx):
@@ -180,7 +181,9 @@ class GPT2(nn.Module):
                 x, h = ops.add_layer_norm(x, blk.mlp(h, fast=True), nxt.weight, nxt.bias, nxt.eps)
             if targets is not None and not return_logits and c.fused_ce and ops.loss.FUSED_XENT:
                 # LM head + loss: one pass over the logits for the loss forward and backward
-                return None, ops.linear_cross_entropy(h, self.lm_head.weight, targets)
+                red = "sum" if cp is not None else "mean"
+                return None, self._cp_loss(ops.linear_cross_entropy(h, self.lm_head.weight, targets, reduction=red),
+                                           targets, cp)
             logits = self.lm_head(h)
         else:
             for blk in self.h:
@@ -189,10 +192,22 @@ class GPT2(nn.Module):
         loss = None
         if targets is not None:
             flat, tgt = logits.view(-1, logits.size(-1)), targets.reshape(-1)
+            red = "sum" if cp is not None else "mean"
             if self.config.fused_ce and logits.is_cuda:
                 from .. import ops
 
-                loss = ops.cross_entropy(flat, tgt, inplace_backward=not return_logits)
+                loss = ops.cross_entropy(flat, tgt, reduction=red, inplace_backward=not return_logits)
             else:
-                loss = F.cross_entropy(flat.float(), tgt)
+                loss = F.cross_entropy(flat.float(), tgt, reduction=red)
+            loss = self._cp_loss(loss, targets, cp)
         return (logits if return_logits or targets is None else None), loss
+
+    @staticmethod
+    def _cp_loss(loss, targets, cp):
+        """Context parallelism (``parallel.context.parallelize_gpt2_context``): ``loss`` is this
+        rank's sum; return its share of the group-wide token mean (``context_loss``)."""
+        if cp is None:
+            return loss
+        from ..parallel.context import context_loss
+
+        return context_loss(loss, (targets != -100).sum(), cp[0])

@@ -201,15 +201,26 @@ class LlamaForCausalLM(_LlamaPreTrained):
             self.lm_head.weight = self.model.embed_tokens.weight
 
     def forward(self, input_ids, labels=None, return_logits: bool = True):
+        """Next-token loss of ``labels`` (shifted here: ``logits[:, t]`` predicts ``labels[:, t+1]``).
+        Under context parallelism (``parallel.context.parallelize_llama_context``) the shard's
+        ``labels`` must come already shifted on the full sequence (``context.shift_labels``) and
+        the loss is this rank's ``context_loss`` share of the group-wide token mean."""
         h = self.model(input_ids)
         logits = self.lm_head(h)
         loss = None
-        if labels is not None:  # next-token prediction
+        if labels is not None:
             V = logits.shape[-1]
-            shift = logits[:, :-1].reshape(-1, V)
-            tgt = labels[:, 1:].reshape(-1)
-            loss = (ops.cross_entropy(shift, tgt) if logits.is_cuda
-                    else F.cross_entropy(shift.float(), tgt, ignore_index=-100))
+            cp = getattr(self, "context_group", None)
+            if cp is None:  # next-token prediction
+                shift, tgt, red = logits[:, :-1].reshape(-1, V), labels[:, 1:].reshape(-1), "mean"
+            else:  # pre-shifted targets, one per position of the shard
+                shift, tgt, red = logits.reshape(-1, V), labels.reshape(-1), "sum"
+            loss = (ops.cross_entropy(shift, tgt, reduction=red) if logits.is_cuda
+                    else F.cross_entropy(shift.float(), tgt, ignore_index=-100, reduction=red))
+            if cp is not None:
+                from ..parallel.context import context_loss
+
+                loss = context_loss(loss, (tgt != -100).sum(), cp[0])
         return loss, (logits if return_logits else None)
 
 

@@ -296,6 +296,33 @@ def ring_attention(q, k, v, causal: bool = True, scale: Optional[float] = None, 
     return _RingAttention.apply(q, k, v, bool(causal), sc, group, layout)
 
 
+def shift_labels(labels, ignore_index: int = -100):
+    """Next-token targets aligned with the input positions (``out[:, t] = labels[:, t + 1]``, the
+    last position ``ignore_index``).  A causal-LM loss under context parallelism must take its
+    targets in this form, shifted on the *full* sequence before :func:`shard_context`: shifting
+    inside a shard would pair the last token of a chunk with the first token of whatever chunk
+    the layout puts next (zigzag: chunk 2n-1-r), and drop every chunk boundary's real target."""
+    out = torch.full_like(labels, ignore_index)
+    out[:, :-1] = labels[:, 1:]
+    return out
+
+
+def context_loss(loss_sum, n_valid, group=None):
+    """This rank's share of the group-wide token mean: ``loss_sum · n / Σ_group n_valid``.
+
+    ``loss_sum`` is the sum of this rank's per-token losses and ``n_valid`` its count of counted
+    (non-``ignore_index``) targets.  Averaging the returned values — and their gradients, as DDP
+    over a group containing the CP group does — over the group gives the mean over every counted
+    token of the full sequences, however the ignored targets are spread over the shards (a plain
+    average of per-shard means is biased as soon as the shards count different numbers of
+    tokens).  The count is all-reduced without autograd; all ranks of ``group`` must call this."""
+    n = _size(group)
+    cnt = n_valid.detach().to(torch.float32).reshape(1).clone()
+    if n > 1:
+        dist.all_reduce(cnt, group=group)
+    return loss_sum * (n / cnt[0])
+
+
 def context_positions(t_local: int, group=None, layout: str = "contiguous", device=None):
     """Global token positions of this rank's ``t_local`` tokens under ``layout``."""
     n, r = _size(group), _rank(group)
@@ -328,13 +355,21 @@ class CPCausalSelfAttention(torch.nn.Module):
 
 def parallelize_gpt2_context(model, group=None, layout: str = "contiguous"):
     """Context parallelism for a (replicated) ``models.GPT2`` in place: every rank feeds its
-    :func:`shard_context` part of each sequence (``idx``/``targets`` [B, T/n]); positions are the
-    global ones, attention is :func:`ring_attention` over ``group``.  Each rank's loss is the mean
-    over its tokens, so averaging losses and gradients over ``group`` (e.g. DDP over a group that
-    contains it) gives exactly the full-sequence loss and gradients.  Returns the model."""
+    :func:`shard_context` part of each sequence (``idx``/``targets`` [B, T/n]; GPT-2's targets are
+    already the next tokens, aligned with ``idx``); positions are the global ones, attention is
+    :func:`ring_attention` over ``group``.  Each rank's loss is its :func:`context_loss` share, so
+    averaging losses and gradients over ``group`` (e.g. DDP over a group that contains it) gives
+    exactly the full-sequence loss and gradients, ignored targets included.  Attention dropout is
+    not implemented in the ring blocks: a model with ``config.dropout > 0`` is refused rather than
+    silently trained without it.  Returns the model."""
+    p = float(getattr(getattr(model, "config", None), "dropout", 0.0) or 0.0)
+    if p > 0.0:
+        raise ValueError(f"parallelize_gpt2_context: dropout {p} is not supported by ring attention "
+                         "(set config.dropout = 0.0)")
     for blk in model.h:
         blk.attn = CPCausalSelfAttention(blk.attn, group, layout)
     model.position_ids = lambda T, device: context_positions(T, group, layout, device)
+    model.context_group = (group,)
     return model
 
 
@@ -367,13 +402,25 @@ class CPLlamaAttention(torch.nn.Module):
 
 
 def parallelize_llama_context(model, group=None, layout: str = "contiguous"):
-    """Context parallelism for a native ``models.llama`` model (``LlamaModel`` or a wrapper with
-    ``.model``) in place: every rank feeds its :func:`shard_context` part of each sequence; RoPE
-    tables are taken at the rank's global positions and attention is :func:`ring_attention` over
-    ``group``.  Returns the model."""
-    from .. import ops
+    """Context parallelism for a native ``models.llama`` ``LlamaModel`` or ``LlamaForCausalLM`` in
+    place: every rank feeds its :func:`shard_context` part of each sequence; RoPE tables are taken
+    at the rank's global positions and attention is :func:`ring_attention` over ``group``.
 
-    base = model.model if hasattr(model, "model") else model
+    ``LlamaForCausalLM`` then expects ``labels`` already shifted on the full sequence
+    (:func:`shift_labels`, then :func:`shard_context`) and returns its :func:`context_loss` share.
+    ``LlamaForSequenceClassification`` is refused: it pools the last non-pad token of the whole
+    sequence, which lives on one rank only.  Returns the model."""
+    from .. import ops
+    from ..models.llama import LlamaForCausalLM, LlamaModel
+
+    if isinstance(model, LlamaForCausalLM):
+        base = model.model
+        model.context_group = (group,)
+    elif isinstance(model, LlamaModel):
+        base = model
+    else:
+        raise TypeError(f"parallelize_llama_context: {type(model).__name__} is not supported (LlamaModel or "
+                        "LlamaForCausalLM; a sequence-classification head pools one token of the whole sequence)")
     c = base.config
     cache = {}
 
@@ -392,5 +439,6 @@ def parallelize_llama_context(model, group=None, layout: str = "contiguous"):
     return model
 
 
-__all__ = ["ring_attention", "shard_context", "gather_context", "context_positions", "CPCausalSelfAttention",
+__all__ = ["ring_attention", "shard_context", "gather_context", "context_positions", "shift_labels", "context_loss",
+           "CPCausalSelfAttention",
            "parallelize_gpt2_context", "CPLlamaAttention", "parallelize_llama_context"]

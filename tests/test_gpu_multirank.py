@@ -320,3 +320,37 @@ def test_context_parallel_ddp_training_two_ranks(sess):
     r = sess.execute("import math\n" + CP_DDP, render=False)
     for rank in (0, 1):
         assert r.results[rank]["echo"] == "(True, True, True)", r.results[rank]
+
+
+CP_LLAMA_LM = """
+from nbdistributed_amd.models.llama import LlamaConfig, LlamaForCausalLM
+from nbdistributed_amd.parallel.context import parallelize_llama_context, shard_context, shift_labels
+torch.manual_seed(5)
+c = LlamaConfig.tiny()
+ref = LlamaForCausalLM(c).to(device, torch.bfloat16)
+cp = LlamaForCausalLM(c).to(device, torch.bfloat16)
+cp.load_state_dict(ref.state_dict())
+parallelize_llama_context(cp, layout="zigzag")
+g = torch.Generator().manual_seed(6)
+ids = torch.randint(0, 512, (2, 512), generator=g)
+labels = ids.clone(); labels[0, :200] = -100
+ids, labels = ids.to(device), labels.to(device)
+lr_, _ = ref(ids, labels)
+lr_.backward()
+sh = lambda t: shard_context(t, dim=1, layout="zigzag")
+l, _ = cp(sh(ids), sh(shift_labels(labels)), return_logits=False)
+l.backward()
+tot = l.detach().float().clone(); dist.all_reduce(tot)
+gq = cp.model.layers[0].self_attn.qkv_proj.weight.grad.float().clone(); dist.all_reduce(gq)
+gr = ref.model.layers[0].self_attn.qkv_proj.weight.grad.float()
+(abs(tot.item() / 2 - lr_.item()) < 2e-2, ((gq / 2 - gr).abs().max() / gr.abs().max()).item() < 5e-2)
+"""
+
+
+def test_context_parallel_llama_causal_lm_hip_path_two_ranks(sess):
+    """parallel.context: bf16 LlamaForCausalLM, labels shifted on the full sequence and zigzag-
+    sharded over 2 ranks, 200 ignored prompt tokens (uneven per shard) — averaged loss and qkv
+    gradient = the unsplit model's (HIP cross-entropy with reduction='sum' + context_loss)."""
+    r = sess.execute(CP_LLAMA_LM, render=False)
+    for rank in (0, 1):
+        assert r.results[rank]["echo"] == "(True, True)", r.results[rank]

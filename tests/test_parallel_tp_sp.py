@@ -310,6 +310,8 @@ def _cp_gpt2_case(rank, n):
         parallelize_gpt2_context(cp, layout=layout)
         idx = torch.randint(0, 128, (2, 32), generator=torch.Generator().manual_seed(1))
         tgt = torch.randint(0, 128, (2, 32), generator=torch.Generator().manual_seed(2))
+        tgt[0, :11] = -100  # ignored targets spread unevenly over the shards
+        tgt[1, 27:] = -100
         _, loss_ref = ref(idx, tgt)
         loss_ref.backward()
         _, loss = cp(shard_context(idx, dim=1, layout=layout), shard_context(tgt, dim=1, layout=layout))
@@ -353,6 +355,57 @@ def _cp_llama_case(rank, n):
             g = p.grad.clone()
             dist.all_reduce(g)
             _close(g, pr.grad, 1e-4)
+
+
+def _cp_llama_causal_case(rank, n):
+    from nbdistributed_amd.models.llama import LlamaConfig, LlamaForCausalLM
+    from nbdistributed_amd.parallel.context import parallelize_llama_context, shard_context, shift_labels
+
+    for layout in ("contiguous", "zigzag"):
+        torch.manual_seed(0)
+        c = LlamaConfig.tiny(vocab_size=64, hidden_size=64, intermediate_size=128, num_attention_heads=4,
+                             num_key_value_heads=2)
+        ref = LlamaForCausalLM(c)
+        cp = LlamaForCausalLM(c)
+        cp.load_state_dict(ref.state_dict())
+        parallelize_llama_context(cp, layout=layout)
+        ids = torch.randint(0, 64, (2, 32), generator=torch.Generator().manual_seed(1))
+        labels = ids.clone()
+        labels[0, :13] = -100  # prompt tokens not trained on: uneven counts per shard
+        loss_ref, _ = ref(ids, labels)
+        loss_ref.backward()
+        sh = lambda t: shard_context(t, dim=1, layout=layout)  # noqa: E731
+        loss, _ = cp(sh(ids), sh(shift_labels(labels)))
+        loss.backward()
+        tot = loss.detach().clone()
+        dist.all_reduce(tot)
+        _close(tot / n, loss_ref.detach(), 1e-5)
+        for (name, p), (_, pr) in zip(cp.named_parameters(), ref.named_parameters()):
+            g = p.grad.clone()
+            dist.all_reduce(g)
+            _close(g / n, pr.grad, 1e-4)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_context_parallel_llama_causal_lm(n):
+    """parallel.context + LlamaForCausalLM: labels shifted on the full sequence before sharding
+    (the zigzag chunk boundaries keep their real next-token targets), loss normalised by the
+    group-wide token count — averaged loss and gradients = the unsplit model's, with unevenly
+    ignored targets."""
+    _spawn(_cp_llama_causal_case, n)
+
+
+def test_context_parallel_refuses_unsupported_models():
+    from nbdistributed_amd.models import GPT2, GPT2Config
+    from nbdistributed_amd.models.llama import LlamaConfig, LlamaForSequenceClassification
+    from nbdistributed_amd.parallel.context import parallelize_gpt2_context, parallelize_llama_context, shift_labels
+
+    with pytest.raises(TypeError):
+        parallelize_llama_context(LlamaForSequenceClassification(LlamaConfig.tiny(num_hidden_layers=1)))
+    with pytest.raises(ValueError):
+        parallelize_gpt2_context(GPT2(GPT2Config(vocab_size=64, n_positions=32, n_embd=32, n_layer=1, n_head=2,
+                                                 dropout=0.1)))
+    assert shift_labels(torch.tensor([[1, 2, 3]])).tolist() == [[2, 3, -100]]
 
 
 @pytest.mark.parametrize("n", [2, 4])
