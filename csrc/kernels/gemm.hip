@@ -43,67 +43,12 @@
 
 #include <type_traits>
 
-#include "nbd_common.h"
+#include "gemm_common.h"
 
 namespace nbd {
 namespace gemm {
 
-typedef short s8v __attribute__((ext_vector_type(8)));
-typedef short s4v __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s4v lds_s4v;
-typedef float f4 __attribute__((ext_vector_type(4)));
-
-constexpr int BK = 64;
 constexpr int NT = 256;
-
-// EPI_ROWSUM (weight-gradient layout): also Σ_k A[m,k] -> aux_out[m] — the Linear's bias gradient
-// (Σ over tokens of dy) from the A fragments already in registers, one extra MFMA per fragment.
-// EPI_SWIGLU (forward layout, B = [gate; up] weights [2I][K]): tile column block tn stages gate
-// rows tn·BN/2.. and up rows I + tn·BN/2.. side by side, so the epilogue has g and u of the same
-// feature: c = silu(g)·u [M][I], aux_out = [g|u] pre-activations [M][2I].
-// EPI_DSWIGLU (dgrad layout, C = dact [M][I] never stored): aux_in = [g|u] [M][2I];
-// c = d[g|u] [M][2I] = [dact·u·σ(g)(1 + g(1−σ(g))) | dact·silu(g)].
-enum Epi : int { EPI_NONE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_ROWSUM = 3, EPI_SWIGLU = 4, EPI_DSWIGLU = 5 };
-
-struct Args {
-  const uint16_t* a;
-  const uint16_t* b;
-  uint16_t* c;             // [M][ldc] bf16
-  float* ws;               // split-K: [splits][M][ldc] fp32 slabs
-  const uint16_t* bias;    // [N] or nullptr
-  const uint16_t* aux_in;  // EPI_DGELU: pre-activation [M][ldc]; EPI_DSWIGLU: [g|u] [M][2N]
-  uint16_t* aux_out;       // EPI_GELU: pre-activation out [M][ldc]; EPI_ROWSUM: row sums [M];
-                           // EPI_SWIGLU: [g|u] out [M][N]
-  int M, N, K;             // K = reduction length handled by one split
-  int64_t lda, ldb, ldc;
-  int tiles_m, tiles_n;
-};
-
-// ---- swizzles ---------------------------------------------------------------------------------
-__device__ __forceinline__ int row_swz(int r) { return (r >> 1) & 7; }  // 16-B chunk XOR, row image
-template <int R>
-__device__ __forceinline__ int tr_swz(int k) {  // 8-B slot XOR, tr image with R-element rows
-  if constexpr (R >= 128)
-    return ((k & 3) | (((k >> 3) & 1) << 2)) << 2;
-  else
-    return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 2;
-}
-
-// 16-B global -> LDS DMA (global_load_lds_dwordx4: lane l lands at lds_wave_base + 16 l).
-// Issued as inline asm on purpose: hipcc cannot prove that an in-flight DMA into one pipeline
-// buffer and the ds_reads of another do not alias, and drains vmcnt(0) before the reads — which
-// serialises a 3-stage pipeline.  Hidden from it, the DMA is counted by our own vmcnt(N) waits
-// (cdna_hip_programming.md §5.7 LDS-DMA recipe: M0 saved, written and restored in one statement).
-__device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* lds_wave_base) {
-  const uint32_t lds = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(lds_wave_base));
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lds)
-      : "memory");
-}
 
 // Stage one 64-deep K-tile of an operand into its LDS image.  R = tile rows (BM or BN).
 // TR = false: global [rows][k] (row r0.., k0..), image [R][64]; TR = true: global [k][rows], image [64][R].
@@ -129,42 +74,6 @@ __device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld
     }
     glds16(src, img + wbase);
   }
-}
-
-// 16x16x32 operand fragment (lane l: rows/cols r0 + (l&15), k = 32kk + 8(l>>4) + 0..7)
-template <int R, bool TR>
-__device__ __forceinline__ s8v frag(const uint8_t* img, int r0, int kk, int lane) {
-  if constexpr (!TR) {
-    const int r = r0 + (lane & 15), c = (lane >> 4) + 4 * kk;
-    return *reinterpret_cast<const s8v*>(img + r * 128 + ((c ^ row_swz(r)) << 4));
-  } else {
-    constexpr int RB = 2 * R;
-    const int i = lane & 15, g = lane >> 4;
-    const int k = 32 * kk + 8 * g + (i >> 2);
-    const int slot = ((r0 + 4 * (i & 3)) >> 2) ^ tr_swz<R>(k);
-    const uint8_t* p = img + k * RB + slot * 8;
-    const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p));
-    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p + 4 * RB));
-    s8v r;
-    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-    return r;
-  }
-}
-
-constexpr float kBeta = 0.7978845608028654f;  // sqrt(2/pi)
-constexpr float kKappa = 0.044715f;
-// tanh(u) = 2σ(2u) − 1 with σ from v_exp_f32 + one reciprocal (libm tanhf's branchy slow path
-// made the fused epilogue cost as much as a separate elementwise pass)
-__device__ __forceinline__ float sig2(float u) { return __fdividef(1.f, 1.f + __expf(-2.f * u)); }
-__device__ __forceinline__ float sigm(float x) { return __fdividef(1.f, 1.f + __expf(-x)); }
-__device__ __forceinline__ float gelu_tanh(float x) {  // 0.5x(1 + tanh u) = x·σ(2u)
-  return x * sig2(kBeta * (x + kKappa * x * x * x));
-}
-__device__ __forceinline__ float dgelu_tanh(float x) {  // d gelu / dx = s + 2x·s(1−s)·β(1 + 3κx²), s = σ(2u)
-  const float x2 = x * x;
-  const float s = sig2(kBeta * (x + kKappa * x2 * x));
-  return s + 2.f * x * s * (1.f - s) * kBeta * (1.f + 3.f * kKappa * x2);
 }
 
 template <int BM, int BN, int STAGES, int KS = 1>
@@ -213,19 +122,8 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
   const int wm = wave / WN, wn = wave % WN;
   uint8_t* smem = smem_all + kg * (STAGES * BUF);   // this group's pipeline buffers
 
-  // XCD-aware bijective remap, then 8-row groups sweeping the column tiles
-  const int nwg = p.tiles_m * p.tiles_n;
-  int bid = blockIdx.x;
-  {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
-  constexpr int G = 8;
-  const int per_group = G * p.tiles_n;
-  const int first_m = (bid / per_group) * G;
-  const int gsz = min(p.tiles_m - first_m, G);
-  const int local = bid % per_group;
-  const int tm = first_m + local % gsz, tn = local / gsz;
+  int tm, tn;
+  tile_coords<8>(p.tiles_m, p.tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   // split-K: grid.y selects the K range
@@ -689,7 +587,9 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
     ws = at::empty({(int64_t)S * M * N + (epi == EPI_ROWSUM ? (int64_t)S * M : 0)}, a.options().dtype(at::kFloat));
     p.ws = ws.data_ptr<float>();
   }
-  if (!a_km && !b_kn)
+  if (t.bm == 256)
+    launch_gemm256(p, a_km, b_kn, (int)epi, grid, st, t.stages - 2);
+  else if (!a_km && !b_kn)
     launch_layout<false, false>((int)epi, t, p, grid, st);
   else if (!a_km && b_kn)
     launch_layout<false, true>((int)epi, t, p, grid, st);
