@@ -90,6 +90,32 @@ __device__ __forceinline__ s8v frag(const uint8_t* img, int r0, int kk, int lane
   }
 }
 
+// Stage one 64-deep K-tile of an operand into its LDS image.  R = tile rows (BM or BN).
+// TR = false: global [rows][k] (row r0.., k0..), image [R][64]; TR = true: global [k][rows], image [64][R].
+// r1 = first global row of the tile's second half (r0 + R/2 for a contiguous tile; EPI_SWIGLU
+// gives the up rows there; row images only).
+template <int R, bool TR, int W>
+__device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld, int r0, int k0, uint8_t* img,
+                                      int wave, int lane, int r1 = -1) {
+  constexpr int PER_WAVE = R / (8 * W);  // (R*64*2 B) / (W waves * 1 KiB)
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int wbase = (i * W + wave) * 1024;
+    const int byte = wbase + lane * 16;
+    const uint16_t* src;
+    if constexpr (!TR) {
+      const int r = byte >> 7, pc = (byte >> 4) & 7;
+      const int row = (r1 >= 0 && r >= R / 2) ? r1 + r - R / 2 : r0 + r;
+      src = g + (int64_t)row * ld + k0 + 8 * (pc ^ row_swz(r));
+    } else {
+      constexpr int RB = 2 * R;
+      const int k = byte / RB, pc = (byte % RB) >> 4;
+      src = g + (int64_t)(k0 + k) * ld + r0 + 8 * (pc ^ (tr_swz<R>(k) >> 1));
+    }
+    glds16(src, img + wbase);
+  }
+}
+
 constexpr float kBeta = 0.7978845608028654f;  // sqrt(2/pi)
 constexpr float kKappa = 0.044715f;
 // tanh(u) = 2Ïƒ(2u) âˆ’ 1 with Ïƒ from v_exp_f32 + one reciprocal (libm tanhf's branchy slow path
@@ -109,9 +135,9 @@ __device__ __forceinline__ float dgelu_tanh(float x) {  // d gelu / dx = s + 2xÂ
 // bijective"), then groups of G tile rows sweeping the column tiles, so the workgroups sharing
 // an A row panel run on the same XCD's L2.
 template <int G>
-__device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, int& tn) {
+__device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, int& tn, int id = -1) {
   const int nwg = tiles_m * tiles_n;
-  int bid = blockIdx.x;
+  int bid = id < 0 ? (int)blockIdx.x : id;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);

@@ -68,15 +68,26 @@ def _ntiles(tile: int, M: int, N: int) -> int:
     return (M // bm) * (N // bn) if M % bm == 0 and N % bn == 0 else 0
 
 
-def config(a_km: bool, b_kn: bool, M: int, N: int, K: int, can_split: bool = True):
+# the 256x256 phase-interleaved kernel (gemm256.hip) with staggered wave groups: forward products
+# with >= 256 such tiles and K >= 1024 (1.29-1.32 PF vs 1.07-1.11 for the 128x128 kernel at
+# 4096^3 / 8192^3: docs/FINDINGS.md §10); its epilogues: none / bias / GELU
+G256 = 86256256
+G256_EPIS = (EPI_NONE, EPI_GELU)
+
+
+def config(a_km: bool, b_kn: bool, M: int, N: int, K: int, can_split: bool = True, epi: int = EPI_NONE):
     """(kernel, splits) for a product: the tuned entry when there is one, else a heuristic —
-    the largest tile with >= 1024 workgroups (128x128), else >= 256 (128x64 / 64x128), else
-    64x64; the 3-stage pipeline when there are < 512 workgroups (one per CU cannot hide a
-    drained pipeline); long-K products with < 400 workgroups split K (the largest tile needing
-    <= 8 splits, each >= 512 deep) — split-K (a second, reducing kernel) only without an epilogue."""
+    large forward products on the 256x256 kernel; else the largest tile with >= 1024 workgroups
+    (128x128), else >= 256 (128x64 / 64x128), else 64x64; the 3-stage pipeline when there are
+    < 512 workgroups (one per CU cannot hide a drained pipeline); long-K products with < 400
+    workgroups split K (the largest tile needing <= 8 splits, each >= 512 deep) — split-K (a
+    second, reducing kernel) only without an epilogue."""
     hit = _TUNED.get((a_km, b_kn, M, N, K))
     if hit is not None and (can_split or hit[1] == 1):
         return hit if KSPLIT else (hit[0] % 100000000, hit[1])
+    if (not a_km and not b_kn and epi in G256_EPIS and M % 256 == 0 and N % 256 == 0
+            and (M // 256) * (N // 256) >= 256 and K >= 1024):
+        return G256, 1
     fits = [t for t in _TILES if _ntiles(t, M, N)]
     if not fits:
         return 0, 1
@@ -129,7 +140,7 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
         if epi == EPI_DSWIGLU and not aux.is_contiguous():
             aux = aux.contiguous()
         if splits == 0 or tile == 0:
-            t, s = config(a_km, b_kn, M, N, K, can_split=(epi in (EPI_NONE, EPI_ROWSUM) and bias is None))
+            t, s = config(a_km, b_kn, M, N, K, can_split=(epi in (EPI_NONE, EPI_ROWSUM) and bias is None), epi=epi)
             tile = tile or t
             splits = splits or s
         torch.ops.nbd.gemm(a, b, c, a_km, b_kn, bias, epi, aux, pre, splits, tile)

@@ -1,0 +1,22 @@
+"""Kernel selection of ops.gemm.config (CPU: pure Python)."""
+from nbdistributed_amd.ops import gemm as G
+
+
+def test_large_forward_products_take_the_256_kernel():
+    assert G.config(False, False, 4096, 4096, 4096) == (G.G256, 1)
+    assert G.config(False, False, 8192, 8192, 8192, epi=G.EPI_GELU) == (G.G256, 1)
+
+
+def test_256_kernel_only_where_it_applies():
+    # transposed layouts, epilogues it lacks, short K, too few tiles, ragged shapes
+    assert G.config(False, True, 4096, 4096, 4096)[0] != G.G256
+    assert G.config(True, True, 4096, 4096, 4096)[0] != G.G256
+    assert G.config(False, False, 4096, 4096, 4096, epi=G.EPI_SWIGLU)[0] != G.G256
+    assert G.config(False, False, 4096, 4096, 512)[0] != G.G256
+    assert G.config(False, False, 2048, 2048, 4096)[0] != G.G256  # 64 tiles
+    assert G.config(False, False, 4096, 4160, 4096)[0] != G.G256
+
+
+def test_tuned_workload_shapes_keep_their_kernels():
+    assert G.config(False, False, 8192, 3072, 768) == (82128128, 1)  # gpt2 c_fc forward
+    assert G.config(True, True, 3072, 768, 8192) == (3064128, 4)  # gpt2 c_fc weight gradient
