@@ -92,10 +92,10 @@ def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small"):
         impl = "flat"   # HIP graphs need a GPU
     torch.manual_seed(0)
     m = GPT2(getattr(GPT2Config, config)()).to(device)
-    amp = impl not in ("flat", "flatgraph")
+    amp = impl not in ("flat", "flatgraph", "zero")
     if not amp:   # bf16 params in the DDP buckets + fp32 master/moments in FlatAdamW
         m = m.to(torch.bfloat16)
-        model = _NbdDDP(m, flat_params=True, grad_mode="bucket")
+        model = _NbdDDP(m, flat_params=True, grad_mode="bucket", shard=impl == "zero")
         opt = _FlatAdamW(model, lr=3e-4, capturable=impl == "flatgraph")
     else:
         model = _nbd_wrap(m, impl, comm_dtype=torch.bfloat16)
@@ -175,6 +175,13 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
         gms = _max_over_ranks(r)
         out.update(graph_ms_per_step=gms, graph_tokens_per_s=n * B * T / (gms / 1e3),
                    graph_recipe="as the primary recipe, whole step captured in one HIP graph (GraphedStep)")
+    try:  # ZeRO-2: reduce-scattered gradients, optimizer on this rank's slice, parameter all-gather
+        r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'zero', {config!r})", render=False)
+        zms = _max_over_ranks(r)
+        out.update(zero2_ms_per_step=zms, zero2_tokens_per_s=n * B * T / (zms / 1e3),
+                   zero2_recipe="as the primary recipe with DistributedDataParallel(shard=True) (ZeRO-2)")
+    except Exception as e:  # noqa: BLE001 - recorded, the other recipes still run
+        out["zero2_error"] = f"{type(e).__name__}: {e}"[:400]
     r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'nbd', {config!r})", render=False)
     ams = _max_over_ranks(r)
     out.update(amp_ms_per_step=ams, amp_tokens_per_s=n * B * T / (ams / 1e3))

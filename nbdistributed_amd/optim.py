@@ -5,12 +5,18 @@ bucket's update with one fused HIP kernel (``nbd::adamw_flat``) that reads the a
 gradient bucket directly — no unflatten, no per-parameter kernels, no fp32→bf16 weight casts in
 the forward (the model runs in bf16; the master copy keeps fp32 precision).  Semantics match
 ``torch.optim.AdamW`` (decoupled weight decay, bias correction).
+
+With ``DistributedDataParallel(..., shard=True)`` (ZeRO-2) the state covers only this rank's
+slice of each bucket (``b.lo .. b.lo + b.shard``): the kernel reads the reduce-scattered gradient
+slice, updates that slice of the bf16 parameters, and an async all-gather per bucket (waited at
+the next DDP forward, or ``ddp.wait_params()``) rebuilds the full parameters on every rank.
 """
 from __future__ import annotations
 
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
+import torch.distributed as dist
 
 from . import ops
 
@@ -41,10 +47,17 @@ class FlatAdamW(torch.optim.Optimizer):
         self.step_t = torch.zeros(1, dtype=torch.float32, device=dev) if capturable else None
         self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev) if capturable else None
         self.flat_state: List[Dict[str, torch.Tensor]] = []
+        self.sharded = bool(getattr(ddp, "shard", False))
         for b in ddp.buckets:
-            master = b.param_flat.detach().float().clone()
+            master = self._param_slice(b).detach().float().clone()
             self.flat_state.append({"master": master, "exp_avg": torch.zeros_like(master),
                                     "exp_avg_sq": torch.zeros_like(master)})
+
+    def _param_slice(self, b):
+        return b.param_flat[b.lo:b.lo + b.shard] if self.sharded else b.param_flat
+
+    def _grad(self, b):
+        return b.grad_shard if self.sharded else b.buffer
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -56,10 +69,18 @@ class FlatAdamW(torch.optim.Optimizer):
             self.step_t.add_(1.0)
             if not _capturing():
                 self.lr_t.fill_(float(g["lr"]))
-        for b, st in zip(self.ddp.buckets, self.flat_state):
-            ops.adamw_flat(b.buffer, b.param_flat, st["master"], st["exp_avg"], st["exp_avg_sq"], g["lr"], b1, b2,
-                           g["eps"], g["weight_decay"], max(self.step_count, 1), grad_scale_t=self._clip_coef,
+        pairs = list(zip(self.ddp.buckets, self.flat_state))
+        if self.sharded:
+            pairs.reverse()  # the last bucket holds the first layers: gather it first
+        for b, st in pairs:
+            ops.adamw_flat(self._grad(b), self._param_slice(b), st["master"], st["exp_avg"], st["exp_avg_sq"], g["lr"],
+                           b1, b2, g["eps"], g["weight_decay"], max(self.step_count, 1), grad_scale_t=self._clip_coef,
                            step_t=self.step_t, lr_t=self.lr_t)
+            if self.sharded:  # rebuild the full bucket from every rank's updated slice
+                b.gather_work = dist.all_gather_into_tensor(b.param_flat, self._param_slice(b), group=self.ddp.pg,
+                                                            async_op=True)
+        if self.sharded and _capturing():
+            self.ddp.wait_params()  # a captured step must join its collectives before it ends
         self._clip_coef = None
         return loss
 
@@ -76,8 +97,10 @@ class FlatAdamW(torch.optim.Optimizer):
         next ``step()`` — no host synchronisation.  Returns the total norm (device tensor)."""
         sq = None
         for b in self.ddp.buckets:
-            n = ops.tensor_summary_raw(b.buffer)[4]
+            n = ops.tensor_summary_raw(self._grad(b))[4]
             sq = n * n if sq is None else sq + n * n
+        if self.sharded:  # the slices partition the gradient: sum the squares over the ranks
+            dist.all_reduce(sq, group=self.ddp.pg)
         total = sq.sqrt().float()
         self._clip_coef = torch.clamp(max_norm / (total + eps), max=1.0).reshape(1).contiguous()
         return total
@@ -87,12 +110,20 @@ class FlatAdamW(torch.optim.Optimizer):
             p.grad = None
 
     def state_dict(self) -> Dict[str, Any]:
+        """Per-bucket fp32 state; with a sharded DDP, this rank's slices only (``shard`` records
+        rank and world: load it on the same rank of a same-size world)."""
         step = int(self.step_t.item()) if self.capturable else self.step_count
-        return {"step": step, "param_groups": [{k: v for k, v in self.param_groups[0].items() if k != "params"}],
-                "buckets": [{k: v for k, v in st.items()} for st in self.flat_state]}
+        sd = {"step": step, "param_groups": [{k: v for k, v in self.param_groups[0].items() if k != "params"}],
+              "buckets": [{k: v for k, v in st.items()} for st in self.flat_state]}
+        if self.sharded:
+            sd["shard"] = {"rank": self.ddp.rank, "world": self.ddp.world}
+        return sd
 
     @torch.no_grad()
     def load_state_dict(self, sd: Dict[str, Any]) -> None:
+        want = {"rank": self.ddp.rank, "world": self.ddp.world} if self.sharded else None
+        if sd.get("shard") != want:
+            raise ValueError(f"FlatAdamW.load_state_dict: state is for shard {sd.get('shard')}, this optimizer is {want}")
         self.step_count = int(sd["step"])
         if self.capturable:
             self.step_t.fill_(float(self.step_count))
@@ -101,4 +132,6 @@ class FlatAdamW(torch.optim.Optimizer):
             for k in st:
                 st[k].copy_(src[k])
         for b, st in zip(self.ddp.buckets, self.flat_state):
-            b.param_flat.copy_(st["master"].to(b.param_flat.dtype))
+            self._param_slice(b).copy_(st["master"].to(b.param_flat.dtype))
+            if self.sharded:
+                dist.all_gather_into_tensor(b.param_flat, self._param_slice(b), group=self.ddp.pg)

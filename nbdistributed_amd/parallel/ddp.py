@@ -20,7 +20,16 @@ designed for MI355X + RCCL over xGMI:
 * parameters that got no gradient this step (unused branches) are flattened as zeros at the end
   of backward so no rank ever waits on a missing bucket;
 * ``no_sync()`` for gradient accumulation, buffers broadcast from rank 0 in forward, parameters
-  broadcast from rank 0 at construction (coalesced through the same flatten kernel).
+  broadcast from rank 0 at construction (coalesced through the same flatten kernel);
+* ``shard=True`` (ZeRO stage 2, with ``flat_params`` + ``grad_mode="bucket"`` and
+  ``nbdistributed_amd.optim.FlatAdamW``): each bucket is REDUCE-SCATTERED instead of all-reduced —
+  rank r keeps only the averaged gradient of its 1/world slice (``b.grad_shard``), the fp32
+  master weights and moments exist only for that slice (optimizer memory / world), the update
+  runs on 1/world of the parameters, and the updated bf16 slices are ALL-GATHERED back into the
+  parameter buckets, one async gather per bucket right after its update (so they overlap the
+  remaining bucket updates), all waited device-side at the next forward.  Same bytes on the
+  wire as the all-reduce (RCCL's ring all-reduce IS a reduce-scatter + all-gather), 1/world of
+  the optimizer work and state.
 
 Also provides DDP communication hooks for stock ``torch.nn.parallel.DistributedDataParallel``
 (``bf16_compress_hook``) built on the same fused kernels.
@@ -50,18 +59,26 @@ class _Bucket:
     work: Any = None
     grads: List[torch.Tensor] = field(default_factory=list)
     param_flat: Optional[torch.Tensor] = None  # flat_params: the parameters live here (views)
+    # shard=True: this rank's slice [lo, lo + shard) of the bucket, its averaged gradient, and
+    # the in-flight all-gather of the updated parameter slices (set by FlatAdamW.step)
+    shard: int = 0
+    lo: int = 0
+    grad_shard: Optional[torch.Tensor] = None
+    gather_work: Any = None
 
 
 class DistributedDataParallel(torch.nn.Module):
     def __init__(self, module: torch.nn.Module, process_group=None, bucket_cap_mb: float = 64.0,
                  first_bucket_mb: float = 4.0, comm_dtype: Optional[torch.dtype] = None,
                  broadcast_buffers: bool = True, init_sync: bool = True, align: int = 64,
-                 flat_params: bool = False, grad_mode: str = "unflatten"):
+                 flat_params: bool = False, grad_mode: str = "unflatten", shard: bool = False):
         """``flat_params``: re-home each bucket's parameters into one contiguous buffer (the
         nn.Parameters become views) so a flat optimizer (``nbdistributed_amd.optim.FlatAdamW``)
         can update a whole bucket in one pass.  ``grad_mode="bucket"``: leave the averaged
         gradients in the bucket buffers (no unflatten, ``p.grad`` released after the flatten) —
-        only for optimizers that read the buckets (FlatAdamW)."""
+        only for optimizers that read the buckets (FlatAdamW).  ``shard=True``: ZeRO-2 —
+        reduce-scatter the buckets, optimizer state and update on this rank's slice only (module
+        docstring); needs ``flat_params=True, grad_mode="bucket"``."""
         super().__init__()
         self.module = module
         self.pg = process_group if process_group is not None else dist.group.WORLD
@@ -77,6 +94,10 @@ class DistributedDataParallel(torch.nn.Module):
             raise ValueError("grad_mode must be 'unflatten' or 'bucket'")
         self.grad_mode = grad_mode
         self.flat_params = flat_params
+        if shard and not (flat_params and grad_mode == "bucket"):
+            raise ValueError("shard=True needs flat_params=True and grad_mode='bucket' (with FlatAdamW)")
+        self.shard = shard
+        self.rank = dist.get_rank(self.pg)
         self._require_sync = True
         self._in_backward = False
         self._capturing = False
@@ -94,11 +115,18 @@ class DistributedDataParallel(torch.nn.Module):
         self.buckets = self._plan(bucket_cap_mb, first_bucket_mb, align)
         self._bucket_of: Dict[int, _Bucket] = {}
         for b in self.buckets:
+            if shard:  # equal, aligned slices: pad the bucket to a multiple of world x align
+                q = self.world * align
+                b.numel = (b.numel + q - 1) // q * q
+                b.shard = b.numel // self.world
+                b.lo = self.rank * b.shard
+                b.grad_shard = torch.zeros(b.shard, dtype=self.comm_dtype, device=self.device)
             b.buffer = torch.zeros(b.numel, dtype=self.comm_dtype, device=self.device)
             for p in b.params:
                 self._bucket_of[id(p)] = b
         if flat_params:
             self._rehome_params()
+
         self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in self.params]
         if init_sync and self.world > 1:
             self._broadcast_tensors([p.data for p in module.parameters()])
@@ -143,8 +171,33 @@ class DistributedDataParallel(torch.nn.Module):
                     p.data = flat[o:o + n].view_as(p)
             b.param_flat = flat
 
+    # ------------------------------------------------------------------ ZeRO parameter gathers
+    @staticmethod
+    def _wait_gathers(buckets) -> None:
+        for b in buckets:
+            if b.gather_work is not None:
+                b.gather_work.wait()  # RCCL: the current stream waits on the collective (device side)
+                b.gather_work = None
+
+    def wait_params(self) -> None:
+        """Make the current stream wait until every parameter all-gather of a sharded step has
+        landed (``shard=True``; forward does this itself — call it before reading the
+        parameters directly)."""
+        self._wait_gathers(self.buckets)
+
+    def _reduce(self, b: _Bucket):
+        if self.shard:  # ZeRO-2: this rank keeps the averaged gradient of its slice only
+            return dist.reduce_scatter_tensor(b.grad_shard, b.buffer, group=self.pg, async_op=True)
+        return dist.all_reduce(b.buffer, group=self.pg, async_op=True)
+
     # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
+        if self.shard:
+            # the updated parameter slices of the last step must be back on every rank.  (Per
+            # module pre-forward waits would let the first layers start earlier, but the models'
+            # fused paths read weights without calling their modules' forward, so the hooks
+            # would not fire: all buckets are waited here.)
+            self._wait_gathers(self.buckets)
         if self._require_sync and self.broadcast_buffers and self.world > 1:
             bufs = [b for b in self.module.buffers() if b.is_floating_point() or b.dtype in (torch.int64, torch.int32)]
             if bufs:
@@ -207,10 +260,10 @@ class DistributedDataParallel(torch.nn.Module):
         unflatten = self.grad_mode == "unflatten"
         if self.cuda and self._capturing:
             ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
-            b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)  # waited in _finalize
+            b.work = self._reduce(b)  # waited in _finalize
         elif self.cuda and not self._side:
             ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
-            b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)
+            b.work = self._reduce(b)
             b.work.wait()
             if unflatten:
                 ops.bucket_unflatten(b.buffer, grads, b.offsets)
@@ -220,7 +273,7 @@ class DistributedDataParallel(torch.nn.Module):
             self.comm_stream.wait_stream(cur)  # the grads were produced on the compute stream
             with torch.cuda.stream(self.comm_stream):
                 ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
-                b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)
+                b.work = self._reduce(b)
                 b.work.wait()  # device-side: the comm stream waits for RCCL's stream
                 if unflatten:
                     ops.bucket_unflatten(b.buffer, grads, b.offsets)
@@ -228,7 +281,7 @@ class DistributedDataParallel(torch.nn.Module):
                 g.record_stream(self.comm_stream)
         else:
             ops.bucket_flatten(grads, b.buffer, b.offsets, scale=scale)
-            b.work = dist.all_reduce(b.buffer, group=self.pg, async_op=True)
+            b.work = self._reduce(b)
         if not unflatten:
             # the averaged gradients live in b.buffer; release the per-parameter grads now
             # (the caching allocator will not reuse them before the comm stream is done)
