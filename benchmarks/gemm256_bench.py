@@ -53,7 +53,13 @@ def main():
         ("lmhead dgrad", 8192, 768, V, False, True),
         ("lmhead wgrad", V, 768, 8192, True, True),
         ("gpt2 c_fc fwd", 8192, 3072, 768, False, False),
+        # Llama-3.2-1B-class Linear forwards at 8192 tokens (hidden 2048, q|k|v 3072, MLP 8192)
+        ("llama1b qkv", 8192, 3072, 2048, False, False),
+        ("llama1b o_proj", 8192, 2048, 2048, False, False),
+        ("llama1b down", 8192, 2048, 8192, False, False),
     ]
+    only = None if a.shapes == "all" else set(a.shapes.split(","))
+    shapes = [sh for sh in shapes if only is None or sh[0].split()[0] in only]
     g = torch.Generator(device="cuda").manual_seed(0)
     res = {}
     for name, M, N, K, a_km, b_kn in shapes:

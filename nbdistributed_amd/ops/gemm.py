@@ -69,10 +69,19 @@ def _ntiles(tile: int, M: int, N: int) -> int:
 
 
 # the 256x256 phase-interleaved kernel (gemm256.hip) with staggered wave groups: forward products
-# with >= 256 such tiles and K >= 1024 (1.29-1.32 PF vs 1.07-1.11 for the 128x128 kernel at
-# 4096^3 / 8192^3: docs/FINDINGS.md §10); its epilogues: none / bias / GELU
+# with whole rounds of 256 such tiles (256, 512, ... or >= 1024) and K >= 1024 (1.22-1.34 PF vs
+# 0.98-1.16 for the 128x128 kernel at 4096^3, 8192^3 and Llama-1B's o_proj / down; 1.5 rounds
+# (Llama-1B q|k|v, 384 tiles) lose: docs/FINDINGS.md §10); its epilogues: none / bias / GELU
 G256 = 86256256
 G256_EPIS = (EPI_NONE, EPI_GELU)
+# Plain products at least this large (FLOPs) with no tuned entry go to hipBLASLt: it measured
+# 1.16-1.61 PF on them, 15-30 % ahead of both hand-written families (profiles/gemm256_bench_r2.txt);
+# the hand-written kernels keep the fused epilogues and the workload shapes they win on.
+LIBRARY_MIN_FLOPS = 2 ** 36
+
+
+def prefer_library(a_km: bool, b_kn: bool, M: int, N: int, K: int, epi: int) -> bool:
+    return (epi == EPI_NONE and (a_km, b_kn, M, N, K) not in _TUNED and 2.0 * M * N * K >= LIBRARY_MIN_FLOPS)
 
 
 def config(a_km: bool, b_kn: bool, M: int, N: int, K: int, can_split: bool = True, epi: int = EPI_NONE):
@@ -85,8 +94,9 @@ def config(a_km: bool, b_kn: bool, M: int, N: int, K: int, can_split: bool = Tru
     hit = _TUNED.get((a_km, b_kn, M, N, K))
     if hit is not None and (can_split or hit[1] == 1):
         return hit if KSPLIT else (hit[0] % 100000000, hit[1])
+    t256 = (M // 256) * (N // 256)
     if (not a_km and not b_kn and epi in G256_EPIS and M % 256 == 0 and N % 256 == 0
-            and (M // 256) * (N // 256) >= 256 and K >= 1024):
+            and (t256 % 256 == 0 or t256 >= 1024) and t256 > 0 and K >= 1024):
         return G256, 1
     fits = [t for t in _TILES if _ntiles(t, M, N)]
     if not fits:
@@ -124,7 +134,8 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
     M = a.shape[1] if a_km else a.shape[0]
     K = a.shape[0] if a_km else a.shape[1]
     N = b.shape[1] if b_kn else b.shape[0]
-    if (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and gemm_ok(M, N, K)
+    library = tile == 0 and splits == 0 and prefer_library(a_km, b_kn, M, N, K, epi)
+    if (not library and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and gemm_ok(M, N, K)
             and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and (out is None or out.data_ptr() % 16 == 0)
             and (bias is None or (bias.data_ptr() % 8 == 0 and bias.dtype == torch.bfloat16))):
         _require()
@@ -145,12 +156,16 @@ def matmul(a, b, a_km: bool = False, b_kn: bool = False, bias=None, epi: int = E
             splits = splits or s
         torch.ops.nbd.gemm(a, b, c, a_km, b_kn, bias, epi, aux, pre, splits, tile)
         return (c, pre) if epi in (EPI_GELU, EPI_ROWSUM, EPI_SWIGLU) else c
-    # reference path (CPU / uncovered shapes): same math through PyTorch
+    # reference path (CPU / uncovered shapes) and large plain products: same math through PyTorch
+    # (hipBLASLt on ROCm)
     A = a.t() if a_km else a
     B = b if b_kn else b.t()
-    c = A @ B
-    if bias is not None:
-        c = c + bias
+    if bias is not None and epi in (EPI_NONE, EPI_GELU):
+        c = torch.addmm(bias, A, B)  # the bias rides in the library GEMM's epilogue
+    else:
+        c = A @ B
+        if bias is not None:
+            c = c + bias
     if epi == EPI_GELU:
         pre = c
         c = torch.nn.functional.gelu(pre, approximate="tanh")

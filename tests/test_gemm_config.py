@@ -5,6 +5,14 @@ from nbdistributed_amd.ops import gemm as G
 def test_large_forward_products_take_the_256_kernel():
     assert G.config(False, False, 4096, 4096, 4096) == (G.G256, 1)
     assert G.config(False, False, 8192, 8192, 8192, epi=G.EPI_GELU) == (G.G256, 1)
+    assert G.config(False, False, 8192, 3072, 2048)[0] != G.G256  # 384 tiles: 1.5 rounds
+
+
+def test_large_plain_products_prefer_hipblaslt():
+    assert G.prefer_library(False, False, 8192, 2048, 8192, G.EPI_NONE)
+    assert not G.prefer_library(False, False, 8192, 2048, 8192, G.EPI_GELU)  # fused epilogue: ours
+    assert not G.prefer_library(False, False, 8192, 3072, 768, G.EPI_NONE)  # GPT-2 c_fc: tuned, ours
+    assert not G.prefer_library(False, False, 2048, 960, 576, G.EPI_NONE)  # small: ours
 
 
 def test_256_kernel_only_where_it_applies():

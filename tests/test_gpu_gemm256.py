@@ -94,3 +94,16 @@ def test_gemm256_matches_128_tile_kernel():
     c256 = G.matmul(a, b, tile=T256, splits=1).float()
     c128 = G.matmul(a, b, tile=2128128, splits=1).float()
     assert _err(c256, c128) < 8e-3
+
+
+def test_large_plain_product_routes_to_library_and_gelu_stays_fused():
+    # 2*M*N*K >= 2^36 without an epilogue -> hipBLASLt; with GELU -> the 256x256 kernel
+    M, N, K = 4096, 4096, 2048
+    a, b = _operands(M, N, K, False, False, seed=8)
+    assert G.prefer_library(False, False, M, N, K, G.EPI_NONE)
+    bias = torch.randn(N, device="cuda").to(torch.bfloat16)
+    ref = _ref(a, b, False, False) + bias.float()
+    assert _err(G.matmul(a, b, bias=bias), ref) < 1e-2
+    g, pre = G.matmul(a, b, bias=bias, epi=G.EPI_GELU)
+    assert G.config(False, False, M, N, K, can_split=False, epi=G.EPI_GELU) == (G.G256, 1)
+    assert _err(pre, ref) < 1e-2
