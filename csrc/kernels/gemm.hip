@@ -142,12 +142,12 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
       }
     }
   };
+  // DMA addressing: per-lane 32-bit offsets computed once, a scalar base per K-step
+  const Pieces<BM, A_KM, W> pa(p.lda, wave, lane);
+  const Pieces<BN, B_KN, W> pb(p.ldb, wave, lane, EPI == EPI_SWIGLU ? (int64_t)(p.N / 2) : 0);
   auto stage_tile = [&](int t, uint8_t* buf) {
-    stage<BM, A_KM, W>(A, p.lda, m0, (t * KS + kg) * BK, buf, wave, lane);
-    if constexpr (EPI == EPI_SWIGLU)
-      stage<BN, B_KN, W>(B, p.ldb, n0 / 2, (t * KS + kg) * BK, buf + A_BYTES, wave, lane, p.N / 2 + n0 / 2);
-    else
-      stage<BN, B_KN, W>(B, p.ldb, n0, (t * KS + kg) * BK, buf + A_BYTES, wave, lane);
+    pa.stage(A, p.lda, m0, (t * KS + kg) * BK, buf, wave);
+    pb.stage(B, p.ldb, EPI == EPI_SWIGLU ? n0 / 2 : n0, (t * KS + kg) * BK, buf + A_BYTES, wave);
   };
 
   if constexpr (STAGES == 2) {
@@ -530,6 +530,12 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   }
   TORCH_CHECK(epi >= EPI_NONE && epi <= EPI_DSWIGLU, "nbd::gemm: epilogue ", epi);
   const Tile t = pick_tile(M, N, tile_hint);
+  // per-lane DMA offsets are 32-bit byte offsets within one tile's rows (gemm_common.h Pieces)
+  {
+    const int64_t ra = a_km ? BK : t.bm, rb = b_kn ? BK : (epi == EPI_SWIGLU ? N / 2 + t.bn : t.bn);
+    TORCH_CHECK(ra * a.size(1) * 2 < (1LL << 32) && rb * b.size(1) * 2 < (1LL << 32),
+                "nbd::gemm: row stride too large for 32-bit DMA offsets");
+  }
   const int tiles = (M / t.bm) * (N / t.bn);
   const int S = splits > 0 ? (int)splits : 1;
   TORCH_CHECK(K % (BK * S * t.ks) == 0, "nbd::gemm: K not divisible into ", S, " splits x ", t.ks, " K-groups");

@@ -45,7 +45,7 @@ __device__ __forceinline__ int hmap(int lr, int X) {
 }
 
 // DMA one half image (16 KiB = 16 wave-pieces of 1 KiB; 2 per wave).  Row image [128][64] or
-// tr image [64][128], the same swizzles as gemm.hip's stage<128, TR>.
+// tr image [64][128], the same swizzles as gemm_common.h's Pieces<128, TR, 8>.
 template <bool TR, int GRP>
 __device__ __forceinline__ void stage_half(const uint16_t* __restrict__ g, int64_t ld, int r0, int k0, uint8_t* img,
                                            int X, int wave, int lane) {

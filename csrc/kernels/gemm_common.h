@@ -68,6 +68,60 @@ __device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* lds_wave_ba
       : "memory");
 }
 
+// 16-B LDS DMA from a uniform (SGPR) base + a 32-bit per-lane byte offset: the saddr form of
+// global_load_lds_dwordx4 — the per-lane part of the address is computed once per kernel, each
+// K-step only moves the scalar base (no 64-bit VALU address arithmetic per DMA)
+__device__ __forceinline__ void glds16s(const uint16_t* sbase_, uint32_t voff, uint8_t* lds_wave_base) {
+  // the base is wave-uniform by construction; readfirstlane lets the compiler keep it in SGPRs
+  const uint64_t b = (uint64_t)(uintptr_t)sbase_;
+  // (the builtin returns int: widen through uint32_t, or the low half sign-extends into the high)
+  const uint64_t sb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint16_t* sbase = (const uint16_t*)(uintptr_t)sb;
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(lds_wave_base));
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds)
+      : "memory");
+}
+
+// Per-lane byte offsets of one thread's DMA pieces of an R-row (or, TR, R-column) operand image
+// (R x 64 K-tile = R/8 wave-pieces of 1 KiB, R/(8W) per wave) with the LDS swizzles above: row
+// image [R][64] (16-B chunk ^ row_swz(row)), tr image [64][R] (16-B chunk ^ tr_swz(k)/2); R1 >= 0: rows R/2.. come from global rows r1.. (SwiGLU's
+// up half), given as an element offset from the tile's first row.  stage() adds the uniform
+// tile / K-step base.  Offsets must fit 32 bits: rows * ld * 2 bytes (asserted on the host).
+template <int R, bool TR, int W>
+struct Pieces {
+  static constexpr int N = R / (8 * W);
+  uint32_t off[N];
+  __device__ __forceinline__ Pieces(int64_t ld, int wave, int lane, int64_t split_rows = 0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int byte = (i * W + wave) * 1024 + lane * 16;
+      int64_t e;
+      if constexpr (!TR) {
+        const int r = byte >> 7, pc = (byte >> 4) & 7;
+        const int64_t row = (split_rows != 0 && r >= R / 2) ? split_rows + r - R / 2 : r;
+        e = row * ld + 8 * (pc ^ row_swz(r));
+      } else {
+        constexpr int RB = 2 * R;
+        const int k = byte / RB, pc = (byte % RB) >> 4;
+        e = (int64_t)k * ld + 8 * (pc ^ (tr_swz<R>(k) >> 1));
+      }
+      off[i] = (uint32_t)(2 * e);
+    }
+  }
+  // K-tile starting at k0 of the operand rows r0.. into img
+  __device__ __forceinline__ void stage(const uint16_t* g, int64_t ld, int r0, int k0, uint8_t* img, int wave) const {
+    const uint16_t* base = TR ? g + (int64_t)k0 * ld + r0 : g + (int64_t)r0 * ld + k0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) glds16s(base, off[i], img + (i * W + wave) * 1024);
+  }
+};
+
 // 16x16x32 operand fragment (lane l: rows/cols r0 + (l&15), k = 32kk + 8(l>>4) + 0..7) from an
 // LDS image with R rows (row image [R][64], 128-B rows) or R columns (tr image [64][R]).
 template <int R, bool TR>
@@ -87,32 +141,6 @@ __device__ __forceinline__ s8v frag(const uint8_t* img, int r0, int kk, int lane
     r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
     r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
     return r;
-  }
-}
-
-// Stage one 64-deep K-tile of an operand into its LDS image.  R = tile rows (BM or BN).
-// TR = false: global [rows][k] (row r0.., k0..), image [R][64]; TR = true: global [k][rows], image [64][R].
-// r1 = first global row of the tile's second half (r0 + R/2 for a contiguous tile; EPI_SWIGLU
-// gives the up rows there; row images only).
-template <int R, bool TR, int W>
-__device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld, int r0, int k0, uint8_t* img,
-                                      int wave, int lane, int r1 = -1) {
-  constexpr int PER_WAVE = R / (8 * W);  // (R*64*2 B) / (W waves * 1 KiB)
-#pragma unroll
-  for (int i = 0; i < PER_WAVE; ++i) {
-    const int wbase = (i * W + wave) * 1024;
-    const int byte = wbase + lane * 16;
-    const uint16_t* src;
-    if constexpr (!TR) {
-      const int r = byte >> 7, pc = (byte >> 4) & 7;
-      const int row = (r1 >= 0 && r >= R / 2) ? r1 + r - R / 2 : r0 + r;
-      src = g + (int64_t)row * ld + k0 + 8 * (pc ^ row_swz(r));
-    } else {
-      constexpr int RB = 2 * R;
-      const int k = byte / RB, pc = (byte % RB) >> 4;
-      src = g + (int64_t)(k0 + k) * ld + r0 + 8 * (pc ^ (tr_swz<R>(k) >> 1));
-    }
-    glds16(src, img + wbase);
   }
 }
 
