@@ -59,3 +59,29 @@ def test_native_llama_notebook_runs_end_to_end(monkeypatch):
     finally:
         if core.session.active:
             core.session.shutdown()
+
+
+NB3 = os.path.join(os.path.dirname(NB), "03_zero_sharded.ipynb")
+
+
+def test_zero_notebook_runs_end_to_end(monkeypatch):
+    monkeypatch.setenv("NBD_NOTEBOOK_TINY", "1")
+    cells = [c for c in json.load(open(NB3))["cells"] if c["cell_type"] == "code"]
+    sh = HeadlessShell()
+    core = sh.load_extension()
+    out = []
+    core.write = core.session.write = out.append
+    try:
+        for c in cells:
+            src = "".join(c["source"])
+            if src.startswith("%load_ext"):
+                continue
+            if src.startswith("%dist_init"):
+                src += " --backend gloo"
+            r = sh.run_cell(src)
+            assert r.success, (src, r.error_in_exec, "".join(out)[-3000:])
+        text = "".join(out)
+        assert "parameters identical to rank 0: True" in text and "step 4: loss" in text
+    finally:
+        if core.session.active:
+            core.session.shutdown()
