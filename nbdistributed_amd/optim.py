@@ -71,6 +71,9 @@ class FlatAdamW(torch.optim.Optimizer):
                 self.lr_t.fill_(float(g["lr"]))
         pairs = list(zip(self.ddp.buckets, self.flat_state))
         if self.sharded:
+            # a previous step's gathers still reading our slices must finish before the update
+            # rewrites them (step() twice without a forward in between)
+            self.ddp.wait_params()
             pairs.reverse()  # the last bucket holds the first layers: gather it first
         for b, st in pairs:
             ops.adamw_flat(self._grad(b), self._param_slice(b), st["master"], st["exp_avg"], st["exp_avg_sq"], g["lr"],
@@ -124,6 +127,8 @@ class FlatAdamW(torch.optim.Optimizer):
         want = {"rank": self.ddp.rank, "world": self.ddp.world} if self.sharded else None
         if sd.get("shard") != want:
             raise ValueError(f"FlatAdamW.load_state_dict: state is for shard {sd.get('shard')}, this optimizer is {want}")
+        if self.sharded:
+            self.ddp.wait_params()
         self.step_count = int(sd["step"])
         if self.capturable:
             self.step_t.fill_(float(self.step_count))

@@ -62,6 +62,11 @@ dist.all_gather(same, flat)
 """
 
 STATE = """
+opt_zero.step(); opt_zero.step()  # back-to-back steps (no forward between): gathers are joined first
+opt_full.step(); opt_full.step()
+zero.wait_params()
+err2 = max(float((p - q).detach().abs().max()) for p, q in zip(full.module.parameters(), zero.module.parameters()))
+assert err2 < 1e-6, err2
 sd = opt_zero.state_dict()
 opt2 = FlatAdamW(zero, lr=1.0)
 opt2.load_state_dict(sd)
