@@ -25,6 +25,7 @@
 #include <torch/library.h>
 
 #include <type_traits>
+#include <vector>
 
 #include "nbd_common.h"
 
@@ -197,6 +198,72 @@ static void dispatch_nch(int64_t C, F&& f) {
 }
 
 // grad_weight [V, C] (dtype of dy) from dy [N, C] and int64 ids [N]
+// ---- token + position embedding forward: out[r] = wte[idx[r]] + wpe[pos[r % T]] ---------------
+// One pass (16 B per lane from each table, fp32 add, one rounding — the same bits as
+// F.embedding(idx, wte) + F.embedding(pos, wpe) in the tables' dtype) instead of two gathers and
+// an add.  Out-of-range ids read as zero rows (F.embedding would raise; the host cannot check
+// without a sync).
+template <typename T>
+__global__ __launch_bounds__(NT) void tokpos_kernel(const int64_t* __restrict__ idx, const int64_t* __restrict__ pos, int T_,
+                                                    const T* __restrict__ wte, int V, const T* __restrict__ wpe, int P, int C,
+                                                    int64_t n8, T* __restrict__ out) {
+  const int c8 = C / 8;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
+    const int64_t r = i / c8;
+    const int c = (int)(i - r * c8) * 8;
+    const int64_t v = idx[r], q = pos[r % T_];
+    float a[8], b[8];
+    if (v >= 0 && v < V)
+      load8<T>(wte + v * C + c, a);
+    else
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = 0.f;
+    if (q >= 0 && q < P)
+      load8<T>(wpe + q * C + c, b);
+    else
+#pragma unroll
+      for (int e = 0; e < 8; ++e) b[e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] += b[e];
+    store8<T>(out + r * C + c, a);
+  }
+}
+
+at::Tensor embedding_tokpos_hip(const at::Tensor& idx, const at::Tensor& wte, const at::Tensor& pos, const at::Tensor& wpe) {
+  TORCH_CHECK(idx.is_cuda() && wte.is_cuda() && pos.is_cuda() && wpe.is_cuda(), "embedding_tokpos: GPU tensors expected");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && pos.scalar_type() == at::kLong && idx.is_contiguous() && pos.is_contiguous() &&
+                  pos.dim() == 1 && pos.numel() > 0 && idx.numel() % pos.numel() == 0,
+              "embedding_tokpos: int64 ids [..., T] and positions [T]");
+  TORCH_CHECK(wte.dim() == 2 && wpe.dim() == 2 && wte.size(1) == wpe.size(1) && wte.is_contiguous() && wpe.is_contiguous() &&
+                  wte.scalar_type() == wpe.scalar_type(),
+              "embedding_tokpos: contiguous [V, C] / [P, C] tables of one dtype");
+  const int64_t C = wte.size(1), N = idx.numel();
+  TORCH_CHECK(C % 8 == 0 && ((uintptr_t)wte.data_ptr() & 15) == 0 && ((uintptr_t)wpe.data_ptr() & 15) == 0,
+              "embedding_tokpos: C % 8 == 0 and 16-B aligned tables");
+  std::vector<int64_t> shape(idx.sizes().begin(), idx.sizes().end());
+  shape.push_back(C);
+  at::Tensor out = at::empty(shape, wte.options());
+  if (N == 0) return out;
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(wte.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  const int64_t n8 = N * C / 8;
+  const int blocks = (int)std::min<int64_t>((n8 + NT - 1) / NT, 4096);
+  auto launch = [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((tokpos_kernel<T>), dim3(blocks), dim3(NT), 0, st, idx.data_ptr<int64_t>(), pos.data_ptr<int64_t>(),
+                       (int)pos.numel(), static_cast<const T*>(wte.data_ptr()), (int)wte.size(0),
+                       static_cast<const T*>(wpe.data_ptr()), (int)wpe.size(0), (int)C, n8, static_cast<T*>(out.data_ptr()));
+  };
+  switch (wte.scalar_type()) {
+    case at::kFloat: launch(float{}); break;
+    case at::kBFloat16: launch(bf16_t{}); break;
+    case at::kHalf: launch(f16_t{}); break;
+    default: TORCH_CHECK(false, "embedding_tokpos: unsupported dtype ", wte.scalar_type());
+  }
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return out;
+}
+
 at::Tensor embedding_bwd_hip(const at::Tensor& dy, const at::Tensor& idx, int64_t V) {
   TORCH_CHECK(dy.is_cuda() && idx.is_cuda(), "embedding_bwd: GPU tensors expected");
   TORCH_CHECK(dy.dim() == 2 && dy.is_contiguous(), "embedding_bwd: dy must be a contiguous [N, C]");
@@ -254,4 +321,7 @@ at::Tensor embedding_bwd_hip(const at::Tensor& dy, const at::Tensor& idx, int64_
 }  // namespace embed
 }  // namespace nbd
 
-TORCH_LIBRARY_IMPL(nbd, CUDA, m) { m.impl("embedding_bwd", &nbd::embed::embedding_bwd_hip); }
+TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
+  m.impl("embedding_bwd", &nbd::embed::embedding_bwd_hip);
+  m.impl("embedding_tokpos", &nbd::embed::embedding_tokpos_hip);
+}

@@ -20,6 +20,7 @@ TORCH_LIBRARY(nbd, m) {
   m.def("rms_fwd(Tensor x, Tensor? delta, Tensor weight, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("rms_bwd(Tensor x, Tensor dy, Tensor? dres, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
   m.def("embedding_bwd(Tensor dy, Tensor idx, int V) -> Tensor");
+  m.def("embedding_tokpos(Tensor idx, Tensor wte, Tensor pos, Tensor wpe) -> Tensor");
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, int n_rot, int head_dim, bool inverse) -> ()");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");

@@ -20,6 +20,8 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
+#include <cstdlib>
+
 #include <tuple>
 #include <type_traits>
 
@@ -156,6 +158,12 @@ constexpr int kRpi = 2;       // rows per wave iteration
 // 16 x 128 tokens: 2048 rows -> 8 per workgroup; with 4, two of the four waves idled and the
 // weight-gradient partial rows doubled)
 static int bwd_rows_per_block(int64_t rows) {
+  static const int forced = [] {  // NBD_LN_BWD_ROWS: A/B override (4 .. 64)
+    const char* e = std::getenv("NBD_LN_BWD_ROWS");
+    const int v = e ? std::atoi(e) : 0;
+    return (v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : 0;
+  }();
+  if (forced) return forced;
   int r = kBwdRows;
   while (r > 8 && (rows + r - 1) / r < 512) r /= 2;
   return r;

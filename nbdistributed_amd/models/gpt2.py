@@ -163,7 +163,7 @@ class GPT2(nn.Module):
         if self._fast_ok(idx):
             from .. import ops
 
-            x = ops.embedding(idx, self.wte.weight) + ops.embedding(pos, self.wpe.weight)
+            x = ops.embedding_tok_pos(idx, self.wte.weight, pos, self.wpe.weight)
         else:
             x = self.wte(idx) + self.wpe(pos)
         if self._fast(x):

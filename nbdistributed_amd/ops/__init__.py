@@ -35,7 +35,7 @@ from ._lib import _require, load_library, native_available
 from .attention import attention_qkv, flash_attention, flash_supported
 from .bucket import (_ref_flatten, _ref_prereduce, _ref_unflatten, bucket_flatten, bucket_unflatten, local_prereduce,
                      plan_offsets)
-from .embedding import embedding
+from .embedding import embedding, embedding_tok_pos
 from .gemm import gemm_linear, mlp_gelu, mlp_swiglu
 from .llama import rope_, rope_tables, swiglu
 from .loss import cross_entropy, linear_cross_entropy
@@ -52,6 +52,6 @@ def __getattr__(name):
 
 __all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "cross_entropy", "linear_cross_entropy",
            "flash_attention", "attention_qkv", "flash_supported", "layer_norm", "add_layer_norm", "linear",
-           "colsum", "embedding", "gemm_linear", "mlp_gelu", "mlp_swiglu", "rms_norm", "add_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary",
+           "colsum", "embedding", "embedding_tok_pos", "gemm_linear", "mlp_gelu", "mlp_swiglu", "rms_norm", "add_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary",
            "tensor_summary_text", "tensor_summary_raw", "plan_offsets", "native_available", "load_library",
            "SUMMARY_FIELDS"]

@@ -188,3 +188,26 @@ def test_cross_entropy_strided_rows_and_sum(dev):
     got = ops.cross_entropy(x, tgt, reduction="sum")
     ref = F.cross_entropy(x.float(), tgt, reduction="sum")
     assert abs(float(got) - float(ref)) < 1e-3 * abs(float(ref))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_embedding_tok_pos_matches_two_lookups(dtype):
+    from nbdistributed_amd import ops
+
+    g = torch.Generator(device="cuda").manual_seed(0)
+    V, P, C, B, T = 1000, 256, 768, 3, 128
+    wte = torch.randn(V, C, device="cuda", generator=g).to(dtype).requires_grad_()
+    wpe = torch.randn(P, C, device="cuda", generator=g).to(dtype).requires_grad_()
+    idx = torch.randint(0, V, (B, T), device="cuda", generator=g)
+    idx[0, :40] = 7  # a frequent id
+    pos = torch.arange(64, 64 + T, device="cuda")
+    y = ops.embedding_tok_pos(idx, wte, pos, wpe)
+    ref = torch.nn.functional.embedding(idx, wte) + torch.nn.functional.embedding(pos, wpe)
+    assert torch.equal(y, ref)  # one fp32 add, one rounding: the same bits
+    dy = torch.randn(B, T, C, device="cuda", generator=g).to(dtype)
+    gt, gp = torch.autograd.grad(y, (wte, wpe), dy)
+    rt, rp = torch.autograd.grad(ref, (wte, wpe), dy)
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    assert (gt.float() - rt.float()).abs().max() <= tol * rt.float().abs().max()
+    assert (gp.float() - rp.float()).abs().max() <= tol * rp.float().abs().max()
+    assert float(gp[:64].float().abs().max()) == 0.0 and float(gp[64 + T:].float().abs().max()) == 0.0
