@@ -74,8 +74,10 @@ class FlatAdamW(torch.optim.Optimizer):
             # a previous step's gathers still reading our slices must finish before the update
             # rewrites them (step() twice without a forward in between)
             self.ddp.wait_params()
-            pairs.reverse()  # the last bucket holds the first layers: gather it first
-        for b, st in pairs:
+        wait = getattr(self.ddp, "wait_grad", None)
+        for b, st in pairs:  # bucket order = the order their collectives were issued
+            if wait is not None:
+                wait(b)
             ops.adamw_flat(self._grad(b), self._param_slice(b), st["master"], st["exp_avg"], st["exp_avg_sq"], g["lr"],
                            b1, b2, g["eps"], g["weight_decay"], max(self.step_count, 1), grad_scale_t=self._clip_coef,
                            step_t=self.step_t, lr_t=self.lr_t)
@@ -99,6 +101,8 @@ class FlatAdamW(torch.optim.Optimizer):
         each averaged bucket; the clip coefficient stays on the device and is applied inside the
         next ``step()`` — no host synchronisation.  Returns the total norm (device tensor)."""
         sq = None
+        if hasattr(self.ddp, "wait_grads"):
+            self.ddp.wait_grads()
         for b in self.ddp.buckets:
             n = ops.tensor_summary_raw(self._grad(b))[4]
             sq = n * n if sq is None else sq + n * n

@@ -65,6 +65,7 @@ class _Bucket:
     lo: int = 0
     grad_shard: Optional[torch.Tensor] = None
     gather_work: Any = None
+    done: Any = None  # side-stream mode: event recorded after this bucket's collective
 
 
 class DistributedDataParallel(torch.nn.Module):
@@ -126,6 +127,16 @@ class DistributedDataParallel(torch.nn.Module):
                 self._bucket_of[id(p)] = b
         if flat_params:
             self._rehome_params()
+        # grad_mode="bucket" on the side stream: the optimizer waits for each bucket's own
+        # collective (an event per bucket) instead of the whole comm stream, so the first
+        # buckets' updates overlap the last buckets' all-reduces — at world > 1 the last bucket
+        # (the tied embedding / LM head, finished only when backward ends) is never overlapped
+        # by backward itself
+        self._per_bucket_wait = self.comm_stream is not None and grad_mode == "bucket"
+        self._joined = True
+        if self._per_bucket_wait:
+            for b in self.buckets:
+                b.done = torch.cuda.Event()
 
         self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in self.params]
         if init_sync and self.world > 1:
@@ -185,6 +196,18 @@ class DistributedDataParallel(torch.nn.Module):
         parameters directly)."""
         self._wait_gathers(self.buckets)
 
+    def wait_grad(self, b: _Bucket) -> None:
+        """Make the current stream wait until bucket ``b``'s averaged gradient is in place
+        (``b.buffer`` / ``b.grad_shard``; a no-op unless the side stream defers the join)."""
+        if not self._joined and b.done is not None:
+            torch.cuda.current_stream(self.device).wait_event(b.done)
+
+    def wait_grads(self) -> None:
+        """Make the current stream wait for every bucket's gradient collective."""
+        if not self._joined:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+            self._joined = True
+
     def _reduce(self, b: _Bucket):
         if self.shard:  # ZeRO-2: this rank keeps the averaged gradient of its slice only
             return dist.reduce_scatter_tensor(b.grad_shard, b.buffer, group=self.pg, async_op=True)
@@ -223,6 +246,7 @@ class DistributedDataParallel(torch.nn.Module):
         # a capture crashes hipStreamEndCapture on this stack (benchmarks/graph_probe.py "side").
         self._capturing = self.cuda and torch.cuda.is_current_stream_capturing()
         self._side = self.comm_stream is not None and not self._capturing
+        self._joined = True  # (re)set by _finalize; under capture every wait stays in the graph
         for b in self.buckets:
             b.pending = len(b.params)
             b.ready = b.launched = False
@@ -277,6 +301,8 @@ class DistributedDataParallel(torch.nn.Module):
                 b.work.wait()  # device-side: the comm stream waits for RCCL's stream
                 if unflatten:
                     ops.bucket_unflatten(b.buffer, grads, b.offsets)
+                if self._per_bucket_wait:
+                    b.done.record(self.comm_stream)
             for g in grads:
                 g.record_stream(self.comm_stream)
         else:
@@ -297,7 +323,9 @@ class DistributedDataParallel(torch.nn.Module):
             if not b.ready:
                 b.ready = True
         self._launch_ready()
-        if self.cuda and self._side:
+        if self.cuda and self._side and self._per_bucket_wait:
+            self._joined = False  # consumers wait per bucket: wait_grad(b) / wait_grads()
+        elif self.cuda and self._side:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
         else:
             for b in self.buckets:
