@@ -1,0 +1,377 @@
+// decode.hip — single-token (decode) attention over a KV cache for generation, gfx950.
+//
+// One new token per sequence: its packed projection row qkv[b] = [q (H·64) | k (Hkv·64) | v (Hkv·64)]
+// attends to cache rows 0..pos[b] of its key/value heads, where row pos[b] IS the new token: the
+// kernel writes its (RoPE-rotated) k and v into the cache and uses the register copies for that
+// key, so append + attention are one launch.  The work is pure streaming (each cached key is 256 B
+// of bf16 K+V read once for G = H/Hkv query heads: G FLOP/B), so the design is about keeping HBM
+// busy, not MFMA:
+//
+//   * grid = B · Hkv · nchunks workgroups; a workgroup owns one key/value head of one sequence and
+//     one chunk of keys (flash-decoding split): the host sizes chunks so a short batch still puts
+//     ≥ 2 workgroups on each of the 256 CUs;
+//   * 256 threads = 32 groups of 8 lanes; a group walks keys grp, grp+32, …  with each lane
+//     holding 8 of the 64 dims, so one wave-instruction loads 8 consecutive 128-B rows (1 KiB,
+//     coalesced); 4 keys per group are in flight per iteration (8 × 16-B loads per lane);
+//   * q·k is an 8-lane sum over DPP (quad_perm xor 1, xor 2, then row_half_mirror) — no LDS;
+//   * online softmax in the exp2 domain per group; groups merge across a wave by lane shuffles
+//     and across the 4 waves through 4 KiB·G of LDS;
+//   * with more than one chunk, each writes its partial (o/l in fp32, log2-sum-exp) and a second
+//     small kernel merges them.  (Merging in the last-arriving chunk instead needs an agent-scope
+//     release/acquire, which on gfx950 is an L2 writeback + invalidate per workgroup — the XCDs'
+//     L2s are not coherent with each other — and measured 3-10x slower than the extra launch.)
+//     The grid shapes depend only on the host's key bound, so a decode step captures into a HIP
+//     graph with the positions living on the device.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "nbd_common.h"
+
+namespace nbd {
+namespace decode {
+
+constexpr int D = 64;
+constexpr int NT = 256;
+constexpr int NW = NT / kWave;  // 4 waves
+constexpr int NG = NT / 8;      // 32 lane groups
+constexpr float kLog2e = 1.4426950408889634f;
+
+struct Params {
+  const uint16_t* qkv;  // [B, W] bf16 rows (row stride qkv_ld elements)
+  int64_t qkv_ld;
+  uint16_t* kc;  // [B, Hkv, Tmax, 64] bf16
+  uint16_t* vc;
+  const int64_t* pos;  // [B]
+  const float* cos;    // [>= Tmax, 32] or nullptr
+  const float* sin;
+  uint16_t* out;  // [B, H·64] bf16
+  float* part_o;  // [B, H, nchunks, 64]
+  float* part_l;  // [B, H, nchunks]
+  int H, Hkv, Tmax, nchunks, chunk;
+  float scale2;  // softmax scale · log2(e)
+};
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// sum over the 8 lanes of a group; every lane gets the total
+__device__ __forceinline__ float sum8(float v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]: xor 1
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]: xor 2
+  v += dpp<0x141>(v);  // row_half_mirror: lane i <- 7-i, i.e. the other quad of the 8
+  return v;
+}
+
+__device__ __forceinline__ void unpack8(const u32x4& w, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
+  u32x4 w;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = (uint32_t)f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
+  return w;
+}
+
+// HF rotate_half RoPE on this lane's 8 dims [8·d8, 8·d8+8); the partner dims (±32) sit in lane d8^4
+__device__ __forceinline__ void rope_lane(float (&x)[8], const float* cos, const float* sin, int64_t t, int d8) {
+  const float4* c4 = reinterpret_cast<const float4*>(cos + t * 32 + (d8 & 3) * 8);
+  const float4* s4 = reinterpret_cast<const float4*>(sin + t * 32 + (d8 & 3) * 8);
+  const float4 ca = c4[0], cb = c4[1], sa = s4[0], sb = s4[1];
+  const float c[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
+  const float s[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+  const float sg = d8 < 4 ? -1.f : 1.f;  // x1·c − x2·s  |  x2·c + x1·s
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float y = __shfl_xor(x[e], 4, kWave);
+    x[e] = x[e] * c[e] + sg * y * s[e];
+  }
+}
+
+template <int G>
+__global__ __launch_bounds__(NT) void decode_kernel(Params p) {
+  constexpr int U = G <= 4 ? 4 : 2;  // keys in flight per group
+  __shared__ float sm_m[NW][G], sm_l[NW][G];
+  __shared__ float sm_o[NW][G][D];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = tid >> 3, d8 = tid & 7;
+  const int c = blockIdx.x % p.nchunks;
+  const int bh = blockIdx.x / p.nchunks;
+  const int b = bh / p.Hkv, kvh = bh % p.Hkv;
+  const int pos = (int)min<int64_t>(max<int64_t>(p.pos[b], 0), p.Tmax - 1);
+  const int len = pos + 1;
+  const int c0 = c * p.chunk;
+  const int c1 = min(c0 + p.chunk, len);
+
+  // queries of the G heads sharing this kv head (scaled into the exp2 domain), and the new k / v
+  const uint16_t* row = p.qkv + (int64_t)b * p.qkv_ld;
+  float q[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    load8<bf16_t>(reinterpret_cast<const bf16_t*>(row + (kvh * G + g) * D + d8 * 8), q[g]);
+    if (p.cos != nullptr) rope_lane(q[g], p.cos, p.sin, pos, d8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[g][e] *= p.scale2;
+  }
+  const int64_t head_base = ((int64_t)b * p.Hkv + kvh) * p.Tmax * D;
+  u32x4 knew, vnew;
+  {
+    float kf[8];
+    load8<bf16_t>(reinterpret_cast<const bf16_t*>(row + (p.H + kvh) * D + d8 * 8), kf);
+    if (p.cos != nullptr) rope_lane(kf, p.cos, p.sin, pos, d8);
+    knew = pack8(kf);
+    vnew = *reinterpret_cast<const u32x4*>(row + (p.H + p.Hkv + kvh) * D + d8 * 8);
+  }
+  if (c0 <= pos && pos < c0 + p.chunk && grp == 0) {  // this chunk owns the new row
+    *reinterpret_cast<u32x4*>(p.kc + head_base + (int64_t)pos * D + d8 * 8) = knew;
+    *reinterpret_cast<u32x4*>(p.vc + head_base + (int64_t)pos * D + d8 * 8) = vnew;
+  }
+
+  float m[G], l[G], o[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    m[g] = -INFINITY;
+    l[g] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[g][e] = 0.f;
+  }
+
+  if (c0 < c1) {
+    const uint16_t* kb = p.kc + head_base + d8 * 8;
+    const uint16_t* vb = p.vc + head_base + d8 * 8;
+    const int iters = (c1 - c0 + NG * U - 1) / (NG * U);
+    for (int it = 0; it < iters; ++it) {
+      int j[U];
+      u32x4 kr[U], vr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        j[u] = c0 + grp + NG * (it * U + u);
+        const int jj = j[u] < c1 ? j[u] : c0;  // in-bounds address for a masked key
+        kr[u] = *reinterpret_cast<const u32x4*>(kb + (int64_t)jj * D);
+        vr[u] = *reinterpret_cast<const u32x4*>(vb + (int64_t)jj * D);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j[u] == pos) {  // the new token: its row in memory may predate this launch's write
+          kr[u] = knew;
+          vr[u] = vnew;
+        }
+      float s[U][G];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float kf[8];
+        unpack8(kr[u], kf);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          float acc = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc += q[g][e] * kf[e];
+          acc = sum8(acc);
+          s[u][g] = j[u] < c1 ? acc : -INFINITY;
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float mx = m[g];
+#pragma unroll
+        for (int u = 0; u < U; ++u) mx = fmaxf(mx, s[u][g]);
+        const float ms = mx == -INFINITY ? 0.f : mx;
+        const float corr = exp2f(m[g] - ms);
+        l[g] *= corr;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[g][e] *= corr;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float pu = exp2f(s[u][g] - ms);
+          l[g] += pu;
+          float vf[8];
+          unpack8(vr[u], vf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[g][e] += pu * vf[e];
+        }
+        m[g] = mx;
+      }
+    }
+  }
+
+  // merge the 8 groups of this wave (lanes d8, d8+8, …, d8+56)
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float mx = m[g];
+    mx = fmaxf(mx, __shfl_xor(mx, 8, kWave));
+    mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+    const float w = mx == -INFINITY ? 0.f : exp2f(m[g] - mx);
+    float lg = l[g] * w;
+    lg += __shfl_xor(lg, 8, kWave);
+    lg += __shfl_xor(lg, 16, kWave);
+    lg += __shfl_xor(lg, 32, kWave);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = o[g][e] * w;
+      x += __shfl_xor(x, 8, kWave);
+      x += __shfl_xor(x, 16, kWave);
+      x += __shfl_xor(x, 32, kWave);
+      o[g][e] = x;
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sm_o[wave][g][lane * 8 + e] = o[g][e];
+      if (lane == 0) {
+        sm_m[wave][g] = mx;
+        sm_l[wave][g] = lg;
+      }
+    }
+  }
+  __syncthreads();
+
+  // merge the 4 waves: wave 0, lane = dim
+  const int H = p.H;
+  if (wave == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) mx = fmaxf(mx, sm_m[w][g]);
+      float L = 0.f, O = 0.f;
+      if (mx != -INFINITY) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const float sc = exp2f(sm_m[w][g] - mx);
+          L += sm_l[w][g] * sc;
+          O += sm_o[w][g][lane] * sc;
+        }
+      }
+      const int h = kvh * G + g;
+      if (p.nchunks == 1) {
+        p.out[(int64_t)b * H * D + h * D + lane] = f32_to_bf16(O / L);
+      } else {
+        const int64_t r = ((int64_t)b * H + h) * p.nchunks + c;
+        p.part_o[r * D + lane] = L > 0.f ? O / L : 0.f;
+        if (lane == 0) p.part_l[r] = L > 0.f ? mx + __log2f(L) : -INFINITY;
+      }
+    }
+  }
+}
+
+// merge the chunk partials of one (b, head) row: one wave, lane = dim
+__global__ __launch_bounds__(kWave) void merge_kernel(Params p) {
+  const int r = blockIdx.x, lane = threadIdx.x;  // r = b·H + h
+  const int64_t r0 = (int64_t)r * p.nchunks;
+  float mx = -INFINITY;
+  for (int k = 0; k < p.nchunks; ++k) mx = fmaxf(mx, p.part_l[r0 + k]);
+  float L = 0.f, O = 0.f;
+  for (int k = 0; k < p.nchunks; ++k) {
+    const float lk = p.part_l[r0 + k];
+    if (lk == -INFINITY) continue;
+    const float w = exp2f(lk - mx);
+    L += w;
+    O += w * p.part_o[(r0 + k) * D + lane];
+  }
+  p.out[(int64_t)r * D + lane] = f32_to_bf16(O / L);
+}
+
+// chunking: enough workgroups for the chip (≥ 512 when the batch allows), ≥ 128 keys per chunk
+static void plan(int64_t BHkv, int64_t kv_len, int& nchunks, int& chunk) {
+  int64_t nc = std::max<int64_t>(1, (512 + BHkv - 1) / BHkv);
+  nc = std::min<int64_t>(nc, std::max<int64_t>(1, (kv_len + 127) / 128));
+  nc = std::min<int64_t>(nc, 64);
+  int64_t ch = (kv_len + nc - 1) / nc;
+  ch = (ch + NG - 1) / NG * NG;
+  nchunks = (int)((kv_len + ch - 1) / ch);
+  chunk = (int)ch;
+}
+
+at::Tensor decode_attn_hip(const at::Tensor& qkv, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                           const at::Tensor& pos, int64_t n_head, double scale, int64_t kv_len_max,
+                           const c10::optional<at::Tensor>& rope_cos, const c10::optional<at::Tensor>& rope_sin,
+                           const at::Tensor& partials) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 2 && qkv.stride(1) == 1 &&
+                  qkv.stride(0) % 8 == 0 && ((uintptr_t)qkv.data_ptr() & 15) == 0,
+              "decode_attn: qkv must be a bf16 [B, (H + 2·Hkv)·64] GPU view, unit last stride, 16-B aligned rows");
+  TORCH_CHECK(k_cache.is_cuda() && k_cache.scalar_type() == at::kBFloat16 && k_cache.is_contiguous() &&
+                  k_cache.dim() == 4 && k_cache.size(3) == D && v_cache.sizes() == k_cache.sizes() &&
+                  v_cache.scalar_type() == at::kBFloat16 && v_cache.is_contiguous() &&
+                  ((uintptr_t)k_cache.data_ptr() & 15) == 0 && ((uintptr_t)v_cache.data_ptr() & 15) == 0,
+              "decode_attn: caches must be contiguous bf16 [B, Hkv, Tmax, 64]");
+  const int64_t B = qkv.size(0), Hkv = k_cache.size(1), Tmax = k_cache.size(2), H = n_head;
+  TORCH_CHECK(k_cache.size(0) == B, "decode_attn: cache batch ", k_cache.size(0), " != ", B);
+  TORCH_CHECK(H > 0 && Hkv > 0 && H % Hkv == 0 && H / Hkv <= 8, "decode_attn: need H % Hkv == 0 and H / Hkv <= 8");
+  TORCH_CHECK(qkv.size(1) == (H + 2 * Hkv) * D, "decode_attn: qkv width ", qkv.size(1), " != (H + 2·Hkv)·64");
+  TORCH_CHECK(pos.is_cuda() && pos.scalar_type() == at::kLong && pos.is_contiguous() && pos.numel() == B,
+              "decode_attn: pos must be a contiguous int64 [B] GPU tensor");
+  TORCH_CHECK(kv_len_max >= 1 && kv_len_max <= Tmax, "decode_attn: kv_len_max must be in [1, Tmax]");
+  const bool hc = rope_cos.has_value() && rope_cos->defined(), hs = rope_sin.has_value() && rope_sin->defined();
+  TORCH_CHECK(hc == hs, "decode_attn: rope_cos and rope_sin go together");
+  if (hc)
+    TORCH_CHECK(rope_cos->is_cuda() && rope_cos->scalar_type() == at::kFloat && rope_cos->is_contiguous() &&
+                    rope_cos->dim() == 2 && rope_cos->size(1) == D / 2 && rope_cos->size(0) >= Tmax &&
+                    rope_sin->sizes() == rope_cos->sizes() && rope_sin->is_contiguous() &&
+                    rope_sin->scalar_type() == at::kFloat,
+                "decode_attn: rope tables must be contiguous float32 [>= Tmax, 32]");
+  int nchunks, chunk;
+  plan(B * Hkv, kv_len_max, nchunks, chunk);
+  TORCH_CHECK(partials.is_cuda() && partials.scalar_type() == at::kFloat && partials.is_contiguous() &&
+                  partials.numel() >= B * H * nchunks * (D + 1),
+              "decode_attn: partials too small: need ", B * H * nchunks * (D + 1), " floats");
+  TORCH_CHECK(B * Hkv * nchunks < (1LL << 31) && Tmax * D * B * Hkv < (1LL << 62), "decode_attn: grid too large");
+  at::Tensor out = at::empty({B, H * D}, qkv.options().memory_format(at::MemoryFormat::Contiguous));
+  Params p;
+  p.qkv = static_cast<const uint16_t*>(qkv.data_ptr());
+  p.qkv_ld = qkv.stride(0);
+  p.kc = static_cast<uint16_t*>(k_cache.data_ptr());
+  p.vc = static_cast<uint16_t*>(v_cache.data_ptr());
+  p.pos = pos.data_ptr<int64_t>();
+  p.cos = hc ? rope_cos->data_ptr<float>() : nullptr;
+  p.sin = hc ? rope_sin->data_ptr<float>() : nullptr;
+  p.out = static_cast<uint16_t*>(out.data_ptr());
+  p.part_o = partials.data_ptr<float>();
+  p.part_l = p.part_o + B * H * nchunks * D;
+  p.H = (int)H;
+  p.Hkv = (int)Hkv;
+  p.Tmax = (int)Tmax;
+  p.nchunks = nchunks;
+  p.chunk = chunk;
+  p.scale2 = (float)scale * kLog2e;
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  const dim3 grid((unsigned)(B * Hkv * nchunks));
+  switch (H / Hkv) {
+#define NBD_DECODE_G(g) \
+  case g:               \
+    hipLaunchKernelGGL((decode_kernel<g>), grid, dim3(NT), 0, st, p); \
+    break;
+    NBD_DECODE_G(1)
+    NBD_DECODE_G(2)
+    NBD_DECODE_G(3)
+    NBD_DECODE_G(4)
+    NBD_DECODE_G(5)
+    NBD_DECODE_G(6)
+    NBD_DECODE_G(7)
+    NBD_DECODE_G(8)
+#undef NBD_DECODE_G
+  }
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  if (nchunks > 1) {
+    hipLaunchKernelGGL(merge_kernel, dim3((unsigned)(B * H)), dim3(kWave), 0, st, p);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+  return out;
+}
+
+}  // namespace decode
+}  // namespace nbd
+
+TORCH_LIBRARY_IMPL(nbd, CUDA, m) { m.impl("decode_attn", &nbd::decode::decode_attn_hip); }

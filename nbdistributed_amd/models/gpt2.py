@@ -54,15 +54,20 @@ class CausalSelfAttention(nn.Module):
         self.dropout = c.dropout
         self.hip_gemm = c.hip_gemm
 
-    def forward(self, x: torch.Tensor, fast: bool = False) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, fast: bool = False, kv=None) -> torch.Tensor:
+        """``kv`` = (KVCache, layer): prefill for generation (k and v of every position stored)."""
         B, T, C = x.shape
         if fast:  # HIP path: bias grads by the column-sum kernel, flash attention on the packed QKV
             from .. import ops
 
             lin = ops.gemm_linear if self.hip_gemm else ops.linear
             qkv = lin(x, self.c_attn.weight, self.c_attn.bias)
+            if kv is not None:
+                kv[0].store(kv[1], qkv)
             return lin(ops.attention_qkv(qkv, self.n_head, causal=True), self.c_proj.weight, self.c_proj.bias)
         qkv = self.c_attn(x)
+        if kv is not None:
+            kv[0].store(kv[1], qkv)
         if self.fused and qkv.is_cuda and (self.dropout == 0.0 or not self.training):
             from .. import ops
 
@@ -103,8 +108,9 @@ class Block(nn.Module):
         self.ln_2 = nn.LayerNorm(c.n_embd, bias=c.bias)
         self.mlp = MLP(c)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = x + self.attn(self.ln_1(x))
+    def forward(self, x: torch.Tensor, kv=None) -> torch.Tensor:
+        h = self.ln_1(x)
+        x = x + (self.attn(h) if kv is None else self.attn(h, kv=kv))
         return x + self.mlp(self.ln_2(x))
 
 
@@ -153,11 +159,10 @@ class GPT2(nn.Module):
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
-    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None, return_logits: bool = True):
-        """Returns (logits, loss).  With ``targets`` and ``return_logits=False`` the logits are
-        not returned (None) and the fused loss writes its gradient over their storage."""
+    def _trunk(self, idx: torch.Tensor, cache=None):
+        """Final-normed hidden states [B, T, C] (and whether the HIP fast path ran); ``cache``
+        (a ``generation.KVCache``) receives every layer's k / v."""
         B, T = idx.shape
-        cp = getattr(self, "context_group", None)  # set by parallel.context: (group,)
         pos_fn = getattr(self, "position_ids", None)  # set by parallel.context (global positions)
         pos = pos_fn(T, idx.device) if pos_fn is not None else torch.arange(T, device=idx.device)
         if self._fast_ok(idx):
@@ -175,20 +180,31 @@ class GPT2(nn.Module):
             ln = self.h[0].ln_1
             h = ops.layer_norm(x, ln.weight, ln.bias, ln.eps)
             for i, blk in enumerate(self.h):
-                x, h = ops.add_layer_norm(x, blk.attn(h, fast=self.fused_attn_ok), blk.ln_2.weight, blk.ln_2.bias,
-                                          blk.ln_2.eps)
+                fa = self.fused_attn_ok
+                a = blk.attn(h, fast=fa) if cache is None else blk.attn(h, fast=fa, kv=(cache, i))
+                x, h = ops.add_layer_norm(x, a, blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps)
                 nxt = self.h[i + 1].ln_1 if i + 1 < c.n_layer else self.ln_f
                 x, h = ops.add_layer_norm(x, blk.mlp(h, fast=True), nxt.weight, nxt.bias, nxt.eps)
-            if targets is not None and not return_logits and c.fused_ce and ops.loss.FUSED_XENT:
+            return h, True
+        for i, blk in enumerate(self.h):
+            x = blk(x) if cache is None else blk(x, kv=(cache, i))
+        return self.ln_f(x), False
+
+    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None, return_logits: bool = True):
+        """Returns (logits, loss).  With ``targets`` and ``return_logits=False`` the logits are
+        not returned (None) and the fused loss writes its gradient over their storage."""
+        cp = getattr(self, "context_group", None)  # set by parallel.context: (group,)
+        h, fast = self._trunk(idx)
+        c = self.config
+        if fast and targets is not None and not return_logits and c.fused_ce:
+            from .. import ops
+
+            if ops.loss.FUSED_XENT:
                 # LM head + loss: one pass over the logits for the loss forward and backward
                 red = "sum" if cp is not None else "mean"
                 return None, self._cp_loss(ops.linear_cross_entropy(h, self.lm_head.weight, targets, reduction=red),
                                            targets, cp)
-            logits = self.lm_head(h)
-        else:
-            for blk in self.h:
-                x = blk(x)
-            logits = self.lm_head(self.ln_f(x))
+        logits = self.lm_head(h)
         loss = None
         if targets is not None:
             flat, tgt = logits.view(-1, logits.size(-1)), targets.reshape(-1)
@@ -201,6 +217,58 @@ class GPT2(nn.Module):
                 loss = F.cross_entropy(flat.float(), tgt, reduction=red)
             loss = self._cp_loss(loss, targets, cp)
         return (logits if return_logits or targets is None else None), loss
+
+    # ------------------------------------------------------------------ generation (generation.py)
+    def kv_layout(self):
+        c = self.config
+        return c.n_layer, c.n_head, c.n_head, c.n_embd // c.n_head
+
+    def max_positions(self) -> int:
+        return self.config.n_positions
+
+    def prefill_length(self, T: int) -> int:
+        """Prompt length the prefill runs at: a multiple of 128 where that selects the HIP path."""
+        p = self.wte.weight
+        return -(-T // 128) * 128 if p.is_cuda and p.dtype in (torch.bfloat16, torch.float16) else T
+
+    @torch.no_grad()
+    def prefill(self, idx: torch.Tensor, cache, lengths: torch.Tensor) -> torch.Tensor:
+        """Run the prompts (right-padded), fill ``cache``; logits [B, V] at positions lengths-1."""
+        h, _ = self._trunk(idx, cache)
+        B, _, C = h.shape
+        last = torch.gather(h, 1, (lengths - 1).view(B, 1, 1).expand(B, 1, C)).squeeze(1)
+        return self.lm_head(last)
+
+    @torch.no_grad()
+    def decode_step(self, tok: torch.Tensor, pos: torch.Tensor, cache) -> torch.Tensor:
+        """Logits [B, V] of one new token per sequence (``tok``, ``pos``: int64 [B]); appends to
+        ``cache``.  Device-side only (graph-capturable)."""
+        from .. import ops
+
+        c = self.config
+        if self._fast_ok(tok):
+            x = ops.embedding_tok_pos(tok.view(1, -1), self.wte.weight, pos, self.wpe.weight).view(-1, c.n_embd)
+        else:
+            x = self.wte(tok) + self.wpe(pos)
+        ln = self.h[0].ln_1
+        h = ops.layer_norm(x, ln.weight, ln.bias, ln.eps)
+        for i, blk in enumerate(self.h):
+            at = blk.attn
+            qkv = F.linear(h, at.c_attn.weight, at.c_attn.bias)
+            a = cache.attend(i, qkv, pos)
+            x, h = ops.add_layer_norm(x, F.linear(a, at.c_proj.weight, at.c_proj.bias), blk.ln_2.weight,
+                                      blk.ln_2.bias, blk.ln_2.eps)
+            m = blk.mlp
+            y = ops.mlp_gelu(h, m.c_fc.weight, m.c_fc.bias, m.c_proj.weight, m.c_proj.bias)
+            nxt = self.h[i + 1].ln_1 if i + 1 < c.n_layer else self.ln_f
+            x, h = ops.add_layer_norm(x, y, nxt.weight, nxt.bias, nxt.eps)
+        return self.lm_head(h)
+
+    def generate(self, idx: torch.Tensor, max_new_tokens: int, **kw) -> torch.Tensor:
+        """``generation.generate`` (KV cache, HIP decode attention, graph-captured decode loop)."""
+        from ..generation import generate
+
+        return generate(self, idx, max_new_tokens, **kw)
 
     @staticmethod
     def _cp_loss(loss, targets, cp):

@@ -91,9 +91,11 @@ class LlamaAttention(nn.Module):
         self.qkv_proj = nn.Linear(c.hidden_size, (self.H + 2 * self.Hkv) * self.D, bias=False)
         self.o_proj = nn.Linear(self.H * self.D, c.hidden_size, bias=False)
 
-    def forward(self, x, cos, sin):
+    def forward(self, x, cos, sin, kv=None):
         # RoPE is applied inside the attention kernels on the HIP path (rope_ + SDPA otherwise)
         qkv = ops.gemm_linear(x, self.qkv_proj.weight)  # HIP MFMA GEMM on GPU bf16, F.linear otherwise
+        if kv is not None:  # (KVCache, layer): generation prefill, before anything rotates qkv in place
+            kv[0].store(kv[1], qkv, rope=(cos, sin))
         a = ops.attention_qkv(qkv, self.H, causal=True, n_kv_head=self.Hkv, rope=(cos, sin))
         return ops.gemm_linear(a, self.o_proj.weight)
 
@@ -135,7 +137,8 @@ class LlamaModel(nn.Module):
             self._rope[key] = ops.rope_tables(T, self.config.head_dim, self.config.rope_theta, device)
         return self._rope[key]
 
-    def forward(self, input_ids):
+    def forward(self, input_ids, cache=None):
+        """``cache`` (a ``generation.KVCache``) receives every layer's rotated k and v."""
         c = self.config
         T = input_ids.shape[1]
         cos, sin = self.rope(T, input_ids.device)
@@ -143,7 +146,7 @@ class LlamaModel(nn.Module):
         # the residual stream: each block's two residual adds are fused with the RMSNorm after them
         h = self.layers[0].input_layernorm(x)
         for i, layer in enumerate(self.layers):
-            a = layer.self_attn(h, cos, sin)
+            a = layer.self_attn(h, cos, sin) if cache is None else layer.self_attn(h, cos, sin, kv=(cache, i))
             x, h = ops.add_rms_norm(x, a, layer.post_attention_layernorm.weight, c.rms_norm_eps)
             m = layer.mlp(h)
             nxt = self.layers[i + 1].input_layernorm if i + 1 < len(self.layers) else self.norm
@@ -222,6 +225,51 @@ class LlamaForCausalLM(_LlamaPreTrained):
 
                 loss = context_loss(loss, (tgt != -100).sum(), cp[0])
         return loss, (logits if return_logits else None)
+
+    # ------------------------------------------------------------------ generation (generation.py)
+    def kv_layout(self):
+        c = self.config
+        return c.num_hidden_layers, c.num_attention_heads, c.num_key_value_heads, c.head_dim
+
+    def max_positions(self) -> int:
+        return self.config.max_position_embeddings
+
+    def prefill_length(self, T: int) -> int:
+        """Prompt length the prefill runs at: a multiple of 128 where that selects the HIP path."""
+        p = self.lm_head.weight
+        return -(-T // 128) * 128 if p.is_cuda and p.dtype in (torch.bfloat16, torch.float16) else T
+
+    @torch.no_grad()
+    def prefill(self, input_ids, cache, lengths):
+        """Run the prompts (right-padded), fill ``cache``; logits [B, V] at positions lengths-1."""
+        h = self.model(input_ids, cache=cache)
+        B, _, C = h.shape
+        last = torch.gather(h, 1, (lengths - 1).view(B, 1, 1).expand(B, 1, C)).squeeze(1)
+        return self.lm_head(last)
+
+    @torch.no_grad()
+    def decode_step(self, tok, pos, cache):
+        """Logits [B, V] of one new token per sequence (``tok``, ``pos``: int64 [B]); appends to
+        ``cache``.  Device-side only (graph-capturable)."""
+        m, c = self.model, self.config
+        rope = m.rope(cache.t_max, tok.device)
+        x = ops.embedding(tok, m.embed_tokens.weight)
+        h = m.layers[0].input_layernorm(x)
+        for i, layer in enumerate(m.layers):
+            at = layer.self_attn
+            a = cache.attend(i, F.linear(h, at.qkv_proj.weight), pos, rope=rope)
+            x, h = ops.add_rms_norm(x, F.linear(a, at.o_proj.weight), layer.post_attention_layernorm.weight,
+                                    c.rms_norm_eps)
+            y = ops.mlp_swiglu(h, layer.mlp.gate_up_proj.weight, layer.mlp.down_proj.weight)
+            nxt = m.layers[i + 1].input_layernorm if i + 1 < len(m.layers) else m.norm
+            x, h = ops.add_rms_norm(x, y, nxt.weight, c.rms_norm_eps)
+        return self.lm_head(h)
+
+    def generate(self, input_ids, max_new_tokens: int, **kw):
+        """``generation.generate`` (KV cache, HIP decode attention, graph-captured decode loop)."""
+        from ..generation import generate
+
+        return generate(self, input_ids, max_new_tokens, **kw)
 
 
 # ---------------------------------------------------------------------------- HF interop

@@ -1,0 +1,88 @@
+"""Decode attention over a KV cache (K13): one new token per sequence, cache append fused.
+
+``csrc/kernels/decode.hip`` on GPU (bf16, head dim 64, up to 8 query heads per key/value head);
+the same math in PyTorch otherwise (CPU, fp32) — also the numerics reference of the GPU tests.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+from ._lib import _require
+
+
+def partials_numel(batch: int, n_head: int, t_max: int) -> int:
+    """fp32 workspace the kernel needs for its chunk partials (worst case over key bounds ≤ ``t_max``)."""
+    nchunks = min(64, max(1, -(-t_max // 128)))
+    return batch * n_head * nchunks * 65
+
+
+def decode_supported(qkv, k_cache, n_head: int) -> bool:
+    import torch
+
+    Hkv = k_cache.shape[1]
+    return (qkv.is_cuda and qkv.dtype == torch.bfloat16 and k_cache.dtype == torch.bfloat16
+            and k_cache.shape[-1] == 64 and n_head % Hkv == 0 and n_head // Hkv <= 8)
+
+
+def _rope_at(x, cos, sin, pos):
+    """HF rotate_half RoPE of x [B, h, D] at per-row positions pos [B] (fp32 math)."""
+    import torch
+
+    half = x.shape[-1] // 2
+    c, s = cos[pos][:, None, :], sin[pos][:, None, :]
+    a, b = x[..., :half].float(), x[..., half:].float()
+    return torch.cat([a * c - b * s, b * c + a * s], -1)
+
+
+def decode_attention_reference(qkv, k_cache, v_cache, pos, n_head: int, scale: Optional[float] = None, rope=None):
+    """PyTorch version of :func:`decode_attention` (writes the caches the same way)."""
+    import torch
+
+    B, W = qkv.shape
+    Hkv, Tmax, D = k_cache.shape[1], k_cache.shape[2], k_cache.shape[3]
+    H, G = n_head, n_head // Hkv
+    sc = float(scale) if scale is not None else D ** -0.5
+    pos = pos.long().clamp(0, Tmax - 1)
+    q = qkv[:, : H * D].view(B, H, D)
+    k = qkv[:, H * D:(H + Hkv) * D].view(B, Hkv, D)
+    v = qkv[:, (H + Hkv) * D:].view(B, Hkv, D)
+    if rope is not None:
+        q = _rope_at(q, rope[0], rope[1], pos)
+        k = _rope_at(k, rope[0], rope[1], pos)
+    bi = torch.arange(B, device=qkv.device)
+    k_cache[bi, :, pos] = k.to(k_cache.dtype)
+    v_cache[bi, :, pos] = v.to(v_cache.dtype)
+    s = torch.einsum("bkgd,bktd->bkgt", q.float().view(B, Hkv, G, D), k_cache.float()) * sc
+    mask = torch.arange(Tmax, device=qkv.device)[None, :] > pos[:, None]  # [B, Tmax]
+    s = s.masked_fill(mask[:, None, None, :], float("-inf"))
+    p = torch.softmax(s, -1)
+    o = torch.einsum("bkgt,bktd->bkgd", p, v_cache.float())
+    return o.reshape(B, H * D).to(qkv.dtype)
+
+
+def decode_attention(qkv, k_cache, v_cache, pos, n_head: int, scale: Optional[float] = None, rope=None,
+                     kv_len_max: Optional[int] = None, workspace=None):
+    """Attention of one new token per sequence over its KV cache.
+
+    ``qkv`` [B, (H + 2·Hkv)·D] is the new tokens' packed projection, ``k_cache``/``v_cache``
+    [B, Hkv, Tmax, D] the caches (rows ≥ ``pos[b]`` are free), ``pos`` int64 [B] the new tokens'
+    positions (on the device: a decode step graph-captures).  The new k (rotated when ``rope`` =
+    (cos, sin) tables) and v are written into the caches at ``pos[b]`` and the token attends to
+    rows 0..pos[b].  ``kv_len_max`` bounds max(pos) + 1 (default Tmax; smaller = fewer idle
+    workgroups); ``workspace`` = fp32 chunk partials [≥ :func:`partials_numel`] (held by
+    ``generation.KVCache``; allocated per call if None).  Returns [B, H·D]."""
+    import torch
+
+    D = k_cache.shape[-1]
+    sc = float(scale) if scale is not None else D ** -0.5
+    if decode_supported(qkv, k_cache, n_head):
+        _require()
+        B, Tmax = k_cache.shape[0], k_cache.shape[2]
+        if workspace is None:
+            workspace = torch.empty(partials_numel(B, n_head, Tmax), dtype=torch.float32, device=qkv.device)
+        cos, sin = rope if rope is not None else (None, None)
+        if qkv.stride(-1) != 1 or qkv.stride(0) % 8 or qkv.data_ptr() % 16:
+            qkv = qkv.contiguous()
+        return torch.ops.nbd.decode_attn(qkv, k_cache, v_cache, pos, int(n_head), sc, int(kv_len_max or Tmax),
+                                         cos, sin, workspace)
+    return decode_attention_reference(qkv, k_cache, v_cache, pos, n_head, sc, rope)

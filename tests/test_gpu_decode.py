@@ -1,0 +1,118 @@
+"""HIP decode attention (csrc/kernels/decode.hip) vs the fp32 PyTorch reference, and GPU
+generation (KV cache + graph-captured decode loop) vs the full forward pass."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from nbdistributed_amd import ops  # noqa: E402
+from nbdistributed_amd.ops.decode import partials_numel  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(require_gpu):
+    ops.load_library()
+
+
+def _case(B, H, Hkv, Tmax, pos, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    D = 64
+    kc = torch.randn(B, Hkv, Tmax, D, device="cuda", generator=g).to(torch.bfloat16)
+    vc = torch.randn(B, Hkv, Tmax, D, device="cuda", generator=g).to(torch.bfloat16)
+    qkv = torch.randn(B, (H + 2 * Hkv) * D, device="cuda", generator=g).to(torch.bfloat16)
+    return qkv, kc, vc, torch.tensor(pos, device="cuda", dtype=torch.int64)
+
+
+def _ws(B, H, Hkv, Tmax):
+    return torch.empty(partials_numel(B, H, Tmax), dtype=torch.float32, device="cuda")
+
+
+def _check(B, H, Hkv, Tmax, pos, rope=False, kv_len_max=None, seed=0):
+    qkv, kc, vc, p = _case(B, H, Hkv, Tmax, pos, seed)
+    tabs = ops.rope_tables(Tmax, 64, 10000.0, "cuda") if rope else None
+    kr, vr = kc.float(), vc.float()
+    ref = ops.decode_attention_reference(qkv.float(), kr, vr, p, H, rope=tabs)
+    ws = _ws(B, H, Hkv, Tmax)
+    out = ops.decode_attention(qkv, kc, vc, p, H, rope=tabs, kv_len_max=kv_len_max, workspace=ws)
+    assert out.shape == (B, H * 64) and out.dtype == torch.bfloat16
+    err = (out.float() - ref).abs().max().item()
+    assert err < 2e-2, err
+    bi = torch.arange(B, device="cuda")
+    torch.testing.assert_close(kc[bi, :, p].float(), kr[bi, :, p].to(torch.bfloat16).float(), atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(vc[bi, :, p].float(), vr[bi, :, p].to(torch.bfloat16).float(), atol=0, rtol=0)
+    return out
+
+
+@pytest.mark.parametrize("H,Hkv", [(12, 12), (4, 2), (9, 3), (8, 2), (16, 2), (7, 1)])
+@pytest.mark.parametrize("rope", [False, True])
+def test_decode_attention_group_sizes(H, Hkv, rope):
+    _check(3, H, Hkv, 300, [0, 129, 299], rope=rope)
+
+
+@pytest.mark.parametrize("B,Tmax", [(1, 4096), (2, 1024), (64, 256), (8, 2000)])
+def test_decode_attention_chunking(B, Tmax):
+    # one sequence over a long cache: up to 64 key chunks merged by the last one; wide batch: 1 chunk
+    pos = [(Tmax - 1 - 37 * b) % Tmax for b in range(B)]
+    _check(B, 12, 4, Tmax, pos, rope=True, seed=B)
+
+
+def test_decode_attention_host_key_bound_and_replays():
+    # kv_len_max below Tmax (eager generation) and repeated launches on one workspace
+    B, H, Hkv, Tmax = 4, 8, 8, 1024
+    for it, bound in enumerate([1, 17, 200, 1024]):
+        pos = [min(bound - 1, x) for x in (0, 5, 150, 1000)]
+        _check(B, H, Hkv, Tmax, pos, kv_len_max=bound, seed=10 + it)
+
+
+def test_decode_attention_graph_replay():
+    B, H, Hkv, Tmax = 2, 6, 2, 512
+    qkv, kc, vc, p = _case(B, H, Hkv, Tmax, [10, 300])
+    ws = _ws(B, H, Hkv, Tmax)
+    ops.decode_attention(qkv, kc, vc, p, H, workspace=ws)  # warm-up
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = ops.decode_attention(qkv, kc, vc, p, H, workspace=ws)
+    for step in range(3):
+        p.add_(1)
+        kref, vref = kc.float(), vc.float()
+        ref = ops.decode_attention_reference(qkv.float(), kref, vref, p, H)
+        g.replay()
+        assert (out.float() - ref).abs().max().item() < 2e-2
+
+
+def _peaked(model):
+    # scale the embedding (tied LM head) so greedy tokens are far from ties under bf16 rounding
+    with torch.no_grad():
+        emb = model.wte.weight if hasattr(model, "wte") else model.model.embed_tokens.weight
+        emb.mul_(8.0)
+    return model
+
+
+@pytest.mark.parametrize("family", ["gpt2", "llama"])
+def test_gpu_generate_graph_matches_eager_and_full_forward(family):
+    from nbdistributed_amd.models import GPT2, GPT2Config
+    from nbdistributed_amd.models.llama import LlamaConfig, LlamaForCausalLM
+
+    torch.manual_seed(0)
+    if family == "gpt2":
+        m = GPT2(GPT2Config(vocab_size=512, n_positions=512, n_embd=256, n_layer=2, n_head=4))
+    else:
+        m = LlamaForCausalLM(LlamaConfig.tiny())
+    m = _peaked(m.to("cuda", torch.bfloat16).eval())
+    ids = torch.randint(1, 512, (4, 40), device="cuda")
+    lens = torch.tensor([40, 33, 12, 1], device="cuda")
+    eager = m.generate(ids, 24, lengths=lens, graph=False)
+    graphed = m.generate(ids, 24, lengths=lens, graph=True)
+    assert torch.equal(eager, graphed)
+    # decode-step logits vs the full forward over the generated prefix (fp32 tolerance on bf16)
+    from nbdistributed_amd.generation import KVCache
+
+    b = 0
+    seq = eager[b:b + 1, :40 + 24]
+    cache = KVCache.for_model(m, 1, 128)
+    m.prefill(torch.nn.functional.pad(seq[:, :40], (0, 88)), cache, torch.tensor([40], device="cuda"))
+    for t in range(40, 48):
+        lg = m.decode_step(seq[:, t], torch.tensor([t], device="cuda"), cache).float()
+        full = (m(seq[:, :t + 1])[0] if family == "gpt2" else m(seq[:, :t + 1])[1])[0, -1].float()
+        assert (lg[0] - full).abs().max().item() < 0.05 * full.abs().max().item()
+        assert int(lg.argmax()) == int(full.argmax())
