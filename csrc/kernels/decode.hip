@@ -283,11 +283,15 @@ __global__ __launch_bounds__(kWave) void merge_kernel(Params p) {
   p.out[(int64_t)r * D + lane] = f32_to_bf16(O / L);
 }
 
-// chunking: enough workgroups for the chip (≥ 512 when the batch allows), ≥ 128 keys per chunk
+// chunking: enough workgroups for the chip (≥ 512 when the batch allows) with ≥ 256 keys per chunk;
+// no split at all up to 512 keys, where the merge kernel's node would cost more than it saves
 static void plan(int64_t BHkv, int64_t kv_len, int& nchunks, int& chunk) {
-  int64_t nc = std::max<int64_t>(1, (512 + BHkv - 1) / BHkv);
-  nc = std::min<int64_t>(nc, std::max<int64_t>(1, (kv_len + 127) / 128));
-  nc = std::min<int64_t>(nc, 64);
+  int64_t nc = 1;
+  if (kv_len > 512) {
+    nc = std::max<int64_t>(1, (512 + BHkv - 1) / BHkv);
+    nc = std::min<int64_t>(nc, (kv_len + 255) / 256);
+    nc = std::min<int64_t>(nc, 64);
+  }
   int64_t ch = (kv_len + nc - 1) / nc;
   ch = (ch + NG - 1) / NG * NG;
   nchunks = (int)((kv_len + ch - 1) / ch);

@@ -250,19 +250,17 @@ class GPT2(nn.Module):
             x = ops.embedding_tok_pos(tok.view(1, -1), self.wte.weight, pos, self.wpe.weight).view(-1, c.n_embd)
         else:
             x = self.wte(tok) + self.wpe(pos)
-        ln = self.h[0].ln_1
-        h = ops.layer_norm(x, ln.weight, ln.bias, ln.eps)
+        # five fused kernels per block (ops.linear_small: norm prologue, bias / GELU / residual epilogue)
         for i, blk in enumerate(self.h):
-            at = blk.attn
-            qkv = F.linear(h, at.c_attn.weight, at.c_attn.bias)
+            at, m = blk.attn, blk.mlp
+            qkv = ops.linear_small(x, at.c_attn.weight, at.c_attn.bias,
+                                   norm=("ln", blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps))
             a = cache.attend(i, qkv, pos)
-            x, h = ops.add_layer_norm(x, F.linear(a, at.c_proj.weight, at.c_proj.bias), blk.ln_2.weight,
-                                      blk.ln_2.bias, blk.ln_2.eps)
-            m = blk.mlp
-            y = ops.mlp_gelu(h, m.c_fc.weight, m.c_fc.bias, m.c_proj.weight, m.c_proj.bias)
-            nxt = self.h[i + 1].ln_1 if i + 1 < c.n_layer else self.ln_f
-            x, h = ops.add_layer_norm(x, y, nxt.weight, nxt.bias, nxt.eps)
-        return self.lm_head(h)
+            x = ops.linear_small(a, at.c_proj.weight, at.c_proj.bias, residual=x)
+            f = ops.linear_small(x, m.c_fc.weight, m.c_fc.bias,
+                                 norm=("ln", blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps), act="gelu")
+            x = ops.linear_small(f, m.c_proj.weight, m.c_proj.bias, residual=x)
+        return ops.linear_small(x, self.lm_head.weight, norm=("ln", self.ln_f.weight, self.ln_f.bias, self.ln_f.eps))
 
     def generate(self, idx: torch.Tensor, max_new_tokens: int, **kw) -> torch.Tensor:
         """``generation.generate`` (KV cache, HIP decode attention, graph-captured decode loop)."""

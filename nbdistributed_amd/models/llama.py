@@ -254,16 +254,18 @@ class LlamaForCausalLM(_LlamaPreTrained):
         m, c = self.model, self.config
         rope = m.rope(cache.t_max, tok.device)
         x = ops.embedding(tok, m.embed_tokens.weight)
-        h = m.layers[0].input_layernorm(x)
+        eps = c.rms_norm_eps
+        # four fused kernels + attention per block (ops.linear_small: RMSNorm prologue, SwiGLU /
+        # residual epilogues)
         for i, layer in enumerate(m.layers):
-            at = layer.self_attn
-            a = cache.attend(i, F.linear(h, at.qkv_proj.weight), pos, rope=rope)
-            x, h = ops.add_rms_norm(x, F.linear(a, at.o_proj.weight), layer.post_attention_layernorm.weight,
-                                    c.rms_norm_eps)
-            y = ops.mlp_swiglu(h, layer.mlp.gate_up_proj.weight, layer.mlp.down_proj.weight)
-            nxt = m.layers[i + 1].input_layernorm if i + 1 < len(m.layers) else m.norm
-            x, h = ops.add_rms_norm(x, y, nxt.weight, c.rms_norm_eps)
-        return self.lm_head(h)
+            at, mlp = layer.self_attn, layer.mlp
+            qkv = ops.linear_small(x, at.qkv_proj.weight, norm=("rms", layer.input_layernorm.weight, eps))
+            a = cache.attend(i, qkv, pos, rope=rope)
+            x = ops.linear_small(a, at.o_proj.weight, residual=x)
+            f = ops.linear_small(x, mlp.gate_up_proj.weight, norm=("rms", layer.post_attention_layernorm.weight, eps),
+                                 act="swiglu")
+            x = ops.linear_small(f, mlp.down_proj.weight, residual=x)
+        return ops.linear_small(x, self.lm_head.weight, norm=("rms", m.norm.weight, eps))
 
     def generate(self, input_ids, max_new_tokens: int, **kw):
         """``generation.generate`` (KV cache, HIP decode attention, graph-captured decode loop)."""

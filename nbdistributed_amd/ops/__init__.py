@@ -23,7 +23,9 @@ gemm_linear /          bf16 GEMM on MFMA 16x16x32: x·Wᵀ, dy·W, dyᵀ·x     
 mlp_gelu /             + bias / GELU / GELU' / SwiGLU / SwiGLU'          swizzles, tr-reads)
 mlp_swiglu (K12)       epilogues, split-K, K-groups
 decode_attention (K13) one-token attention over a KV cache: RoPE +      decode.hip (split keys,
-                       cache append + softmax·V + chunk merge           last-chunk merge)
+                       cache append + softmax·V + chunk merge           merge kernel)
+linear_small (K14)     decode linear: LN/RMS prologue + x·Wᵀ (MFMA) +   smallm.hip
+                       bias / GELU / SwiGLU / residual epilogue, M ≤ 64
 =====================  ==============================================  =========================
 
 GPU tensors always go to the HIP kernels; if ``libnbd_ops.so`` cannot be loaded on a GPU box the
@@ -37,7 +39,7 @@ from ._lib import _require, load_library, native_available
 from .attention import attention_qkv, flash_attention, flash_supported
 from .bucket import (_ref_flatten, _ref_prereduce, _ref_unflatten, bucket_flatten, bucket_unflatten, local_prereduce,
                      plan_offsets)
-from .decode import decode_attention, decode_attention_reference
+from .decode import decode_attention, decode_attention_reference, linear_small, linear_small_reference
 from .embedding import embedding, embedding_tok_pos
 from .gemm import gemm_linear, mlp_gelu, mlp_swiglu
 from .llama import rope_, rope_tables, swiglu
@@ -54,7 +56,7 @@ def __getattr__(name):
 
 
 __all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "cross_entropy", "linear_cross_entropy",
-           "flash_attention", "attention_qkv", "decode_attention", "decode_attention_reference", "flash_supported", "layer_norm", "add_layer_norm", "linear",
+           "flash_attention", "attention_qkv", "decode_attention", "decode_attention_reference", "linear_small", "linear_small_reference", "flash_supported", "layer_norm", "add_layer_norm", "linear",
            "colsum", "embedding", "embedding_tok_pos", "gemm_linear", "mlp_gelu", "mlp_swiglu", "rms_norm", "add_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary",
            "tensor_summary_text", "tensor_summary_raw", "plan_offsets", "native_available", "load_library",
            "SUMMARY_FIELDS"]

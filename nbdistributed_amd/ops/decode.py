@@ -86,3 +86,80 @@ def decode_attention(qkv, k_cache, v_cache, pos, n_head: int, scale: Optional[fl
         return torch.ops.nbd.decode_attn(qkv, k_cache, v_cache, pos, int(n_head), sc, int(kv_len_max or Tmax),
                                          cos, sin, workspace)
     return decode_attention_reference(qkv, k_cache, v_cache, pos, n_head, sc, rope)
+
+
+# ------------------------------------------------------------------ small-M fused linear (K14)
+_NORM = {None: 0, "ln": 1, "rms": 2}
+_ACT = {"none": 0, "gelu": 1, "swiglu": 2}
+
+
+def _lds_bytes(M: int, K: int, norm: int, act: int) -> int:
+    mt = -(-M // 16)
+    return (mt * 16 * (K + 8) * 2 if norm else 0) + 8 * (2 if act == 2 else 1) * mt * 256 * 4
+
+
+def linear_small_supported(x, w, norm=None, act: str = "none") -> bool:
+    import torch
+
+    M, K = x.shape
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and 1 <= M <= 64
+            and K % 32 == 0 and K <= 4096 and x.stride(-1) == 1
+            and _lds_bytes(M, K, _NORM[norm[0] if norm else None], _ACT[act]) <= 160 * 1024)
+
+
+def linear_small_reference(x, w, bias=None, norm=None, act: str = "none", residual=None):
+    """PyTorch version of :func:`linear_small` (fp32 math, output in x's dtype)."""
+    import torch
+    import torch.nn.functional as F
+
+    h = x
+    if norm is not None:
+        if norm[0] == "ln":
+            h = F.layer_norm(x.float(), (x.shape[-1],), norm[1].float(), norm[2].float(), norm[3]).to(x.dtype)
+        else:
+            xf = x.float()
+            h = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + norm[2]) * norm[1].float()).to(x.dtype)
+    y = h.float() @ w.float().t()
+    if act == "swiglu":
+        g, u = y.chunk(2, -1)
+        y = F.silu(g) * u
+    if bias is not None:
+        y = y + bias.float()
+    if act == "gelu":
+        y = F.gelu(y, approximate="tanh")
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(x.dtype)
+
+
+def linear_small(x, w, bias=None, norm=None, act: str = "none", residual=None):
+    """``residual + act(norm(x) · Wᵀ + bias)`` for a few token rows (decode), one HIP kernel.
+
+    ``x`` [M ≤ 64, K]; ``w`` [N, K] (``act="swiglu"``: [gate; up] = [2N, K], out = silu(g)·u);
+    ``norm`` = ``("ln", γ, β, eps)`` or ``("rms", γ, eps)`` applied to x first; ``residual``
+    [M, N].  GPU bf16 → ``csrc/kernels/smallm.hip``; elsewhere the same math in PyTorch."""
+    import torch
+    import torch.nn.functional as F
+
+    if act == "swiglu" and bias is not None:
+        raise ValueError("linear_small: no bias with SwiGLU")
+    if linear_small_supported(x, w, norm, act):
+        _require()
+        nk = _NORM[norm[0] if norm else None]
+        nw = norm[1] if norm else None
+        nb = norm[2] if norm and norm[0] == "ln" else None
+        eps = float(norm[-1]) if norm else 0.0
+        return torch.ops.nbd.linear_small(x, w, bias, nw, nb, eps, nk, _ACT[act], residual)
+    # the same steps as separate ops (more rows than the kernel takes, CPU, other dtypes)
+    from .llama import swiglu
+    from .norm import layer_norm, rms_norm
+
+    h = x
+    if norm is not None:
+        h = layer_norm(x, norm[1], norm[2], norm[3]) if norm[0] == "ln" else rms_norm(x, norm[1], norm[2])
+    y = F.linear(h, w, bias)
+    if act == "gelu":
+        y = F.gelu(y, approximate="tanh")
+    elif act == "swiglu":
+        y = swiglu(y)
+    return y if residual is None else residual + y

@@ -85,3 +85,29 @@ def test_zero_notebook_runs_end_to_end(monkeypatch):
     finally:
         if core.session.active:
             core.session.shutdown()
+
+
+NB4 = os.path.join(os.path.dirname(NB), "04_train_and_generate.ipynb")
+
+
+def test_generate_notebook_runs_end_to_end(monkeypatch):
+    monkeypatch.setenv("NBD_NOTEBOOK_TINY", "1")
+    cells = [c for c in json.load(open(NB4))["cells"] if c["cell_type"] == "code"]
+    sh = HeadlessShell()
+    core = sh.load_extension()
+    out = []
+    core.write = core.session.write = out.append
+    try:
+        for c in cells:
+            src = "".join(c["source"])
+            if src.startswith("%load_ext"):
+                continue
+            if src.startswith("%dist_init"):
+                src += " --backend gloo"
+            r = sh.run_cell(src)
+            assert r.success, (src, r.error_in_exec, "".join(out)[-3000:])
+        text = "".join(out)
+        assert "step 300: loss" in text and "counting continuation correct: True" in text, text[-3000:]
+    finally:
+        if core.session.active:
+            core.session.shutdown()
