@@ -102,6 +102,12 @@ def main():
             row[name + "_ms_per_token"] = round(t / a.new * 1e3, 3)
             if name == "nbd_graph":
                 g_out = holder["o"]
+        # steady-state decode cost: the marginal time per token between two lengths (prefill,
+        # cache allocation and graph capture cancel out)
+        t_short = timed(lambda: m.generate(ids, 32, graph=True))
+        t_long = timed(lambda: m.generate(ids, 32 + a.new, graph=True))
+        row["nbd_graph_marginal_ms_per_token"] = round((t_long - t_short) / a.new * 1e3, 3)
+        row["nbd_graph_marginal_tok_per_s"] = round(B * a.new / (t_long - t_short), 1)
         if hf is not None:
             holder = {}
             t = timed(lambda: holder.__setitem__("o", hf.generate(ids, attention_mask=torch.ones_like(ids),

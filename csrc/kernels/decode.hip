@@ -375,7 +375,92 @@ at::Tensor decode_attn_hip(const at::Tensor& qkv, const at::Tensor& k_cache, con
   return out;
 }
 
+// ============================================================================ greedy advance
+// The end of a greedy decode step in one launch: per sequence b, tok[b] = argmax(logits[b])
+// (first index among equal maxima, like torch.argmax); finished rows keep emitting eos (done[b]
+// sticks once eos appears); pos[b] += 1; out[b, pos[b]] = tok[b].  One 1024-thread workgroup per
+// row, 16-B loads (8 logits per lane per step), wave then LDS arg-max reduction.  Replaces torch's
+// arg-max reduction (≈19 µs on a 50k vocabulary row) plus three bookkeeping kernels.
+constexpr int GT = 1024;
+
+__device__ __forceinline__ void argmax_merge(float& v, int& i, float v2, int i2) {
+  if (v2 > v || (v2 == v && i2 < i)) {
+    v = v2;
+    i = i2;
+  }
+}
+
+__global__ __launch_bounds__(GT) void greedy_kernel(const uint16_t* __restrict__ logits, int64_t ld, int V,
+                                                    int64_t* __restrict__ tok, int64_t* __restrict__ pos,
+                                                    int64_t* __restrict__ out, int64_t out_ld, int out_T,
+                                                    bool* __restrict__ done, int64_t eos) {
+  __shared__ float sv[GT / kWave];
+  __shared__ int si[GT / kWave];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const uint16_t* row = logits + (int64_t)b * ld;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  const int V8 = (((uintptr_t)row & 15) == 0) ? V / 8 * 8 : 0;
+  for (int v = tid * 8; v < V8; v += GT * 8) {
+    float f[8];
+    load8<bf16_t>(reinterpret_cast<const bf16_t*>(row + v), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) argmax_merge(best, bi, f[e], v + e);
+  }
+  for (int v = V8 + tid; v < V; v += GT) argmax_merge(best, bi, bf16_to_f32(row[v]), v);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float v2 = __shfl_xor(best, off, kWave);
+    const int i2 = __shfl_xor(bi, off, kWave);
+    argmax_merge(best, bi, v2, i2);
+  }
+  if ((tid & 63) == 0) {
+    sv[tid >> 6] = best;
+    si[tid >> 6] = bi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < GT / kWave; ++w) argmax_merge(best, bi, sv[w], si[w]);
+    int64_t t = bi == 0x7fffffff ? 0 : bi;  // an all-NaN row picks token 0
+    if (done != nullptr) {
+      if (done[b]) t = eos;
+      if (t == eos) done[b] = true;
+    }
+    tok[b] = t;
+    const int64_t p = pos[b] + 1;
+    pos[b] = p;
+    if (p >= 0 && p < out_T) out[(int64_t)b * out_ld + p] = t;
+  }
+}
+
+void greedy_advance_hip(const at::Tensor& logits, const at::Tensor& tok, const at::Tensor& pos, const at::Tensor& out,
+                        const c10::optional<at::Tensor>& done, int64_t eos) {
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kBFloat16 && logits.dim() == 2 && logits.stride(1) == 1,
+              "greedy_advance: logits must be a bf16 [B, V] GPU view with unit last stride");
+  const int64_t B = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(V >= 1 && V < (1LL << 31) && B >= 1 && B < (1LL << 31), "greedy_advance: bad shape");
+  auto chk = [&](const at::Tensor& t, at::ScalarType ty, const char* name) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == ty && t.is_contiguous() && t.dim() == 1 && t.size(0) == B,
+                "greedy_advance: ", name, " must be a contiguous [B] GPU tensor of ", ty);
+  };
+  chk(tok, at::kLong, "tok");
+  chk(pos, at::kLong, "pos");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kLong && out.dim() == 2 && out.size(0) == B && out.stride(1) == 1,
+              "greedy_advance: out must be an int64 [B, T] GPU view with unit last stride");
+  const bool hd = done.has_value() && done->defined();
+  if (hd) chk(*done, at::kBool, "done");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  hipLaunchKernelGGL(greedy_kernel, dim3((unsigned)B), dim3(GT), 0, st, static_cast<const uint16_t*>(logits.data_ptr()),
+                     logits.stride(0), (int)V, tok.data_ptr<int64_t>(), pos.data_ptr<int64_t>(), out.data_ptr<int64_t>(),
+                     out.stride(0), (int)out.size(1), hd ? done->data_ptr<bool>() : nullptr, eos);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
 }  // namespace decode
 }  // namespace nbd
 
-TORCH_LIBRARY_IMPL(nbd, CUDA, m) { m.impl("decode_attn", &nbd::decode::decode_attn_hip); }
+TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
+  m.impl("decode_attn", &nbd::decode::decode_attn_hip);
+  m.impl("greedy_advance", &nbd::decode::greedy_advance_hip);
+}

@@ -15,6 +15,7 @@ TORCH_LIBRARY(nbd, m) {
         "Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor? rope_cos=None, Tensor? rope_sin=None) -> ()");
   m.def("decode_attn(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor pos, int n_head, float scale, "
         "int kv_len_max, Tensor? rope_cos, Tensor? rope_sin, Tensor(c!) partials) -> Tensor");
+  m.def("greedy_advance(Tensor logits, Tensor(a!) tok, Tensor(b!) pos, Tensor(c!) out, Tensor(d!)? done, int eos) -> ()");
   m.def("linear_small(Tensor x, Tensor w, Tensor? bias, Tensor? norm_w, Tensor? norm_b, float eps, int norm, "
         "int act, Tensor? residual) -> Tensor");
   m.def("attn_merge_(Tensor(a!) o_acc, Tensor(b!) lse_acc, Tensor o_b, Tensor lse_b, Tensor(c!)? out=None) -> ()");

@@ -53,7 +53,7 @@ struct Args {
   const uint16_t* nb;    // LayerNorm β [K] or nullptr
   const uint16_t* res;   // [M, N] or nullptr (row stride N)
   uint16_t* out;         // [M, N]
-  int M, N, K, norm, ntiles, up_off;  // up_off: first "up" row of W for SwiGLU (= N)
+  int M, N, K, norm, stage, ntiles, up_off;  // stage: x image in LDS; up_off: SwiGLU's first up row
   float eps;
 };
 
@@ -63,117 +63,162 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 }
 __device__ __forceinline__ float silu(float x) { return x * __fdividef(1.f, 1.f + __expf(-x)); }
 
+__device__ __forceinline__ void unpack8(const u32x4& w, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
   return v;
 }
 
-// LayerNorm / RMSNorm of rows [0, M) into the LDS image xs[MT·16][K + XPAD] (rows ≥ M zero)
+// the x image xs[MT·16][K + XPAD] in LDS, rows [0, M) only (the MFMA loop substitutes zeros for
+// the rest): every thread loads its 16-B pieces of the whole [M, K] block at once (one memory
+// round trip); with a norm, wave w then normalises rows w, w+8, … in place — all of its rows
+// interleaved, so their LDS reads and cross-lane reductions overlap — with the same bf16
+// rounding as the standalone LayerNorm / RMSNorm kernels
 template <int MT>
-__device__ __forceinline__ void prologue(const Args& a, uint16_t* xs, int wave, int lane) {
+__device__ __forceinline__ void prologue(const Args& a, const uint16_t* x, int M, uint16_t* xs, int tid) {
   const int ld = a.K + XPAD;
-  for (int r = wave; r < MT * 16; r += NW) {
-    uint16_t* dst = xs + r * ld;
-    if (r >= a.M) {
-      for (int c = lane * 8; c < a.K; c += kWave * 8) *reinterpret_cast<u32x4*>(dst + c) = u32x4{0, 0, 0, 0};
-      continue;
-    }
-    const uint16_t* src = a.x + (int64_t)r * a.ldx;
-    constexpr int MAXCH = 8;  // K ≤ 4096
-    float v[MAXCH][8];
-    float s = 0.f;
+  const int total = M * a.K;
+#pragma unroll 4
+  for (int idx = tid * 8; idx < total; idx += NT * 8) {
+    const int r = idx / a.K, c = idx - r * a.K;
+    *reinterpret_cast<u32x4*>(xs + r * ld + c) = *reinterpret_cast<const u32x4*>(x + (int64_t)r * a.ldx + c);
+  }
+  if (a.norm == NORM_NONE) return;
+  __syncthreads();
+  constexpr int RPW = MT * 16 / NW;  // rows per wave
+  const int lane = tid & 63, wave = tid >> 6;
+  float s[RPW], q[RPW], mean[RPW], rstd[RPW];
 #pragma unroll
-    for (int i = 0; i < MAXCH; ++i) {
-      const int c = lane * 8 + i * kWave * 8;
-      if (c < a.K) {
-        load8<bf16_t>(reinterpret_cast<const bf16_t*>(src + c), v[i]);
+  for (int j = 0; j < RPW; ++j) s[j] = q[j] = 0.f;
+  if (a.norm == NORM_LN) {
+    for (int c = lane * 8; c < a.K; c += kWave * 8) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s += v[i][e];
-      }
-    }
-    const float mean = a.norm == NORM_LN ? wave_sum(s) / (float)a.K : 0.f;
-    float q = 0.f;
+      for (int j = 0; j < RPW; ++j) {
+        const int r = wave + NW * j;
+        if (r < M) {
+          float f[8];
+          unpack8(*reinterpret_cast<const u32x4*>(xs + r * ld + c), f);
 #pragma unroll
-    for (int i = 0; i < MAXCH; ++i) {
-      const int c = lane * 8 + i * kWave * 8;
-      if (c < a.K) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float d = v[i][e] - mean;
-          q = fmaf(d, d, q);
+          for (int e = 0; e < 8; ++e) s[j] += f[e];
         }
       }
     }
-    const float rstd = rsqrtf(wave_sum(q) / (float)a.K + a.eps);
+  }
 #pragma unroll
-    for (int i = 0; i < MAXCH; ++i) {
-      const int c = lane * 8 + i * kWave * 8;
-      if (c < a.K) {
-        float g[8], b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, o[8];
-        load8<bf16_t>(reinterpret_cast<const bf16_t*>(a.nw + c), g);
-        if (a.norm == NORM_LN) load8<bf16_t>(reinterpret_cast<const bf16_t*>(a.nb + c), b);
+  for (int j = 0; j < RPW; ++j) mean[j] = a.norm == NORM_LN ? wave_sum(s[j]) / (float)a.K : 0.f;
+  for (int c = lane * 8; c < a.K; c += kWave * 8) {  // two passes, like the standalone kernels
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = fmaf((v[i][e] - mean) * rstd, g[e], b[e]);
-        store8<bf16_t>(reinterpret_cast<bf16_t*>(dst + c), o);
+    for (int j = 0; j < RPW; ++j) {
+      const int r = wave + NW * j;
+      if (r < M) {
+        float f[8];
+        unpack8(*reinterpret_cast<const u32x4*>(xs + r * ld + c), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = f[e] - mean[j];
+          q[j] = fmaf(d, d, q[j]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) rstd[j] = rsqrtf(wave_sum(q[j]) / (float)a.K + a.eps);
+  for (int c = lane * 8; c < a.K; c += kWave * 8) {
+    float g[8], b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    load8<bf16_t>(reinterpret_cast<const bf16_t*>(a.nw + c), g);
+    if (a.norm == NORM_LN) load8<bf16_t>(reinterpret_cast<const bf16_t*>(a.nb + c), b);
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int r = wave + NW * j;
+      if (r < M) {
+        float f[8], o[8];
+        unpack8(*reinterpret_cast<const u32x4*>(xs + r * ld + c), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = fmaf((f[e] - mean[j]) * rstd[j], g[e], b[e]);
+        store8<bf16_t>(reinterpret_cast<bf16_t*>(xs + r * ld + c), o);
       }
     }
   }
 }
 
+// Latency plan (a decode GEMM is ~1 µs of HBM traffic, so every serial memory round trip shows):
+// all of a wave's weight fragments for a tile are loaded before anything else — before the
+// prologue, whose x loads and norm then overlap them — and the next tile's fragments are issued
+// before this tile's cross-wave reduction.  SMAX = the most k-steps one wave owns (K ≤ 4096, or
+// 2048 with SwiGLU's two weight rows per column).
 template <int MT, int ACT>
 __global__ __launch_bounds__(NT) void linear_small_kernel(Args a) {
   constexpr int NACC = ACT == ACT_SWIGLU ? 2 : 1;
+  constexpr int SMAX = ACT == ACT_SWIGLU ? 8 : 16;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool lds_x = a.norm != NORM_NONE;
+  const bool lds_x = a.stage != 0;
   const int ldx_s = a.K + XPAD;
   uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
   float* red = reinterpret_cast<float*>(smem + (lds_x ? (size_t)MT * 16 * ldx_s * 2 : 0));
 
+  // this workgroup's rows: m-group blockIdx.y of MT·16 rows
+  const int row0 = blockIdx.y * MT * 16;
+  const int M = min(MT * 16, a.M - row0);
+  const uint16_t* x = a.x + (int64_t)row0 * a.ldx;
+  const int g = lane >> 4, li = lane & 15;
+  const int steps = a.K >> 5;  // MFMA k-steps (8 k per lane per step)
+  const int s0 = wave * steps / NW, ns = (wave + 1) * steps / NW - s0;
+  const int kg = g * (a.K >> 2) + s0 * 8;  // lane group g walks its own contiguous quarter of K
+
+  s8v wf[NACC][SMAX];
+  auto load_w = [&](int tile) {
+    const int nr = min(tile * 16 + li, a.N - 1);  // clamped for a ragged last tile
+    const uint16_t* w0 = a.w + (int64_t)nr * a.K + kg;
+    const uint16_t* w1 = a.w + (int64_t)(a.up_off + nr) * a.K + kg;
+#pragma unroll
+    for (int i = 0; i < SMAX; ++i)
+      if (i < ns) {
+        wf[0][i] = *reinterpret_cast<const s8v*>(w0 + i * 8);
+        if (ACT == ACT_SWIGLU) wf[NACC - 1][i] = *reinterpret_cast<const s8v*>(w1 + i * 8);
+      }
+  };
+  load_w(blockIdx.x);
   if (lds_x) {
-    prologue<MT>(a, xs, wave, lane);
+    prologue<MT>(a, x, M, xs, tid);
     __syncthreads();
   }
 
-  const int g = lane >> 4, li = lane & 15;
-  const int quarter = a.K >> 2;       // each lane group's contiguous k range
-  const int steps = a.K >> 5;         // MFMA k-steps (8 k per lane per step)
-  const int s0 = wave * steps / NW, s1 = (wave + 1) * steps / NW;
-  const int kg = g * quarter;
-
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     const int n0 = tile * 16;
-    // weight rows of this lane (clamped into range for a ragged last tile)
-    const int nr = min(n0 + li, a.N - 1);
-    const uint16_t* wrow = a.w + (int64_t)nr * a.K + kg;
-    const uint16_t* wrow2 = ACT == ACT_SWIGLU ? a.w + (int64_t)(a.up_off + nr) * a.K + kg : nullptr;
     f4 acc[NACC][MT];
 #pragma unroll
     for (int j = 0; j < NACC; ++j)
 #pragma unroll
       for (int t = 0; t < MT; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll 4
-    for (int s = s0; s < s1; ++s) {
-      const int k = s * 8;
-      const s8v wa = *reinterpret_cast<const s8v*>(wrow + k);
-      s8v wb;
-      if (ACT == ACT_SWIGLU) wb = *reinterpret_cast<const s8v*>(wrow2 + k);
 #pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const int m = t * 16 + li;
-        s8v xf;
-        if (lds_x) {
-          xf = *reinterpret_cast<const s8v*>(xs + m * ldx_s + kg + k);
-        } else {
-          xf = m < a.M ? *reinterpret_cast<const s8v*>(a.x + (int64_t)m * a.ldx + kg + k) : s8v{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < SMAX; ++i) {
+      if (i < ns) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          const int m = t * 16 + li;
+          s8v xf;
+          if (lds_x)
+            xf = m < M ? *reinterpret_cast<const s8v*>(xs + m * ldx_s + kg + i * 8) : s8v{0, 0, 0, 0, 0, 0, 0, 0};
+          else
+            xf = m < M ? *reinterpret_cast<const s8v*>(x + (int64_t)m * a.ldx + kg + i * 8)
+                         : s8v{0, 0, 0, 0, 0, 0, 0, 0};
+          acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0][i], xf, acc[0][t], 0, 0, 0);
+          if (ACT == ACT_SWIGLU)
+            acc[NACC - 1][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[NACC - 1][i], xf, acc[NACC - 1][t], 0, 0, 0);
         }
-        acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xf, acc[0][t], 0, 0, 0);
-        if (ACT == ACT_SWIGLU) acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb, xf, acc[1][t], 0, 0, 0);
       }
     }
+    if (tile + (int)gridDim.x < a.ntiles) load_w(tile + gridDim.x);  // in flight across the reduction
     // partial tiles of the 8 waves -> LDS: red[wave][j][t][m_local][n_local]
 #pragma unroll
     for (int j = 0; j < NACC; ++j)
@@ -183,32 +228,33 @@ __global__ __launch_bounds__(NT) void linear_small_kernel(Args a) {
     __syncthreads();
     for (int q = tid; q < MT * 256; q += NT) {
       const int t = q >> 8, p = q & 255;
-      const int m = t * 16 + (p >> 4), n = n0 + (p & 15);
+      const int ml = t * 16 + (p >> 4), n = n0 + (p & 15);
+      const int64_t m = row0 + ml;
       float v0 = 0.f, v1 = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
         v0 += red[((w * NACC + 0) * MT + t) * 256 + p];
         if (ACT == ACT_SWIGLU) v1 += red[((w * NACC + 1) * MT + t) * 256 + p];
       }
-      if (m < a.M && n < a.N) {
+      if (ml < M && n < a.N) {
         float y = v0;
         if (a.bias != nullptr) y += bf16_to_f32(a.bias[n]);
         if (ACT == ACT_GELU) y = gelu_tanh(y);
         if (ACT == ACT_SWIGLU) y = silu(y) * v1;
-        if (a.res != nullptr) y += bf16_to_f32(a.res[(int64_t)m * a.N + n]);
-        a.out[(int64_t)m * a.N + n] = f32_to_bf16(y);
+        if (a.res != nullptr) y += bf16_to_f32(a.res[m * a.N + n]);
+        a.out[m * a.N + n] = f32_to_bf16(y);
       }
     }
     __syncthreads();  // red is reused by the next tile
   }
 }
 
-static size_t lds_bytes(int MT, int K, int norm, int act) {
-  const size_t xs = norm != NORM_NONE ? (size_t)MT * 16 * (K + XPAD) * 2 : 0;
+constexpr size_t kMaxLds = 160 * 1024;
+
+static size_t lds_bytes(int MT, int K, bool stage, int act) {
+  const size_t xs = stage ? (size_t)MT * 16 * (K + XPAD) * 2 : 0;
   return xs + (size_t)NW * (act == ACT_SWIGLU ? 2 : 1) * MT * 256 * 4;
 }
-
-constexpr size_t kMaxLds = 160 * 1024;
 
 at::Tensor linear_small_hip(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                             const c10::optional<at::Tensor>& norm_w, const c10::optional<at::Tensor>& norm_b,
@@ -221,7 +267,8 @@ at::Tensor linear_small_hip(const at::Tensor& x, const at::Tensor& w, const c10:
               "linear_small: w must be a contiguous bf16 [N, K] GPU tensor");
   const int64_t M = x.size(0), K = x.size(1);
   TORCH_CHECK(M >= 1 && M <= 64, "linear_small: 1 <= M <= 64 rows");
-  TORCH_CHECK(K == w.size(1) && K % 32 == 0 && K <= 4096, "linear_small: K must match w, K % 32 == 0, K <= 4096");
+  TORCH_CHECK(K == w.size(1) && K % 32 == 0 && K <= (act == ACT_SWIGLU ? 2048 : 4096),
+              "linear_small: K must match w, K % 32 == 0, K <= 4096 (2048 with SwiGLU)");
   TORCH_CHECK(norm >= 0 && norm <= 2 && act >= 0 && act <= 2, "linear_small: bad norm / act");
   const bool swiglu = act == ACT_SWIGLU;
   TORCH_CHECK(!swiglu || w.size(0) % 2 == 0, "linear_small: SwiGLU needs w = [gate; up]");
@@ -253,11 +300,19 @@ at::Tensor linear_small_hip(const at::Tensor& x, const at::Tensor& w, const c10:
   a.ntiles = (int)((N + 15) / 16);
   a.up_off = (int)N;
   a.eps = (float)eps;
-  const int MT = (int)((M + 15) / 16);
-  const size_t lds = lds_bytes(MT, (int)K, (int)norm, (int)act);
+  // m-tiles per workgroup: all of them (weights read once) unless the x image would not fit in
+  // LDS, or the column tiles alone leave most CUs idle — then one m-tile per workgroup and a
+  // second grid dimension over the row groups (the weights are re-read from L2)
+  const int MT_all = (int)((M + 15) / 16);
+  int MT = MT_all;
+  if (MT > 1 && (a.ntiles < 128 || lds_bytes(MT, (int)K, true, (int)act) > kMaxLds)) MT = 1;
+  const int mgroups = (MT_all + MT - 1) / MT;
+  // the x image goes to LDS whenever it fits (a norm prologue requires it)
+  a.stage = norm != NORM_NONE || lds_bytes(MT, (int)K, true, (int)act) <= kMaxLds;
+  const size_t lds = lds_bytes(MT, (int)K, a.stage != 0, (int)act);
   TORCH_CHECK(lds <= kMaxLds, "linear_small: needs ", lds, " B of LDS (> 160 KiB); normalise separately");
   // the prologue is recomputed per workgroup: cap the grid there (workgroups loop over tiles)
-  const int grid = norm != NORM_NONE ? std::min(a.ntiles, 512) : a.ntiles;
+  const int grid = a.stage ? std::min(a.ntiles, 512) : a.ntiles;
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   auto launch = [&](auto kern) {
@@ -267,7 +322,7 @@ at::Tensor linear_small_hip(const at::Tensor& x, const at::Tensor& w, const c10:
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
       attr_set = true;
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, st, a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid, (unsigned)mgroups), dim3(NT), lds, st, a);
   };
 #define NBD_SMALLM(mt)                                                    \
   case mt:                                                                \

@@ -106,6 +106,16 @@ class _DecodeLoop:
 
     def step(self):
         logits = self.model.decode_step(self.tok, self.pos, self.cache)
+        if (self.sampling["temperature"] <= 0.0 and logits.is_cuda and logits.dtype == torch.bfloat16
+                and logits.stride(-1) == 1 and self.out.dtype == torch.int64):
+            # greedy: arg-max, eos bookkeeping, position and output update in one HIP kernel
+            from .ops._lib import _require
+
+            _require()
+            torch.ops.nbd.greedy_advance(logits, self.tok, self.pos, self.out,
+                                         self.done if self.eos is not None else None,
+                                         -1 if self.eos is None else int(self.eos))
+            return
         nxt = sample(logits, **self.sampling)
         if self.eos is not None:
             nxt = torch.where(self.done, torch.full_like(nxt, self.eos), nxt)

@@ -94,7 +94,7 @@ _ACT = {"none": 0, "gelu": 1, "swiglu": 2}
 
 
 def _lds_bytes(M: int, K: int, norm: int, act: int) -> int:
-    mt = -(-M // 16)
+    mt = 1 if norm else -(-M // 16)  # the kernel falls back to one m-tile per workgroup
     return (mt * 16 * (K + 8) * 2 if norm else 0) + 8 * (2 if act == 2 else 1) * mt * 256 * 4
 
 
@@ -103,8 +103,14 @@ def linear_small_supported(x, w, norm=None, act: str = "none") -> bool:
 
     M, K = x.shape
     return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and 1 <= M <= 64
-            and K % 32 == 0 and K <= 4096 and x.stride(-1) == 1
+            and K % 32 == 0 and K <= (2048 if act == "swiglu" else 4096) and x.stride(-1) == 1
             and _lds_bytes(M, K, _NORM[norm[0] if norm else None], _ACT[act]) <= 160 * 1024)
+
+
+def _apply_norm(x, norm):
+    from .norm import layer_norm, rms_norm
+
+    return layer_norm(x, norm[1], norm[2], norm[3]) if norm[0] == "ln" else rms_norm(x, norm[1], norm[2])
 
 
 def linear_small_reference(x, w, bias=None, norm=None, act: str = "none", residual=None):
@@ -132,6 +138,15 @@ def linear_small_reference(x, w, bias=None, norm=None, act: str = "none", residu
     return y.to(x.dtype)
 
 
+# Measured on MI355X (benchmarks/smallm_bench.py, profiles/smallm_bench_r2.txt), graph-replayed:
+# the in-kernel norm prologue is recomputed by every workgroup — a win up to ~8 rows (one node
+# instead of two), a loss beyond (+10 µs at 64 rows vs a 2-3 µs norm kernel); and hipBLASLt
+# beats this kernel on the LM head (N ≈ 50k) from a few rows up.
+FUSE_NORM_MAX_ROWS = 8
+LIBRARY_MIN_N = 16384
+LIBRARY_MIN_ROWS = 4
+
+
 def linear_small(x, w, bias=None, norm=None, act: str = "none", residual=None):
     """``residual + act(norm(x) · Wᵀ + bias)`` for a few token rows (decode), one HIP kernel.
 
@@ -143,6 +158,11 @@ def linear_small(x, w, bias=None, norm=None, act: str = "none", residual=None):
 
     if act == "swiglu" and bias is not None:
         raise ValueError("linear_small: no bias with SwiGLU")
+    M = x.shape[0]
+    if norm is not None and x.is_cuda and M > FUSE_NORM_MAX_ROWS:
+        x, norm = _apply_norm(x, norm), None
+    if x.is_cuda and M >= LIBRARY_MIN_ROWS and w.shape[0] >= LIBRARY_MIN_N and act == "none" and residual is None:
+        return F.linear(x if norm is None else _apply_norm(x, norm), w, bias)
     if linear_small_supported(x, w, norm, act):
         _require()
         nk = _NORM[norm[0] if norm else None]
@@ -152,11 +172,8 @@ def linear_small(x, w, bias=None, norm=None, act: str = "none", residual=None):
         return torch.ops.nbd.linear_small(x, w, bias, nw, nb, eps, nk, _ACT[act], residual)
     # the same steps as separate ops (more rows than the kernel takes, CPU, other dtypes)
     from .llama import swiglu
-    from .norm import layer_norm, rms_norm
 
-    h = x
-    if norm is not None:
-        h = layer_norm(x, norm[1], norm[2], norm[3]) if norm[0] == "ln" else rms_norm(x, norm[1], norm[2])
+    h = x if norm is None else _apply_norm(x, norm)
     y = F.linear(h, w, bias)
     if act == "gelu":
         y = F.gelu(y, approximate="tanh")

@@ -155,3 +155,33 @@ def test_linear_small_ragged_vocab_head():
     y = ops.linear_small(x, w, norm=nrm)
     ref = ops.linear_small_reference(x, w, norm=nrm).float()
     assert ((y.float() - ref).abs().max() / ref.abs().max()).item() < 2e-2
+
+
+@pytest.mark.parametrize("V,offset", [(50257, 0), (512, 0), (1001, 3)])
+@pytest.mark.parametrize("with_eos", [False, True])
+def test_greedy_advance_matches_torch(V, offset, with_eos):
+    B, T = 5, 12
+    g = torch.Generator(device="cuda").manual_seed(V)
+    base = torch.randn(B, V + offset, device="cuda", generator=g).to(torch.bfloat16)
+    logits = base[:, offset:]  # offset 3: rows not 16-B aligned (scalar path)
+    logits[1, 7] = logits[1, 9] = 50.0  # tie: the first index wins, like torch.argmax
+    tok = torch.zeros(B, dtype=torch.int64, device="cuda")
+    pos = torch.tensor([0, 3, 5, 10, 11], device="cuda")
+    out = torch.zeros(B, T, dtype=torch.int64, device="cuda")
+    eos = int(logits[2].float().argmax()) if with_eos else -1
+    done = torch.tensor([False, False, False, True, False], device="cuda") if with_eos else None
+    want = logits.float().argmax(-1)
+    want_done = None
+    if with_eos:
+        want = torch.where(done, torch.full_like(want, eos), want)
+        want_done = done | (want == eos)
+    want_pos = pos + 1
+    want_out = out.clone()
+    for b in range(B):
+        if want_pos[b] < T:
+            want_out[b, want_pos[b]] = want[b]
+    torch.ops.nbd.greedy_advance(logits, tok, pos, out, done, eos)
+    assert torch.equal(tok, want) and torch.equal(pos, want_pos) and torch.equal(out, want_out)
+    assert int(tok[1]) == 7
+    if with_eos:
+        assert torch.equal(done, want_done)
