@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--prompt", type=int, default=128)
     ap.add_argument("--new", type=int, default=256)
     ap.add_argument("--no-hf", action="store_true")
+    ap.add_argument("--model", default="gpt2", choices=["gpt2", "smollm2"])
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from nbdistributed_amd import ops
@@ -73,9 +74,24 @@ def main():
 
     ops.load_library()
     torch.manual_seed(0)
-    m = GPT2(GPT2Config.small()).to("cuda", torch.bfloat16).eval()
     hf = None
-    if not a.no_hf:
+    if a.model == "smollm2":
+        # SmolLM2-135M architecture (random init), built in HF and converted (models.llama.from_hf)
+        from transformers import LlamaConfig as HLC, LlamaForCausalLM as HLM
+
+        from nbdistributed_amd.models import SMOLLM2_135M
+        from nbdistributed_amd.models.llama import from_hf
+
+        cfg = dict(SMOLLM2_135M)
+        cfg.pop("hidden_act", None)
+        hf = HLM(HLC(**cfg)).to(torch.bfloat16)
+        m = from_hf(hf).to("cuda").eval()
+        hf = None if a.no_hf else hf.to("cuda").eval()
+        vocab, name = cfg["vocab_size"], "SmolLM2-135M (random init)"
+    else:
+        m = GPT2(GPT2Config.small()).to("cuda", torch.bfloat16).eval()
+        vocab, name = 50257, "gpt2-small (124M, random init)"
+    if a.model == "gpt2" and not a.no_hf:
         try:
             from transformers import GPT2Config as HFC, GPT2LMHeadModel
 
@@ -90,9 +106,9 @@ def main():
             hf = hf.to("cuda", torch.bfloat16).eval()
         except Exception as e:  # pragma: no cover
             print("HF baseline unavailable:", e, flush=True)
-    res = {"model": "gpt2-small (124M, random init)", "dtype": "bf16", "prompt": a.prompt, "new_tokens": a.new, "runs": []}
+    res = {"model": name, "dtype": "bf16", "prompt": a.prompt, "new_tokens": a.new, "runs": []}
     for B in [int(x) for x in a.batches.split(",")]:
-        ids = torch.randint(0, 50257, (B, a.prompt), device="cuda")
+        ids = torch.randint(1, vocab, (B, a.prompt), device="cuda")
         row = {"batch": B}
         g_out = None
         for name, kw in (("nbd_graph", dict(graph=True)), ("nbd_eager", dict(graph=False))):
@@ -121,6 +137,11 @@ def main():
             row["tokens_agreeing_with_hf_mean"] = round(float(same.mean()), 1)
         print(json.dumps(row), flush=True)
         res["runs"].append(row)
+    if a.model != "gpt2":
+        if a.out:
+            with open(a.out, "w") as f:
+                json.dump(res, f, indent=1)
+        return
     res["decode_kernel"] = kernel_bench([(1, 12, 12, 1024), (8, 12, 12, 1024), (32, 12, 12, 1024), (8, 32, 8, 8192),
                                          (1, 32, 8, 32768), (64, 12, 12, 2048)])
     if a.out:

@@ -218,6 +218,34 @@ class GPT2(nn.Module):
             loss = self._cp_loss(loss, targets, cp)
         return (logits if return_logits or targets is None else None), loss
 
+    @classmethod
+    def from_hf(cls, hf_model) -> "GPT2":
+        """The equivalent model from an instantiated HF ``GPT2LMHeadModel`` / ``GPT2Model`` (weights
+        copied; HF's Conv1D [in, out] weights transposed to nn.Linear [out, in])."""
+        hc = hf_model.config
+        if getattr(hc, "activation_function", "gelu_new") not in ("gelu_new", "gelu_pytorch_tanh"):
+            raise NotImplementedError(f"GPT2.from_hf: activation {hc.activation_function!r}")
+        c = GPT2Config(vocab_size=hc.vocab_size, n_positions=hc.n_positions, n_embd=hc.n_embd, n_layer=hc.n_layer,
+                       n_head=hc.n_head, tie_weights=bool(getattr(hc, "tie_word_embeddings", True)))
+        m = cls(c)
+        for blk in m.h:
+            for ln in (blk.ln_1, blk.ln_2):
+                ln.eps = hc.layer_norm_epsilon
+        m.ln_f.eps = hc.layer_norm_epsilon
+        sd = {}
+        for k, v in hf_model.state_dict().items():
+            k = k[len("transformer."):] if k.startswith("transformer.") else k
+            if k.endswith(".attn.bias") or k.endswith(".attn.masked_bias"):
+                continue  # causal-mask buffers of older transformers
+            if k.endswith(".weight") and any(f".{n}.weight" in "." + k for n in ("c_attn", "c_proj", "c_fc")):
+                v = v.t()
+            sd[k] = v
+        missing, unexpected = m.load_state_dict(sd, strict=False)
+        missing = [k for k in missing if not (k == "lm_head.weight" and c.tie_weights)]
+        if missing or unexpected:
+            raise ValueError(f"GPT2.from_hf: missing {missing}, unexpected {unexpected}")
+        return m.to(next(hf_model.parameters()).dtype)
+
     # ------------------------------------------------------------------ generation (generation.py)
     def kv_layout(self):
         c = self.config

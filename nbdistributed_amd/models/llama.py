@@ -45,10 +45,17 @@ class LlamaConfig:
     num_labels: int = 2
     pad_token_id: Optional[int] = 0
     initializer_range: float = 0.02
+    # family variants: Qwen2 (biased q/k/v), Llama with attention_bias (q/k/v and o), Mistral
+    # (explicit head_dim, sliding window), Llama 3.x rope scaling ({"rope_type": "llama3", ...})
+    qkv_bias: bool = False
+    o_bias: bool = False
+    explicit_head_dim: Optional[int] = None
+    sliding_window: Optional[int] = None
+    rope_scaling: Optional[Dict[str, Any]] = None
 
     @property
     def head_dim(self) -> int:
-        return self.hidden_size // self.num_attention_heads
+        return self.explicit_head_dim or self.hidden_size // self.num_attention_heads
 
     @classmethod
     def smollm2_135m(cls, **kw) -> "LlamaConfig":
@@ -63,15 +70,38 @@ class LlamaConfig:
 
     @classmethod
     def from_hf(cls, hf) -> "LlamaConfig":
-        rope = getattr(hf, "rope_theta", None)
-        if rope is None:
-            rope = (getattr(hf, "rope_parameters", None) or {}).get("rope_theta", 10000.0)
+        """From an HF ``LlamaConfig`` / ``Qwen2Config`` / ``MistralConfig`` (transformers 4.x or 5.x)."""
+        kind = getattr(hf, "model_type", "llama")
+        if kind not in ("llama", "qwen2", "mistral"):
+            raise NotImplementedError(f"LlamaConfig.from_hf: model_type {kind!r}")
+        params = dict(getattr(hf, "rope_parameters", None) or {})
+        legacy = getattr(hf, "rope_scaling", None)  # transformers 4.x
+        if legacy:
+            params.update(legacy)
+        rope = getattr(hf, "rope_theta", None) or params.get("rope_theta", 10000.0)
+        rtype = params.get("rope_type", params.get("type", "default"))
+        if rtype not in ("default", "llama3"):
+            raise NotImplementedError(f"LlamaConfig.from_hf: rope_type {rtype!r}")
+        scaling = None
+        if rtype == "llama3":
+            scaling = {k: float(params[k]) for k in ("factor", "low_freq_factor", "high_freq_factor",
+                                                     "original_max_position_embeddings")}
+        if getattr(hf, "mlp_bias", False):
+            raise NotImplementedError("LlamaConfig.from_hf: mlp_bias")
+        attn_bias = bool(getattr(hf, "attention_bias", False))
+        window = getattr(hf, "sliding_window", None)
+        if kind == "qwen2" and not getattr(hf, "use_sliding_window", False):
+            window = None
+        hd = getattr(hf, "head_dim", None)
         return cls(vocab_size=hf.vocab_size, hidden_size=hf.hidden_size, intermediate_size=hf.intermediate_size,
                    num_hidden_layers=hf.num_hidden_layers, num_attention_heads=hf.num_attention_heads,
                    num_key_value_heads=hf.num_key_value_heads or hf.num_attention_heads,
                    max_position_embeddings=hf.max_position_embeddings, rms_norm_eps=hf.rms_norm_eps,
                    rope_theta=float(rope), tie_word_embeddings=bool(getattr(hf, "tie_word_embeddings", False)),
-                   num_labels=getattr(hf, "num_labels", 2), pad_token_id=getattr(hf, "pad_token_id", None))
+                   num_labels=getattr(hf, "num_labels", 2), pad_token_id=getattr(hf, "pad_token_id", None),
+                   qkv_bias=kind == "qwen2" or attn_bias, o_bias=kind != "qwen2" and attn_bias,
+                   explicit_head_dim=hd if hd and hd != hf.hidden_size // hf.num_attention_heads else None,
+                   sliding_window=window, rope_scaling=scaling)
 
 
 class RMSNorm(nn.Module):
@@ -88,16 +118,19 @@ class LlamaAttention(nn.Module):
     def __init__(self, c: LlamaConfig):
         super().__init__()
         self.H, self.Hkv, self.D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
-        self.qkv_proj = nn.Linear(c.hidden_size, (self.H + 2 * self.Hkv) * self.D, bias=False)
-        self.o_proj = nn.Linear(self.H * self.D, c.hidden_size, bias=False)
+        self.qkv_proj = nn.Linear(c.hidden_size, (self.H + 2 * self.Hkv) * self.D, bias=c.qkv_bias)
+        self.o_proj = nn.Linear(self.H * self.D, c.hidden_size, bias=c.o_bias)
+        self.window = c.sliding_window
 
     def forward(self, x, cos, sin, kv=None):
+        if self.window is not None and x.shape[1] > self.window:
+            raise NotImplementedError(f"sliding-window attention: {x.shape[1]} positions > window {self.window}")
         # RoPE is applied inside the attention kernels on the HIP path (rope_ + SDPA otherwise)
-        qkv = ops.gemm_linear(x, self.qkv_proj.weight)  # HIP MFMA GEMM on GPU bf16, F.linear otherwise
+        qkv = ops.gemm_linear(x, self.qkv_proj.weight, self.qkv_proj.bias)  # HIP MFMA GEMM on GPU bf16
         if kv is not None:  # (KVCache, layer): generation prefill, before anything rotates qkv in place
             kv[0].store(kv[1], qkv, rope=(cos, sin))
         a = ops.attention_qkv(qkv, self.H, causal=True, n_kv_head=self.Hkv, rope=(cos, sin))
-        return ops.gemm_linear(a, self.o_proj.weight)
+        return ops.gemm_linear(a, self.o_proj.weight, self.o_proj.bias)
 
 
 class LlamaMLP(nn.Module):
@@ -134,7 +167,8 @@ class LlamaModel(nn.Module):
     def rope(self, T: int, device) -> tuple:
         key = (str(device), T)
         if key not in self._rope:  # built once per (device, length), outside any graph capture
-            self._rope[key] = ops.rope_tables(T, self.config.head_dim, self.config.rope_theta, device)
+            self._rope[key] = ops.rope_tables(T, self.config.head_dim, self.config.rope_theta, device,
+                                              scaling=self.config.rope_scaling)
         return self._rope[key]
 
     def forward(self, input_ids, cache=None):
@@ -160,6 +194,8 @@ class _LlamaPreTrained(nn.Module):
         for m in self.modules():
             if isinstance(m, (nn.Linear, nn.Embedding)):
                 nn.init.normal_(m.weight, mean=0.0, std=std)
+            if isinstance(m, nn.Linear) and m.bias is not None:
+                nn.init.zeros_(m.bias)
 
 
 class LlamaForSequenceClassification(_LlamaPreTrained):
@@ -259,9 +295,10 @@ class LlamaForCausalLM(_LlamaPreTrained):
         # residual epilogues)
         for i, layer in enumerate(m.layers):
             at, mlp = layer.self_attn, layer.mlp
-            qkv = ops.linear_small(x, at.qkv_proj.weight, norm=("rms", layer.input_layernorm.weight, eps))
+            qkv = ops.linear_small(x, at.qkv_proj.weight, at.qkv_proj.bias,
+                                   norm=("rms", layer.input_layernorm.weight, eps))
             a = cache.attend(i, qkv, pos, rope=rope)
-            x = ops.linear_small(a, at.o_proj.weight, residual=x)
+            x = ops.linear_small(a, at.o_proj.weight, at.o_proj.bias, residual=x)
             f = ops.linear_small(x, mlp.gate_up_proj.weight, norm=("rms", layer.post_attention_layernorm.weight, eps),
                                  act="swiglu")
             x = ops.linear_small(f, mlp.down_proj.weight, residual=x)
@@ -291,6 +328,9 @@ def hf_to_nbd_state_dict(sd: Dict[str, torch.Tensor], c: LlamaConfig) -> Dict[st
         p = f"model.layers.{i}"
         out[f"{p}.self_attn.qkv_proj.weight"] = torch.cat(
             [sd[f"{p}.self_attn.q_proj.weight"], sd[f"{p}.self_attn.k_proj.weight"], sd[f"{p}.self_attn.v_proj.weight"]])
+        if f"{p}.self_attn.q_proj.bias" in sd:
+            out[f"{p}.self_attn.qkv_proj.bias"] = torch.cat(
+                [sd[f"{p}.self_attn.q_proj.bias"], sd[f"{p}.self_attn.k_proj.bias"], sd[f"{p}.self_attn.v_proj.bias"]])
         out[f"{p}.mlp.gate_up_proj.weight"] = torch.cat([sd[f"{p}.mlp.gate_proj.weight"], sd[f"{p}.mlp.up_proj.weight"]])
     return out
 

@@ -73,11 +73,23 @@ def _llama_fns():
     _LlamaFns = (_RMSNorm, _AddRMSNorm, _Rope, _SwiGLU)
     return _LlamaFns
 
-def rope_tables(T: int, head_dim: int, theta: float, device) -> tuple:
-    """cos/sin [T, head_dim/2] float32 for :func:`rope_` (HF default rope)."""
+def rope_tables(T: int, head_dim: int, theta: float, device, scaling=None) -> tuple:
+    """cos/sin [T, head_dim/2] float32 for :func:`rope_` (HF default rope; ``scaling`` = Llama 3.x
+    frequency scaling {factor, low_freq_factor, high_freq_factor, original_max_position_embeddings})."""
+    import math
+
     import torch
 
     inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float32, device=device) / head_dim))
+    if scaling is not None:  # long wavelengths slowed by `factor`, short kept, a smooth blend between
+        f, lo, hi = scaling["factor"], scaling["low_freq_factor"], scaling["high_freq_factor"]
+        ctx = scaling["original_max_position_embeddings"]
+        wavelen = 2 * math.pi / inv
+        scaled = torch.where(wavelen > ctx / lo, inv / f, inv)
+        smooth = (ctx / wavelen - lo) / (hi - lo)
+        blended = (1 - smooth) * scaled / f + smooth * scaled
+        medium = (wavelen >= ctx / hi) & (wavelen <= ctx / lo)
+        inv = torch.where(medium, blended, scaled)
     f = torch.outer(torch.arange(T, dtype=torch.float32, device=device), inv)
     return f.cos().contiguous(), f.sin().contiguous()
 

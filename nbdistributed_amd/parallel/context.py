@@ -428,7 +428,7 @@ def parallelize_llama_context(model, group=None, layout: str = "contiguous"):
         key = (str(device), T)
         if key not in cache:
             n = _size(group)
-            cos, sin = ops.rope_tables(T * n, c.head_dim, c.rope_theta, device)
+            cos, sin = ops.rope_tables(T * n, c.head_dim, c.rope_theta, device, scaling=c.rope_scaling)
             pos = context_positions(T, group, layout, device)
             cache[key] = (cos[pos].contiguous(), sin[pos].contiguous())
         return cache[key]

@@ -88,7 +88,7 @@ def _peaked(model):
     return model
 
 
-@pytest.mark.parametrize("family", ["gpt2", "llama"])
+@pytest.mark.parametrize("family", ["gpt2", "llama", "qwen2"])
 def test_gpu_generate_graph_matches_eager_and_full_forward(family):
     from nbdistributed_amd.models import GPT2, GPT2Config
     from nbdistributed_amd.models.llama import LlamaConfig, LlamaForCausalLM
@@ -96,6 +96,11 @@ def test_gpu_generate_graph_matches_eager_and_full_forward(family):
     torch.manual_seed(0)
     if family == "gpt2":
         m = GPT2(GPT2Config(vocab_size=512, n_positions=512, n_embd=256, n_layer=2, n_head=4))
+    elif family == "qwen2":  # biased q|k|v through the prefill GEMM and the decode kernel's bias epilogue
+        m = LlamaForCausalLM(LlamaConfig.tiny(qkv_bias=True))
+        with torch.no_grad():
+            for layer in m.model.layers:
+                layer.self_attn.qkv_proj.bias.normal_(0, 0.5)
     else:
         m = LlamaForCausalLM(LlamaConfig.tiny())
     m = _peaked(m.to("cuda", torch.bfloat16).eval())
@@ -113,7 +118,8 @@ def test_gpu_generate_graph_matches_eager_and_full_forward(family):
     m.prefill(torch.nn.functional.pad(seq[:, :40], (0, 88)), cache, torch.tensor([40], device="cuda"))
     for t in range(40, 48):
         lg = m.decode_step(seq[:, t], torch.tensor([t], device="cuda"), cache).float()
-        full = (m(seq[:, :t + 1])[0] if family == "gpt2" else m(seq[:, :t + 1])[1])[0, -1].float()
+        with torch.no_grad():
+            full = (m(seq[:, :t + 1])[0] if family == "gpt2" else m(seq[:, :t + 1])[1])[0, -1].float()
         assert (lg[0] - full).abs().max().item() < 0.05 * full.abs().max().item()
         assert int(lg.argmax()) == int(full.argmax())
 
