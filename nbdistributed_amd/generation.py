@@ -135,7 +135,9 @@ class _DecodeLoop:
         for t, s in zip((self.tok, self.pos, self.out, self.done), saved):
             t.copy_(s)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # thread_local: tensor-parallel decode steps hold RCCL all-reduces, and ProcessGroupNCCL's
+        # watchdog thread keeps querying its events during capture
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.step()
         # capture does not execute: the state is still the pre-capture one
 

@@ -82,6 +82,15 @@ class CausalSelfAttention(nn.Module):
         return self.c_proj(y)
 
 
+    def decode(self, x, ln, cache, layer: int, pos):
+        """One token per sequence (generation): ``x + c_proj(attn(ln(x)))``, three fused kernels."""
+        from .. import ops
+
+        qkv = ops.linear_small(x, self.c_attn.weight, self.c_attn.bias, norm=("ln", ln.weight, ln.bias, ln.eps))
+        a = cache.attend(layer, qkv, pos)
+        return ops.linear_small(a, self.c_proj.weight, self.c_proj.bias, residual=x)
+
+
 class MLP(nn.Module):
     def __init__(self, c: GPT2Config):
         super().__init__()
@@ -98,6 +107,13 @@ class MLP(nn.Module):
             h = F.gelu(ops.linear(x, self.c_fc.weight, self.c_fc.bias), approximate="tanh")
             return ops.linear(h, self.c_proj.weight, self.c_proj.bias)
         return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
+
+    def decode(self, x, ln):
+        """``x + mlp(ln(x))`` for a few token rows: two fused kernels (norm + GELU, bias + residual)."""
+        from .. import ops
+
+        f = ops.linear_small(x, self.c_fc.weight, self.c_fc.bias, norm=("ln", ln.weight, ln.bias, ln.eps), act="gelu")
+        return ops.linear_small(f, self.c_proj.weight, self.c_proj.bias, residual=x)
 
 
 class Block(nn.Module):
@@ -248,8 +264,10 @@ class GPT2(nn.Module):
 
     # ------------------------------------------------------------------ generation (generation.py)
     def kv_layout(self):
+        """(layers, query heads, kv heads, head dim) of this rank's cache (its heads under TP)."""
         c = self.config
-        return c.n_layer, c.n_head, c.n_head, c.n_embd // c.n_head
+        h = self.h[0].attn.n_head
+        return c.n_layer, h, h, c.n_embd // c.n_head
 
     def max_positions(self) -> int:
         return self.config.n_positions
@@ -278,16 +296,11 @@ class GPT2(nn.Module):
             x = ops.embedding_tok_pos(tok.view(1, -1), self.wte.weight, pos, self.wpe.weight).view(-1, c.n_embd)
         else:
             x = self.wte(tok) + self.wpe(pos)
-        # five fused kernels per block (ops.linear_small: norm prologue, bias / GELU / residual epilogue)
+        # five fused kernels per block (ops.linear_small: norm prologue, bias / GELU / residual
+        # epilogue); tensor-parallel blocks (parallel.tensor) add one all-reduce after each half
         for i, blk in enumerate(self.h):
-            at, m = blk.attn, blk.mlp
-            qkv = ops.linear_small(x, at.c_attn.weight, at.c_attn.bias,
-                                   norm=("ln", blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps))
-            a = cache.attend(i, qkv, pos)
-            x = ops.linear_small(a, at.c_proj.weight, at.c_proj.bias, residual=x)
-            f = ops.linear_small(x, m.c_fc.weight, m.c_fc.bias,
-                                 norm=("ln", blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps), act="gelu")
-            x = ops.linear_small(f, m.c_proj.weight, m.c_proj.bias, residual=x)
+            x = blk.attn.decode(x, blk.ln_1, cache, i, pos)
+            x = blk.mlp.decode(x, blk.ln_2)
         return ops.linear_small(x, self.lm_head.weight, norm=("ln", self.ln_f.weight, self.ln_f.bias, self.ln_f.eps))
 
     def generate(self, idx: torch.Tensor, max_new_tokens: int, **kw) -> torch.Tensor:

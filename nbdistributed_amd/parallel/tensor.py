@@ -215,11 +215,27 @@ class TPCausalSelfAttention(nn.Module):
         self.c_attn = ColumnParallelLinear.from_linear(attn.c_attn, group, rows=rows)
         self.c_proj = RowParallelLinear.from_linear(attn.c_proj, group)
 
-    def forward(self, x, fast: bool = False):
+    def forward(self, x, fast: bool = False, kv=None):
         from .. import ops
 
         qkv = self.c_attn(x)
+        if kv is not None:  # generation prefill: this rank's heads into its cache
+            kv[0].store(kv[1], qkv)
         return self.c_proj(ops.attention_qkv(qkv, self.n_head, causal=True))
+
+    def decode(self, x, ln, cache, layer: int, pos):
+        """Generation step on this rank's heads: fused norm + q|k|v shard, decode attention on the
+        local cache, the row-parallel projection's partial product (rank 0 adds bias and
+        residual), one all-reduce."""
+        from .. import ops
+
+        first = _rank(self.group) == 0
+        qkv = ops.linear_small(x, self.c_attn.weight, self.c_attn.bias, norm=("ln", ln.weight, ln.bias, ln.eps))
+        a = cache.attend(layer, qkv, pos)
+        y = ops.linear_small(a, self.c_proj.weight, self.c_proj.bias if first else None, residual=x if first else None)
+        if _size(self.group) > 1:
+            dist.all_reduce(y, group=self.group)
+        return y
 
 
 class TPMLP(nn.Module):
@@ -239,6 +255,17 @@ class TPMLP(nn.Module):
         y = ops.mlp_gelu(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, None)
         y = reduce_from_tp(y, self.group)
         return y + self.c_proj.bias if self.c_proj.bias is not None else y
+
+    def decode(self, x, ln):
+        """Generation step on this rank's MLP features (one all-reduce; rank 0 adds bias + residual)."""
+        from .. import ops
+
+        first = _rank(self.group) == 0
+        f = ops.linear_small(x, self.c_fc.weight, self.c_fc.bias, norm=("ln", ln.weight, ln.bias, ln.eps), act="gelu")
+        y = ops.linear_small(f, self.c_proj.weight, self.c_proj.bias if first else None, residual=x if first else None)
+        if _size(self.group) > 1:
+            dist.all_reduce(y, group=self.group)
+        return y
 
 
 def parallelize_gpt2(model, group=None):

@@ -393,3 +393,28 @@ def test_zero2_gpt2_matches_unsharded_two_ranks(sess):
     r = sess.execute(ZERO_GPT2, render=False)
     for rank in (0, 1):
         assert r.results[rank]["echo"] == "(True, True, True, True)", r.results[rank]
+
+
+TP_GENERATE = """
+import copy
+from nbdistributed_amd.models import GPT2, GPT2Config
+from nbdistributed_amd.parallel.tensor import parallelize_gpt2
+torch.manual_seed(6)
+ref = GPT2(GPT2Config(vocab_size=512, n_positions=256, n_embd=256, n_layer=2, n_head=4)).to(device, torch.bfloat16).eval()
+with torch.no_grad():
+    ref.wte.weight.mul_(8.0)              # peaked logits: greedy tokens far from bf16 ties
+tp = parallelize_gpt2(copy.deepcopy(ref))
+ids = torch.randint(1, 512, (3, 40), generator=torch.Generator().manual_seed(4)).to(device)
+lens = torch.tensor([40, 23, 7], device=device)
+want = ref.generate(ids, 16, lengths=lens, graph=False)
+got = tp.generate(ids, 16, lengths=lens, graph=False)   # gloo all-reduces: no graph capture
+(bool(torch.equal(got, want)), tp.kv_layout()[1])
+"""
+
+
+def test_tensor_parallel_generation_two_ranks(sess):
+    """Generation with heads / MLP features and the KV cache split over 2 ranks (decode kernels on
+    the shards, one all-reduce per half block) = the unsharded bf16 model's tokens."""
+    r = sess.execute(TP_GENERATE, render=False)
+    for rank in (0, 1):
+        assert r.results[rank]["echo"] == "(True, 2)", r.results[rank]

@@ -131,8 +131,36 @@ def _ulysses_case(rank, n):
     _close(head_to_seq(seq_to_head(x)), x, 0)
 
 
-@pytest.mark.parametrize("case", [_tp_linear_case, _tp_gpt2_case, _ulysses_case],
-                         ids=["tp_linear", "tp_gpt2", "ulysses"])
+def _tp_generate_case(rank, n):
+    # tensor-parallel generation: heads / MLP features and the KV cache split over the ranks, one
+    # all-reduce per half block — the same tokens as one process, decode logits to fp32 rounding
+    from nbdistributed_amd.generation import KVCache
+    from nbdistributed_amd.models import GPT2, GPT2Config
+    from nbdistributed_amd.parallel.tensor import parallelize_gpt2
+
+    torch.manual_seed(0)
+    ref = GPT2(GPT2Config(vocab_size=256, n_positions=128, n_embd=64, n_layer=2, n_head=4)).eval()
+    with torch.no_grad():
+        ref.wte.weight.mul_(8.0)  # peaked logits: greedy tokens far from ties
+    import copy
+
+    tp = parallelize_gpt2(copy.deepcopy(ref))
+    ids = torch.randint(1, 256, (2, 9), generator=torch.Generator().manual_seed(1))
+    lens = torch.tensor([9, 5])
+    want = ref.generate(ids, 7, lengths=lens)
+    got = tp.generate(ids, 7, lengths=lens)
+    assert torch.equal(got, want), (got, want)
+    assert tp.kv_layout()[1] == 4 // n
+    c_ref, c_tp = KVCache.for_model(ref, 2, 16), KVCache.for_model(tp, 2, 16)
+    ref.prefill(ids[:, :5], c_ref, torch.tensor([5, 5]))
+    tp.prefill(ids[:, :5], c_tp, torch.tensor([5, 5]))
+    for t in range(5, 9):
+        p = torch.full((2,), t)
+        _close(tp.decode_step(ids[:, t], p, c_tp), ref.decode_step(ids[:, t], p, c_ref), tol=1e-4)
+
+
+@pytest.mark.parametrize("case", [_tp_linear_case, _tp_gpt2_case, _ulysses_case, _tp_generate_case],
+                         ids=["tp_linear", "tp_gpt2", "ulysses", "tp_generate"])
 def test_two_ranks(case):
     _spawn(case, 2)
 
