@@ -132,6 +132,13 @@ class LlamaAttention(nn.Module):
         a = ops.attention_qkv(qkv, self.H, causal=True, n_kv_head=self.Hkv, rope=(cos, sin))
         return ops.gemm_linear(a, self.o_proj.weight, self.o_proj.bias)
 
+    def decode(self, x, norm_w, eps, cache, layer: int, pos, rope):
+        """Generation step: ``x + o_proj(attn(rms(x)))`` — fused norm + q|k|v, decode attention
+        (RoPE, cache append), fused o_proj + residual."""
+        qkv = ops.linear_small(x, self.qkv_proj.weight, self.qkv_proj.bias, norm=("rms", norm_w, eps))
+        a = cache.attend(layer, qkv, pos, rope=rope)
+        return ops.linear_small(a, self.o_proj.weight, self.o_proj.bias, residual=x)
+
 
 class LlamaMLP(nn.Module):
     def __init__(self, c: LlamaConfig):
@@ -142,6 +149,10 @@ class LlamaMLP(nn.Module):
     def forward(self, x):
         # SwiGLU (and its backward) run in the gate|up GEMM's (the down dgrad's) epilogue
         return ops.mlp_swiglu(x, self.gate_up_proj.weight, self.down_proj.weight)
+
+    def decode(self, x, norm_w, eps):
+        f = ops.linear_small(x, self.gate_up_proj.weight, norm=("rms", norm_w, eps), act="swiglu")
+        return ops.linear_small(f, self.down_proj.weight, residual=x)
 
 
 class LlamaDecoderLayer(nn.Module):
@@ -264,8 +275,9 @@ class LlamaForCausalLM(_LlamaPreTrained):
 
     # ------------------------------------------------------------------ generation (generation.py)
     def kv_layout(self):
-        c = self.config
-        return c.num_hidden_layers, c.num_attention_heads, c.num_key_value_heads, c.head_dim
+        """(layers, query heads, kv heads, head dim) of this rank's cache (its heads under TP)."""
+        at = self.model.layers[0].self_attn
+        return self.config.num_hidden_layers, at.H, at.Hkv, self.config.head_dim
 
     def max_positions(self) -> int:
         return self.config.max_position_embeddings
@@ -292,16 +304,10 @@ class LlamaForCausalLM(_LlamaPreTrained):
         x = ops.embedding(tok, m.embed_tokens.weight)
         eps = c.rms_norm_eps
         # four fused kernels + attention per block (ops.linear_small: RMSNorm prologue, SwiGLU /
-        # residual epilogues)
+        # residual epilogues); tensor-parallel layers (parallel.tensor) add one all-reduce per half
         for i, layer in enumerate(m.layers):
-            at, mlp = layer.self_attn, layer.mlp
-            qkv = ops.linear_small(x, at.qkv_proj.weight, at.qkv_proj.bias,
-                                   norm=("rms", layer.input_layernorm.weight, eps))
-            a = cache.attend(i, qkv, pos, rope=rope)
-            x = ops.linear_small(a, at.o_proj.weight, at.o_proj.bias, residual=x)
-            f = ops.linear_small(x, mlp.gate_up_proj.weight, norm=("rms", layer.post_attention_layernorm.weight, eps),
-                                 act="swiglu")
-            x = ops.linear_small(f, mlp.down_proj.weight, residual=x)
+            x = layer.self_attn.decode(x, layer.input_layernorm.weight, eps, cache, i, pos, rope)
+            x = layer.mlp.decode(x, layer.post_attention_layernorm.weight, eps)
         return ops.linear_small(x, self.lm_head.weight, norm=("rms", m.norm.weight, eps))
 
     def generate(self, input_ids, max_new_tokens: int, **kw):

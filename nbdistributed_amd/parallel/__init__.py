@@ -6,7 +6,7 @@ from .backend import abort_process_group, init_data_plane, rccl_version, registe
 
 __all__ = ["abort_process_group", "init_data_plane", "rccl_version", "register_rccl_backend", "resolve_backend",
            "DistributedDataParallel", "bf16_compress_hook", "allreduce_hook", "broadcast_params", "broadcast_tensors",
-           "tensor", "sequence", "expert", "pipeline", "pipeline_step", "MoE", "parallelize_gpt2", "ColumnParallelLinear", "RowParallelLinear", "ulysses_attention", "context", "ring_attention", "mesh", "ParallelMesh"]
+           "tensor", "sequence", "expert", "pipeline", "pipeline_step", "MoE", "parallelize_gpt2", "parallelize_llama", "ColumnParallelLinear", "RowParallelLinear", "ulysses_attention", "context", "ring_attention", "mesh", "ParallelMesh"]
 
 
 def __getattr__(name):
@@ -19,7 +19,7 @@ def __getattr__(name):
         import importlib
 
         return importlib.import_module(f".{name}", __name__)
-    if name in ("parallelize_gpt2", "ColumnParallelLinear", "RowParallelLinear"):
+    if name in ("parallelize_gpt2", "parallelize_llama", "ColumnParallelLinear", "RowParallelLinear"):
         from . import tensor
 
         return getattr(tensor, name)

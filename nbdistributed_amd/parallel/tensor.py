@@ -278,5 +278,89 @@ def parallelize_gpt2(model, group=None):
     return model
 
 
+class TPLlamaAttention(nn.Module):
+    """Llama / Qwen2 / Mistral attention with this rank's query heads and the key/value heads they
+    read (grouped-query attention splits by kv-head groups: ``Hkv`` must divide by the TP size);
+    RoPE inside the HIP attention kernels as in the unsharded model; row-parallel ``o_proj``."""
+
+    def __init__(self, attn, group=None):
+        super().__init__()
+        n, r = _size(group), _rank(group)
+        H, Hkv, D = attn.H, attn.Hkv, attn.D
+        if Hkv % n:
+            raise ValueError(f"num_key_value_heads={Hkv} is not divisible by the TP size {n}")
+        q0, q1 = r * (H // n) * D, (r + 1) * (H // n) * D
+        k0, k1 = r * (Hkv // n) * D, (r + 1) * (Hkv // n) * D
+        rows = torch.cat([torch.arange(q0, q1), H * D + torch.arange(k0, k1), (H + Hkv) * D + torch.arange(k0, k1)])
+        self.group, self.H, self.Hkv, self.D, self.window = group, H // n, Hkv // n, D, attn.window
+        self.qkv_proj = ColumnParallelLinear.from_linear(attn.qkv_proj, group, rows=rows)
+        self.o_proj = RowParallelLinear.from_linear(attn.o_proj, group)
+
+    def forward(self, x, cos, sin, kv=None):
+        from .. import ops
+
+        qkv = self.qkv_proj(x)
+        if kv is not None:
+            kv[0].store(kv[1], qkv, rope=(cos, sin))
+        return self.o_proj(ops.attention_qkv(qkv, self.H, causal=True, n_kv_head=self.Hkv, rope=(cos, sin)))
+
+    def decode(self, x, norm_w, eps, cache, layer: int, pos, rope):
+        from .. import ops
+
+        first = _rank(self.group) == 0
+        qkv = ops.linear_small(x, self.qkv_proj.weight, self.qkv_proj.bias, norm=("rms", norm_w, eps))
+        a = cache.attend(layer, qkv, pos, rope=rope)
+        y = ops.linear_small(a, self.o_proj.weight, self.o_proj.bias if first else None, residual=x if first else None)
+        if _size(self.group) > 1:
+            dist.all_reduce(y, group=self.group)
+        return y
+
+
+class TPLlamaMLP(nn.Module):
+    """SwiGLU MLP with this rank's intermediate features: its gate rows and the matching up rows
+    (so SwiGLU stays in the GEMM epilogue on the shard), row-parallel ``down_proj``."""
+
+    def __init__(self, mlp, group=None):
+        super().__init__()
+        n, r = _size(group), _rank(group)
+        inter = mlp.down_proj.in_features
+        if inter % n:
+            raise ValueError(f"intermediate_size={inter} is not divisible by the TP size {n}")
+        i0, i1 = r * inter // n, (r + 1) * inter // n
+        rows = torch.cat([torch.arange(i0, i1), inter + torch.arange(i0, i1)])
+        self.group = group
+        self.gate_up_proj = ColumnParallelLinear.from_linear(mlp.gate_up_proj, group, rows=rows)
+        self.down_proj = RowParallelLinear.from_linear(mlp.down_proj, group)
+
+    def forward(self, x):
+        from .. import ops
+
+        x = copy_to_tp(x, self.group)
+        return reduce_from_tp(ops.mlp_swiglu(x, self.gate_up_proj.weight, self.down_proj.weight), self.group)
+
+    def decode(self, x, norm_w, eps):
+        from .. import ops
+
+        first = _rank(self.group) == 0
+        f = ops.linear_small(x, self.gate_up_proj.weight, norm=("rms", norm_w, eps), act="swiglu")
+        y = ops.linear_small(f, self.down_proj.weight, residual=x if first else None)
+        if _size(self.group) > 1:
+            dist.all_reduce(y, group=self.group)
+        return y
+
+
+def parallelize_llama(model, group=None):
+    """Tensor parallelism for the native Llama family (``models.llama``: ``LlamaModel`` or a
+    wrapper with ``.model``), in place on a replicated, identically initialised model: query /
+    key-value heads and MLP features split over ``group``; embeddings, norms and heads
+    replicated.  Training (autograd collectives) and generation (per-rank KV caches) both work."""
+    inner = model.model if hasattr(model, "model") else model
+    for layer in inner.layers:
+        layer.self_attn = TPLlamaAttention(layer.self_attn, group)
+        layer.mlp = TPLlamaMLP(layer.mlp, group)
+    return model
+
+
 __all__ = ["copy_to_tp", "reduce_from_tp", "gather_from_tp", "scatter_to_tp", "ColumnParallelLinear",
-           "RowParallelLinear", "TPCausalSelfAttention", "TPMLP", "parallelize_gpt2"]
+           "RowParallelLinear", "TPCausalSelfAttention", "TPMLP", "parallelize_gpt2", "TPLlamaAttention",
+           "TPLlamaMLP", "parallelize_llama"]

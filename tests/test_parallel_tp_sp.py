@@ -159,8 +159,42 @@ def _tp_generate_case(rank, n):
         _close(tp.decode_step(ids[:, t], p, c_tp), ref.decode_step(ids[:, t], p, c_ref), tol=1e-4)
 
 
-@pytest.mark.parametrize("case", [_tp_linear_case, _tp_gpt2_case, _ulysses_case, _tp_generate_case],
-                         ids=["tp_linear", "tp_gpt2", "ulysses", "tp_generate"])
+def _tp_llama_case(rank, n):
+    # Llama-family TP (GQA heads split by kv group, SwiGLU features split, biased q|k|v like Qwen2):
+    # loss and gradients = the unsharded model; generation = the unsharded model's tokens
+    import copy
+
+    from nbdistributed_amd.models.llama import LlamaConfig, LlamaForCausalLM
+    from nbdistributed_amd.parallel.tensor import parallelize_llama
+
+    torch.manual_seed(0)
+    ref = LlamaForCausalLM(LlamaConfig.tiny(hidden_size=128, num_attention_heads=4, num_key_value_heads=2,
+                                            qkv_bias=True))
+    with torch.no_grad():
+        for layer in ref.model.layers:
+            layer.self_attn.qkv_proj.bias.normal_(0, 0.3)
+    tp = parallelize_llama(copy.deepcopy(ref))
+    ids = torch.randint(1, 512, (2, 12), generator=torch.Generator().manual_seed(2))
+    l_ref, _ = ref(ids, labels=ids)
+    l_tp, _ = tp(ids, labels=ids)
+    _close(l_tp.detach(), l_ref.detach())
+    l_ref.backward()
+    l_tp.backward()
+    inter = ref.config.intermediate_size
+    sl = slice(rank * inter // n, (rank + 1) * inter // n)
+    _close(tp.model.layers[0].mlp.gate_up_proj.weight.grad[: inter // n], ref.model.layers[0].mlp.gate_up_proj.weight.grad[sl])
+    _close(tp.model.embed_tokens.weight.grad, ref.model.embed_tokens.weight.grad)
+    ref.eval(), tp.eval()
+    with torch.no_grad():
+        ref.model.embed_tokens.weight.mul_(8.0)
+        tp.model.embed_tokens.weight.mul_(8.0)
+    lens = torch.tensor([12, 6])
+    assert torch.equal(tp.generate(ids, 6, lengths=lens), ref.generate(ids, 6, lengths=lens))
+    assert tp.kv_layout()[1:3] == (4 // n, 2 // n)
+
+
+@pytest.mark.parametrize("case", [_tp_linear_case, _tp_gpt2_case, _ulysses_case, _tp_generate_case, _tp_llama_case],
+                         ids=["tp_linear", "tp_gpt2", "ulysses", "tp_generate", "tp_llama"])
 def test_two_ranks(case):
     _spawn(case, 2)
 
