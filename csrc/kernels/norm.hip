@@ -279,6 +279,149 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, con
   }
 }
 
+// ln_bwd for 2-byte types with C % 256 == 0 (GPT-2: 768): half a wave per row, so every lane
+// moves 16 B per access (8 elements; the 64-lane version above moves 8 B) and a wave has four
+// rows' loads in flight; row values stay packed (bf16 / f16) in registers until used.  Column
+// partials are combined across the two halves, then across the waves as above.
+template <typename T>
+__device__ __forceinline__ void unpack8v(const u32x4& w, float (&v)[8]);
+template <>
+__device__ __forceinline__ void unpack8v<bf16_t>(const u32x4& w, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
+}
+template <>
+__device__ __forceinline__ void unpack8v<f16_t>(const u32x4& w, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = f16_to_f32((uint16_t)(w[j] & 0xffffu));
+    v[2 * j + 1] = f16_to_f32((uint16_t)(w[j] >> 16));
+  }
+}
+
+__device__ __forceinline__ float hsum(float v) {  // sum over the 32 lanes of a half-wave
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+constexpr int kRpi16 = 1;  // one row pair per wave iteration: 192 VGPRs (two pairs: 256, and slower — 16.8 vs 16.2 µs)
+
+template <typename T, typename W, bool RES, int NCH, bool RMS = false>
+__global__ __launch_bounds__(NT) void ln_bwd16_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                      const T* __restrict__ dres, const W* __restrict__ gamma,
+                                                      const float* __restrict__ mean_in,
+                                                      const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                      float* __restrict__ part_g, int64_t rows, int C, int rpb) {
+  static_assert(sizeof(T) == 2, "ln_bwd16: 2-byte element types");
+  __shared__ float red[2][NT / kWave - 1][NCH * 256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
+  float g[NCH][8], ag[NCH][8], ab[NCH][8];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    load8<W>(gamma + 8 * hl + 256 * k, g[k]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ag[k][e] = ab[k][e] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  for (int i = wave * 2 * kRpi16; i < rpb; i += (NT / kWave) * 2 * kRpi16) {
+    u32x4 xv[kRpi16][NCH], dv[kRpi16][NCH], rv[kRpi16][NCH];
+    float mean[kRpi16], rstd[kRpi16];
+    bool live[kRpi16];
+#pragma unroll
+    for (int j = 0; j < kRpi16; ++j) {
+      const int li = i + 2 * j + half;
+      const int64_t row = r0 + li;
+      live[j] = row < rows && li < rpb;
+      const int64_t rr = live[j] ? row : r0;  // dead rows re-read a live one; nothing of theirs is kept
+      mean[j] = RMS ? 0.f : mean_in[rr];
+      rstd[j] = rstd_in[rr];
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int64_t o = rr * C + 8 * hl + 256 * k;
+        xv[j][k] = *reinterpret_cast<const u32x4*>(x + o);
+        dv[j][k] = *reinterpret_cast<const u32x4*>(dy + o);
+        if (RES) rv[j][k] = *reinterpret_cast<const u32x4*>(dres + o);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kRpi16; ++j) {
+      const float lv = live[j] ? 1.f : 0.f;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        float xf[8], df[8];
+        unpack8v<T>(xv[j][k], xf);
+        unpack8v<T>(dv[j][k], df);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xh = (xf[e] - mean[j]) * rstd[j];
+          const float gy = df[e] * g[k][e];
+          s1 += gy;
+          s2 = fmaf(gy, xh, s2);
+          ag[k][e] = fmaf(df[e] * lv, xh, ag[k][e]);
+          ab[k][e] = fmaf(df[e], lv, ab[k][e]);
+        }
+      }
+      const float m1 = RMS ? 0.f : hsum(s1) / (float)C, m2 = hsum(s2) / (float)C;
+      if (live[j]) {
+        const int64_t base = (r0 + i + 2 * j + half) * C;
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+          float xf[8], df[8], o[8];
+          unpack8v<T>(xv[j][k], xf);
+          unpack8v<T>(dv[j][k], df);
+          float rf[8];
+          if (RES) unpack8v<T>(rv[j][k], rf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xh = (xf[e] - mean[j]) * rstd[j];
+            o[e] = rstd[j] * (df[e] * g[k][e] - m1 - xh * m2);
+            if (RES) o[e] += rf[e];
+          }
+          store8<T>(dx + base + 8 * hl + 256 * k, o);
+        }
+      }
+    }
+  }
+  // the two halves hold the same columns: fold, then waves 1..3 -> LDS -> wave 0
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      ag[k][e] += __shfl_xor(ag[k][e], 32, kWave);
+      ab[k][e] += __shfl_xor(ab[k][e], 32, kWave);
+    }
+  if (wave > 0 && half == 0) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[0][wave - 1][8 * hl + 256 * k + e] = ag[k][e];
+        red[1][wave - 1][8 * hl + 256 * k + e] = ab[k][e];
+      }
+  }
+  __syncthreads();
+  if (wave == 0 && half == 0) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = 8 * hl + 256 * k;
+#pragma unroll
+      for (int w = 0; w < NT / kWave - 1; ++w)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          ag[k][e] += red[0][w][c + e];
+          ab[k][e] += red[1][w][c + e];
+        }
+      store8<float>(part_g + (int64_t)blockIdx.x * 2 * C + c, ag[k]);
+      store8<float>(part_g + (int64_t)blockIdx.x * 2 * C + C + c, ab[k]);
+    }
+  }
+}
+
 // ============================================================================ column sums
 constexpr int kColRows = 64;  // rows per workgroup
 
@@ -433,6 +576,44 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ln_fwd_hip(const at::
   return {y, xsum, mean, rstd};
 }
 
+// one LayerNorm / RMSNorm backward launch: the 16-B half-wave kernel where it applies (2-byte
+// types, C a multiple of 256; NBD_LN_BWD16=0 forces the 8-B kernel for A/B runs)
+static bool bwd16_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NBD_LN_BWD16");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <typename T, typename W, int N, bool RMS>
+static void launch_bwd(bool res, const at::Tensor& x, const at::Tensor& dy, const T* dr, const at::Tensor& weight,
+                       const float* mean, const float* rstd, const at::Tensor& dx, const at::Tensor& pg, int64_t rows,
+                       int64_t C, int rpb, int nblk, hipStream_t st) {
+  const T* xp = static_cast<const T*>(x.data_ptr());
+  const T* dyp = static_cast<const T*>(dy.data_ptr());
+  const W* wp = static_cast<const W*>(weight.data_ptr());
+  T* dxp = static_cast<T*>(dx.data_ptr());
+  float* pgp = pg.data_ptr<float>();
+  if constexpr (sizeof(T) == 2) {
+    if (C == 256 * N && bwd16_enabled()) {
+      if (res)
+        hipLaunchKernelGGL((ln_bwd16_kernel<T, W, true, N, RMS>), dim3(nblk), dim3(NT), 0, st, xp, dyp, dr, wp, mean,
+                           rstd, dxp, pgp, rows, (int)C, rpb);
+      else
+        hipLaunchKernelGGL((ln_bwd16_kernel<T, W, false, N, RMS>), dim3(nblk), dim3(NT), 0, st, xp, dyp, dr, wp, mean,
+                           rstd, dxp, pgp, rows, (int)C, rpb);
+      return;
+    }
+  }
+  if (res)
+    hipLaunchKernelGGL((ln_bwd_kernel<T, W, true, N, RMS>), dim3(nblk), dim3(NT), 0, st, xp, dyp, dr, wp, mean, rstd,
+                       dxp, pgp, rows, (int)C, rpb);
+  else
+    hipLaunchKernelGGL((ln_bwd_kernel<T, W, false, N, RMS>), dim3(nblk), dim3(NT), 0, st, xp, dyp, dr, wp, mean, rstd,
+                       dxp, pgp, rows, (int)C, rpb);
+}
+
 // returns (dx, dweight, dbias); dx includes dres when given
 std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_hip(const at::Tensor& x, const at::Tensor& dy,
                                                           const c10::optional<at::Tensor>& dres,
@@ -467,16 +648,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_hip(const at::Tensor& x, c
     using W = decltype(w);
     constexpr int N = decltype(nch)::value;
     const T* dr = res ? static_cast<const T*>(dres->data_ptr()) : nullptr;
-    if (res)
-      hipLaunchKernelGGL((ln_bwd_kernel<T, W, true, N>), dim3(nblk), dim3(NT), 0, st,
-                         static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
-                         static_cast<const W*>(weight.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C, rpb);
-    else
-      hipLaunchKernelGGL((ln_bwd_kernel<T, W, false, N>), dim3(nblk), dim3(NT), 0, st,
-                         static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
-                         static_cast<const W*>(weight.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C, rpb);
+    launch_bwd<T, W, N, false>(res, x, dy, dr, weight, mean.data_ptr<float>(), rstd.data_ptr<float>(), dx, pg, rows,
+                               C, rpb, nblk, st);
    });
   });
   C10_HIP_KERNEL_LAUNCH_CHECK();
@@ -557,16 +730,8 @@ std::tuple<at::Tensor, at::Tensor> rms_bwd_hip(const at::Tensor& x, const at::Te
     using W = decltype(w);
     constexpr int N = decltype(nch)::value;
     const T* dr = res ? static_cast<const T*>(dres->data_ptr()) : nullptr;
-    if (res)
-      hipLaunchKernelGGL((ln_bwd_kernel<T, W, true, N, true>), dim3(nblk), dim3(NT), 0, st,
-                         static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
-                         static_cast<const W*>(weight.data_ptr()), rstd.data_ptr<float>(), rstd.data_ptr<float>(),
-                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C, rpb);
-    else
-      hipLaunchKernelGGL((ln_bwd_kernel<T, W, false, N, true>), dim3(nblk), dim3(NT), 0, st,
-                         static_cast<const T*>(x.data_ptr()), static_cast<const T*>(dy.data_ptr()), dr,
-                         static_cast<const W*>(weight.data_ptr()), rstd.data_ptr<float>(), rstd.data_ptr<float>(),
-                         static_cast<T*>(dx.data_ptr()), pg.data_ptr<float>(), rows, (int)C, rpb);
+    launch_bwd<T, W, N, true>(res, x, dy, dr, weight, rstd.data_ptr<float>(), rstd.data_ptr<float>(), dx, pg, rows, C,
+                              rpb, nblk, st);
    });
   });
   C10_HIP_KERNEL_LAUNCH_CHECK();
