@@ -152,9 +152,9 @@ __global__ __launch_bounds__(NT) void decode_kernel(Params p) {
     const uint16_t* kb = p.kc + head_base + d8 * 8;
     const uint16_t* vb = p.vc + head_base + d8 * 8;
     const int iters = (c1 - c0 + NG * U - 1) / (NG * U);
-    for (int it = 0; it < iters; ++it) {
-      int j[U];
-      u32x4 kr[U], vr[U];
+    // two register buffers: the keys / values of iteration it+1 are in flight while iteration it
+    // is computed (a chunk is only a few iterations long, so each exposed round trip shows)
+    auto load = [&](int it, int (&j)[U], u32x4 (&kr)[U], u32x4 (&vr)[U]) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         j[u] = c0 + grp + NG * (it * U + u);
@@ -162,6 +162,8 @@ __global__ __launch_bounds__(NT) void decode_kernel(Params p) {
         kr[u] = *reinterpret_cast<const u32x4*>(kb + (int64_t)jj * D);
         vr[u] = *reinterpret_cast<const u32x4*>(vb + (int64_t)jj * D);
       }
+    };
+    auto compute = [&](const int (&j)[U], u32x4 (&kr)[U], u32x4 (&vr)[U]) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (j[u] == pos) {  // the new token: its row in memory may predate this launch's write
@@ -202,6 +204,17 @@ __global__ __launch_bounds__(NT) void decode_kernel(Params p) {
           for (int e = 0; e < 8; ++e) o[g][e] += pu * vf[e];
         }
         m[g] = mx;
+      }
+    };
+    int ja[U], jb[U];
+    u32x4 ka[U], va[U], kbuf[U], vbuf[U];
+    load(0, ja, ka, va);
+    for (int it = 0; it < iters; it += 2) {
+      if (it + 1 < iters) load(it + 1, jb, kbuf, vbuf);
+      compute(ja, ka, va);
+      if (it + 1 < iters) {
+        if (it + 2 < iters) load(it + 2, ja, ka, va);
+        compute(jb, kbuf, vbuf);
       }
     }
   }

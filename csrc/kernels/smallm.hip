@@ -83,9 +83,16 @@ __device__ __forceinline__ float wave_sum(float v) {
 // interleaved, so their LDS reads and cross-lane reductions overlap — with the same bf16
 // rounding as the standalone LayerNorm / RMSNorm kernels
 template <int MT>
-__device__ __forceinline__ void prologue(const Args& a, const uint16_t* x, int M, uint16_t* xs, int tid) {
+__device__ __forceinline__ void prologue(const Args& a, const uint16_t* x, int M, uint16_t* xs, uint16_t* gb,
+                                         int tid) {
   const int ld = a.K + XPAD;
   const int total = M * a.K;
+  // γ (and β) travel into LDS in the same memory round trip as x
+  if (a.norm != NORM_NONE)
+    for (int c = tid * 8; c < a.K; c += NT * 8) {
+      *reinterpret_cast<u32x4*>(gb + c) = *reinterpret_cast<const u32x4*>(a.nw + c);
+      if (a.norm == NORM_LN) *reinterpret_cast<u32x4*>(gb + a.K + c) = *reinterpret_cast<const u32x4*>(a.nb + c);
+    }
 #pragma unroll 4
   for (int idx = tid * 8; idx < total; idx += NT * 8) {
     const int r = idx / a.K, c = idx - r * a.K;
@@ -133,8 +140,8 @@ __device__ __forceinline__ void prologue(const Args& a, const uint16_t* x, int M
   for (int j = 0; j < RPW; ++j) rstd[j] = rsqrtf(wave_sum(q[j]) / (float)a.K + a.eps);
   for (int c = lane * 8; c < a.K; c += kWave * 8) {
     float g[8], b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    load8<bf16_t>(reinterpret_cast<const bf16_t*>(a.nw + c), g);
-    if (a.norm == NORM_LN) load8<bf16_t>(reinterpret_cast<const bf16_t*>(a.nb + c), b);
+    unpack8(*reinterpret_cast<const u32x4*>(gb + c), g);
+    if (a.norm == NORM_LN) unpack8(*reinterpret_cast<const u32x4*>(gb + a.K + c), b);
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       const int r = wave + NW * j;
@@ -164,7 +171,8 @@ __global__ __launch_bounds__(NT) void linear_small_kernel(Args a) {
   const bool lds_x = a.stage != 0;
   const int ldx_s = a.K + XPAD;
   uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
-  float* red = reinterpret_cast<float*>(smem + (lds_x ? (size_t)MT * 16 * ldx_s * 2 : 0));
+  uint16_t* gb = xs + (lds_x ? (size_t)MT * 16 * ldx_s : 0);  // γ | β (norm prologue only)
+  float* red = reinterpret_cast<float*>(gb + (a.norm != NORM_NONE ? 2 * a.K : 0));
 
   // this workgroup's rows: m-group blockIdx.y of MT·16 rows
   const int row0 = blockIdx.y * MT * 16;
@@ -188,8 +196,19 @@ __global__ __launch_bounds__(NT) void linear_small_kernel(Args a) {
       }
   };
   load_w(blockIdx.x);
+  // the first tile's epilogue operands (bias, residual) are fetched now, not after the reduction
+  constexpr int QPT = (MT * 256 + NT - 1) / NT;
+  float pre_b[QPT], pre_r[QPT];
+#pragma unroll
+  for (int u = 0; u < QPT; ++u) {
+    const int q = tid + u * NT, t = q >> 8, p = q & 255;
+    const int ml = t * 16 + (p >> 4), n = blockIdx.x * 16 + (p & 15);
+    const bool ok = q < MT * 256 && ml < M && n < a.N;
+    pre_b[u] = ok && a.bias != nullptr ? bf16_to_f32(a.bias[n]) : 0.f;
+    pre_r[u] = ok && a.res != nullptr ? bf16_to_f32(a.res[(int64_t)(row0 + ml) * a.N + n]) : 0.f;
+  }
   if (lds_x) {
-    prologue<MT>(a, x, M, xs, tid);
+    prologue<MT>(a, x, M, xs, gb, tid);
     __syncthreads();
   }
 
@@ -226,7 +245,11 @@ __global__ __launch_bounds__(NT) void linear_small_kernel(Args a) {
       for (int t = 0; t < MT; ++t)
         *reinterpret_cast<f4*>(red + (((wave * NACC + j) * MT + t) * 256) + li * 16 + 4 * g) = acc[j][t];
     __syncthreads();
-    for (int q = tid; q < MT * 256; q += NT) {
+    const bool first = tile == (int)blockIdx.x;
+#pragma unroll
+    for (int u = 0; u < QPT; ++u) {
+      const int q = tid + u * NT;
+      if (q >= MT * 256) break;
       const int t = q >> 8, p = q & 255;
       const int ml = t * 16 + (p >> 4), n = n0 + (p & 15);
       const int64_t m = row0 + ml;
@@ -238,10 +261,10 @@ __global__ __launch_bounds__(NT) void linear_small_kernel(Args a) {
       }
       if (ml < M && n < a.N) {
         float y = v0;
-        if (a.bias != nullptr) y += bf16_to_f32(a.bias[n]);
+        if (a.bias != nullptr) y += first ? pre_b[u] : bf16_to_f32(a.bias[n]);
         if (ACT == ACT_GELU) y = gelu_tanh(y);
         if (ACT == ACT_SWIGLU) y = silu(y) * v1;
-        if (a.res != nullptr) y += bf16_to_f32(a.res[m * a.N + n]);
+        if (a.res != nullptr) y += first ? pre_r[u] : bf16_to_f32(a.res[m * a.N + n]);
         a.out[m * a.N + n] = f32_to_bf16(y);
       }
     }
@@ -251,9 +274,10 @@ __global__ __launch_bounds__(NT) void linear_small_kernel(Args a) {
 
 constexpr size_t kMaxLds = 160 * 1024;
 
-static size_t lds_bytes(int MT, int K, bool stage, int act) {
+static size_t lds_bytes(int MT, int K, bool stage, int act, int norm) {
   const size_t xs = stage ? (size_t)MT * 16 * (K + XPAD) * 2 : 0;
-  return xs + (size_t)NW * (act == ACT_SWIGLU ? 2 : 1) * MT * 256 * 4;
+  const size_t gb = norm != NORM_NONE ? (size_t)2 * K * 2 : 0;
+  return xs + gb + (size_t)NW * (act == ACT_SWIGLU ? 2 : 1) * MT * 256 * 4;
 }
 
 at::Tensor linear_small_hip(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
@@ -305,11 +329,11 @@ at::Tensor linear_small_hip(const at::Tensor& x, const at::Tensor& w, const c10:
   // second grid dimension over the row groups (the weights are re-read from L2)
   const int MT_all = (int)((M + 15) / 16);
   int MT = MT_all;
-  if (MT > 1 && (a.ntiles < 128 || lds_bytes(MT, (int)K, true, (int)act) > kMaxLds)) MT = 1;
+  if (MT > 1 && (a.ntiles < 128 || lds_bytes(MT, (int)K, true, (int)act, (int)norm) > kMaxLds)) MT = 1;
   const int mgroups = (MT_all + MT - 1) / MT;
   // the x image goes to LDS whenever it fits (a norm prologue requires it)
-  a.stage = norm != NORM_NONE || lds_bytes(MT, (int)K, true, (int)act) <= kMaxLds;
-  const size_t lds = lds_bytes(MT, (int)K, a.stage != 0, (int)act);
+  a.stage = norm != NORM_NONE || lds_bytes(MT, (int)K, true, (int)act, (int)norm) <= kMaxLds;
+  const size_t lds = lds_bytes(MT, (int)K, a.stage != 0, (int)act, (int)norm);
   TORCH_CHECK(lds <= kMaxLds, "linear_small: needs ", lds, " B of LDS (> 160 KiB); normalise separately");
   // the prologue is recomputed per workgroup: cap the grid there (workgroups loop over tiles)
   const int grid = a.stage ? std::min(a.ntiles, 512) : a.ntiles;

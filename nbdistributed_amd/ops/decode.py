@@ -95,7 +95,7 @@ _ACT = {"none": 0, "gelu": 1, "swiglu": 2}
 
 def _lds_bytes(M: int, K: int, norm: int, act: int) -> int:
     mt = 1 if norm else -(-M // 16)  # the kernel falls back to one m-tile per workgroup
-    return (mt * 16 * (K + 8) * 2 if norm else 0) + 8 * (2 if act == 2 else 1) * mt * 256 * 4
+    return (mt * 16 * (K + 8) * 2 + 4 * K if norm else 0) + 8 * (2 if act == 2 else 1) * mt * 256 * 4
 
 
 def linear_small_supported(x, w, norm=None, act: str = "none") -> bool:
