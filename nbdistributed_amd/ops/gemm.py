@@ -19,7 +19,47 @@ from ._lib import _require
 # NBD_HIP_GEMM=0 routes gemm_linear / mlp_gelu to PyTorch (hipBLASLt) — for A/B measurements
 ENABLED = os.environ.get("NBD_HIP_GEMM", "1") != "0"
 KSPLIT = os.environ.get("NBD_GEMM_KSPLIT", "1") != "0"
-FUSED_SWIGLU = os.environ.get("NBD_FUSED_SWIGLU", "1") != "0"  # 0: separate swiglu kernels (A/B)  # 0: tuned K-split kernels run as one K-group (A/B)
+FUSED_SWIGLU = os.environ.get("NBD_FUSED_SWIGLU", "1") != "0"  # 0: separate swiglu kernels (A/B)
+# backward: the weight-gradient GEMM on a side stream, concurrent with the input-gradient GEMM
+# (the wgrad products of a GPT-2 block have 144-576 tiles — too few for 256 CUs alone).  Off by
+# default (measured, docs/FINDINGS.md §12): inside a GraphedStep capture the forked step replays
+# 3 % faster (12.9 -> 12.5 ms), but once such a two-stream graph exists every later eager step
+# in the process runs ~7 % slower (13.3 -> 14.4 ms; per-kernel cost, with 4 or 8 HW queues), and
+# forking eagerly costs more host time than the overlap saves.  NBD_CONCURRENT_BWD = 0 (default)
+# | graph (GraphedStep captures only; they raise CAPTURING) | 1 (always).
+CONCURRENT_BWD = os.environ.get("NBD_CONCURRENT_BWD", "0")
+CAPTURING = 0
+_side_streams = {}
+
+
+def _side_stream(device):
+    import torch
+
+    s = _side_streams.get(device)
+    if s is None:
+        s = _side_streams[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+def _concurrent(dgrad_fn, wgrad_fn, ref):
+    """(dgrad_fn(), wgrad_fn()) with wgrad_fn running on a side stream forked from and joined back
+    into the current one — two independent GEMMs share the CUs (also inside graph capture, as a
+    parallel branch).  Outputs made on the side stream are recorded on the current stream."""
+    import torch
+
+    if CONCURRENT_BWD == "0" or (CONCURRENT_BWD != "1" and not CAPTURING) or not ref.is_cuda:
+        return dgrad_fn(), wgrad_fn()
+    cur = torch.cuda.current_stream(ref.device)
+    side = _side_stream(ref.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        w = wgrad_fn()
+    d = dgrad_fn()
+    cur.wait_stream(side)
+    for t in (w if isinstance(w, tuple) else (w,)):
+        if t is not None:
+            t.record_stream(cur)
+    return d, w
 
 EPI_NONE, EPI_GELU, EPI_DGELU, EPI_ROWSUM, EPI_SWIGLU, EPI_DSWIGLU = 0, 1, 2, 3, 4, 5
 
@@ -236,15 +276,19 @@ def _fns():
             x2, w = ctx.saved_tensors
             dy2 = _c(dy).view(-1, dy.shape[-1])
             dx = dw = db = None
-            if ctx.needs_input_grad[0]:
-                dx = matmul(dy2, w, b_kn=True).view(ctx.xshape)
             want_db = ctx.has_bias and ctx.needs_input_grad[2]
-            if ctx.needs_input_grad[1] and want_db:  # bias grad rides in the weight-grad GEMM
-                dw, db = matmul(dy2, x2, a_km=True, b_kn=True, epi=EPI_ROWSUM)
-            elif ctx.needs_input_grad[1]:
-                dw = matmul(dy2, x2, a_km=True, b_kn=True)
-            elif want_db:
-                db = _colsum(dy2, w.dtype)
+
+            def wgrad():
+                if ctx.needs_input_grad[1] and want_db:  # bias grad rides in the weight-grad GEMM
+                    return matmul(dy2, x2, a_km=True, b_kn=True, epi=EPI_ROWSUM)
+                if ctx.needs_input_grad[1]:
+                    return matmul(dy2, x2, a_km=True, b_kn=True), None
+                return None, (_colsum(dy2, w.dtype) if want_db else None)
+
+            if ctx.needs_input_grad[0]:
+                dx, (dw, db) = _concurrent(lambda: matmul(dy2, w, b_kn=True).view(ctx.xshape), wgrad, dy2)
+            else:
+                dw, db = wgrad()
             return dx, dw, db
 
     class _MLPGelu(torch.autograd.Function):
@@ -264,17 +308,23 @@ def _fns():
         def backward(ctx, dy):
             x2, w1, w2, pre, g = ctx.saved_tensors
             dy2 = _c(dy).view(-1, dy.shape[-1])
-            dpre = matmul(dy2, w2, b_kn=True, epi=EPI_DGELU, aux=pre)
-            db1 = db2 = None
-            if ctx.bias[1]:
-                dw2, db2 = matmul(dy2, g, a_km=True, b_kn=True, epi=EPI_ROWSUM)
+
+            def wgrad2():
+                if ctx.bias[1]:
+                    return matmul(dy2, g, a_km=True, b_kn=True, epi=EPI_ROWSUM)
+                return matmul(dy2, g, a_km=True, b_kn=True), None
+
+            dpre, (dw2, db2) = _concurrent(lambda: matmul(dy2, w2, b_kn=True, epi=EPI_DGELU, aux=pre), wgrad2, dy2)
+
+            def wgrad1():
+                if ctx.bias[0]:
+                    return matmul(dpre, x2, a_km=True, b_kn=True, epi=EPI_ROWSUM)
+                return matmul(dpre, x2, a_km=True, b_kn=True), None
+
+            if ctx.needs_input_grad[0]:
+                dx, (dw1, db1) = _concurrent(lambda: matmul(dpre, w1, b_kn=True).view(ctx.xshape), wgrad1, dpre)
             else:
-                dw2 = matmul(dy2, g, a_km=True, b_kn=True)
-            dx = matmul(dpre, w1, b_kn=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-            if ctx.bias[0]:
-                dw1, db1 = matmul(dpre, x2, a_km=True, b_kn=True, epi=EPI_ROWSUM)
-            else:
-                dw1 = matmul(dpre, x2, a_km=True, b_kn=True)
+                dx, (dw1, db1) = None, wgrad1()
             return dx, dw1, db1, dw2, db2
 
     class _MLPSwiGLU(torch.autograd.Function):
@@ -294,10 +344,13 @@ def _fns():
         def backward(ctx, dy):
             x2, w_gu, w_down, pre, act = ctx.saved_tensors
             dy2 = _c(dy).view(-1, dy.shape[-1])
-            dgu = matmul(dy2, w_down, b_kn=True, epi=EPI_DSWIGLU, aux=pre)
-            dw_down = matmul(dy2, act, a_km=True, b_kn=True)
-            dx = matmul(dgu, w_gu, b_kn=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-            dw_gu = matmul(dgu, x2, a_km=True, b_kn=True)
+            dgu, dw_down = _concurrent(lambda: matmul(dy2, w_down, b_kn=True, epi=EPI_DSWIGLU, aux=pre),
+                                       lambda: matmul(dy2, act, a_km=True, b_kn=True), dy2)
+            if ctx.needs_input_grad[0]:
+                dx, dw_gu = _concurrent(lambda: matmul(dgu, w_gu, b_kn=True).view(ctx.xshape),
+                                        lambda: matmul(dgu, x2, a_km=True, b_kn=True), dgu)
+            else:
+                dx, dw_gu = None, matmul(dgu, x2, a_km=True, b_kn=True)
             return dx, dw_gu, dw_down
 
     _Fns = (_Linear, _MLPGelu, _MLPSwiGLU)
