@@ -41,6 +41,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "gemm_common.h"
@@ -80,16 +81,16 @@ __device__ __forceinline__ void wait_barrier() {
 // and the groups' fp32 tiles are summed in LDS before the epilogue — twice the independent work
 // per CU for small, latency-bound products (few tiles, one workgroup per CU), with no extra
 // global traffic or second kernel (unlike split-K across workgroups).
+// The kernel body as a device function: `bx` = tile index (before the XCD remap), `by` = split
+// index, `S` = number of splits, `smem_all` = the launch's single LDS object.  gemm_kernel runs one
+// product per launch; pair_kernel (below) runs two independent products in one grid.
 template <int BM, int BN, bool A_KM, bool B_KN, int EPI, int STAGES, int W, int KS>
-__global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args p) {
+__device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, uint8_t* smem_all) {
   constexpr int NTW = 64 * W * KS, WM = 2, WN = W / 2;
   constexpr int FM = BM / (16 * WM), FN = BN / (16 * WN);  // 16-wide fragments per wave along m / n
   using SM = Smem<BM, BN, STAGES, KS>;
   constexpr int A_BYTES = BM * BK * 2, BUF = SM::BUF, LDC = SM::LDC;
   constexpr int NPT = (BM + BN) / (8 * W);  // glds per thread per K-tile
-  // one __shared__ array for everything (a second LDS object de-pipelines the glds loop:
-  // cdna_hip_programming.md §5 "Projection GEMM" item 4a)
-  __shared__ __attribute__((aligned(1024))) uint8_t smem_all[SM::BYTES];
 
   const int lane = threadIdx.x & 63, wave_all = threadIdx.x >> 6;
   const int kg = wave_all / W, wave = wave_all % W;  // K-split group, wave within the group
@@ -97,11 +98,11 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
   uint8_t* smem = smem_all + kg * (STAGES * BUF);   // this group's pipeline buffers
 
   int tm, tn;
-  tile_coords<8>(p.tiles_m, p.tiles_n, tm, tn);
+  tile_coords<8>(p.tiles_m, p.tiles_n, tm, tn, bx);
   const int m0 = tm * BM, n0 = tn * BN;
 
-  // split-K: grid.y selects the K range
-  const int64_t kz = (int64_t)blockIdx.y * p.K;
+  // split-K: `by` selects the K range
+  const int64_t kz = (int64_t)by * p.K;
   const uint16_t* A = p.a + (A_KM ? kz * p.lda : kz);
   const uint16_t* B = p.b + (B_KN ? kz * p.ldb : kz);
 
@@ -247,7 +248,6 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
   }
 
   constexpr int CPR = BN / 8;  // 8-column chunks per row
-  const int S = gridDim.y;
   if constexpr (ROWSUM) {
     // lanes 0..15 hold row m = .. + lane in element 0 (all four elements are equal)
     if (do_rs && kg == 0 && lane < 16) {
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
       for (int j = 0; j < FM; ++j) {
         const int m = m0 + wm * (BM / WM) + 16 * j + lane;
         if (S > 1)
-          p.ws[(int64_t)S * p.M * p.ldc + (int64_t)blockIdx.y * p.M + m] = accb[j][0];
+          p.ws[(int64_t)S * p.M * p.ldc + (int64_t)by * p.M + m] = accb[j][0];
         else
           p.aux_out[m] = f32_to_bf16(accb[j][0]);
       }
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
     // split-K: this split's fp32 slab; reduce_kernel sums the slabs.  (A last-arriver in-kernel
     // reduction measured slower here: its serial read of S-1 slabs of 16-64 KiB per tile costs
     // more than the extra launch — profiles/gemm_bench_r1.txt.)
-    float* slab = p.ws + (int64_t)blockIdx.y * p.M * p.ldc;
+    float* slab = p.ws + (int64_t)by * p.M * p.ldc;
     for (int c = threadIdx.x; c < BM * CPR; c += NTW) {
       const int r = c / CPR, cn = (c % CPR) * 8;
       float* dst = slab + (int64_t)(m0 + r) * p.ldc + n0 + cn;
@@ -356,6 +356,35 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
       for (int e = 0; e < 8; ++e) v[e] *= dgelu_tanh(h[e]);
     }
     store8<bf16_t>(reinterpret_cast<bf16_t*>(p.c) + off, v);
+  }
+}
+
+template <int BM, int BN, bool A_KM, bool B_KN, int EPI, int STAGES, int W, int KS>
+__global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args p) {
+  // one __shared__ array for everything (a second LDS object de-pipelines the glds loop:
+  // cdna_hip_programming.md §5 "Projection GEMM" item 4a)
+  __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<BM, BN, STAGES, KS>::BYTES];
+  gemm_body<BM, BN, A_KM, B_KN, EPI, STAGES, W, KS>(p, blockIdx.x, blockIdx.y, gridDim.y, smem_all);
+}
+
+// A Linear layer's backward as one launch: blocks [0, nb1) compute the input gradient
+// dx = dy·W (dgrad layout, optional GELU′ epilogue), blocks [nb1, …) the weight gradient
+// dW = dyᵀ·x (split s2 ways, optional bias-gradient row sums).  The weight-gradient products of
+// a GPT-2 block alone have 144-576 work units — too few for 256 CUs at two workgroups each —
+// and the two products are independent, so one grid lets them share the chip (two streams do
+// too, but a graph with a parallel branch slowed every later eager step: docs/FINDINGS.md §12).
+// Both halves: 128x128 tiles, 8 waves, 2 stages (the same threads and LDS, two workgroups per
+// CU).  nb1 is rounded up to a multiple of 8 so each half's block ids keep the XCD mapping.
+template <int EPI1, int EPI2>
+__global__ __launch_bounds__(512, 2) void pair_kernel(Args p1, int t1, int nb1, Args p2, int t2, int s2) {
+  __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<128, 128, 2, 1>::BYTES];
+  const int b = blockIdx.x;
+  if (b < nb1) {
+    if (b >= t1) return;  // padding to the XCD boundary
+    gemm_body<128, 128, false, true, EPI1, 2, 8, 1>(p1, b, 0, 1, smem_all);
+  } else {
+    const int l = b - nb1;
+    gemm_body<128, 128, true, true, EPI2, 2, 8, 1>(p2, l % t2, l / t2, s2, smem_all);
   }
 }
 
@@ -584,7 +613,91 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   }
 }
 
+// A Linear layer's two backward products in one launch (pair_kernel): c1 = a1·b1 in the dgrad
+// layout (a1 [M1][K1], b1 as [K1][N1]) with epi1 ∈ {none, GELU′ (aux_in1 = pre-activation)}, and
+// c2 = a2ᵀ·b2 in the wgrad layout (a2 as [K2][M2], b2 as [K2][N2]) with epi2 ∈ {none, row sums
+// into aux_out2}, split s2 ways along K2 (fp32 slabs + reduce_kernel).  128x128 tiles only.
+void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor& c1, int64_t epi1,
+                   const c10::optional<at::Tensor>& aux_in1, const at::Tensor& a2, const at::Tensor& b2,
+                   const at::Tensor& c2, int64_t epi2, const c10::optional<at::Tensor>& aux_out2, int64_t splits2) {
+  for (const at::Tensor* x : {&a1, &b1, &c1, &a2, &b2, &c2}) {
+    TORCH_CHECK(x->dim() == 2 && x->scalar_type() == at::kBFloat16 && x->is_contiguous() && x->is_cuda() &&
+                    reinterpret_cast<uintptr_t>(x->data_ptr()) % 16 == 0,
+                "nbd::gemm_pair: contiguous 16-B aligned bf16 2-D GPU operands");
+  }
+  TORCH_CHECK(epi1 == EPI_NONE || epi1 == EPI_DGELU, "nbd::gemm_pair: epi1 must be none or GELU'");
+  TORCH_CHECK(epi2 == EPI_NONE || epi2 == EPI_ROWSUM, "nbd::gemm_pair: epi2 must be none or row sums");
+  // product 1: dgrad layout
+  const int M1 = a1.size(0), K1 = a1.size(1), N1 = b1.size(1);
+  TORCH_CHECK(b1.size(0) == K1 && c1.size(0) == M1 && c1.size(1) == N1, "nbd::gemm_pair: product 1 shapes");
+  // product 2: wgrad layout
+  const int K2 = a2.size(0), M2 = a2.size(1), N2 = b2.size(1);
+  TORCH_CHECK(b2.size(0) == K2 && c2.size(0) == M2 && c2.size(1) == N2, "nbd::gemm_pair: product 2 shapes");
+  const int S = splits2 > 0 ? (int)splits2 : 1;
+  TORCH_CHECK(M1 % 128 == 0 && N1 % 128 == 0 && M2 % 128 == 0 && N2 % 128 == 0 && K1 % BK == 0 && K1 > 0 &&
+                  K2 % (BK * S) == 0 && K2 > 0,
+              "nbd::gemm_pair: 128x128 tiles and K divisible into 64-deep tiles (x ", S, " splits)");
+  if (epi1 == EPI_DGELU)
+    TORCH_CHECK(aux_in1 && aux_in1->sizes() == c1.sizes() && aux_in1->is_contiguous() &&
+                    aux_in1->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(aux_in1->data_ptr()) % 16 == 0,
+                "nbd::gemm_pair: aux_in1 (pre-activation)");
+  if (epi2 == EPI_ROWSUM)
+    TORCH_CHECK(aux_out2 && aux_out2->numel() == M2 && aux_out2->is_contiguous() &&
+                    aux_out2->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(aux_out2->data_ptr()) % 16 == 0,
+                "nbd::gemm_pair: aux_out2 (row sums)");
+  // per-lane DMA offsets are 32-bit byte offsets within one tile's rows (gemm_common.h Pieces)
+  TORCH_CHECK((int64_t)128 * a1.size(1) * 2 < (1LL << 32) && (int64_t)BK * b1.size(1) * 2 < (1LL << 32) &&
+                  (int64_t)BK * a2.size(1) * 2 < (1LL << 32) && (int64_t)BK * b2.size(1) * 2 < (1LL << 32),
+              "nbd::gemm_pair: row stride too large for 32-bit DMA offsets");
+  Args p1{}, p2{};
+  p1.a = static_cast<const uint16_t*>(a1.data_ptr());
+  p1.b = static_cast<const uint16_t*>(b1.data_ptr());
+  p1.c = static_cast<uint16_t*>(c1.data_ptr());
+  p1.aux_in = epi1 == EPI_DGELU ? static_cast<const uint16_t*>(aux_in1->data_ptr()) : nullptr;
+  p1.M = M1; p1.N = N1; p1.K = K1;
+  p1.lda = a1.size(1); p1.ldb = b1.size(1); p1.ldc = N1;
+  p1.tiles_m = M1 / 128; p1.tiles_n = N1 / 128;
+  p2.a = static_cast<const uint16_t*>(a2.data_ptr());
+  p2.b = static_cast<const uint16_t*>(b2.data_ptr());
+  p2.c = static_cast<uint16_t*>(c2.data_ptr());
+  p2.aux_out = epi2 == EPI_ROWSUM ? static_cast<uint16_t*>(aux_out2->data_ptr()) : nullptr;
+  p2.M = M2; p2.N = N2; p2.K = K2 / S;
+  p2.lda = a2.size(1); p2.ldb = b2.size(1); p2.ldc = N2;
+  p2.tiles_m = M2 / 128; p2.tiles_n = N2 / 128;
+  at::Tensor ws;
+  if (S > 1) {
+    ws = at::empty({(int64_t)S * M2 * N2 + (epi2 == EPI_ROWSUM ? (int64_t)S * M2 : 0)}, a1.options().dtype(at::kFloat));
+    p2.ws = ws.data_ptr<float>();
+  }
+  const int t1 = p1.tiles_m * p1.tiles_n, t2 = p2.tiles_m * p2.tiles_n;
+  const int nb1 = (t1 + 7) / 8 * 8;
+  const int64_t nblocks = (int64_t)nb1 + (int64_t)t2 * S;
+  TORCH_CHECK(nblocks < (1LL << 31), "nbd::gemm_pair: grid too large");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(a1.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  const dim3 grid((unsigned)nblocks);
+  if (epi1 == EPI_NONE && epi2 == EPI_NONE)
+    hipLaunchKernelGGL((pair_kernel<EPI_NONE, EPI_NONE>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
+  else if (epi1 == EPI_NONE)
+    hipLaunchKernelGGL((pair_kernel<EPI_NONE, EPI_ROWSUM>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
+  else if (epi2 == EPI_NONE)
+    hipLaunchKernelGGL((pair_kernel<EPI_DGELU, EPI_NONE>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
+  else
+    hipLaunchKernelGGL((pair_kernel<EPI_DGELU, EPI_ROWSUM>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  if (S > 1) {
+    const int64_t n8 = (int64_t)M2 * N2 / 8, m8 = epi2 == EPI_ROWSUM ? M2 / 8 : 0;
+    const int blocks = (int)std::min<int64_t>((n8 + m8 + 255) / 256, 2048);
+    hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, p2.ws, S, n8, (int64_t)M2 * N2, p2.c, m8,
+                       p2.aux_out);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+}
+
 }  // namespace gemm
 }  // namespace nbd
 
-TORCH_LIBRARY_IMPL(nbd, CUDA, m) { m.impl("gemm", &nbd::gemm::gemm_hip); }
+TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
+  m.impl("gemm", &nbd::gemm::gemm_hip);
+  m.impl("gemm_pair", &nbd::gemm::gemm_pair_hip);
+}

@@ -34,6 +34,8 @@ TORCH_LIBRARY(nbd, m) {
   m.def("xent_fused(Tensor(a!) logits, Tensor target, int ignore_index, Tensor scale) -> (Tensor, Tensor)");
   m.def("gemm(Tensor a, Tensor b, Tensor(a!) c, bool a_km, bool b_kn, Tensor? bias, int epi, Tensor? aux_in, "
         "Tensor(b!)? aux_out, int splits, int tile) -> ()");
+  m.def("gemm_pair(Tensor a1, Tensor b1, Tensor(a!) c1, int epi1, Tensor? aux_in1, Tensor a2, Tensor b2, "
+        "Tensor(b!) c2, int epi2, Tensor(c!)? aux_out2, int splits2) -> ()");
   m.def("adamw_flat(Tensor grad, Tensor(a!) param, Tensor(b!) master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "
         "float lr, float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, Tensor? grad_scale_t=None, Tensor? step_t=None, Tensor? lr_t=None) -> ()");
 }

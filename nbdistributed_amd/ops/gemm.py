@@ -28,6 +28,9 @@ FUSED_SWIGLU = os.environ.get("NBD_FUSED_SWIGLU", "1") != "0"  # 0: separate swi
 # forking eagerly costs more host time than the overlap saves.  NBD_CONCURRENT_BWD = 0 (default)
 # | graph (GraphedStep captures only; they raise CAPTURING) | 1 (always).
 CONCURRENT_BWD = os.environ.get("NBD_CONCURRENT_BWD", "0")
+# backward: a Linear's input- and weight-gradient GEMMs as one grouped launch (nbd::gemm_pair,
+# 128x128 tiles): the weight-gradient tiles fill the CUs the input-gradient grid leaves idle
+PAIR_BWD = os.environ.get("NBD_GEMM_PAIR", "1") != "0"
 CAPTURING = 0
 _side_streams = {}
 
@@ -62,6 +65,40 @@ def _concurrent(dgrad_fn, wgrad_fn, ref):
     return d, w
 
 EPI_NONE, EPI_GELU, EPI_DGELU, EPI_ROWSUM, EPI_SWIGLU, EPI_DSWIGLU = 0, 1, 2, 3, 4, 5
+
+
+def pair_splits(M2: int, N2: int, K2: int) -> int:
+    """K splits of the weight-gradient half of a grouped backward launch: enough units to cover
+    the CUs (≥ 256 with the input-gradient tiles running alongside), each split ≥ 1024 deep."""
+    t2 = (M2 // 128) * (N2 // 128)
+    s = 1
+    while t2 * s < 256 and s < 8 and K2 % (64 * 2 * s) == 0 and K2 // (2 * s) >= 1024:
+        s *= 2
+    return s
+
+
+def backward_pair(dy2, w, x2, epi1: int = EPI_NONE, aux1=None, bias_grad: bool = False):
+    """(dy2·w [· gelu′(aux1)], dy2ᵀ·x2, Σ_rows dy2 or None) — a Linear's input gradient, weight
+    gradient and bias gradient from one grouped HIP launch; None when the shapes / dtypes do
+    not fit it (the caller then runs the products one by one)."""
+    import torch
+
+    if not (PAIR_BWD and ENABLED and dy2.is_cuda and dy2.dtype == w.dtype == x2.dtype == torch.bfloat16
+            and not torch.is_autocast_enabled()):
+        return None
+    M, N = dy2.shape
+    K = w.shape[1]
+    if (M % 128 or N % 128 or K % 128 or w.shape[0] != N or x2.shape != (M, K) or not dy2.is_contiguous()
+            or not w.is_contiguous() or not x2.is_contiguous()
+            or (aux1 is not None and not aux1.is_contiguous())):
+        return None
+    _require()
+    dx = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
+    dw = torch.empty(N, K, dtype=dy2.dtype, device=dy2.device)
+    db = torch.empty(N, dtype=dy2.dtype, device=dy2.device) if bias_grad else None
+    torch.ops.nbd.gemm_pair(dy2, w, dx, epi1, aux1, dy2, x2, dw, EPI_ROWSUM if bias_grad else EPI_NONE, db,
+                            pair_splits(N, K, M))
+    return dx, dw, db
 
 
 def gemm_ok(M: int, N: int, K: int) -> bool:
@@ -285,6 +322,10 @@ def _fns():
                     return matmul(dy2, x2, a_km=True, b_kn=True), None
                 return None, (_colsum(dy2, w.dtype) if want_db else None)
 
+            if ctx.needs_input_grad[0] and ctx.needs_input_grad[1]:
+                r = backward_pair(dy2, w, x2, bias_grad=want_db)
+                if r is not None:
+                    return r[0].view(ctx.xshape), r[1], r[2]
             if ctx.needs_input_grad[0]:
                 dx, (dw, db) = _concurrent(lambda: matmul(dy2, w, b_kn=True).view(ctx.xshape), wgrad, dy2)
             else:
@@ -308,6 +349,18 @@ def _fns():
         def backward(ctx, dy):
             x2, w1, w2, pre, g = ctx.saved_tensors
             dy2 = _c(dy).view(-1, dy.shape[-1])
+            r2 = backward_pair(dy2, w2, g, EPI_DGELU, pre, bias_grad=ctx.bias[1])
+            if r2 is not None:
+                dpre, dw2, db2 = r2
+                r1 = backward_pair(dpre, w1, x2, bias_grad=ctx.bias[0]) if ctx.needs_input_grad[0] else None
+                if r1 is not None:
+                    return r1[0].view(ctx.xshape), r1[1], r1[2], dw2, db2
+                if ctx.bias[0]:
+                    dw1, db1 = matmul(dpre, x2, a_km=True, b_kn=True, epi=EPI_ROWSUM)
+                else:
+                    dw1, db1 = matmul(dpre, x2, a_km=True, b_kn=True), None
+                dx = matmul(dpre, w1, b_kn=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+                return dx, dw1, db1, dw2, db2
 
             def wgrad2():
                 if ctx.bias[1]:
