@@ -17,7 +17,7 @@ import re
 from collections import defaultdict
 
 FAMILIES = [
-    ("gemm (nbd)", r"nbd::gemm::gemm_kernel|nbd::gemm::g256"),
+    ("gemm (nbd)", r"nbd::gemm::gemm_kernel|nbd::gemm::g256|nbd::gemm::pair_kernel"),
     ("gemm (hipBLASLt)", r"^Cijk_|^Custom_Cijk"),
     ("gemm split-K reduce", r"nbd::gemm::reduce_kernel"),
     ("attention", r"nbd::attn::"),

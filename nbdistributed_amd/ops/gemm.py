@@ -31,6 +31,7 @@ CONCURRENT_BWD = os.environ.get("NBD_CONCURRENT_BWD", "0")
 # backward: a Linear's input- and weight-gradient GEMMs as one grouped launch (nbd::gemm_pair,
 # 128x128 tiles): the weight-gradient tiles fill the CUs the input-gradient grid leaves idle
 PAIR_BWD = os.environ.get("NBD_GEMM_PAIR", "1") != "0"
+PAIR_UNITS = int(os.environ.get("NBD_GEMM_PAIR_UNITS", "256"))  # weight-gradient units to split up to
 CAPTURING = 0
 _side_streams = {}
 
@@ -72,7 +73,7 @@ def pair_splits(M2: int, N2: int, K2: int) -> int:
     the CUs (≥ 256 with the input-gradient tiles running alongside), each split ≥ 1024 deep."""
     t2 = (M2 // 128) * (N2 // 128)
     s = 1
-    while t2 * s < 256 and s < 8 and K2 % (64 * 2 * s) == 0 and K2 // (2 * s) >= 1024:
+    while t2 * s < PAIR_UNITS and s < 8 and K2 % (64 * 2 * s) == 0 and K2 // (2 * s) >= 1024:
         s *= 2
     return s
 
