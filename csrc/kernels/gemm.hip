@@ -368,23 +368,25 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
 }
 
 // A Linear layer's backward as one launch: blocks [0, nb1) compute the input gradient
-// dx = dy·W (dgrad layout, optional GELU′ epilogue), blocks [nb1, …) the weight gradient
-// dW = dyᵀ·x (split s2 ways, optional bias-gradient row sums).  The weight-gradient products of
-// a GPT-2 block alone have 144-576 work units — too few for 256 CUs at two workgroups each —
-// and the two products are independent, so one grid lets them share the chip (two streams do
-// too, but a graph with a parallel branch slowed every later eager step: docs/FINDINGS.md §12).
-// Both halves: 128x128 tiles, 8 waves, 2 stages (the same threads and LDS, two workgroups per
-// CU).  nb1 is rounded up to a multiple of 8 so each half's block ids keep the XCD mapping.
-template <int EPI1, int EPI2>
-__global__ __launch_bounds__(512, 2) void pair_kernel(Args p1, int t1, int nb1, Args p2, int t2, int s2) {
-  __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<128, 128, 2, 1>::BYTES];
+// dx = dy·W (dgrad layout, optional GELU′ / SwiGLU′ epilogue), blocks [nb1, …) the weight
+// gradient dW = dyᵀ·x (split s2 ways, optional bias-gradient row sums).  The weight-gradient
+// products of a GPT-2 block alone have 144-576 work units — too few for 256 CUs at two
+// workgroups each — and the two products are independent, so one grid lets them share the chip
+// (two streams do too, but a graph with a parallel branch slowed every later eager step:
+// docs/FINDINGS.md §12).  Both halves use the same tile / waves / stages, so the workgroups are
+// interchangeable (128x128 / 8 waves / 2 stages; 64x64 / 4 waves / 3 stages for 64-granular
+// shapes such as SmolLM2's).  nb1 is rounded up to a multiple of 8 so each half's block ids keep
+// the XCD mapping.
+template <int BM, int BN, int W, int STAGES, int EPI1, int EPI2>
+__global__ __launch_bounds__(64 * W, 2) void pair_kernel(Args p1, int t1, int nb1, Args p2, int t2, int s2) {
+  __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<BM, BN, STAGES, 1>::BYTES];
   const int b = blockIdx.x;
   if (b < nb1) {
     if (b >= t1) return;  // padding to the XCD boundary
-    gemm_body<128, 128, false, true, EPI1, 2, 8, 1>(p1, b, 0, 1, smem_all);
+    gemm_body<BM, BN, false, true, EPI1, STAGES, W, 1>(p1, b, 0, 1, smem_all);
   } else {
     const int l = b - nb1;
-    gemm_body<128, 128, true, true, EPI2, 2, 8, 1>(p2, l % t2, l / t2, s2, smem_all);
+    gemm_body<BM, BN, true, true, EPI2, STAGES, W, 1>(p2, l % t2, l / t2, s2, smem_all);
   }
 }
 
@@ -625,45 +627,50 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
                     reinterpret_cast<uintptr_t>(x->data_ptr()) % 16 == 0,
                 "nbd::gemm_pair: contiguous 16-B aligned bf16 2-D GPU operands");
   }
-  TORCH_CHECK(epi1 == EPI_NONE || epi1 == EPI_DGELU, "nbd::gemm_pair: epi1 must be none or GELU'");
+  TORCH_CHECK(epi1 == EPI_NONE || epi1 == EPI_DGELU || epi1 == EPI_DSWIGLU,
+              "nbd::gemm_pair: epi1 must be none, GELU' or SwiGLU'");
   TORCH_CHECK(epi2 == EPI_NONE || epi2 == EPI_ROWSUM, "nbd::gemm_pair: epi2 must be none or row sums");
   // product 1: dgrad layout
   const int M1 = a1.size(0), K1 = a1.size(1), N1 = b1.size(1);
-  TORCH_CHECK(b1.size(0) == K1 && c1.size(0) == M1 && c1.size(1) == N1, "nbd::gemm_pair: product 1 shapes");
+  // SwiGLU′ writes d[g|u] [M][2N] from the saved pre-activations [g|u] [M][2N]
+  const int64_t c1N = epi1 == EPI_DSWIGLU ? 2 * (int64_t)N1 : N1;
+  TORCH_CHECK(b1.size(0) == K1 && c1.size(0) == M1 && c1.size(1) == c1N, "nbd::gemm_pair: product 1 shapes");
   // product 2: wgrad layout
   const int K2 = a2.size(0), M2 = a2.size(1), N2 = b2.size(1);
   TORCH_CHECK(b2.size(0) == K2 && c2.size(0) == M2 && c2.size(1) == N2, "nbd::gemm_pair: product 2 shapes");
   const int S = splits2 > 0 ? (int)splits2 : 1;
-  TORCH_CHECK(M1 % 128 == 0 && N1 % 128 == 0 && M2 % 128 == 0 && N2 % 128 == 0 && K1 % BK == 0 && K1 > 0 &&
+  const bool big = M1 % 128 == 0 && N1 % 128 == 0 && M2 % 128 == 0 && N2 % 128 == 0;
+  const int TB = big ? 128 : 64;
+  TORCH_CHECK(M1 % TB == 0 && N1 % TB == 0 && M2 % TB == 0 && N2 % TB == 0 && K1 % BK == 0 && K1 > 0 &&
                   K2 % (BK * S) == 0 && K2 > 0,
-              "nbd::gemm_pair: 128x128 tiles and K divisible into 64-deep tiles (x ", S, " splits)");
-  if (epi1 == EPI_DGELU)
+              "nbd::gemm_pair: 64-granular shapes and K divisible into 64-deep tiles (x ", S, " splits)");
+  if (epi1 != EPI_NONE)
     TORCH_CHECK(aux_in1 && aux_in1->sizes() == c1.sizes() && aux_in1->is_contiguous() &&
                     aux_in1->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(aux_in1->data_ptr()) % 16 == 0,
-                "nbd::gemm_pair: aux_in1 (pre-activation)");
+                "nbd::gemm_pair: aux_in1 (pre-activations)");
   if (epi2 == EPI_ROWSUM)
     TORCH_CHECK(aux_out2 && aux_out2->numel() == M2 && aux_out2->is_contiguous() &&
                     aux_out2->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(aux_out2->data_ptr()) % 16 == 0,
                 "nbd::gemm_pair: aux_out2 (row sums)");
   // per-lane DMA offsets are 32-bit byte offsets within one tile's rows (gemm_common.h Pieces)
-  TORCH_CHECK((int64_t)128 * a1.size(1) * 2 < (1LL << 32) && (int64_t)BK * b1.size(1) * 2 < (1LL << 32) &&
+  TORCH_CHECK((int64_t)TB * a1.size(1) * 2 < (1LL << 32) && (int64_t)BK * b1.size(1) * 2 < (1LL << 32) &&
                   (int64_t)BK * a2.size(1) * 2 < (1LL << 32) && (int64_t)BK * b2.size(1) * 2 < (1LL << 32),
               "nbd::gemm_pair: row stride too large for 32-bit DMA offsets");
   Args p1{}, p2{};
   p1.a = static_cast<const uint16_t*>(a1.data_ptr());
   p1.b = static_cast<const uint16_t*>(b1.data_ptr());
   p1.c = static_cast<uint16_t*>(c1.data_ptr());
-  p1.aux_in = epi1 == EPI_DGELU ? static_cast<const uint16_t*>(aux_in1->data_ptr()) : nullptr;
+  p1.aux_in = epi1 != EPI_NONE ? static_cast<const uint16_t*>(aux_in1->data_ptr()) : nullptr;
   p1.M = M1; p1.N = N1; p1.K = K1;
-  p1.lda = a1.size(1); p1.ldb = b1.size(1); p1.ldc = N1;
-  p1.tiles_m = M1 / 128; p1.tiles_n = N1 / 128;
+  p1.lda = a1.size(1); p1.ldb = b1.size(1); p1.ldc = c1N;
+  p1.tiles_m = M1 / TB; p1.tiles_n = N1 / TB;
   p2.a = static_cast<const uint16_t*>(a2.data_ptr());
   p2.b = static_cast<const uint16_t*>(b2.data_ptr());
   p2.c = static_cast<uint16_t*>(c2.data_ptr());
   p2.aux_out = epi2 == EPI_ROWSUM ? static_cast<uint16_t*>(aux_out2->data_ptr()) : nullptr;
   p2.M = M2; p2.N = N2; p2.K = K2 / S;
   p2.lda = a2.size(1); p2.ldb = b2.size(1); p2.ldc = N2;
-  p2.tiles_m = M2 / 128; p2.tiles_n = N2 / 128;
+  p2.tiles_m = M2 / TB; p2.tiles_n = N2 / TB;
   at::Tensor ws;
   if (S > 1) {
     ws = at::empty({(int64_t)S * M2 * N2 + (epi2 == EPI_ROWSUM ? (int64_t)S * M2 : 0)}, a1.options().dtype(at::kFloat));
@@ -676,14 +683,26 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(a1.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   const dim3 grid((unsigned)nblocks);
-  if (epi1 == EPI_NONE && epi2 == EPI_NONE)
-    hipLaunchKernelGGL((pair_kernel<EPI_NONE, EPI_NONE>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
-  else if (epi1 == EPI_NONE)
-    hipLaunchKernelGGL((pair_kernel<EPI_NONE, EPI_ROWSUM>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
-  else if (epi2 == EPI_NONE)
-    hipLaunchKernelGGL((pair_kernel<EPI_DGELU, EPI_NONE>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
-  else
-    hipLaunchKernelGGL((pair_kernel<EPI_DGELU, EPI_ROWSUM>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
+  auto launch = [&](auto e1, auto e2) {
+    constexpr int E1 = decltype(e1)::value, E2 = decltype(e2)::value;
+    if (big)
+      hipLaunchKernelGGL((pair_kernel<128, 128, 8, 2, E1, E2>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
+    else
+      hipLaunchKernelGGL((pair_kernel<64, 64, 4, 3, E1, E2>), grid, dim3(256), 0, st, p1, t1, nb1, p2, t2, S);
+  };
+  using I0 = std::integral_constant<int, EPI_NONE>;
+  using I2 = std::integral_constant<int, EPI_DGELU>;
+  using I3 = std::integral_constant<int, EPI_ROWSUM>;
+  using I5 = std::integral_constant<int, EPI_DSWIGLU>;
+  if (epi2 == EPI_NONE) {
+    if (epi1 == EPI_NONE) launch(I0{}, I0{});
+    else if (epi1 == EPI_DGELU) launch(I2{}, I0{});
+    else launch(I5{}, I0{});
+  } else {
+    if (epi1 == EPI_NONE) launch(I0{}, I3{});
+    else if (epi1 == EPI_DGELU) launch(I2{}, I3{});
+    else launch(I5{}, I3{});
+  }
   C10_HIP_KERNEL_LAUNCH_CHECK();
   if (S > 1) {
     const int64_t n8 = (int64_t)M2 * N2 / 8, m8 = epi2 == EPI_ROWSUM ? M2 / 8 : 0;

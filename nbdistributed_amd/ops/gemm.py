@@ -68,10 +68,10 @@ def _concurrent(dgrad_fn, wgrad_fn, ref):
 EPI_NONE, EPI_GELU, EPI_DGELU, EPI_ROWSUM, EPI_SWIGLU, EPI_DSWIGLU = 0, 1, 2, 3, 4, 5
 
 
-def pair_splits(M2: int, N2: int, K2: int) -> int:
+def pair_splits(M2: int, N2: int, K2: int, tile: int = 128) -> int:
     """K splits of the weight-gradient half of a grouped backward launch: enough units to cover
     the CUs (≥ 256 with the input-gradient tiles running alongside), each split ≥ 1024 deep."""
-    t2 = (M2 // 128) * (N2 // 128)
+    t2 = (M2 // tile) * (N2 // tile)
     s = 1
     while t2 * s < PAIR_UNITS and s < 8 and K2 % (64 * 2 * s) == 0 and K2 // (2 * s) >= 1024:
         s *= 2
@@ -79,9 +79,11 @@ def pair_splits(M2: int, N2: int, K2: int) -> int:
 
 
 def backward_pair(dy2, w, x2, epi1: int = EPI_NONE, aux1=None, bias_grad: bool = False):
-    """(dy2·w [· gelu′(aux1)], dy2ᵀ·x2, Σ_rows dy2 or None) — a Linear's input gradient, weight
-    gradient and bias gradient from one grouped HIP launch; None when the shapes / dtypes do
-    not fit it (the caller then runs the products one by one)."""
+    """(dy2·w [· act′(aux1)], dy2ᵀ·x2, Σ_rows dy2 or None) — a Linear's input gradient, weight
+    gradient and bias gradient from one grouped HIP launch (``epi1`` = EPI_DGELU with the GELU
+    pre-activation, or EPI_DSWIGLU with the [g|u] pre-activations: the input gradient is then
+    d[g|u] [M, 2K]); None when the shapes / dtypes do not fit it (the caller then runs the
+    products one by one)."""
     import torch
 
     if not (PAIR_BWD and ENABLED and dy2.is_cuda and dy2.dtype == w.dtype == x2.dtype == torch.bfloat16
@@ -89,16 +91,18 @@ def backward_pair(dy2, w, x2, epi1: int = EPI_NONE, aux1=None, bias_grad: bool =
         return None
     M, N = dy2.shape
     K = w.shape[1]
-    if (M % 128 or N % 128 or K % 128 or w.shape[0] != N or x2.shape != (M, K) or not dy2.is_contiguous()
+    cols = 2 * K if epi1 == EPI_DSWIGLU else K
+    if (M % 64 or N % 64 or K % 64 or w.shape[0] != N or x2.shape != (M, K) or not dy2.is_contiguous()
             or not w.is_contiguous() or not x2.is_contiguous()
-            or (aux1 is not None and not aux1.is_contiguous())):
+            or (aux1 is not None and (not aux1.is_contiguous() or aux1.shape != (M, cols)))):
         return None
     _require()
-    dx = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
+    tile = 128 if M % 128 == 0 and N % 128 == 0 and K % 128 == 0 else 64
+    dx = torch.empty(M, cols, dtype=dy2.dtype, device=dy2.device)
     dw = torch.empty(N, K, dtype=dy2.dtype, device=dy2.device)
     db = torch.empty(N, dtype=dy2.dtype, device=dy2.device) if bias_grad else None
     torch.ops.nbd.gemm_pair(dy2, w, dx, epi1, aux1, dy2, x2, dw, EPI_ROWSUM if bias_grad else EPI_NONE, db,
-                            pair_splits(N, K, M))
+                            pair_splits(N, K, M, tile))
     return dx, dw, db
 
 
@@ -398,6 +402,14 @@ def _fns():
         def backward(ctx, dy):
             x2, w_gu, w_down, pre, act = ctx.saved_tensors
             dy2 = _c(dy).view(-1, dy.shape[-1])
+            r2 = backward_pair(dy2, w_down, act, EPI_DSWIGLU, pre)
+            if r2 is not None:
+                dgu, dw_down, _ = r2
+                r1 = backward_pair(dgu, w_gu, x2) if ctx.needs_input_grad[0] else None
+                if r1 is not None:
+                    return r1[0].view(ctx.xshape), r1[1], dw_down
+                dx = matmul(dgu, w_gu, b_kn=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+                return dx, matmul(dgu, x2, a_km=True, b_kn=True), dw_down
             dgu, dw_down = _concurrent(lambda: matmul(dy2, w_down, b_kn=True, epi=EPI_DSWIGLU, aux=pre),
                                        lambda: matmul(dy2, act, a_km=True, b_kn=True), dy2)
             if ctx.needs_input_grad[0]:

@@ -230,7 +230,8 @@ def test_gemm_rowsum_epilogue_is_the_bias_gradient(splits, tile):
 # ---------------------------------------------------------------- grouped backward (gemm_pair)
 @pytest.mark.parametrize("dgelu", [False, True])
 @pytest.mark.parametrize("bias_grad", [False, True])
-@pytest.mark.parametrize("M,N,K", [(8192, 768, 3072), (8192, 3072, 768), (1024, 256, 384), (8192, 768, 768)])
+@pytest.mark.parametrize("M,N,K", [(8192, 768, 3072), (8192, 3072, 768), (1024, 256, 384), (8192, 768, 768),
+                                   (2048, 576, 960), (2048, 1536, 576)])  # 64-granular: SmolLM2 (64x64 tiles)
 def test_gemm_pair_matches_separate_products(dgelu, bias_grad, M, N, K):
     """dx = dy·W (· gelu'(pre)), dW = dyᵀ·x, db = Σ dy from one grouped launch = the fp32 reference."""
     from nbdistributed_amd.ops import gemm as G
@@ -253,3 +254,22 @@ def test_gemm_pair_matches_separate_products(dgelu, bias_grad, M, N, K):
         assert rel(db, dy.float().sum(0)) < 1e-2
     else:
         assert db is None
+
+
+@pytest.mark.parametrize("M,N,I", [(2048, 576, 1536), (1024, 512, 1024)])
+def test_gemm_pair_swiglu_backward(M, N, I):
+    """Llama MLP backward through the grouped launch: d[g|u] (SwiGLU′ epilogue) + dW_down."""
+    from nbdistributed_amd.ops import gemm as G
+
+    g = torch.Generator(device="cuda").manual_seed(M + I)
+    dy = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+    w_down = (torch.randn(N, I, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    act = torch.randn(M, I, device="cuda", generator=g).to(torch.bfloat16)
+    pre = torch.randn(M, 2 * I, device="cuda", generator=g).to(torch.bfloat16)
+    r = G.backward_pair(dy, w_down, act, G.EPI_DSWIGLU, pre)
+    assert r is not None
+    dgu, dw, db = r
+    ref = G._dswiglu_ref((dy.float() @ w_down.float()).to(torch.bfloat16), pre).float()
+    rel = lambda a, b: float((a.float() - b).abs().max() / b.abs().max())  # noqa: E731
+    assert dgu.shape == (M, 2 * I) and rel(dgu, ref) < 2e-2
+    assert rel(dw, dy.float().t() @ act.float()) < 1e-2 and db is None
