@@ -85,14 +85,8 @@ class GraphedStep:
         # thread_local: only this thread's calls are checked during capture — ProcessGroupNCCL's
         # watchdog thread keeps querying its events meanwhile, which "global" mode turns into a
         # hipErrorStreamCaptureUnsupported abort (seen intermittently on this stack)
-        from .ops import gemm as _gemm
-
-        _gemm.CAPTURING += 1  # backward GEMMs fork their weight gradients onto a side stream
-        try:
-            with torch.cuda.graph(self.graph, pool=pool, capture_error_mode="thread_local"):
-                self.static_out = fn(*self.static_args)
-        finally:
-            _gemm.CAPTURING -= 1
+        with torch.cuda.graph(self.graph, pool=pool, capture_error_mode="thread_local"):
+            self.static_out = fn(*self.static_args)
         torch.cuda.synchronize()
 
     def _sync_hyper(self) -> None:

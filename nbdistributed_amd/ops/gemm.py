@@ -20,50 +20,10 @@ from ._lib import _require
 ENABLED = os.environ.get("NBD_HIP_GEMM", "1") != "0"
 KSPLIT = os.environ.get("NBD_GEMM_KSPLIT", "1") != "0"
 FUSED_SWIGLU = os.environ.get("NBD_FUSED_SWIGLU", "1") != "0"  # 0: separate swiglu kernels (A/B)
-# backward: the weight-gradient GEMM on a side stream, concurrent with the input-gradient GEMM
-# (the wgrad products of a GPT-2 block have 144-576 tiles — too few for 256 CUs alone).  Off by
-# default (measured, docs/FINDINGS.md §12): inside a GraphedStep capture the forked step replays
-# 3 % faster (12.9 -> 12.5 ms), but once such a two-stream graph exists every later eager step
-# in the process runs ~7 % slower (13.3 -> 14.4 ms; per-kernel cost, with 4 or 8 HW queues), and
-# forking eagerly costs more host time than the overlap saves.  NBD_CONCURRENT_BWD = 0 (default)
-# | graph (GraphedStep captures only; they raise CAPTURING) | 1 (always).
-CONCURRENT_BWD = os.environ.get("NBD_CONCURRENT_BWD", "0")
 # backward: a Linear's input- and weight-gradient GEMMs as one grouped launch (nbd::gemm_pair,
 # 128x128 tiles): the weight-gradient tiles fill the CUs the input-gradient grid leaves idle
 PAIR_BWD = os.environ.get("NBD_GEMM_PAIR", "1") != "0"
 PAIR_UNITS = int(os.environ.get("NBD_GEMM_PAIR_UNITS", "256"))  # weight-gradient units to split up to
-CAPTURING = 0
-_side_streams = {}
-
-
-def _side_stream(device):
-    import torch
-
-    s = _side_streams.get(device)
-    if s is None:
-        s = _side_streams[device] = torch.cuda.Stream(device=device)
-    return s
-
-
-def _concurrent(dgrad_fn, wgrad_fn, ref):
-    """(dgrad_fn(), wgrad_fn()) with wgrad_fn running on a side stream forked from and joined back
-    into the current one — two independent GEMMs share the CUs (also inside graph capture, as a
-    parallel branch).  Outputs made on the side stream are recorded on the current stream."""
-    import torch
-
-    if CONCURRENT_BWD == "0" or (CONCURRENT_BWD != "1" and not CAPTURING) or not ref.is_cuda:
-        return dgrad_fn(), wgrad_fn()
-    cur = torch.cuda.current_stream(ref.device)
-    side = _side_stream(ref.device)
-    side.wait_stream(cur)
-    with torch.cuda.stream(side):
-        w = wgrad_fn()
-    d = dgrad_fn()
-    cur.wait_stream(side)
-    for t in (w if isinstance(w, tuple) else (w,)):
-        if t is not None:
-            t.record_stream(cur)
-    return d, w
 
 EPI_NONE, EPI_GELU, EPI_DGELU, EPI_ROWSUM, EPI_SWIGLU, EPI_DSWIGLU = 0, 1, 2, 3, 4, 5
 
@@ -332,9 +292,8 @@ def _fns():
                 if r is not None:
                     return r[0].view(ctx.xshape), r[1], r[2]
             if ctx.needs_input_grad[0]:
-                dx, (dw, db) = _concurrent(lambda: matmul(dy2, w, b_kn=True).view(ctx.xshape), wgrad, dy2)
-            else:
-                dw, db = wgrad()
+                dx = matmul(dy2, w, b_kn=True).view(ctx.xshape)
+            dw, db = wgrad()
             return dx, dw, db
 
     class _MLPGelu(torch.autograd.Function):
@@ -372,17 +331,16 @@ def _fns():
                     return matmul(dy2, g, a_km=True, b_kn=True, epi=EPI_ROWSUM)
                 return matmul(dy2, g, a_km=True, b_kn=True), None
 
-            dpre, (dw2, db2) = _concurrent(lambda: matmul(dy2, w2, b_kn=True, epi=EPI_DGELU, aux=pre), wgrad2, dy2)
+            dpre = matmul(dy2, w2, b_kn=True, epi=EPI_DGELU, aux=pre)
+            dw2, db2 = wgrad2()
 
             def wgrad1():
                 if ctx.bias[0]:
                     return matmul(dpre, x2, a_km=True, b_kn=True, epi=EPI_ROWSUM)
                 return matmul(dpre, x2, a_km=True, b_kn=True), None
 
-            if ctx.needs_input_grad[0]:
-                dx, (dw1, db1) = _concurrent(lambda: matmul(dpre, w1, b_kn=True).view(ctx.xshape), wgrad1, dpre)
-            else:
-                dx, (dw1, db1) = None, wgrad1()
+            dx = matmul(dpre, w1, b_kn=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+            dw1, db1 = wgrad1()
             return dx, dw1, db1, dw2, db2
 
     class _MLPSwiGLU(torch.autograd.Function):
@@ -410,14 +368,10 @@ def _fns():
                     return r1[0].view(ctx.xshape), r1[1], dw_down
                 dx = matmul(dgu, w_gu, b_kn=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
                 return dx, matmul(dgu, x2, a_km=True, b_kn=True), dw_down
-            dgu, dw_down = _concurrent(lambda: matmul(dy2, w_down, b_kn=True, epi=EPI_DSWIGLU, aux=pre),
-                                       lambda: matmul(dy2, act, a_km=True, b_kn=True), dy2)
-            if ctx.needs_input_grad[0]:
-                dx, dw_gu = _concurrent(lambda: matmul(dgu, w_gu, b_kn=True).view(ctx.xshape),
-                                        lambda: matmul(dgu, x2, a_km=True, b_kn=True), dgu)
-            else:
-                dx, dw_gu = None, matmul(dgu, x2, a_km=True, b_kn=True)
-            return dx, dw_gu, dw_down
+            dgu = matmul(dy2, w_down, b_kn=True, epi=EPI_DSWIGLU, aux=pre)
+            dw_down = matmul(dy2, act, a_km=True, b_kn=True)
+            dx = matmul(dgu, w_gu, b_kn=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+            return dx, matmul(dgu, x2, a_km=True, b_kn=True), dw_down
 
     _Fns = (_Linear, _MLPGelu, _MLPSwiGLU)
     return _Fns
