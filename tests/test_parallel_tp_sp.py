@@ -521,3 +521,8 @@ def test_mesh_single_process_and_shape_check():
         ParallelMesh(dp=3)
     with pytest.raises(ValueError):
         ParallelMesh()
+
+
+def test_four_ranks_tp_generation():
+    # one GPT-2 head per rank: the per-rank caches hold a single head each
+    _spawn(_tp_generate_case, 4)
