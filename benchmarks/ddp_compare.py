@@ -57,11 +57,6 @@ def main():
                 if hasattr(mod, "hip_gemm"):
                     mod.hip_gemm = False
         kind = impl[:-4] if impl.endswith("blas") else impl
-        if kind == "flatov":  # FlatAdamW(overlap=True): bucket updates during the backward
-            m = m.to(torch.bfloat16)
-            w = NbdDDP(m, flat_params=True, grad_mode="bucket")
-            models[impl] = (w, FlatAdamW(w, lr=3e-4, overlap=True), False)
-            continue
         if kind in ("flat", "flatgraph"):
             # bf16 parameters re-homed into the DDP buckets, fp32 master/moments inside FlatAdamW,
             # one fused HIP AdamW kernel per bucket; no autocast casts in the forward

@@ -31,19 +31,11 @@ class FlatAdamW(torch.optim.Optimizer):
     (the bucket kernels apply one lr / weight decay to the whole model)."""
 
     def __init__(self, ddp, lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 1e-2, capturable: bool = False, overlap: bool = False):
+                 weight_decay: float = 1e-2, capturable: bool = False):
         """``capturable=True``: the step counter and lr live in device memory (``step_t``,
         ``lr_t``) so the update can be captured in a HIP graph and replayed
         (:class:`nbdistributed_amd.graphs.GraphedStep` calls :meth:`sync_hyper` before each
-        replay to push the current ``param_groups[0]['lr']``).
-
-        ``overlap=True``: each bucket's update is issued during the backward, on the DDP
-        communication stream right after that bucket's collective, so the memory-bound AdamW
-        passes run alongside the remaining backward GEMMs; :meth:`step` then only joins them.
-        A bucket is complete only after its earliest layer's backward ran, so no later backward
-        op reads a weight that was already updated.  Needs the eager side-stream path (no graph
-        capture: there the update stays in :meth:`step`) and excludes :meth:`clip_grad_norm_`
-        (the global norm needs every gradient before any update)."""
+        replay to push the current ``param_groups[0]['lr']``)."""
         if not getattr(ddp, "flat_params", False) or ddp.grad_mode != "bucket":
             raise ValueError("FlatAdamW needs DistributedDataParallel(..., flat_params=True, grad_mode='bucket')")
         super().__init__(list(ddp.params), dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
@@ -56,12 +48,6 @@ class FlatAdamW(torch.optim.Optimizer):
         self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev) if capturable else None
         self.flat_state: List[Dict[str, torch.Tensor]] = []
         self.sharded = bool(getattr(ddp, "shard", False))
-        self.overlap = overlap
-        self._applied = 0  # buckets already updated by the backward (overlap mode)
-        if overlap:
-            if capturable or self.sharded:
-                raise ValueError("FlatAdamW(overlap=True): not with capturable=True or a sharded DDP")
-            ddp.bucket_update = self._update_in_backward
         for b in ddp.buckets:
             master = self._param_slice(b).detach().float().clone()
             self.flat_state.append({"master": master, "exp_avg": torch.zeros_like(master),
@@ -74,27 +60,8 @@ class FlatAdamW(torch.optim.Optimizer):
         return b.grad_shard if self.sharded else b.buffer
 
     @torch.no_grad()
-    @torch.no_grad()
-    def _update_in_backward(self, b) -> None:
-        """DDP calls this on its communication stream once bucket ``b``'s collective is queued."""
-        if self._applied == 0:
-            self.step_count += 1  # the first bucket of this backward opens the step
-        i = self.ddp.buckets.index(b)
-        st, g = self.flat_state[i], self.param_groups[0]
-        b1, b2 = g["betas"]
-        ops.adamw_flat(self._grad(b), self._param_slice(b), st["master"], st["exp_avg"], st["exp_avg_sq"], g["lr"],
-                       b1, b2, g["eps"], g["weight_decay"], self.step_count)
-        self._applied += 1
-
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        if self.overlap and self._applied:
-            if self._applied != len(self.ddp.buckets):
-                raise RuntimeError(f"FlatAdamW(overlap=True): {self._applied} of {len(self.ddp.buckets)} buckets "
-                                   "were updated in the backward")
-            self.ddp.wait_grads()  # the updates ran on the communication stream
-            self._applied = 0
-            return loss
         g = self.param_groups[0]
         self.step_count += 1
         b1, b2 = g["betas"]
@@ -133,8 +100,6 @@ class FlatAdamW(torch.optim.Optimizer):
         comes from the one-pass summary kernel (``ops.tensor_summary_raw``, float64 partials) over
         each averaged bucket; the clip coefficient stays on the device and is applied inside the
         next ``step()`` — no host synchronisation.  Returns the total norm (device tensor)."""
-        if self.overlap:
-            raise RuntimeError("FlatAdamW(overlap=True) updates during the backward: clip_grad_norm_ is not available")
         sq = None
         if hasattr(self.ddp, "wait_grads"):
             self.ddp.wait_grads()

@@ -133,7 +133,6 @@ class DistributedDataParallel(torch.nn.Module):
         # (the tied embedding / LM head, finished only when backward ends) is never overlapped
         # by backward itself
         self._per_bucket_wait = self.comm_stream is not None and grad_mode == "bucket"
-        self.bucket_update = None  # FlatAdamW(overlap=True): callback run after each bucket's collective
         self._joined = True
         if self._per_bucket_wait:
             for b in self.buckets:
@@ -302,8 +301,6 @@ class DistributedDataParallel(torch.nn.Module):
                 b.work.wait()  # device-side: the comm stream waits for RCCL's stream
                 if unflatten:
                     ops.bucket_unflatten(b.buffer, grads, b.offsets)
-                if self.bucket_update is not None:
-                    self.bucket_update(b)  # optimizer step of this bucket, overlapping the backward
                 if self._per_bucket_wait:
                     b.done.record(self.comm_stream)
             for g in grads:
@@ -336,8 +333,6 @@ class DistributedDataParallel(torch.nn.Module):
                     b.work.wait()
                     if self.grad_mode == "unflatten":
                         ops.bucket_unflatten(b.buffer, b.grads, b.offsets)
-                    if self.bucket_update is not None and not self._capturing:
-                        self.bucket_update(b)  # no side stream here: update as each bucket lands
         for b in self.buckets:
             b.grads = []
             b.work = None

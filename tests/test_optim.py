@@ -135,42 +135,3 @@ def test_flat_adamw_drives_lr_scheduler(sess):
 def test_flat_adamw_requires_bucket_mode(sess):
     r = sess.execute("FlatAdamW(NbdDDP(copy.deepcopy(base)))", render=False, raise_on_error=False)
     assert not r.ok and "flat_params=True" in str(r.errors)
-
-
-OVERLAP = """
-torch.manual_seed(7 + rank)
-base2 = Net()
-plain = NbdDDP(copy.deepcopy(base2), bucket_cap_mb=0.01, first_bucket_mb=0.005, flat_params=True, grad_mode="bucket")
-over = NbdDDP(copy.deepcopy(base2), bucket_cap_mb=0.01, first_bucket_mb=0.005, flat_params=True, grad_mode="bucket")
-o_plain = FlatAdamW(plain, lr=3e-3, weight_decay=0.05)
-o_over = FlatAdamW(over, lr=3e-3, weight_decay=0.05, overlap=True)
-sched = torch.optim.lr_scheduler.LambdaLR(o_over, lambda s: 1.0 / (1 + s))
-sched_p = torch.optim.lr_scheduler.LambdaLR(o_plain, lambda s: 1.0 / (1 + s))
-g = torch.Generator().manual_seed(2000 + rank)
-for step in range(4):
-    x = torch.randn(16, 32, generator=g)
-    for model, o, sc in ((plain, o_plain, sched_p), (over, o_over, sched)):
-        model(x).square().mean().backward()
-        o.step(); o.zero_grad(); sc.step()
-    if step == 1:  # gradient accumulation: no update until the synchronising backward
-        with over.no_sync():
-            over(x).square().mean().backward()
-        with plain.no_sync():
-            plain(x).square().mean().backward()
-err = max(float((p - q).detach().abs().max()) for p, q in zip(plain.module.parameters(), over.module.parameters()))
-try:
-    o_over.clip_grad_norm_(1.0)
-    clip_refused = False
-except RuntimeError:
-    clip_refused = True
-(err == 0.0, o_over.step_count == o_plain.step_count == 4, clip_refused)
-"""
-
-
-def test_flat_adamw_overlap_matches_step_after_backward(sess):
-    # FlatAdamW(overlap=True): each bucket updated as its collective lands (here: in the DDP
-    # finalize; on a GPU on the communication stream during the backward) = the usual step
-    r = sess.execute(OVERLAP, render=False)
-    assert r.ok, r.errors
-    for rank in (0, 1):
-        assert r.results[rank]["echo"] == "(True, True, True)", r.results[rank]
