@@ -69,6 +69,8 @@ def plain(obj: Any) -> Any:
     return str(obj)
 
 
+_PHASE_TIMING = os.environ.get("NBD_WORKER_TIMING") == "1"
+
 class DistributedWorker:
     def __init__(self, rank: int, world_size: int, master_addr: str, master_port: int, coord: str,
                  gpu_id: Optional[int] = None, device_index: Optional[int] = None, backend: str = "auto",
@@ -302,6 +304,7 @@ class DistributedWorker:
         return done
 
     def handle_execute(self, seq: int, data: Any, flags: int) -> Dict[str, Any]:
+        tm = [time.perf_counter()] if _PHASE_TIMING else None  # NBD_WORKER_TIMING=1: per-phase µs
         if isinstance(data, dict):  # subset cell: {"code": ..., "ranks": [...]}
             code = data["code"]
             self.guard.enter(data.get("ranks"), self.world_size)
@@ -311,6 +314,8 @@ class DistributedWorker:
         self._set_stream_seq(seq)
         gpu_prev = self._collect_gpu_times()
         ev0 = self._gpu_events()
+        if tm is not None:
+            tm.append(time.perf_counter())
         self.cell_seq = seq
         self.in_cell = True
         try:
@@ -319,6 +324,8 @@ class DistributedWorker:
         finally:
             self.in_cell = False
             self.guard.exit()
+        if tm is not None:
+            tm.append(time.perf_counter())
         out = ""
         if res.has_value:
             try:
@@ -333,7 +340,11 @@ class DistributedWorker:
             sys.stderr.flush()
         except Exception:
             pass
+        if tm is not None:
+            tm.append(time.perf_counter())
         self.sock.stream_flush()
+        if tm is not None:
+            tm.append(time.perf_counter())
         resp: Dict[str, Any] = {"status": "success" if res.status == "ok" else res.status, "rank": self.rank,
                                 "output": out, "exec_s": res.exec_s, "t_start": res.t_start, "t_end": res.t_end}
         if gpu_prev:
@@ -349,6 +360,10 @@ class DistributedWorker:
                 resp["ns_delta"] = self.tracker.delta(self.ns)
             except Exception as e:
                 resp["ns_delta_error"] = str(e)
+        if tm is not None:
+            tm.append(time.perf_counter())
+            resp["timing_us"] = {k: round((tm[i + 1] - tm[i]) * 1e6, 1) for i, k in
+                                 enumerate(("prologue", "exec", "format+events+flush", "stream_flush", "ns_delta"))}
         return resp
 
     def handle_get_var(self, data: Any) -> Dict[str, Any]:
