@@ -210,6 +210,9 @@ struct nbd_socket {
   std::atomic<int64_t> flush_us{2000};
   std::atomic<size_t> stream_max{1 << 16};
   std::atomic<size_t> hwm{0};
+  // latency options: a receiver that expects a reply within tens of microseconds polls instead
+  // of sleeping on a futex / in epoll_wait (each sleep -> wake hop costs 5-30 us on an idle core)
+  std::atomic<int64_t> recv_spin_us{0}, io_spin_us{0};
 
   int ep = -1, evfd = -1;
   std::thread io;
@@ -232,6 +235,8 @@ struct nbd_socket {
   std::condition_variable icv;
   std::deque<Msg*> inbox;
   bool inbox_closed = false;
+  std::atomic<size_t> inbox_n{0};     // inbox.size(), readable without imu (receiver spin)
+  std::atomic<bool> wake_pending{false};  // set by nbd_wake_recv, consumed by one receive call
 
   std::mutex cmu;  // capture state; lock order: cmu -> mu -> Peer::omu
   Capture cap[2];
@@ -246,6 +251,21 @@ struct nbd_socket {
     (void)r;
   }
 
+  // Receiver-side poll (NBD_OPT_RECV_SPIN_US): up to recv_spin_us (bounded by the call's
+  // timeout) watching inbox_n / wake_pending, so a reply that lands within the window is taken
+  // without a futex sleep.
+  void spin_for_inbox(int timeout_ms) {
+    int64_t us = recv_spin_us.load(std::memory_order_relaxed);
+    if (timeout_ms >= 0) us = std::min<int64_t>(us, (int64_t)timeout_ms * 1000);
+    if (us <= 0) return;
+    const auto end = Clock::now() + std::chrono::microseconds(us);
+    for (int i = 0;; ++i) {
+      if (inbox_n.load(std::memory_order_acquire) > 0 || closing.load() || wake_pending.load()) break;
+      __builtin_ia32_pause();
+      if ((i & 63) == 63 && Clock::now() >= end) break;
+    }
+  }
+
   void push_inbox(Msg* m) {
     {
       std::lock_guard<std::mutex> lk(imu);
@@ -254,6 +274,7 @@ struct nbd_socket {
         return;
       }
       inbox.push_back(m);
+      inbox_n.store(inbox.size(), std::memory_order_release);
     }
     icv.notify_one();
   }
@@ -821,8 +842,24 @@ struct nbd_socket {
     sigfillset(&all);
     pthread_sigmask(SIG_BLOCK, &all, nullptr);  // signals belong to the application threads
     epoll_event evs[64];
+    auto active_until = Clock::now(), last_timers = active_until;
     while (!stop.load()) {
-      int n = epoll_wait(ep, evs, 64, next_timeout_ms());
+      // poll window (NBD_OPT_IO_SPIN_US): non-blocking epoll_wait for a while after activity.
+      // It takes no lock (timers() runs at most every 500 us meanwhile), so it does not contend
+      // with the application threads' sends and stream flushes.
+      const int64_t spin = io_spin_us.load(std::memory_order_relaxed);
+      const auto t = Clock::now();
+      const bool polling = spin > 0 && t < active_until;
+      int n = epoll_wait(ep, evs, 64, polling ? 0 : next_timeout_ms());
+      if (n > 0 && spin > 0) active_until = Clock::now() + std::chrono::microseconds(spin);
+      if (polling && n == 0) {
+        if (t - last_timers >= std::chrono::microseconds(500)) {
+          timers();
+          last_timers = t;
+        }
+        __builtin_ia32_pause();
+        continue;
+      }
       if (n < 0) {
         if (errno == EINTR) continue;
         break;
@@ -847,6 +884,7 @@ struct nbd_socket {
         }
       }
       timers();
+      last_timers = Clock::now();
     }
   }
 
@@ -960,6 +998,8 @@ int nbd_setopt_int(nbd_socket* s, int opt, int64_t v) {
     case NBD_OPT_STREAM_MAX_BYTES: s->stream_max = (size_t)v; break;
     case NBD_OPT_RECONNECT_IVL_MS: s->reconnect_ivl_ms = (int)std::max<int64_t>(1, v); break;
     case NBD_OPT_SNDHWM_BYTES: s->hwm = (size_t)v; break;
+    case NBD_OPT_RECV_SPIN_US: s->recv_spin_us = std::max<int64_t>(0, v); break;
+    case NBD_OPT_IO_SPIN_US: s->io_spin_us = std::max<int64_t>(0, v); break;
     default: return fail("EINVAL: option");
   }
   s->wake();
@@ -1111,16 +1151,22 @@ int nbd_send_multi(nbd_socket* s, int nidents, const void* const* iptrs, const s
 int nbd_recv(nbd_socket* s, int timeout_ms, nbd_msg** out) {
   Guard g(s);
   if (!g.ok) return -1;
+  s->spin_for_inbox(timeout_ms);
   std::unique_lock<std::mutex> lk(s->imu);
-  auto pred = [s] { return !s->inbox.empty() || s->inbox_closed; };
+  auto pred = [s] { return !s->inbox.empty() || s->inbox_closed || s->wake_pending.load(); };
   if (timeout_ms < 0) s->icv.wait(lk, pred);
   // system_clock deadline -> pthread_cond_timedwait (steady_clock would use
   // pthread_cond_clockwait, which older ThreadSanitizer runtimes do not intercept)
   else if (!s->icv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms), pred))
     return 1;
-  if (s->inbox.empty()) return -1;
+  if (s->inbox.empty()) {
+    if (s->inbox_closed) return -1;
+    s->wake_pending = false;  // woken by nbd_wake_recv
+    return 1;
+  }
   Msg* m = s->inbox.front();
   s->inbox.pop_front();
+  s->inbox_n.store(s->inbox.size(), std::memory_order_release);
   auto* w = new nbd_msg;
   w->m = std::move(*m);
   delete m;
@@ -1132,12 +1178,17 @@ int nbd_recv_batch(nbd_socket* s, int timeout_ms, void* buf, size_t cap, size_t*
   Guard g(s);
   if (!g.ok) return -1;
   *used = 0;
+  s->spin_for_inbox(timeout_ms);
   std::unique_lock<std::mutex> lk(s->imu);
-  auto pred = [s] { return !s->inbox.empty() || s->inbox_closed; };
+  auto pred = [s] { return !s->inbox.empty() || s->inbox_closed || s->wake_pending.load(); };
   if (timeout_ms < 0) s->icv.wait(lk, pred);
   else if (!s->icv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms), pred))
     return 0;
-  if (s->inbox.empty()) return -1;
+  if (s->inbox.empty()) {
+    if (s->inbox_closed) return -1;
+    s->wake_pending = false;  // woken by nbd_wake_recv
+    return 0;
+  }
   // serialise queued messages: u32 kind, u32 event, u32 nframes, then (u64 len, bytes) per frame
   char* out = static_cast<char*>(buf);
   size_t pos = 0;
@@ -1167,8 +1218,20 @@ int nbd_recv_batch(nbd_socket* s, int timeout_ms, void* buf, size_t cap, size_t*
     delete m;
     ++n;
   }
+  s->inbox_n.store(s->inbox.size(), std::memory_order_release);
   *used = pos;
   return n;
+}
+
+int nbd_wake_recv(nbd_socket* s) {
+  Guard g(s);
+  if (!g.ok) return fail("ECLOSED");
+  {
+    std::lock_guard<std::mutex> lk(s->imu);
+    s->wake_pending = true;
+  }
+  s->icv.notify_all();
+  return 0;
 }
 
 int nbd_msg_kind(const nbd_msg* m) { return m->m.kind; }

@@ -56,7 +56,9 @@ enum {
   NBD_OPT_STREAM_MAX_BYTES = 7,  /* int: flush captured output once this many bytes are buffered */
   NBD_OPT_SIGNAL_PREFIX = 8,     /* bytes: inbound frame-0 prefix that raises SIGINT */
   NBD_OPT_RECONNECT_IVL_MS = 9,  /* int: DEALER reconnect interval */
-  NBD_OPT_SNDHWM_BYTES = 10      /* int: max queued outbound bytes per peer before send blocks */
+  NBD_OPT_SNDHWM_BYTES = 10,     /* int: max queued outbound bytes per peer before send blocks */
+  NBD_OPT_RECV_SPIN_US = 11,     /* int: nbd_recv / nbd_recv_batch poll the inbox this long before sleeping */
+  NBD_OPT_IO_SPIN_US = 12        /* int: the I/O thread polls its descriptors this long after activity */
 };
 
 typedef struct nbd_socket nbd_socket;
@@ -93,6 +95,10 @@ int nbd_recv(nbd_socket* s, int timeout_ms, nbd_msg** out);
  * closed, -2 if the first queued message needs more than cap bytes (*used = the size needed;
  * it stays queued).  One call replaces recv + 5 accessor calls + free per message. */
 int nbd_recv_batch(nbd_socket* s, int timeout_ms, void* buf, size_t cap, size_t* used, int max_msgs);
+/* Make the nbd_recv / nbd_recv_batch call blocked right now — or, if none is, the next one that
+ * finds the inbox empty — return as on a timeout (1 / 0).  Sticky until consumed, so a wake
+ * cannot be lost to a receiver that is just about to block. */
+int nbd_wake_recv(nbd_socket* s);
 int nbd_msg_kind(const nbd_msg* m);
 int nbd_msg_event(const nbd_msg* m);
 int nbd_msg_nframes(const nbd_msg* m);

@@ -13,6 +13,11 @@ Re-design:
   subset — completes through the same lock-protected table of ``PendingRequest`` objects whose
   completion and live events (stream chunks, responses, deaths) are pushed the instant they
   arrive (D-4);
+* leader/follower receive: a thread that waits for a request (``wait`` / ``pump``) parks the
+  receive thread and drains the socket itself, so a reply costs no thread hand-off (receive
+  thread -> Event -> waiter: ≈15-30 us per cell, ``benchmarks/transport_pingpong.py``); the
+  receive thread takes over again as soon as nobody waits.  Both ends poll for up to
+  ``Config.spin_us`` before sleeping (native ``NBD_OPT_RECV_SPIN_US`` / ``NBD_OPT_IO_SPIN_US``);
 * fail-fast: a rank that dies (process exit reported by the launcher, socket EOF, or heartbeat
   timeout) resolves every request waiting on it with a ``dead`` entry, keeping the other ranks'
   results (D-18); a send to a disconnected rank fails immediately (ROUTER_MANDATORY);
@@ -31,6 +36,8 @@ import os
 import queue
 import secrets
 import shutil
+import signal
+import _signal  # the C module: no enum round trip per call (pump swaps the SIGINT handler per wait)
 import tempfile
 import threading
 import time
@@ -39,13 +46,17 @@ from typing import Any, Callable, Dict, Iterable, List, Optional
 from . import protocol as P
 from .protocol import Message  # noqa: F401  (re-exported: reference API)
 from .transport import (EV_AUTH_FAILED, EV_CONNECTED, EV_DISCONNECTED, EV_HANDSHAKE_FAILED, EV_HEARTBEAT_TIMEOUT,
-                        ROUTER, HostUnreachable, Socket, TransportError)
+                        OPT_IO_SPIN_US, OPT_RECV_SPIN_US, ROUTER, HostUnreachable, Socket, TransportError)
 
 OutputCallback = Callable[[int, str, str], None]
 
 MAX_CAPTURED_OUTPUT = 1 << 20  # per rank per request, kept for programmatic callers
 
 log = logging.getLogger("nbdistributed_amd.comm")
+
+LEAD_GRACE_S = 0.02  # the receive thread stays parked this long after a waiter stops draining
+_SIGINT = int(signal.SIGINT)
+_MAIN = threading.main_thread()
 
 
 class RankDied(RuntimeError):
@@ -167,8 +178,16 @@ class CommunicationManager:
                            heartbeat_ivl_ms=cfg.heartbeat_ivl_ms if heartbeat_ivl_ms is None else heartbeat_ivl_ms,
                            heartbeat_timeout_ms=cfg.heartbeat_timeout_ms if heartbeat_timeout_ms is None else heartbeat_timeout_ms,
                            mandatory=True)
+        if cfg.spin_us > 0:
+            self.sock.set_int(OPT_RECV_SPIN_US, cfg.spin_us)
+            self.sock.set_int(OPT_IO_SPIN_US, cfg.spin_us)
         self.endpoint = self.sock.bind(endpoint)
         self._seq = itertools.count(1)
+        # who drains the socket: the receive thread, or one waiting thread (the "leader")
+        self._pcv = threading.Condition()
+        self._bg_pumping = False   # the receive thread is inside recv_batch / handling a batch
+        self._leader: Optional[threading.Thread] = None  # the waiting thread draining the socket
+        self._lead_end = 0.0
         self._lock = threading.Lock()
         self.pending: Dict[int, PendingRequest] = {}
         self.ready: Dict[int, Dict[str, Any]] = {}
@@ -240,13 +259,76 @@ class CommunicationManager:
 
     def wait(self, req: PendingRequest, timeout: Optional[float] = None) -> PendingRequest:
         t = self.default_timeout if timeout is None else timeout
-        ok = req.done.wait(t) if t is not None else _wait_forever(req.done)
+        ok = self.pump(req.done.is_set, t)
+        if ok is None:  # another thread is draining the socket: it completes our request too
+            ok = req.done.wait(t) if t is not None else _wait_forever(req.done)
         self._forget(req)
         if not ok:
             missing = [r for r in req.ranks if r not in req.responses and r not in req.dead]
             log.warning("%s seq %d timed out after %ss; no reply from %s", req.msg_type, req.seq, t, missing)
             raise RequestTimeout(f"{req.msg_type}: no reply from ranks {missing} within {t}s", req.results())
         return req
+
+    def pump(self, ready: Callable[[], bool], timeout: Optional[float]) -> Optional[bool]:
+        """Drain the socket from the calling thread until ``ready()`` (True) or ``timeout``
+        seconds pass (False; None = no limit).  Returns None without waiting if another thread
+        already leads — the caller then waits on its request's Event, which the leader sets.
+
+        The receive thread is parked (woken out of its native wait) for the duration, so replies
+        are decoded by the waiter itself.  In the main thread SIGINT is deferred to batch
+        boundaries: a KeyboardInterrupt raised between the native dequeue and the handling of a
+        batch would lose replies, so the handler only records it and wakes the native wait, and
+        the interrupt is raised here once the batch is handled."""
+        if ready():
+            return True
+        me = threading.current_thread()
+        prev = hit = None
+        try:  # (leadership is released in `finally` whatever interrupts this)
+            with self._pcv:
+                if self._leader is not None or not self.running:
+                    return None
+                self._leader = me  # the receive thread parks while a leader is set
+                while self._bg_pumping:
+                    self.sock.wake_recv()
+                    self._pcv.wait(0.05)
+            if me is _MAIN:
+                cur = _signal.getsignal(_SIGINT)
+                if callable(cur):  # (SIG_IGN / SIG_DFL / a C-level handler: left alone)
+                    hit = []
+
+                    def _deferred(signum, frame):
+                        hit.append(signum)
+                        self.sock.wake_recv()
+
+                    try:
+                        _signal.signal(_SIGINT, _deferred)
+                        prev = cur
+                    except (ValueError, TypeError):  # not the main interpreter
+                        hit = None
+            deadline = None if timeout is None else time.monotonic() + timeout
+            while True:
+                if ready():
+                    return True
+                if hit:  # a deferred Ctrl-C: the previous handler, now that no reply can be lost
+                    hit.clear()
+                    prev(_SIGINT, None)  # (default: raises KeyboardInterrupt)
+                remaining = None if deadline is None else deadline - time.monotonic()
+                if remaining is not None and remaining <= 0:
+                    return False
+                try:
+                    batch = self.sock.recv_batch(timeout=0.5 if remaining is None else min(0.5, remaining))
+                except TransportError:
+                    return ready()
+                for m in batch:
+                    self._handle_message(m)
+        finally:
+            if prev is not None:
+                _signal.signal(_SIGINT, prev)
+            if self._leader is me:
+                # no notify: the receive thread resumes on its own after LEAD_GRACE_S, so
+                # back-to-back cells never wake it (and never have to park it again)
+                self._lead_end = time.monotonic()
+                self._leader = None
 
     def _forget(self, req: PendingRequest) -> None:
         with self._lock:
@@ -313,12 +395,27 @@ class CommunicationManager:
 
     def _message_handler(self) -> None:
         while self.running:
+            with self._pcv:
+                # a waiting thread drains the socket meanwhile; after it stops, wait LEAD_GRACE_S
+                # more in case the next cell follows at once (output that arrives while nobody
+                # waits is delivered at most that late)
+                while self.running and (self._leader is not None or
+                                        time.monotonic() - self._lead_end < LEAD_GRACE_S):
+                    self._pcv.wait(LEAD_GRACE_S)
+                if not self.running:
+                    break
+                self._bg_pumping = True
             try:
-                batch = self.sock.recv_batch(timeout=None)  # every queued reply in one native call
-            except TransportError:
-                break
-            for m in batch:
-                self._handle_message(m)
+                try:
+                    batch = self.sock.recv_batch(timeout=None)  # every queued reply in one native call
+                except TransportError:
+                    break
+                for m in batch:
+                    self._handle_message(m)
+            finally:
+                with self._pcv:
+                    self._bg_pumping = False
+                    self._pcv.notify_all()
 
     def _handle_message(self, m) -> None:
         if True:
@@ -396,6 +493,8 @@ class CommunicationManager:
         for req in reqs:
             for r in req.ranks:
                 req.on_dead(r, "coordinator shut down")
+        with self._pcv:
+            self._pcv.notify_all()
         self.sock.close()
         self.thread.join(timeout=2.0)
         if self._tmpdir:

@@ -34,6 +34,9 @@ class Config:
     heartbeat_ivl_ms: int = field(default_factory=lambda: _env("NBD_HEARTBEAT_IVL_MS", 1000, int))
     heartbeat_timeout_ms: int = field(default_factory=lambda: _env("NBD_HEARTBEAT_TIMEOUT_MS", 15000, int))
     stream_flush_us: int = field(default_factory=lambda: _env("NBD_STREAM_FLUSH_US", 2000, int))
+    # receivers (coordinator and worker main threads, native I/O threads) poll this long before
+    # sleeping: a reply within the window costs no futex / epoll wake-up (0 = always sleep)
+    spin_us: int = field(default_factory=lambda: _env("NBD_SPIN_US", 200, int))
     use_token: bool = field(default_factory=lambda: _env("NBD_TOKEN_AUTH", True, bool))
     # data plane
     backend: str = field(default_factory=lambda: _env("NBD_BACKEND", "auto"))  # auto | rccl | nccl | gloo

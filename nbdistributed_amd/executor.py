@@ -23,11 +23,13 @@ import sys
 import time
 import traceback
 import types
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Any, Dict, Optional
 
 _TOP_LEVEL_AWAIT = getattr(ast, "PyCF_ALLOW_TOP_LEVEL_AWAIT", 0)
 _THIS_FILE = __file__
+_COMPILED_CACHE = 256  # compiled cells kept for re-runs
 
 
 @dataclass
@@ -58,6 +60,7 @@ class CellExecutor:
         self.ns: Dict[str, Any] = self.module.__dict__
         self.tag = tag
         self.count = 0
+        self._compiled: "OrderedDict[tuple, tuple]" = OrderedDict()  # (source, echo) -> (filename, body, expr)
         if install_as_main:
             sys.modules["__main__"] = self.module
 
@@ -88,28 +91,43 @@ class CellExecutor:
         injected exception is reported like the cell's own)."""
         t0 = time.time()
         p0 = time.perf_counter()
-        filename = self._register_source(code)
+        # a re-run cell (same source, same echo mode) reuses its compiled code and its filename
+        # (whose source is still registered): no parse / compile on the round trip
+        hit = self._compiled.get((code, echo))
+        if hit is not None:
+            self._compiled.move_to_end((code, echo))
+            filename = hit[0]
+        else:
+            filename = self._register_source(code)
         res = ExecResult(status="ok", t_start=t0, filename=filename)
         try:
             if pre is not None:
                 pre()
-            try:
-                tree = ast.parse(code, filename=filename, mode="exec")
-            except SyntaxError as e:
-                res.status = "error"
-                res.ename = type(e).__name__
-                res.error = str(e)
-                res.traceback = "".join(traceback.format_exception_only(type(e), e))
-                return res
-            last = None
-            if echo and tree.body and isinstance(tree.body[-1], ast.Expr):
-                last = tree.body.pop()
-            if tree.body:
-                body = compile(tree, filename, "exec", flags=_TOP_LEVEL_AWAIT, dont_inherit=True)
+            if hit is not None:
+                _, body, expr = hit
+            else:
+                try:
+                    tree = ast.parse(code, filename=filename, mode="exec")
+                except SyntaxError as e:
+                    res.status = "error"
+                    res.ename = type(e).__name__
+                    res.error = str(e)
+                    res.traceback = "".join(traceback.format_exception_only(type(e), e))
+                    return res
+                last = body = expr = None
+                if echo and tree.body and isinstance(tree.body[-1], ast.Expr):
+                    last = tree.body.pop()
+                if tree.body:
+                    body = compile(tree, filename, "exec", flags=_TOP_LEVEL_AWAIT, dont_inherit=True)
+                if last is not None:
+                    expr = compile(ast.Expression(last.value), filename, "eval", flags=_TOP_LEVEL_AWAIT,
+                                   dont_inherit=True)
+                self._compiled[(code, echo)] = (filename, body, expr)
+                if len(self._compiled) > _COMPILED_CACHE:
+                    self._compiled.popitem(last=False)
+            if body is not None:
                 self._run_code(body)
-            if last is not None:
-                expr = compile(ast.Expression(last.value), filename, "eval", flags=_TOP_LEVEL_AWAIT,
-                               dont_inherit=True)
+            if expr is not None:
                 value = self._run_code(expr)
                 if value is not None:
                     res.value = value

@@ -329,7 +329,12 @@ class Session:
         while True:
             wait = 0.5 if deadline is None else max(0.0, min(0.5, deadline - time.monotonic()))
             try:
-                ev = events.get(timeout=wait)
+                # drain the socket from this thread until an event is queued (no hand-off from the
+                # receive thread); another thread leading already -> block on the queue as before
+                if self.comm.pump(lambda: not events.empty(), wait) is None:
+                    ev = events.get(timeout=wait)
+                else:
+                    ev = events.get_nowait()
             except queue.Empty:
                 if deadline is not None and time.monotonic() >= deadline:
                     missing = [r for r in req.ranks if r not in req.responses and r not in req.dead]

@@ -47,6 +47,8 @@ OPT_STREAM_MAX_BYTES = 7
 OPT_SIGNAL_PREFIX = 8
 OPT_RECONNECT_IVL_MS = 9
 OPT_SNDHWM_BYTES = 10
+OPT_RECV_SPIN_US = 11
+OPT_IO_SPIN_US = 12
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -87,6 +89,7 @@ def _load():
                                        ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), ctypes.POINTER(i)]
         lib.nbd_recv.argtypes = [vp, i, ctypes.POINTER(vp)]
         lib.nbd_recv_batch.argtypes = [vp, i, vp, sz, ctypes.POINTER(sz), i]
+        lib.nbd_wake_recv.argtypes = [vp]
         lib.nbd_msg_kind.argtypes = [vp]
         lib.nbd_msg_event.argtypes = [vp]
         lib.nbd_msg_nframes.argtypes = [vp]
@@ -151,6 +154,7 @@ class Socket:
         self.kind = kind
         self._closed = False
         self._close_lock = threading.Lock()
+        self._idcache: dict = {}
         if identity is not None:
             self.set_bytes(OPT_IDENTITY, identity)
         if token:
@@ -208,10 +212,15 @@ class Socket:
         fr = [f if isinstance(f, bytes) else bytes(f) for f in frames]
         ptrs = (ctypes.c_char_p * n)(*fr)
         lens = (ctypes.c_size_t * n)(*[len(f) for f in fr])
-        iptrs = (ctypes.c_char_p * k)(*identities)
-        ilens = (ctypes.c_size_t * k)(*[len(x) for x in identities])
+        # the identity arrays of a rank set are built once (every cell goes to the same ranks)
+        key = tuple(identities)
+        cached = self._idcache.get(key)
+        if cached is None:
+            if len(self._idcache) > 64:
+                self._idcache.clear()
+            cached = self._idcache[key] = ((ctypes.c_char_p * k)(*key), (ctypes.c_size_t * k)(*[len(x) for x in key]))
         status = (ctypes.c_int * k)()
-        if self._lib.nbd_send_multi(self._h, k, iptrs, ilens, n, ptrs, lens, status) < 0:
+        if self._lib.nbd_send_multi(self._h, k, cached[0], cached[1], n, ptrs, lens, status) < 0:
             raise TransportError(_err(self._lib))
         return list(status)
 
@@ -249,6 +258,11 @@ class Socket:
                 pos += ln
             out.append(Received(kind, frames, event))
         return out
+
+    def wake_recv(self) -> None:
+        """Make the recv / recv_batch call blocked right now (or the next one that would block)
+        return as on a timeout."""
+        self._lib.nbd_wake_recv(self._h)
 
     def recv(self, timeout: Optional[float] = None) -> Optional[Received]:
         """Block up to ``timeout`` seconds (None = forever).  Returns None on timeout; raises

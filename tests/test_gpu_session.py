@@ -55,6 +55,20 @@ def test_cell_latency_on_gpu_worker(gpu_session):
     assert lat[len(lat) // 2] < 0.005  # < 5 ms p50 (reference: 111.6 ms)
 
 
+def test_cell_gpu_time_reaches_the_timeline(gpu_session):
+    # the end event is recorded after the reply and the time reported with a later cell
+    code = ("a = torch.randn(4096, 4096, device=device)\n"
+            "for _ in range(20):\n    a = (a @ a).tanh_()\n")
+    gpu_session.execute(code, render=False)
+    gpu_session.execute("torch.cuda.synchronize()", render=False)
+    gpu_session.execute("1", render=False)
+    recs = gpu_session.timeline.to_list()
+    timed = [x for x in recs if "a @ a" in x["code_preview"] and x["per_rank"].get(0, {}).get("gpu_ms")]
+    assert timed, recs[-3:]
+    ms = timed[-1]["per_rank"][0]["gpu_ms"]
+    assert 0.5 < ms < 60_000, ms  # 20 fp32 4096^3 products: milliseconds of GPU time
+
+
 def test_nbd_ddp_on_gpu_matches_plain_backward(gpu_session):
     code = (
         "import copy\n"

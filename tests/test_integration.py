@@ -192,6 +192,65 @@ def test_interrupt_running_python_cell(nb):
     assert sh.run_cell("'still alive'").success  # workers survive the interrupt
 
 
+def test_sigint_in_the_coordinator_while_it_drains_the_socket(nb):
+    # the waiting main thread is the socket's leader: a real SIGINT is deferred to a batch
+    # boundary (no reply lost), then raised; the workers are interrupted and the receive thread
+    # takes over again afterwards
+    import signal
+    import threading
+
+    sh, core, cap = nb
+    s = core.session
+    before = signal.getsignal(signal.SIGINT)
+    threading.Timer(0.5, lambda: os.kill(os.getpid(), signal.SIGINT)).start()
+    t = time.time()
+    r = sh.run_cell("import time\nwhile True:\n    time.sleep(0.01)")
+    assert time.time() - t < 15
+    assert isinstance(r.error_in_exec, DistributedExecutionError)
+    assert all(e.get("status") == "interrupted" for e in r.error_in_exec.result.errors.values())
+    assert signal.getsignal(signal.SIGINT) is before
+    assert s.comm._leader is None
+    cap.take()
+    # background output (no request waiting) reaches the output callback through the receive thread
+    got = []
+    s.comm.set_output_callback(lambda rank, text, stream: got.append(text))
+    try:
+        s.execute("import threading\nthreading.Timer(0.2, lambda: print('late-bg', flush=True)).start()", render=False)
+        deadline = time.time() + 10
+        while sum("late-bg" in g for g in got) < 2 and time.time() < deadline:
+            time.sleep(0.05)
+        assert sum("late-bg" in g for g in got) == 2
+    finally:
+        s.comm.set_output_callback(None)
+    assert sh.run_cell("'still alive'").success
+
+
+def test_concurrent_waiters_share_one_leader(nb):
+    # several threads wait at once: one drains the socket, the others are completed by it
+    import threading
+
+    sh, core, cap = nb
+    comm = core.session.comm
+    out, errs = {}, []
+
+    def go(i):
+        try:
+            res = comm.send_to_ranks([i % 2], "execute", f"__import__('time').sleep(0.05 * {i % 3}); {i} * 7", timeout=30)
+            out[i] = res[i % 2]
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ths = [threading.Thread(target=go, args=(i,)) for i in range(6)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(60)
+    assert not errs and len(out) == 6
+    for i, d in out.items():
+        assert str(i * 7) in str(d.get("output", d)), d
+    assert comm._leader is None
+
+
 def test_cell_latency_is_sub_millisecond_scale(nb):
     sh, core, cap = nb
     lat = []

@@ -83,6 +83,20 @@ def ex():
     return CellExecutor(make_namespace_module("__cell_test__"), install_as_main=False)
 
 
+def test_rerun_cell_reuses_compiled_code(ex):
+    ex.run("n_runs = 0")
+    a = ex.run("n_runs += 1\nn_runs * 10")
+    b = ex.run("n_runs += 1\nn_runs * 10")
+    assert (a.value, b.value) == (10, 20) and a.filename == b.filename  # executed again, not cached
+    c = ex.run("n_runs += 1\nn_runs * 10", echo=False)  # other echo mode: compiled separately
+    assert not c.has_value and ex.ns["n_runs"] == 3
+    for _ in range(2):  # a re-run failing cell still points at its own source line
+        e = ex.run("ok = 1\nraise ValueError('boom')")
+        assert e.status == "error" and "raise ValueError('boom')" in e.traceback
+    s = ex.run("def (:")
+    assert s.status == "error" and s.ename == "SyntaxError"
+
+
 def test_expression_and_trailing_expression(ex):
     r = ex.run("1 + 2")
     assert r.status == "ok" and r.value == 3 and r.has_value
