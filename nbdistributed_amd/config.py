@@ -37,6 +37,8 @@ class Config:
     # receivers (coordinator and worker main threads, native I/O threads) poll this long before
     # sleeping: a reply within the window costs no futex / epoll wake-up (0 = always sleep)
     spin_us: int = field(default_factory=lambda: _env("NBD_SPIN_US", 200, int))
+    # the workers' poll window (-1 = spin_us when the machine has a spare CPU per polling thread)
+    worker_spin_us: int = field(default_factory=lambda: _env("NBD_WORKER_SPIN_US", -1, int))
     use_token: bool = field(default_factory=lambda: _env("NBD_TOKEN_AUTH", True, bool))
     # data plane
     backend: str = field(default_factory=lambda: _env("NBD_BACKEND", "auto"))  # auto | rccl | nccl | gloo

@@ -72,6 +72,28 @@ def plain(obj: Any) -> Any:
 
 _PHASE_TIMING = os.environ.get("NBD_WORKER_TIMING") == "1"
 
+def _cpu_budget() -> float:
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2 CPU quota."""
+    try:
+        n = float(len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        n = float(os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, int(quota) / int(period))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _spare_cpus(world_size: int) -> bool:
+    # polling threads: 2 per worker (main + I/O) and 2 in the coordinator, plus one busy thread
+    # per worker while cells run: polling only pays when none of them has to share a CPU
+    return _cpu_budget() >= 3 * world_size + 2
+
+
 class DistributedWorker:
     def __init__(self, rank: int, world_size: int, master_addr: str, master_port: int, coord: str,
                  gpu_id: Optional[int] = None, device_index: Optional[int] = None, backend: str = "auto",
@@ -121,8 +143,11 @@ class DistributedWorker:
                    heartbeat_timeout_ms=max(self.cfg.heartbeat_timeout_ms * 4, 60000))
         s.set_bytes(OPT_SIGNAL_PREFIX, P.INTERRUPT_PREFIX)
         s.set_int(OPT_STREAM_FLUSH_US, self.cfg.stream_flush_us)
-        s.set_int(OPT_RECV_SPIN_US, self.cfg.spin_us)
-        s.set_int(OPT_IO_SPIN_US, self.cfg.spin_us)
+        spin = self.cfg.worker_spin_us
+        if spin < 0:
+            spin = self.cfg.spin_us if _spare_cpus(self.world_size) else 0
+        s.set_int(OPT_RECV_SPIN_US, spin)
+        s.set_int(OPT_IO_SPIN_US, spin)
         s.connect(self.coord)
         self.sock = s
         self._set_stream_seq(0)
