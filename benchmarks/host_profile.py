@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="smollm2", choices=["smollm2", "gpt2"])
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--cprofile", action="store_true", help="Python-level cProfile instead of the torch profiler")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29561")
@@ -65,6 +66,19 @@ def main():
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t) / a.steps * 1e3
     print(f"{a.model}: wall {wall:.2f} ms/step, host issue {host:.2f} ms/step", flush=True)
+    if a.cprofile:
+        import cProfile
+        import pstats
+
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        pr.disable()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(35)
+        dist.destroy_process_group()
+        return
     from torch.profiler import ProfilerActivity, profile
 
     with profile(activities=[ProfilerActivity.CPU]) as prof:

@@ -1,0 +1,438 @@
+// autograd.hip — the Linear / MLP autograd nodes of the model paths in C++.
+//
+// An eager training step of a small model is host-bound: SmolLM2-135M at 16x128 tokens spends
+// ≈11 ms issuing what the GPU runs in 7 ms (graph replay), and a Python torch.autograd.Function
+// costs ≈20-25 µs per call before its kernels (ctx object, saved tensors, Python wrappers around
+// every GEMM) — forward and again backward (benchmarks/host_profile.py --cprofile).  These nodes
+// run the same kernels (gemm.hip: fused bias / GELU / SwiGLU epilogues, the grouped dgrad + wgrad
+// backward launch) with no Python between the dispatcher and the launches.
+//
+// Which kernel (tile, split-K, or the hipBLASLt library GEMM) runs each product is decided in
+// Python once per shape (ops/gemm.py `native_plan`: the tuned table and heuristics of
+// `ops.gemm.config` / `prefer_library`) and passed down as an int list, so the two paths pick
+// identical kernels.  Plan layout: a sequence of products, 3 ints each (library?, tile, splits),
+// then the grouped-launch split counts (-1 = run the backward products one by one):
+//   linear_ag     [fwd, dgrad, wgrad]               + [pair]
+//   mlp_gelu_ag   [fc, proj, proj dgrad, proj wgrad, fc dgrad, fc wgrad]   + [pair proj, pair fc]
+//   mlp_swiglu_ag [gate_up, down, down dgrad, down wgrad, gu dgrad, gu wgrad] + [pair down, pair gu]
+// Python reference: ops/gemm.py _Linear / _MLPGelu / _MLPSwiGLU (same math, same kernels).
+// Also here: the (add +) RMSNorm / LayerNorm nodes (ops/llama.py _RMSNorm / _AddRMSNorm, ops/norm.py
+// _LayerNorm / _AddLayerNorm) and attention from a packed q|k|v projection (ops/attention.py
+// _FlashAttentionQKV).
+#include <ATen/ATen.h>
+#include <torch/csrc/autograd/custom_function.h>
+#include <torch/library.h>
+
+#include "gemm_common.h"
+
+namespace nbd {
+namespace gemm {
+void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_km, bool b_kn,
+              const c10::optional<at::Tensor>& bias, int64_t epi, const c10::optional<at::Tensor>& aux_in,
+              const c10::optional<at::Tensor>& aux_out, int64_t splits, int64_t tile_hint);
+void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor& c1, int64_t epi1,
+                   const c10::optional<at::Tensor>& aux_in1, const at::Tensor& a2, const at::Tensor& b2,
+                   const at::Tensor& c2, int64_t epi2, const c10::optional<at::Tensor>& aux_out2, int64_t splits2);
+}  // namespace gemm
+namespace norm {
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ln_fwd_hip(const at::Tensor& x,
+                                                                      const c10::optional<at::Tensor>& delta,
+                                                                      const at::Tensor& weight,
+                                                                      const at::Tensor& bias, double eps);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_hip(const at::Tensor& x, const at::Tensor& dy,
+                                                          const c10::optional<at::Tensor>& dres,
+                                                          const at::Tensor& weight, const at::Tensor& mean,
+                                                          const at::Tensor& rstd);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rms_fwd_hip(const at::Tensor& x, const c10::optional<at::Tensor>& delta,
+                                                           const at::Tensor& weight, double eps);
+std::tuple<at::Tensor, at::Tensor> rms_bwd_hip(const at::Tensor& x, const at::Tensor& dy,
+                                               const c10::optional<at::Tensor>& dres, const at::Tensor& weight,
+                                               const at::Tensor& rstd);
+}  // namespace norm
+namespace attn {
+std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                                bool causal, double scale, const c10::optional<at::Tensor>& rope_cos,
+                                                const c10::optional<at::Tensor>& rope_sin);
+void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                  const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
+                  const at::Tensor& dk, const at::Tensor& dv, const c10::optional<at::Tensor>& rope_cos,
+                  const c10::optional<at::Tensor>& rope_sin);
+}  // namespace attn
+
+namespace ag {
+using at::Tensor;
+using c10::optional;
+using torch::autograd::AutogradContext;
+using torch::autograd::variable_list;
+using namespace nbd::gemm;
+
+struct Prod {
+  bool lib;
+  int64_t tile, splits;
+};
+
+static Prod prod(at::IntArrayRef plan, int i) {
+  TORCH_CHECK((int64_t)plan.size() >= 3 * (i + 1), "nbd autograd: plan too short");
+  return {plan[3 * i] != 0, plan[3 * i + 1], plan[3 * i + 2]};
+}
+
+static bool aligned(const Tensor& t, int bytes = 16) {
+  return reinterpret_cast<uintptr_t>(t.data_ptr()) % bytes == 0;
+}
+
+static Tensor bf16c(const Tensor& t) {
+  Tensor r = t.scalar_type() == at::kBFloat16 ? t : t.to(at::kBFloat16);
+  return r.is_contiguous() ? r : r.contiguous();
+}
+
+// c = A·B (layouts as gemm.hip), `epi` with its operands; returns (c, aux_out).  The library path
+// (hipBLASLt through at::mm / addmm) serves plain products the plan routes there, and any plain
+// product whose operands are not 16-byte aligned (as ops.gemm.matmul does).
+static std::pair<Tensor, Tensor> run(const Tensor& a, const Tensor& b, bool a_km, bool b_kn, const Prod& p,
+                                     int epi = EPI_NONE, const optional<Tensor>& bias = c10::nullopt,
+                                     const optional<Tensor>& aux = c10::nullopt) {
+  const int64_t M = a_km ? a.size(1) : a.size(0), N = b_kn ? b.size(1) : b.size(0);
+  const bool bias_ok = !bias || (bias->is_contiguous() && aligned(*bias, 8) && bias->scalar_type() == at::kBFloat16);
+  if (epi == EPI_NONE && (p.lib || !aligned(a) || !aligned(b) || !bias_ok)) {
+    const Tensor A = a_km ? a.t() : a, B = b_kn ? b : b.t();
+    return {bias ? at::addmm(*bias, A, B) : at::mm(A, B), Tensor()};
+  }
+  const int64_t cN = epi == EPI_SWIGLU ? N / 2 : epi == EPI_DSWIGLU ? 2 * N : N;
+  Tensor c = at::empty({M, cN}, a.options());
+  Tensor out;
+  if (epi == EPI_GELU) out = at::empty_like(c);
+  if (epi == EPI_ROWSUM) out = at::empty({M}, a.options());
+  if (epi == EPI_SWIGLU) out = at::empty({M, N}, a.options());
+  gemm_hip(a, b, c, a_km, b_kn, bias, epi, aux, out.defined() ? optional<Tensor>(out) : c10::nullopt, p.splits,
+           p.tile);
+  return {c, out};
+}
+
+// dx = dy·W [· act′(aux)], dW = dyᵀ·x [, db = Σ dy] in one grouped launch (gemm_pair_hip)
+static std::tuple<Tensor, Tensor, Tensor> pair(const Tensor& dy, const Tensor& w, const Tensor& x, int epi1,
+                                               const optional<Tensor>& aux1, bool bias_grad, int64_t splits) {
+  const int64_t M = dy.size(0), N = dy.size(1), K = w.size(1);
+  Tensor dx = at::empty({M, epi1 == EPI_DSWIGLU ? 2 * K : K}, dy.options());
+  Tensor dw = at::empty({N, K}, dy.options());
+  Tensor db = bias_grad ? at::empty({N}, dy.options()) : Tensor();
+  gemm_pair_hip(dy, w, dx, epi1, aux1, dy, x, dw, bias_grad ? EPI_ROWSUM : EPI_NONE,
+                bias_grad ? optional<Tensor>(db) : c10::nullopt, splits);
+  return {dx, dw, db};
+}
+
+static std::vector<int64_t> out_shape(const Tensor& x, int64_t n) {
+  std::vector<int64_t> s(x.sizes().begin(), x.sizes().end());
+  s.back() = n;
+  return s;
+}
+
+// ------------------------------------------------------------------------------------- Linear
+static Tensor linear_forward(const Tensor& x2, const Tensor& w, const optional<Tensor>& b, at::IntArrayRef plan) {
+  return run(x2, w, false, false, prod(plan, 0), EPI_NONE, b).first;
+}
+
+struct LinearFn : public torch::autograd::Function<LinearFn> {
+  static Tensor forward(AutogradContext* ctx, const Tensor& x, const Tensor& w, const optional<Tensor>& b,
+                        at::IntArrayRef plan) {
+    at::AutoDispatchBelowADInplaceOrView guard;
+    const Tensor x2 = bf16c(x).view({-1, x.size(-1)});
+    ctx->save_for_backward({x2, w});
+    ctx->saved_data["plan"] = plan.vec();
+    ctx->saved_data["need"] = std::vector<bool>{x.requires_grad(), w.requires_grad(), b && b->requires_grad()};
+    ctx->saved_data["xshape"] = x.sizes().vec();
+    return linear_forward(x2, w, b, plan).view(out_shape(x, w.size(0)));
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const auto saved = ctx->get_saved_variables();
+    const Tensor &x2 = saved[0], &w = saved[1];
+    const auto plan = ctx->saved_data["plan"].toIntVector();
+    const auto need = ctx->saved_data["need"].toBoolList();
+    const auto xshape = ctx->saved_data["xshape"].toIntVector();
+    const bool nx = need[0], nw = need[1], nb = need[2];
+    const Tensor dy = bf16c(grads[0]).view({-1, w.size(0)});
+    Tensor dx, dw, db;
+    if (nx && nw && plan[9] >= 0) {
+      std::tie(dx, dw, db) = pair(dy, w, x2, EPI_NONE, c10::nullopt, nb, plan[9]);
+    } else {
+      if (nx) dx = run(dy, w, false, true, prod(plan, 1)).first;
+      if (nw && nb) std::tie(dw, db) = run(dy, x2, true, true, prod(plan, 2), EPI_ROWSUM);
+      else if (nw) dw = run(dy, x2, true, true, prod(plan, 2)).first;
+      else if (nb) db = dy.sum(0, false, at::kFloat).to(dy.scalar_type());
+    }
+    return {dx.defined() ? dx.view(xshape) : dx, dw, db, Tensor()};
+  }
+};
+
+Tensor linear_ag(const Tensor& x, const Tensor& w, const optional<Tensor>& b, at::IntArrayRef plan) {
+  return LinearFn::apply(x, w, b, plan);
+}
+
+Tensor linear_noag(const Tensor& x, const Tensor& w, const optional<Tensor>& b, at::IntArrayRef plan) {
+  return linear_forward(bf16c(x).view({-1, x.size(-1)}), w, b, plan).view(out_shape(x, w.size(0)));
+}
+
+// ------------------------------------------------------------------------------ GPT-2 MLP (GELU)
+struct MLPGeluFn : public torch::autograd::Function<MLPGeluFn> {
+  static Tensor forward(AutogradContext* ctx, const Tensor& x, const Tensor& w1, const optional<Tensor>& b1,
+                        const Tensor& w2, const optional<Tensor>& b2, at::IntArrayRef plan) {
+    at::AutoDispatchBelowADInplaceOrView guard;
+    const Tensor x2 = bf16c(x).view({-1, x.size(-1)});
+    auto [g, pre] = run(x2, w1, false, false, prod(plan, 0), EPI_GELU, b1);
+    const Tensor y = run(g, w2, false, false, prod(plan, 1), EPI_NONE, b2).first;
+    ctx->save_for_backward({x2, w1, w2, pre, g});
+    ctx->saved_data["plan"] = plan.vec();
+    ctx->saved_data["need"] = std::vector<bool>{x.requires_grad(), b1.has_value(), b2.has_value()};
+    ctx->saved_data["xshape"] = x.sizes().vec();
+    return y.view(out_shape(x, w2.size(0)));
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const auto s = ctx->get_saved_variables();
+    const Tensor &x2 = s[0], &w1 = s[1], &w2 = s[2], &pre = s[3], &g = s[4];
+    const auto plan = ctx->saved_data["plan"].toIntVector();
+    const auto need = ctx->saved_data["need"].toBoolList();
+    const auto xshape = ctx->saved_data["xshape"].toIntVector();
+    const bool nx = need[0], hb1 = need[1], hb2 = need[2];
+    const Tensor dy = bf16c(grads[0]).view({-1, w2.size(0)});
+    Tensor dpre, dw2, db2, dx, dw1, db1;
+    if (plan[18] >= 0) {
+      std::tie(dpre, dw2, db2) = pair(dy, w2, g, EPI_DGELU, pre, hb2, plan[18]);
+    } else {
+      dpre = run(dy, w2, false, true, prod(plan, 2), EPI_DGELU, c10::nullopt, pre).first;
+      if (hb2) std::tie(dw2, db2) = run(dy, g, true, true, prod(plan, 3), EPI_ROWSUM);
+      else dw2 = run(dy, g, true, true, prod(plan, 3)).first;
+    }
+    if (nx && plan[19] >= 0) {
+      std::tie(dx, dw1, db1) = pair(dpre, w1, x2, EPI_NONE, c10::nullopt, hb1, plan[19]);
+    } else {
+      if (nx) dx = run(dpre, w1, false, true, prod(plan, 4)).first;
+      if (hb1) std::tie(dw1, db1) = run(dpre, x2, true, true, prod(plan, 5), EPI_ROWSUM);
+      else dw1 = run(dpre, x2, true, true, prod(plan, 5)).first;
+    }
+    return {dx.defined() ? dx.view(xshape) : dx, dw1, db1, dw2, db2, Tensor()};
+  }
+};
+
+Tensor mlp_gelu_ag(const Tensor& x, const Tensor& w1, const optional<Tensor>& b1, const Tensor& w2,
+                   const optional<Tensor>& b2, at::IntArrayRef plan) {
+  return MLPGeluFn::apply(x, w1, b1, w2, b2, plan);
+}
+
+Tensor mlp_gelu_noag(const Tensor& x, const Tensor& w1, const optional<Tensor>& b1, const Tensor& w2,
+                     const optional<Tensor>& b2, at::IntArrayRef plan) {
+  const Tensor x2 = bf16c(x).view({-1, x.size(-1)});
+  const Tensor g = run(x2, w1, false, false, prod(plan, 0), EPI_GELU, b1).first;
+  return run(g, w2, false, false, prod(plan, 1), EPI_NONE, b2).first.view(out_shape(x, w2.size(0)));
+}
+
+// ----------------------------------------------------------------------------- Llama MLP (SwiGLU)
+struct MLPSwiGLUFn : public torch::autograd::Function<MLPSwiGLUFn> {
+  static Tensor forward(AutogradContext* ctx, const Tensor& x, const Tensor& w_gu, const Tensor& w_down,
+                        at::IntArrayRef plan) {
+    at::AutoDispatchBelowADInplaceOrView guard;
+    const Tensor x2 = bf16c(x).view({-1, x.size(-1)});
+    auto [act, pre] = run(x2, w_gu, false, false, prod(plan, 0), EPI_SWIGLU);
+    const Tensor y = run(act, w_down, false, false, prod(plan, 1)).first;
+    ctx->save_for_backward({x2, w_gu, w_down, pre, act});
+    ctx->saved_data["plan"] = plan.vec();
+    ctx->saved_data["nx"] = x.requires_grad();
+    ctx->saved_data["xshape"] = x.sizes().vec();
+    return y.view(out_shape(x, w_down.size(0)));
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const auto s = ctx->get_saved_variables();
+    const Tensor &x2 = s[0], &w_gu = s[1], &w_down = s[2], &pre = s[3], &act = s[4];
+    const auto plan = ctx->saved_data["plan"].toIntVector();
+    const bool nx = ctx->saved_data["nx"].toBool();
+    const auto xshape = ctx->saved_data["xshape"].toIntVector();
+    const Tensor dy = bf16c(grads[0]).view({-1, w_down.size(0)});
+    Tensor dgu, dw_down, dx, dw_gu, unused;
+    if (plan[18] >= 0) {
+      std::tie(dgu, dw_down, unused) = pair(dy, w_down, act, EPI_DSWIGLU, pre, false, plan[18]);
+    } else {
+      dgu = run(dy, w_down, false, true, prod(plan, 2), EPI_DSWIGLU, c10::nullopt, pre).first;
+      dw_down = run(dy, act, true, true, prod(plan, 3)).first;
+    }
+    if (nx && plan[19] >= 0) {
+      std::tie(dx, dw_gu, unused) = pair(dgu, w_gu, x2, EPI_NONE, c10::nullopt, false, plan[19]);
+    } else {
+      if (nx) dx = run(dgu, w_gu, false, true, prod(plan, 4)).first;
+      dw_gu = run(dgu, x2, true, true, prod(plan, 5)).first;
+    }
+    return {dx.defined() ? dx.view(xshape) : dx, dw_gu, dw_down, Tensor()};
+  }
+};
+
+Tensor mlp_swiglu_ag(const Tensor& x, const Tensor& w_gu, const Tensor& w_down, at::IntArrayRef plan) {
+  return MLPSwiGLUFn::apply(x, w_gu, w_down, plan);
+}
+
+Tensor mlp_swiglu_noag(const Tensor& x, const Tensor& w_gu, const Tensor& w_down, at::IntArrayRef plan) {
+  const Tensor x2 = bf16c(x).view({-1, x.size(-1)});
+  const Tensor act = run(x2, w_gu, false, false, prod(plan, 0), EPI_SWIGLU).first;
+  return run(act, w_down, false, false, prod(plan, 1)).first.view(out_shape(x, w_down.size(0)));
+}
+
+// ------------------------------------------------------------ (add +) RMSNorm / LayerNorm nodes
+// The residual add and the norm in one pass forward (s = x + delta, y = norm(s)), their
+// backward in one pass too (dx = ds + norm′(dy)).  ``delta`` absent: the plain norm (one output).
+static c10::optional<Tensor> opt(const Tensor& t) { return t.defined() ? c10::optional<Tensor>(t.contiguous()) : c10::nullopt; }
+
+struct RMSFn : public torch::autograd::Function<RMSFn> {
+  static variable_list forward(AutogradContext* ctx, const Tensor& x, const optional<Tensor>& delta, const Tensor& w,
+                               double eps) {
+    at::AutoDispatchBelowADInplaceOrView guard;
+    ctx->set_materialize_grads(false);
+    auto [y, sum, rstd] = norm::rms_fwd_hip(x, delta, w, eps);
+    const bool add = delta.has_value();
+    ctx->save_for_backward({add ? sum : x, w, rstd});
+    ctx->saved_data["add"] = add;
+    if (add) return {sum, y};
+    return {y};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const auto sv = ctx->get_saved_variables();
+    const bool add = ctx->saved_data["add"].toBool();
+    const Tensor ds = add ? grads[0] : Tensor(), dy = add ? grads[1] : grads[0];
+    if (!dy.defined()) return {ds, ds, Tensor(), Tensor()};
+    auto [dx, dw] = norm::rms_bwd_hip(sv[0], dy.contiguous(), opt(ds), sv[1], sv[2]);
+    return {dx, add ? dx : Tensor(), dw, Tensor()};
+  }
+};
+
+struct LNFn : public torch::autograd::Function<LNFn> {
+  static variable_list forward(AutogradContext* ctx, const Tensor& x, const optional<Tensor>& delta, const Tensor& w,
+                               const Tensor& b, double eps) {
+    at::AutoDispatchBelowADInplaceOrView guard;
+    ctx->set_materialize_grads(false);
+    auto [y, sum, mean, rstd] = norm::ln_fwd_hip(x, delta, w, b, eps);
+    const bool add = delta.has_value();
+    ctx->save_for_backward({add ? sum : x, w, mean, rstd});
+    ctx->saved_data["add"] = add;
+    if (add) return {sum, y};
+    return {y};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const auto sv = ctx->get_saved_variables();
+    const bool add = ctx->saved_data["add"].toBool();
+    const Tensor ds = add ? grads[0] : Tensor(), dy = add ? grads[1] : grads[0];
+    if (!dy.defined()) return {ds, ds, Tensor(), Tensor(), Tensor()};
+    auto [dx, dw, db] = norm::ln_bwd_hip(sv[0], dy.contiguous(), opt(ds), sv[1], sv[2], sv[3]);
+    return {dx, add ? dx : Tensor(), dw, db, Tensor()};
+  }
+};
+
+Tensor rms_norm_ag(const Tensor& x, const Tensor& w, double eps) { return RMSFn::apply(x, c10::nullopt, w, eps)[0]; }
+std::tuple<Tensor, Tensor> add_rms_norm_ag(const Tensor& x, const Tensor& delta, const Tensor& w, double eps) {
+  auto r = RMSFn::apply(x, optional<Tensor>(delta), w, eps);
+  return {r[0], r[1]};
+}
+Tensor layer_norm_ag(const Tensor& x, const Tensor& w, const Tensor& b, double eps) {
+  return LNFn::apply(x, c10::nullopt, w, b, eps)[0];
+}
+std::tuple<Tensor, Tensor> add_layer_norm_ag(const Tensor& x, const Tensor& delta, const Tensor& w, const Tensor& b,
+                                             double eps) {
+  auto r = LNFn::apply(x, optional<Tensor>(delta), w, b, eps);
+  return {r[0], r[1]};
+}
+Tensor rms_norm_noag(const Tensor& x, const Tensor& w, double eps) {
+  return std::get<0>(norm::rms_fwd_hip(x, c10::nullopt, w, eps));
+}
+std::tuple<Tensor, Tensor> add_rms_norm_noag(const Tensor& x, const Tensor& delta, const Tensor& w, double eps) {
+  auto r = norm::rms_fwd_hip(x, delta, w, eps);
+  return {std::get<1>(r), std::get<0>(r)};
+}
+Tensor layer_norm_noag(const Tensor& x, const Tensor& w, const Tensor& b, double eps) {
+  return std::get<0>(norm::ln_fwd_hip(x, c10::nullopt, w, b, eps));
+}
+std::tuple<Tensor, Tensor> add_layer_norm_noag(const Tensor& x, const Tensor& delta, const Tensor& w, const Tensor& b,
+                                               double eps) {
+  auto r = norm::ln_fwd_hip(x, delta, w, b, eps);
+  return {std::get<1>(r), std::get<0>(r)};
+}
+
+// ------------------------------------------------------------------ attention from packed q|k|v
+// [B, T, (H + 2·Hkv)·D] in, [B, T, H·D] out; the backward writes the packed gradient directly.
+// Python reference: ops/attention.py _FlashAttentionQKV.
+static std::tuple<Tensor, Tensor, Tensor> split_qkv(const Tensor& qkv, int64_t H, int64_t Hkv) {
+  const int64_t B = qkv.size(0), T = qkv.size(1), D = qkv.size(2) / (H + 2 * Hkv);
+  return {qkv.narrow(2, 0, H * D).view({B, T, H, D}).transpose(1, 2),
+          qkv.narrow(2, H * D, Hkv * D).view({B, T, Hkv, D}).transpose(1, 2),
+          qkv.narrow(2, (H + Hkv) * D, Hkv * D).view({B, T, Hkv, D}).transpose(1, 2)};
+}
+
+struct AttnQKVFn : public torch::autograd::Function<AttnQKVFn> {
+  static Tensor forward(AutogradContext* ctx, const Tensor& qkv, int64_t H, int64_t Hkv, bool causal, double scale,
+                        const optional<Tensor>& cos, const optional<Tensor>& sin) {
+    at::AutoDispatchBelowADInplaceOrView guard;
+    auto [q, k, v] = split_qkv(qkv, H, Hkv);
+    auto [o, lse] = attn::attn_fwd_hip(q, k, v, causal, scale, cos, sin);
+    const bool rope = cos.has_value();
+    if (rope) ctx->save_for_backward({qkv, o, lse, *cos, *sin});
+    else ctx->save_for_backward({qkv, o, lse});
+    ctx->saved_data["H"] = H;
+    ctx->saved_data["Hkv"] = Hkv;
+    ctx->saved_data["causal"] = causal;
+    ctx->saved_data["scale"] = scale;
+    return o.transpose(1, 2).reshape({qkv.size(0), qkv.size(1), -1});  // o is stored [B, T, H, D]: a view
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const auto sv = ctx->get_saved_variables();
+    const Tensor &qkv = sv[0], &o = sv[1], &lse = sv[2];
+    const bool rope = sv.size() > 3;
+    const int64_t H = ctx->saved_data["H"].toInt(), Hkv = ctx->saved_data["Hkv"].toInt();
+    const int64_t B = qkv.size(0), T = qkv.size(1), D = qkv.size(2) / (H + 2 * Hkv);
+    auto [q, k, v] = split_qkv(qkv, H, Hkv);
+    Tensor dqkv = at::empty_like(qkv, at::MemoryFormat::Contiguous);
+    auto [dq, dk, dv] = split_qkv(dqkv, H, Hkv);
+    const Tensor dout = grads[0].contiguous().view({B, T, H, D}).transpose(1, 2);
+    attn::attn_bwd_hip(dout, q, k, v, o, lse, ctx->saved_data["causal"].toBool(), ctx->saved_data["scale"].toDouble(),
+                       dq, dk, dv, rope ? optional<Tensor>(sv[3]) : c10::nullopt,
+                       rope ? optional<Tensor>(sv[4]) : c10::nullopt);
+    return {dqkv, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
+  }
+};
+
+Tensor attn_qkv_ag(const Tensor& qkv, int64_t H, int64_t Hkv, bool causal, double scale, const optional<Tensor>& cos,
+                   const optional<Tensor>& sin) {
+  return AttnQKVFn::apply(qkv, H, Hkv, causal, scale, cos, sin);
+}
+
+Tensor attn_qkv_noag(const Tensor& qkv, int64_t H, int64_t Hkv, bool causal, double scale, const optional<Tensor>& cos,
+                     const optional<Tensor>& sin) {
+  auto [q, k, v] = split_qkv(qkv, H, Hkv);
+  auto [o, lse] = attn::attn_fwd_hip(q, k, v, causal, scale, cos, sin);
+  return o.transpose(1, 2).reshape({qkv.size(0), qkv.size(1), -1});
+}
+
+}  // namespace ag
+}  // namespace nbd
+
+// Autograd key: the nodes above.  CUDA key (reached under torch.inference_mode / no autograd):
+// the forward alone.
+TORCH_LIBRARY_IMPL(nbd, Autograd, m) {
+  m.impl("linear_ag", &nbd::ag::linear_ag);
+  m.impl("mlp_gelu_ag", &nbd::ag::mlp_gelu_ag);
+  m.impl("mlp_swiglu_ag", &nbd::ag::mlp_swiglu_ag);
+  m.impl("rms_norm_ag", &nbd::ag::rms_norm_ag);
+  m.impl("add_rms_norm_ag", &nbd::ag::add_rms_norm_ag);
+  m.impl("layer_norm_ag", &nbd::ag::layer_norm_ag);
+  m.impl("add_layer_norm_ag", &nbd::ag::add_layer_norm_ag);
+  m.impl("attn_qkv_ag", &nbd::ag::attn_qkv_ag);
+}
+
+TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
+  m.impl("rms_norm_ag", &nbd::ag::rms_norm_noag);
+  m.impl("add_rms_norm_ag", &nbd::ag::add_rms_norm_noag);
+  m.impl("layer_norm_ag", &nbd::ag::layer_norm_noag);
+  m.impl("add_layer_norm_ag", &nbd::ag::add_layer_norm_noag);
+  m.impl("attn_qkv_ag", &nbd::ag::attn_qkv_noag);
+  m.impl("linear_ag", &nbd::ag::linear_noag);
+  m.impl("mlp_gelu_ag", &nbd::ag::mlp_gelu_noag);
+  m.impl("mlp_swiglu_ag", &nbd::ag::mlp_swiglu_noag);
+}

@@ -36,6 +36,15 @@ TORCH_LIBRARY(nbd, m) {
         "Tensor(b!)? aux_out, int splits, int tile) -> ()");
   m.def("gemm_pair(Tensor a1, Tensor b1, Tensor(a!) c1, int epi1, Tensor? aux_in1, Tensor a2, Tensor b2, "
         "Tensor(b!) c2, int epi2, Tensor(c!)? aux_out2, int splits2) -> ()");
+  // autograd nodes of the fused Linear / MLP paths (autograd.hip); plan = ops/gemm.py native_plan
+  m.def("linear_ag(Tensor x, Tensor w, Tensor? b, int[] plan) -> Tensor");
+  m.def("mlp_gelu_ag(Tensor x, Tensor w1, Tensor? b1, Tensor w2, Tensor? b2, int[] plan) -> Tensor");
+  m.def("mlp_swiglu_ag(Tensor x, Tensor w_gu, Tensor w_down, int[] plan) -> Tensor");
+  m.def("rms_norm_ag(Tensor x, Tensor w, float eps) -> Tensor");
+  m.def("add_rms_norm_ag(Tensor x, Tensor delta, Tensor w, float eps) -> (Tensor, Tensor)");
+  m.def("layer_norm_ag(Tensor x, Tensor w, Tensor b, float eps) -> Tensor");
+  m.def("add_layer_norm_ag(Tensor x, Tensor delta, Tensor w, Tensor b, float eps) -> (Tensor, Tensor)");
+  m.def("attn_qkv_ag(Tensor qkv, int n_head, int n_kv, bool causal, float scale, Tensor? cos, Tensor? sin) -> Tensor");
   m.def("adamw_flat(Tensor grad, Tensor(a!) param, Tensor(b!) master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "
         "float lr, float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, Tensor? grad_scale_t=None, Tensor? step_t=None, Tensor? lr_t=None) -> ()");
 }

@@ -116,6 +116,10 @@ def attention_qkv(qkv, n_head: int, causal: bool = True, scale: Optional[float] 
             and n_head % Hkv == 0):
         _require()
         cos, sin = rope if rope is not None else (None, None)
+        from .gemm import _native
+
+        if _native():  # the C++ autograd node (csrc/kernels/autograd.hip)
+            return torch.ops.nbd.attn_qkv_ag(qkv, int(n_head), int(Hkv), bool(causal), sc, cos, sin)
         return _attn_fns()[1].apply(qkv, int(n_head), int(Hkv), bool(causal), sc, cos, sin)
     if rope is not None:
         from .llama import rope_

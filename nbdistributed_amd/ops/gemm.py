@@ -24,6 +24,9 @@ FUSED_SWIGLU = os.environ.get("NBD_FUSED_SWIGLU", "1") != "0"  # 0: separate swi
 # 128x128 tiles): the weight-gradient tiles fill the CUs the input-gradient grid leaves idle
 PAIR_BWD = os.environ.get("NBD_GEMM_PAIR", "1") != "0"
 PAIR_UNITS = int(os.environ.get("NBD_GEMM_PAIR_UNITS", "256"))  # weight-gradient units to split up to
+# the Linear / MLP autograd nodes in C++ (csrc/kernels/autograd.hip) instead of the Python
+# autograd.Functions below: same kernels, no Python between the dispatcher and the launches
+NATIVE_AUTOGRAD = os.environ.get("NBD_NATIVE_AUTOGRAD", "1") != "0"
 
 EPI_NONE, EPI_GELU, EPI_DGELU, EPI_ROWSUM, EPI_SWIGLU, EPI_DSWIGLU = 0, 1, 2, 3, 4, 5
 
@@ -377,6 +380,68 @@ def _fns():
     return _Fns
 
 
+# ---------------------------------------------------------------- plans for the C++ autograd nodes
+_PLANS: dict = {}
+
+
+def _prod(a_km: bool, b_kn: bool, M: int, N: int, K: int, epi: int = EPI_NONE, can_split: bool = True) -> list:
+    """[library?, tile, splits] — exactly what ``matmul`` picks for this product."""
+    t, s = config(a_km, b_kn, M, N, K, can_split=can_split, epi=epi)
+    return [1 if prefer_library(a_km, b_kn, M, N, K, epi) else 0, t, s]
+
+
+def _pair_plan(M: int, N: int, K: int) -> int:
+    """Split count of the grouped backward launch for dy [M, N], W [N, K] (``backward_pair``), or
+    -1 when the grouped launch is off."""
+    if not PAIR_BWD:
+        return -1
+    tile = 128 if M % 128 == 0 and N % 128 == 0 and K % 128 == 0 else 64
+    return pair_splits(N, K, M, tile)
+
+
+def native_plan(kind: str, M: int, H: int, I: int, bias1: bool = False, bias2: bool = False) -> list:
+    """The int plan of ``torch.ops.nbd.{linear,mlp_gelu,mlp_swiglu}_ag`` (layout: autograd.hip),
+    cached per shape.  ``linear``: x [M, I] -> [M, H] (W [H, I]); MLPs: x [M, H], hidden I."""
+    key = (kind, M, H, I, bias1, bias2)
+    p = _PLANS.get(key)
+    if p is not None:
+        return p
+    R = EPI_ROWSUM
+    if kind == "linear":
+        N, K = H, I
+        p = (_prod(False, False, M, N, K, can_split=not bias1) + _prod(False, True, M, K, N)
+             + _prod(True, True, N, K, M, R if bias1 else EPI_NONE) + [_pair_plan(M, N, K)])
+    elif kind == "mlp_gelu":
+        p = (_prod(False, False, M, I, H, EPI_GELU, can_split=False) + _prod(False, False, M, H, I, can_split=not bias2)
+             + _prod(False, True, M, I, H, EPI_DGELU, can_split=False) + _prod(True, True, H, I, M, R if bias2 else EPI_NONE)
+             + _prod(False, True, M, H, I) + _prod(True, True, I, H, M, R if bias1 else EPI_NONE)
+             + [_pair_plan(M, H, I), _pair_plan(M, I, H)])
+    elif kind == "mlp_swiglu":
+        p = (_prod(False, False, M, 2 * I, H, EPI_SWIGLU, can_split=False) + _prod(False, False, M, H, I)
+             + _prod(False, True, M, I, H, EPI_DSWIGLU, can_split=False) + _prod(True, True, H, I, M)
+             + _prod(False, True, M, H, 2 * I) + _prod(True, True, 2 * I, H, M)
+             + [_pair_plan(M, H, I), _pair_plan(M, 2 * I, H)])
+    else:
+        raise ValueError(kind)
+    _PLANS[key] = p
+    return p
+
+
+_native_ready = None
+
+
+def _native(*biases) -> bool:
+    global _native_ready
+    if not NATIVE_AUTOGRAD:
+        return False
+    if _native_ready is None:
+        _require()  # a GPU path without its extension fails loudly
+        _native_ready = True
+    import torch
+
+    return all(b is None or b.dtype == torch.bfloat16 for b in biases)
+
+
 def _fast(x, *ws) -> bool:
     import torch
 
@@ -390,6 +455,11 @@ def _fast(x, *ws) -> bool:
 def gemm_linear(x, weight, bias=None):
     """``F.linear`` on the HIP MFMA GEMM (bf16, dims multiple of 64); PyTorch otherwise."""
     if _fast(x, weight):
+        if _native(bias):
+            import torch
+
+            plan = native_plan("linear", x.numel() // x.shape[-1], weight.shape[0], weight.shape[1], bias is not None)
+            return torch.ops.nbd.linear_ag(x, weight, bias, plan)
         return _fns()[0].apply(x, weight, bias)
     import torch.nn.functional as F
 
@@ -399,6 +469,11 @@ def gemm_linear(x, weight, bias=None):
 def mlp_gelu(x, w1, b1, w2, b2):
     """``F.linear(gelu_tanh(F.linear(x, w1, b1)), w2, b2)`` with the activation fused into the GEMMs."""
     if _fast(x, w1, w2):
+        if _native(b1, b2):
+            import torch
+
+            plan = native_plan("mlp_gelu", x.numel() // x.shape[-1], w1.shape[1], w1.shape[0], b1 is not None, b2 is not None)
+            return torch.ops.nbd.mlp_gelu_ag(x, w1, b1, w2, b2, plan)
         return _fns()[1].apply(x, w1, b1, w2, b2)
     import torch.nn.functional as F
 
@@ -409,6 +484,11 @@ def mlp_swiglu(x, w_gu, w_down):
     """Llama MLP ``down(silu(g)·u)`` with ``[g|u] = F.linear(x, w_gu)`` (``w_gu`` = [gate; up],
     [2I, H]) — SwiGLU and its backward fused into the GEMM epilogues on the GPU path."""
     if FUSED_SWIGLU and _fast(x, w_gu, w_down):
+        if _native():
+            import torch
+
+            plan = native_plan("mlp_swiglu", x.numel() // x.shape[-1], w_gu.shape[1], w_down.shape[1])
+            return torch.ops.nbd.mlp_swiglu_ag(x, w_gu, w_down, plan)
         return _fns()[2].apply(x, w_gu, w_down)
     if not FUSED_SWIGLU:
         return gemm_linear(_swiglu(gemm_linear(x, w_gu)), w_down)

@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 from ._lib import _require
+from .gemm import _native
 from .llama import _llama_fns
 
 
@@ -78,25 +79,31 @@ def _norm_ok(x, C: int) -> bool:
 
 def layer_norm(x, weight, bias, eps: float = 1e-5):
     """LayerNorm over the last dim (HIP kernels on GPU; ``F.layer_norm`` otherwise)."""
+    import torch
     import torch.nn.functional as F
 
     C = x.shape[-1]
     if _norm_ok(x, C) and weight is not None and bias is not None and weight.dtype == x.dtype:
         _require()
+        if _native():
+            return torch.ops.nbd.layer_norm_ag(x if x.is_contiguous() else x.contiguous(), weight, bias, float(eps))
         return _norm_fns()[0].apply(x if x.is_contiguous() else x.contiguous(), weight, bias, float(eps))
     return F.layer_norm(x, (C,), weight, bias, eps)
 
 def add_layer_norm(x, delta, weight, bias, eps: float = 1e-5):
     """``s = x + delta; return s, LayerNorm(s)`` — the residual add and the norm in one HIP pass
     (and their backward in one pass: dx includes the residual stream's gradient)."""
+    import torch
     import torch.nn.functional as F
 
     C = x.shape[-1]
     if (_norm_ok(x, C) and weight is not None and bias is not None and weight.dtype == x.dtype
             and delta.dtype == x.dtype and delta.shape == x.shape):
         _require()
-        return _norm_fns()[1].apply(x if x.is_contiguous() else x.contiguous(),
-                                    delta if delta.is_contiguous() else delta.contiguous(), weight, bias, float(eps))
+        x, delta = (x if x.is_contiguous() else x.contiguous()), (delta if delta.is_contiguous() else delta.contiguous())
+        if _native():
+            return torch.ops.nbd.add_layer_norm_ag(x, delta, weight, bias, float(eps))
+        return _norm_fns()[1].apply(x, delta, weight, bias, float(eps))
     s = x + delta
     return s, F.layer_norm(s, (C,), weight, bias, eps)
 
@@ -135,6 +142,8 @@ def rms_norm(x, weight, eps: float = 1e-6):
 
     if _rms_ok(x, weight):
         _require()
+        if _native():
+            return torch.ops.nbd.rms_norm_ag(x if x.is_contiguous() else x.contiguous(), weight, float(eps))
         return _llama_fns()[0].apply(x if x.is_contiguous() else x.contiguous(), weight, float(eps))
     xf = x.float()
     return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype) * weight
@@ -143,7 +152,11 @@ def add_rms_norm(x, delta, weight, eps: float = 1e-6):
     """``s = x + delta; return s, RMSNorm(s)`` in one HIP pass (and one for the backward)."""
     if _rms_ok(x, weight) and delta.dtype == x.dtype and delta.shape == x.shape:
         _require()
-        return _llama_fns()[1].apply(x if x.is_contiguous() else x.contiguous(),
-                                     delta if delta.is_contiguous() else delta.contiguous(), weight, float(eps))
+        x, delta = (x if x.is_contiguous() else x.contiguous()), (delta if delta.is_contiguous() else delta.contiguous())
+        if _native():
+            import torch
+
+            return torch.ops.nbd.add_rms_norm_ag(x, delta, weight, float(eps))
+        return _llama_fns()[1].apply(x, delta, weight, float(eps))
     s = x + delta
     return s, rms_norm(s, weight, eps)
