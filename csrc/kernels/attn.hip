@@ -352,7 +352,7 @@ __device__ __forceinline__ void tile_delta(const Stage2& dO, const Stage2& O, fl
     acc += __shfl_xor(acc, 1, 64);
     acc += __shfl_xor(acc, 2, 64);
     acc += __shfl_xor(acc, 4, 64);
-    if ((tid & 7) == 0) Ds[(tid + i * NT) >> 3] = acc;
+    if ((tid & 7) == 0) Ds[(tid + i * NT) >> 3] = -acc;  // stored negated: the dP accumulator's start
   }
 }
 
@@ -368,7 +368,7 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
   __shared__ __attribute__((aligned(16))) uint16_t Qs[TILE * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Os[TILE * RS];  // dO tile
   __shared__ __attribute__((aligned(16))) float Ls[TILE];           // lse * log2(e)
-  __shared__ __attribute__((aligned(16))) float Ds[TILE];           // delta
+  __shared__ __attribute__((aligned(16))) float Ds[TILE];           // -delta
   const int per = nblocks / nblk;
   const int bhs = blk % per;
   const int kb0 = blk / per;  // key block; block 0 has the most query tiles under a causal mask
@@ -409,7 +409,7 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
     so.store(Os, RS, tid);
     if (tid < TILE) {
       Ls[tid] = lv;
-      if constexpr (!FD) Ds[tid] = dlv;
+      if constexpr (!FD) Ds[tid] = -dlv;
     }
     if constexpr (FD) tile_delta(so, sov, Ds, tid);
     __syncthreads();
@@ -429,21 +429,30 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
         for (int qb = 0; qb < 2; ++qb) {
           const int qr0 = qt0 + qb * 32;
           if (CAUSAL && qr0 + 31 < key0) continue;  // this 32-query block sees none of our keys
-          // S[q][key] = Q . K^T (key on the lane)
-          f16x sacc = zero16(), dp = zero16();
+          // S[q][key] = Q . K^T (key on the lane); dP starts from -δ (row constant as the initial
+          // accumulator: dS = P·(dP − δ) is then one multiply)
+          f16x sacc = zero16(), dp;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) dp[i] = Ds[qb * 32 + crow(i, h)];
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
             sacc = mfma(ld16(Qs + (qb * 32 + r) * RS + 16 * s + 8 * h), kf[s], sacc);
             dp = mfma(ld16(Os + (qb * 32 + r) * RS + 16 * s + 8 * h), vf[s], dp);
           }
-          const bool diag = CAUSAL && (qr0 < key0 + 31);
+          // causal mask only on the diagonal 32x32 block, behind a wave-uniform branch: a
+          // per-element select in every block cost 3 VALU + 1 SALU per score
+          if (CAUSAL && __builtin_amdgcn_readfirstlane((int)(qr0 < key0 + 31))) {
+            const int thr = ki - qr0 - 4 * h;  // masked where (i&3) + 8(i>>2) < thr
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if ((i & 3) + 8 * (i >> 2) < thr) sacc[i] = -INFINITY;
+          }
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int qrow = qb * 32 + crow(i, h);
-            float p = __builtin_amdgcn_exp2f(fmaf(sacc[i], sc2, -Ls[qrow]));
-            if (diag && ki > qt0 + qrow) p = 0.f;
-            sacc[i] = p;                      // P
-            dp[i] = p * (dp[i] - Ds[qrow]);   // dS
+            const float p = __builtin_amdgcn_exp2f(fmaf(sacc[i], sc2, -Ls[qrow]));
+            sacc[i] = p;          // P
+            dp[i] = p * dp[i];    // dS
           }
           // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . dS[q][key]
 #pragma unroll
@@ -469,7 +478,7 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
         so.store(Os, RS, tid);
         if (tid < TILE) {
           Ls[tid] = lv;
-          if constexpr (!FD) Ds[tid] = dlv;
+          if constexpr (!FD) Ds[tid] = -dlv;
         }
         if constexpr (FD) tile_delta(so, sov, Ds, tid);
         __syncthreads();
@@ -541,9 +550,6 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
     }
     const int k0 = t * TILE;
     if (!CAUSAL || k0 <= q0 + 31) {
-      // (a diagonal-only masked copy of this body, as in the forward, pushes the combined
-      // backward kernel past 256 VGPRs into scratch; the per-element mask stays here)
-      const bool diag = CAUSAL && (k0 + TILE - 1 > q0);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         f16x sacc = zero16(), dp = zero16();
@@ -552,10 +558,18 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
           sacc = mfma(ld16(Ks + (kb * 32 + r) * RS + 16 * s + 8 * h), qf[s], sacc);
           dp = mfma(ld16(Vs + (kb * 32 + r) * RS + 16 * s + 8 * h), of[s], dp);
         }
+        // causal mask only where this 32-key block crosses the wave's queries (wave-uniform
+        // branch; keys past every query of the wave were skipped with the whole tile)
+        const int kr0 = k0 + kb * 32;
+        if (CAUSAL && __builtin_amdgcn_readfirstlane((int)(kr0 + 31 > q0))) {
+          const int thr = qi - kr0 - 4 * h;  // masked where (i&3) + 8(i>>2) > thr
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if ((i & 3) + 8 * (i >> 2) > thr) sacc[i] = -INFINITY;
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float p = __builtin_amdgcn_exp2f(fmaf(sacc[i], sc2, -l2));
-          if (diag && k0 + kb * 32 + crow(i, h) > qi) p = 0.f;
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[i], sc2, -l2));
           dp[i] = p * (dp[i] - dl);  // dS^T[key][q]
         }
         // dQ^T[d][q] += K^T[d][key] . dS^T[key][q]
