@@ -56,6 +56,7 @@ constexpr int RS = 72;      // LDS row stride (elements) of row-read images: 144
 constexpr int RSV = 96;     // LDS row stride of transpose-only images: 192 B (tr reads conflict-free)
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kDeferLog2 = 4.f;  // forward: skip the O rescale while the max grows by <= 2^4
 
 struct View {
   const uint16_t* p;
@@ -255,9 +256,21 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
           mt = fmaxf(mt, sacc[kb][i]);
         }
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      // deferred rescale (cdna_hip_programming.md T13): the O / l rescale by exp2(m − m') runs
+      // only when some query of the wave saw its running max grow by more than kDeferLog2;
+      // otherwise the stale max is kept and this tile's p are bounded by 2^kDeferLog2 (bf16's
+      // relative precision does not depend on the magnitude; O and l accumulate in fp32)
       const float mn = fmaxf(m, mt * sc2);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      const float nmn = -mn;
+      if (__any(mn > m + kDeferLog2)) {
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+        l *= alpha;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc_o[db][i] *= alpha;
+        m = mn;
+      }
+      const float nmn = -m;
       float rs0 = 0.f, rs1 = 0.f;  // two chains; scalar adds (no v_pk_add_f32: -fno-slp-vectorize)
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
@@ -272,12 +285,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
         }
       float rs = rs0 + rs1;
       rs += __shfl_xor(rs, 32, 64);
-      l = l * alpha + rs;
-      m = mn;
-#pragma unroll
-      for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc_o[db][i] *= alpha;
+      l += rs;
       // O^T[d][q] += V^T[d][key] . P[key][q]
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
