@@ -438,6 +438,10 @@ static void launch_epi(const Tile& t, const Args& a, dim3 grid, hipStream_t st) 
     NBD_GEMM_CASE(128, 64, 2)  // intra-workgroup K-split: small, latency-bound products
     NBD_GEMM_CASE(64, 128, 2)
     NBD_GEMM_CASE(64, 64, 2)
+    // 128x96 (row images only: the transposed-image swizzles assume 64- or 128-wide tiles):
+    // N = 768 / 2304 forwards fill whole rounds of 2 workgroups per CU (512 / 1536 tiles)
+    // where 128x128 leaves 0.75 / 2.25 rounds
+    if constexpr (!A_KM && !B_KN) NBD_GEMM_CASE(128, 96, 1)
   } while (0);
   if (t.bm == 128 && t.bn == 128 && t.waves == 8 && t.ks == 1) {  // 8 waves: 128x128 only
     if (t.stages == 3) NBD_GEMM_K(128, 128, 3, 8, 1);

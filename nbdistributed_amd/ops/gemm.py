@@ -82,13 +82,13 @@ _TUNED = {
     (False, False, 8192, 2304, 768): (82128128, 1),  # gpt2.c_attn fwd 44.5 us
     (False, True, 8192, 768, 2304): (82128128, 1),  # gpt2.c_attn dgrad 42.3 us
     (True, True, 2304, 768, 8192): (203128064, 1),  # gpt2.c_attn wgrad 49.7 us (K-split groups)
-    (False, False, 8192, 768, 768): (82128128, 1),  # gpt2.attn.c_proj fwd 21.0 us
+    (False, False, 8192, 768, 768): (2128096, 1),  # gpt2.attn.c_proj fwd 14.8 us (128x128/8 waves 16.5: 512 tiles = one round)
     (False, True, 8192, 768, 768): (2128064, 1),  # gpt2.attn.c_proj dgrad 21.8 us
     (True, True, 768, 768, 8192): (203064064, 1),  # gpt2.attn.c_proj wgrad 32.7 us (no reduce kernel)
     (False, False, 8192, 3072, 768): (82128128, 1),  # gpt2.c_fc fwd 49.7 us
     (False, True, 8192, 768, 3072): (2128128, 1),  # gpt2.c_fc dgrad 50.9 us
     (True, True, 3072, 768, 8192): (3064128, 4),  # gpt2.c_fc wgrad 72.6 us
-    (False, False, 8192, 768, 3072): (2128128, 1),  # gpt2.mlp.c_proj fwd 50.5 us
+    (False, False, 8192, 768, 3072): (2128096, 1),  # gpt2.mlp.c_proj fwd 48.2 us (128x128 50.0; profiles/gemm96_r2.txt)
     (False, True, 8192, 3072, 768): (82128128, 1),  # gpt2.mlp.c_proj dgrad 50.9 us
     (True, True, 768, 3072, 8192): (82128128, 2),  # gpt2.mlp.c_proj wgrad 68.9 us
     (False, False, 2048, 960, 576): (3064064, 1),  # smollm2.qkv fwd 13.5 us
@@ -105,7 +105,7 @@ _TUNED = {
     (True, True, 576, 1536, 2048): (203064064, 1),  # smollm2.down wgrad 13.7 us (15.6)
 }
 
-_TILES = (128128, 128064, 64128, 64064)
+_TILES = (128128, 128064, 64128, 64064)  # (+ 128096: forward only, tuned entries)
 
 
 def _ntiles(tile: int, M: int, N: int) -> int:

@@ -48,6 +48,26 @@ def test_gemm_layouts_and_tiles(layout, tile, shape):
     assert _err(c, _ref(a, b, a_km, b_kn)) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [2128096, 3128096])
+@pytest.mark.parametrize("shape", [(256, 576, 320), (384, 192, 192), (128, 384, 64), (512, 768, 1216)])  # N % 192 == 0
+@pytest.mark.parametrize("epi", [0, 1])
+def test_gemm_forward_128x96_tile(tile, shape, epi):
+    """The 128x96 forward tile (row images only), plain and with the bias + GELU epilogue."""
+    M, N, K = shape
+    a, b = _operands(M, N, K, False, False, seed=3)
+    bias = torch.randn(N, device="cuda").to(torch.bfloat16)
+    ref = _ref(a, b, False, False) + bias.float()
+    if epi == G.EPI_GELU:
+        act, pre = G.matmul(a, b, bias=bias, epi=epi, tile=tile, splits=1)
+        assert _err(pre, ref) < 1e-2
+        assert _err(act, torch.nn.functional.gelu(ref, approximate="tanh")) < 1e-2
+    else:
+        c = G.matmul(a, b, bias=bias, tile=tile, splits=1)
+        assert c.shape == (M, N) and _err(c, ref) < 1e-2
+    with pytest.raises(RuntimeError):  # transposed images: not built for 96-wide tiles
+        G.matmul(*_operands(M, N, K, False, True), b_kn=True, tile=tile, splits=1)
+
+
 @pytest.mark.parametrize("layout", LAYOUTS, ids=["fwd", "dgrad", "wgrad"])
 @pytest.mark.parametrize("tile,K", [(3064064, 1216), (3128128, 704), (203064064, 1280), (203128064, 1408),
                                     (83128128, 1216)])
