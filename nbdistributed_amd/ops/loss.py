@@ -48,21 +48,35 @@ def _xent_fn():
 
         @staticmethod
         def forward(ctx, h2, w, target, ignore_index, reduction):
-            logits = torch.mm(h2, w.t())
+            # vocabulary padded to a multiple of VOCAB_ALIGN for the three GEMMs (hipBLASLt: GPT-2's
+            # 50257 -> 50304 takes the LM head from 2.18 to 1.75 ms per step, profiles/lmhead_r2.txt):
+            # zero weight rows give exactly-zero pad logits, the loss reads only the first V columns
+            # (row stride Vp), so the pad columns stay 0 as gradients and dW's pad rows are dropped
+            V = w.shape[0]
+            Vp = -(-V // VOCAB_ALIGN) * VOCAB_ALIGN if V >= VOCAB_PAD_MIN else V
+            if Vp != V:
+                wp = torch.empty(Vp, w.shape[1], dtype=w.dtype, device=w.device)
+                wp[:V].copy_(w)
+                wp[V:].zero_()
+            else:
+                wp = w
+            logits_p = torch.mm(h2, wp.t())
             if reduction == "mean":
                 scale = (1.0 / (target != ignore_index).sum().float()).reshape(1)  # inf (-> nan loss) if none
             else:
                 scale = torch.ones(1, dtype=torch.float32, device=h2.device)
-            loss_rows, _ = torch.ops.nbd.xent_fused(logits, target, ignore_index, scale)
-            ctx.save_for_backward(h2, w, logits)  # logits now hold d(loss)/d(logits) for grad_out = 1
+            loss_rows, _ = torch.ops.nbd.xent_fused(logits_p[:, :V] if Vp != V else logits_p, target, ignore_index,
+                                                    scale)
+            ctx.save_for_backward(h2, wp, logits_p)  # logits now hold d(loss)/d(logits) for grad_out = 1
+            ctx.V = V
             return loss_rows.sum() * scale[0]
 
         @staticmethod
         def backward(ctx, grad):
-            h2, w, dlogits = ctx.saved_tensors
+            h2, wp, dlogits = ctx.saved_tensors
             g = grad.to(h2.dtype)
-            dh = torch.mm(dlogits, w).mul_(g) if ctx.needs_input_grad[0] else None
-            dw = torch.mm(dlogits.t(), h2 * g) if ctx.needs_input_grad[1] else None
+            dh = torch.mm(dlogits, wp).mul_(g) if ctx.needs_input_grad[0] else None
+            dw = torch.mm(dlogits.t(), h2 * g)[:ctx.V] if ctx.needs_input_grad[1] else None
             return dh, dw, None, None, None
 
     _XentFn = (_FusedCrossEntropy, _LinearCrossEntropy)
@@ -89,6 +103,10 @@ def cross_entropy(logits, target, ignore_index: int = -100, reduction: str = "me
 
 
 FUSED_MAX_VOCAB = 256 * 8 * 32  # xent_fused keeps a row in registers: 256 lanes x 32 chunks x 8
+# LM-head GEMMs run on a vocabulary padded to this multiple (only from VOCAB_PAD_MIN up: the
+# [V, C] weight copy costs one pass over it); the padded width must stay <= FUSED_MAX_VOCAB + 14
+VOCAB_ALIGN = max(1, int(__import__("os").environ.get("NBD_VOCAB_ALIGN", "128")))  # 1 = no padding (A/B)
+VOCAB_PAD_MIN = 4096
 
 
 def linear_cross_entropy(h, weight, target, ignore_index: int = -100, reduction: str = "mean"):
