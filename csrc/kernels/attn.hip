@@ -22,7 +22,9 @@
 //         dK^T += Q^T·dS — dK/dV stay in 64 accumulator registers; K, V in registers.
 //   dq    one workgroup = 128 queries, wave = 32 queries on the lane; sweeps 64-key tiles:
 //         S^T = K·Q^T, dP^T = V·dO^T, dS^T = P^T(dP^T − δ), dQ^T += K^T·dS^T.
-// Causal: workgroups are launched heaviest-first; fully masked tiles are skipped per wave.
+// Causal: workgroups are launched heaviest-first; fully masked tiles are skipped per wave, and
+// the mask is applied only to the 32x32 blocks the diagonal crosses (wave-uniform branches).
+// Forward: the O / l rescale is deferred while the running max grows by <= 2^kDeferLog2.
 // GQA: query head h reads key/value head h / group; dkdv runs per key/value head and sweeps its
 // group of query heads, accumulating dK/dV in the same registers (no atomics).
 // RoPE (optional, Llama family): q and k are rotated as they are loaded (Q/K fragments in
@@ -322,25 +324,27 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
 }
 
 // ============================================================================ backward: δ
+// δ[row] = Σ_d dO·O: 8 lanes per row, each a 16-B chunk of dO and of O (one 128-B line per row
+// and operand: coalesced), reduced over the 8 lanes; 32 rows per workgroup
 __global__ __launch_bounds__(NT) void bwd_pre_kernel(View dout, View out, float* __restrict__ delta, int H, int T,
                                                      int64_t rows) {
-  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (i >= rows) return;
-  const int t = (int)(i % T);
-  const int64_t bh = i / T;
-  const int b = (int)(bh / H), hh = (int)(bh % H);
-  const uint16_t* a = dout.row(b, hh, t);
-  const uint16_t* c = out.row(b, hh, t);
+  const int64_t i = (int64_t)blockIdx.x * (NT / 8) + (threadIdx.x >> 3);
+  const int c = threadIdx.x & 7;
   float acc = 0.f;
-#pragma unroll
-  for (int j = 0; j < D; j += 8) {
+  if (i < rows) {
+    const int t = (int)(i % T);
+    const int64_t bh = i / T;
+    const int b = (int)(bh / H), hh = (int)(bh % H);
     float x[8], y[8];
-    load8<bf16_t>(reinterpret_cast<const bf16_t*>(a + j), x);
-    load8<bf16_t>(reinterpret_cast<const bf16_t*>(c + j), y);
+    load8<bf16_t>(reinterpret_cast<const bf16_t*>(dout.row(b, hh, t) + 8 * c), x);
+    load8<bf16_t>(reinterpret_cast<const bf16_t*>(out.row(b, hh, t) + 8 * c), y);
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc = fmaf(x[e], y[e], acc);
   }
-  delta[i] = acc;
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (i < rows && c == 0) delta[i] = acc;
 }
 
 // ============================================================================ backward: dK, dV
@@ -733,7 +737,7 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
   if (!fd) {
     delta = at::empty({B, H, T}, lse.options());
     const int64_t rows = (int64_t)B * H * T;
-    hipLaunchKernelGGL(bwd_pre_kernel, dim3((unsigned)((rows + NT - 1) / NT)), dim3(NT), 0, st, dov, ov,
+    hipLaunchKernelGGL(bwd_pre_kernel, dim3((unsigned)((rows + NT / 8 - 1) / (NT / 8))), dim3(NT), 0, st, dov, ov,
                        delta.data_ptr<float>(), H, T, rows);
     C10_HIP_KERNEL_LAUNCH_CHECK();
   }
