@@ -546,6 +546,9 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
     dl = delta[(int64_t)bh * T + qi];
   }
   f16x dqt[2] = {zero16(), zero16()};
+  f16x ndl;  // −δ of this lane's query in every register: the dP^T accumulator's start (dS = P·dP)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) ndl[i] = -dl;
   const int ntiles = CAUSAL ? (qb * BLK + BLK) / TILE : T / TILE;
   StagePair sk;
   Stage2 sv;
@@ -564,7 +567,7 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
     if (!CAUSAL || k0 <= q0 + 31) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        f16x sacc = zero16(), dp = zero16();
+        f16x sacc = zero16(), dp = ndl;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           sacc = mfma(ld16(Ks + (kb * 32 + r) * RS + 16 * s + 8 * h), qf[s], sacc);
@@ -582,7 +585,7 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float p = __builtin_amdgcn_exp2f(fmaf(sacc[i], sc2, -l2));
-          dp[i] = p * (dp[i] - dl);  // dS^T[key][q]
+          dp[i] = p * dp[i];  // dS^T[key][q]
         }
         // dQ^T[d][q] += K^T[d][key] . dS^T[key][q]
 #pragma unroll
