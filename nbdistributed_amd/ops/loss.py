@@ -105,7 +105,7 @@ def cross_entropy(logits, target, ignore_index: int = -100, reduction: str = "me
 FUSED_MAX_VOCAB = 256 * 8 * 32  # xent_fused keeps a row in registers: 256 lanes x 32 chunks x 8
 # LM-head GEMMs run on a vocabulary padded to this multiple (only from VOCAB_PAD_MIN up: the
 # [V, C] weight copy costs one pass over it); the padded width must stay <= FUSED_MAX_VOCAB + 14
-VOCAB_ALIGN = max(1, int(__import__("os").environ.get("NBD_VOCAB_ALIGN", "128")))  # 1 = no padding (A/B)
+VOCAB_ALIGN = max(1, int(os.environ.get("NBD_VOCAB_ALIGN", "128")))  # 1 = no padding (A/B)
 VOCAB_PAD_MIN = 4096
 
 
