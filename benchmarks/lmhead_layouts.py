@@ -18,7 +18,9 @@ def t_ms(fn, n=20):
     return s.elapsed_time(e) / n
 
 
-for V in (50257, 50304):
+import sys
+
+for V in ([int(v) for v in sys.argv[1:]] or [50257, 50304]):
     N, C = 8192, 768
     dl = torch.randn(N, V, device="cuda", dtype=torch.bfloat16)
     h = torch.randn(N, C, device="cuda", dtype=torch.bfloat16)
