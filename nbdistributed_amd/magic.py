@@ -98,14 +98,16 @@ def rank_nospace_transform(lines: List[str]) -> List[str]:
 class MagicCore:
     """All magic behaviour, independent of IPython."""
 
-    def __init__(self, shell: Any = None, writer: Optional[Callable[[str], None]] = None):
+    def __init__(self, shell: Any = None, writer: Optional[Callable[[str], None]] = None,
+                 session: Optional[Session] = None):
+        """``session``: drive an existing (e.g. attached) session instead of creating one."""
         self.shell = shell
         self.write = writer or _default_writer
-        self.session = Session(writer=self.write)
+        self.session = session if session is not None else Session(writer=self.write)
         self.proxies = ProxyTable()
         self.auto_mode = False
         self.ide_sync = self.session.cfg.ide_sync
-        if self.session.cfg.zygote:
+        if session is None and self.session.cfg.zygote:
             # pre-warm the worker fork server while the user reads the notebook: %dist_init then
             # forks workers that already have torch imported
             try:

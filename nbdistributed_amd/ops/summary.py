@@ -63,7 +63,4 @@ def tensor_summary_text(x) -> str:
     return f"[{shape} {str(x.dtype).replace('torch.', '')} {x.device}] " + " ".join(parts)
 
 
-__all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "cross_entropy",
-           "flash_attention", "attention_qkv", "flash_supported", "layer_norm", "add_layer_norm", "linear",
-           "colsum", "embedding", "rms_norm", "add_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary", "tensor_summary_text",
-           "tensor_summary_raw", "plan_offsets", "native_available", "load_library", "SUMMARY_FIELDS"]
+__all__ = ["tensor_summary", "tensor_summary_text", "tensor_summary_raw", "SUMMARY_FIELDS"]

@@ -124,7 +124,13 @@ class ProcessManager:
             vis = worker_visible_devices(gpus)
             env_base["HIP_VISIBLE_DEVICES"] = vis
             env_base["CUDA_VISIBLE_DEVICES"] = vis
-        env_base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL P2P
+        # No RCCL/HSA knob is forced on the workers (the reference sets none either,
+        # worker.py:128-151): they inherit the kernel's environment.  Opt-in only —
+        # NBD_DMABUF_IPC=1 exports HSA_ENABLE_IPC_MODE_LEGACY=0 for hosts whose driver supports
+        # only dmabuf IPC (RCCL P2P / CUDA-tensor sharing then fails with "hipIpcGetMemHandle:
+        # invalid argument" without it).  Its effect on RCCL bandwidth is unmeasured here.
+        if os.environ.get("NBD_DMABUF_IPC") == "1":
+            env_base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         env_base["PYTHONUNBUFFERED"] = "1"
         repo_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         env_base["PYTHONPATH"] = repo_root + (os.pathsep + env_base["PYTHONPATH"] if env_base.get("PYTHONPATH") else "")

@@ -41,10 +41,11 @@ class HeadlessShell:
         name = magic_name or fn.__name__
         (self.line_magics if magic_kind == "line" else self.cell_magics)[name] = fn
 
-    def load_extension(self) -> Any:
+    def load_extension(self, session: Any = None, writer: Any = None) -> Any:
+        """``session``: drive an existing Session (bench.py's attached coordinator)."""
         from ..magic import MagicCore, _safe, CELL_MAGICS, LINE_MAGICS, rank_nospace_transform
 
-        core = MagicCore(self)
+        core = MagicCore(self, writer=writer, session=session)
         for n in LINE_MAGICS:
             self.register_magic_function(_safe(core, getattr(core, n)), "line", n)
         for n in CELL_MAGICS:

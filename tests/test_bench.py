@@ -104,3 +104,33 @@ def test_bench_py_contract_cpu(n):
     assert res.returncode == 0 and len(lines) == 1, res.stdout[-2000:] + res.stderr[-3000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == n and d["steps"] == 20 and d["value"] > 0 and d["config"]["parallelism"] == f"dp{n}"
+    # the magic path (auto transformer + %%distributed + ide_sync delta + renderer) is timed too
+    assert d["cell_magic_p50_ms"] > 0 and "ide_sync=True" in d["cell_magic_note"]
+    # every worker reports the process group it sees
+    assert d["rccl_world_size"] == {str(r): n for r in range(n)}
+
+
+def test_world1_reports_no_bandwidth():
+    """At world size 1 an all_reduce / broadcast is a no-op: no GB/s may be printed for it."""
+    s = Session(writer=lambda t: None)
+    s.start(1, backend="gloo")
+    try:
+        ar = B.bench_allreduce(s, nbytes=1 << 16, iters=3, warm=1)
+        assert ar["correct"] and ar["algbw_GBps"] is None and ar["busbw_GBps"] is None
+        sw = B.bench_sweep(s, max_bytes=1 << 12, min_bytes=1 << 10)
+        assert all(r["algbw_GBps"] is None and r["busbw_GBps"] is None for r in sw)
+        rb = B.bench_rank_broadcast(s, dim=64, iters=2, warm=1)
+        assert rb["per_param_GBps"] is None and rb["coalesced_GBps"] is None
+        cells = {"p50_ms": 1.0, "p90_ms": 1.0, "min_ms": 1.0, "mean_ms": 1.0}
+        line = B.result_line({"cell": cells, "allreduce": ar, "sweep": sw}, 1, 1, 1)
+        assert line["allreduce_algbw_GBps"] is None and line["allreduce_busbw_GBps"] is None
+        assert "allreduce_peak_busbw_GBps" not in line and "no-op" in line["allreduce_note"]
+        w = B.bench_world(s)
+        assert w["world_sizes"] == [1]
+    finally:
+        s.shutdown()
+
+
+def test_magic_path_cells(sess):
+    r = B.bench_cells_magic(sess, steps=5, warmup=2)
+    assert r["p50_ms"] > 0 and r["ide_sync"] is True and r["rendered_bytes"] > 0
