@@ -22,6 +22,8 @@
 // lane group g = l/16 walks its own contiguous quarter of K: each lane streams 16-B pieces of one
 // weight row in address order.  Workgroups loop over column tiles (grid capped when the
 // prologue is recomputed per workgroup, e.g. the LM head's 3,142 tiles).
+#include <mutex>
+#include <set>
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -340,11 +342,15 @@ at::Tensor linear_small_hip(const at::Tensor& x, const at::Tensor& w, const c10:
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   auto launch = [&](auto kern) {
-    static bool attr_set = false;  // one per kernel instantiation (generic lambda)
-    if (!attr_set) {
-      C10_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
-      attr_set = true;
+    // every instantiation has the same pointer type, so the "set once" state is keyed by
+    // (device, kernel pointer) — a per-lambda static would cover only the first kernel launched
+    static std::mutex mu;
+    static std::set<std::pair<int, const void*>> done;
+    const void* fp = reinterpret_cast<const void*>(kern);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (done.insert({(int)x.get_device(), fp}).second)
+        C10_HIP_CHECK(hipFuncSetAttribute(fp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)grid, (unsigned)mgroups), dim3(NT), lds, st, a);
   };

@@ -58,6 +58,26 @@ LEAD_GRACE_S = 0.02  # the receive thread stays parked this long after a waiter 
 _SIGINT = int(signal.SIGINT)
 _MAIN = threading.main_thread()
 
+# Reference-order bring-up (``ProcessManager().start_workers(n, addr, gpu_ids)`` -> port, then
+# ``CommunicationManager(n, port, ...)``, reference magic.py:493-504): the launcher picks the port
+# and the session token and records them here; the CommunicationManager that later binds that port
+# picks up the token.  Workers' DEALERs retry their connect until the ROUTER is bound, and requests
+# wait for the READY handshake, so the first message after init cannot be lost (reference D-2).
+_SPAWNED: Dict[int, Dict[str, Any]] = {}
+_SPAWNED_LOCK = threading.Lock()
+
+
+def register_spawned(port: int, token: Optional[str], num_processes: int) -> None:
+    with _SPAWNED_LOCK:
+        _SPAWNED[port] = {"token": token, "n": num_processes}
+
+
+def _claim_spawned(port: Optional[int]) -> Optional[Dict[str, Any]]:
+    if port is None:
+        return None
+    with _SPAWNED_LOCK:
+        return _SPAWNED.pop(port, None)
+
 
 class RankDied(RuntimeError):
     def __init__(self, rank: int, reason: str):
@@ -158,6 +178,11 @@ class CommunicationManager:
         self.num_processes = num_processes
         self.output_callback = output_callback
         self.default_timeout = default_timeout
+        spawned = _claim_spawned(base_port) if endpoint is None and token is None else None
+        # workers spawned before this bind: requests wait for their READY (reference order)
+        self._await_ready: Optional[float] = cfg.startup_timeout_s if spawned is not None else None
+        if spawned is not None:
+            token, use_token = spawned["token"], spawned["token"] is not None
         if use_token is None:
             use_token = cfg.use_token
         self.token = token if token is not None else (secrets.token_hex(16) if use_token else None)
@@ -232,6 +257,11 @@ class CommunicationManager:
 
     # ------------------------------------------------------------------ async API
     def submit(self, ranks: List[int], msg_type: str, data: Any = None, flags: int = 0, live: bool = True) -> PendingRequest:
+        if self._await_ready is not None:
+            # first request after a reference-order bring-up: the workers were spawned before this
+            # socket was bound; wait for their READY instead of routing into the void
+            self.wait_ready(list(range(self.num_processes)), self._await_ready)
+            self._await_ready = None
         mtype = P.TYPE_CODES[msg_type]
         seq = next(self._seq)
         req = PendingRequest(seq, msg_type, ranks, live)

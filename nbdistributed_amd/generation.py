@@ -125,6 +125,9 @@ class _DecodeLoop:
         self.out.scatter_(1, self.pos.view(-1, 1), nxt.view(-1, 1))
 
     def capture(self, warmup: int = 2):
+        """Warm up ``warmup`` real steps on a side stream, restore the state, capture one step.
+        The caller bounds ``warmup`` by the number of decode steps it will run, so the warm-up's
+        position advances stay inside ``out`` and the cache (every step scatters at pos + 1)."""
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         saved = [t.clone() for t in (self.tok, self.pos, self.out, self.done)]
@@ -176,6 +179,12 @@ def generate(model, input_ids: torch.Tensor, max_new_tokens: int, *, lengths: Op
     limit = model.max_positions()
     if t_max < need or (limit is not None and need > limit):
         raise ValueError(f"generate: needs {need} positions (t_max {t_max}, model limit {limit})")
+    window = getattr(getattr(model, "config", None), "sliding_window", None)
+    if window is not None and max_len + max_new_tokens > window:
+        # the decode kernel attends over every cached position: past the window its logits would
+        # silently differ from a sliding-window model's (the training forward refuses T > window too)
+        raise NotImplementedError(f"generate: {max_len + max_new_tokens} positions exceed the model's "
+                                  f"sliding window ({window}); sliding-window decoding is not implemented")
     cache = KVCache.for_model(model, B, t_max, device=device)
     ids = input_ids
     if t_pad > T0:
@@ -195,13 +204,16 @@ def generate(model, input_ids: torch.Tensor, max_new_tokens: int, *, lengths: Op
     loop = _DecodeLoop(model, cache, tok, pos, out, done, eos_token_id, sampling)
     n = max_new_tokens - 1
     if graph and n > 0:
-        loop.capture()
-    for i in range(n):
-        if not graph:
-            cache.kv_len_max = max_len + i + 1  # known on the host: fewer idle workgroups
-        loop()
-        if eos_token_id is not None and (i + 1) % sync_every == 0 and bool(done.all()):
-            break
+        loop.capture(warmup=min(2, n))
+    try:
+        for i in range(n):
+            if not graph:
+                cache.kv_len_max = max_len + i + 1  # known on the host: fewer idle workgroups
+            loop()
+            if eos_token_id is not None and (i + 1) % sync_every == 0 and bool(done.all()):
+                break
+    finally:
+        cache.kv_len_max = None  # the bound only held inside this call (a returned cache is reused later)
     return (out, cache) if return_cache else out
 
 

@@ -415,9 +415,30 @@ class MagicCore:
         self.p(f"✓ Synchronized {n} names from rank 0 into the local namespace")
 
     def timeline_save(self, line: str = "") -> None:
-        path = line.strip() or f"nbd_timeline_{int(time.time())}.json"
-        out = self.session.timeline.save(path)
+        """%timeline_save [PATH] [--notebook] [--ipynb NB.ipynb] — JSON + Chrome trace files; with
+        ``--notebook`` also ONE write of ``execution_timelines`` into the notebook metadata (the
+        reference's display(Javascript) hook, magic.py:163-240, done once instead of every cell);
+        ``--ipynb`` writes the metadata into that .ipynb file directly (any frontend)."""
+        p = _parser("%timeline_save")
+        p.add_argument("path", nargs="?", default=None)
+        p.add_argument("--notebook", action="store_true", help="write execution_timelines into the notebook metadata")
+        p.add_argument("--ipynb", default=None, help="write execution_timelines into this .ipynb file")
+        args = p.parse_args(shlex.split(line))
+        tl = self.session.timeline
+        path = args.path or f"nbd_timeline_{int(time.time())}.json"
+        out = tl.save(path)
         self.p(f"✓ Timeline saved: {out['json']}  (Chrome trace: {out['trace']})")
+        if args.notebook:
+            try:
+                from IPython.display import Javascript, display
+            except ImportError:
+                self.p("⚠️  --notebook needs IPython's display (use --ipynb PATH in a headless shell)")
+            else:
+                display(Javascript(tl.notebook_metadata_js()))
+                self.p(f"✓ {len(tl.records)} timeline record(s) written to the notebook metadata (execution_timelines)")
+        if args.ipynb:
+            n = tl.write_ipynb_metadata(args.ipynb)
+            self.p(f"✓ {n} timeline record(s) written to {args.ipynb} metadata (execution_timelines)")
 
     def timeline_debug(self, line: str = "") -> None:
         if self.session.active:

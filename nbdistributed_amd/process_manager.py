@@ -77,6 +77,7 @@ class ProcessManager:
         self.master_addr = "127.0.0.1"
         self.master_port: Optional[int] = None
         self.comm_endpoint: Optional[str] = None
+        self.comm_port: Optional[int] = None  # reference attribute (reference-order bring-up)
         self.gpu_assignments: Dict[int, Optional[int]] = {}
         self.output_callback = output_callback
         self.exit_callback = exit_callback
@@ -103,14 +104,29 @@ class ProcessManager:
     def start_workers(self, num_processes: int, master_addr: str = "localhost", gpu_ids: Optional[List[int]] = None,
                       comm_endpoint: Optional[str] = None, token: Optional[str] = None, backend: str = "auto",
                       python: Optional[str] = None, extra_env: Optional[Dict[str, str]] = None,
-                      worker_args: Optional[List[str]] = None) -> str:
-        """Spawn ``num_processes`` workers that connect to ``comm_endpoint``.  Returns the endpoint
-        (the reference returned the ZMQ port)."""
-        if comm_endpoint is None:
-            raise ValueError("comm_endpoint is required: bind the coordinator socket before spawning")
+                      worker_args: Optional[List[str]] = None):
+        """Spawn ``num_processes`` workers that connect to ``comm_endpoint`` and return it.
+
+        Reference order (``comm_endpoint`` omitted, reference process_manager.py:57-152 /
+        magic.py:493-504): pick a free loopback port and a session token, spawn the workers
+        against ``tcp://<bind host>:<port>`` and return the **port** (an int, as the reference
+        does); ``CommunicationManager(num_processes, port, ...)`` binds it afterwards and picks up
+        the token.  The workers' connects retry until it is bound and the first request waits
+        for every READY."""
         from .config import get_config
 
         cfg = get_config()
+        ref_port = None
+        if comm_endpoint is None:
+            import secrets
+
+            from .communication import register_spawned
+
+            ref_port = find_free_port(cfg.bind_host)
+            if token is None and cfg.use_token:
+                token = secrets.token_hex(16)
+            comm_endpoint = f"tcp://{cfg.bind_host}:{ref_port}"
+            register_spawned(ref_port, token, num_processes)
         self.num_processes = num_processes
         self.master_addr = "127.0.0.1" if master_addr in ("localhost", None, "") else master_addr
         self.master_port = find_free_port(self.master_addr)
@@ -178,6 +194,9 @@ class ProcessManager:
             t = threading.Thread(target=self._wait, args=(w,), daemon=True, name=f"nbd-wait-{rank}")
             t.start()
             self._threads.append(t)
+        if ref_port is not None:
+            self.comm_port = ref_port
+            return ref_port
         return comm_endpoint
 
     def _drain(self, rank: int, stream: str, pipe) -> None:

@@ -135,6 +135,39 @@ class Timeline:
             json.dump(self.to_chrome_trace(), f, default=str)
         return {"json": jp, "trace": tp}
 
+    # ------------------------------------------------------------------ notebook metadata
+    def metadata(self) -> Dict[str, Any]:
+        """``execution_timelines`` as the reference stores it in the notebook metadata
+        (reference magic.py:163-283): a dict keyed by cell id."""
+        return {r["cell_id"]: r for r in json.loads(json.dumps(self.to_list(), default=str))}
+
+    def notebook_metadata_js(self) -> str:
+        """One ``display(Javascript(...))`` payload writing ``execution_timelines`` into the
+        classic Notebook's metadata (the reference's mechanism, magic.py:163-240) — emitted once,
+        on demand from ``%timeline_save --notebook``, never per cell (reference D-5)."""
+        payload = json.dumps(self.metadata())
+        return ("(function(){var t=" + payload + ";"
+                "if(typeof Jupyter!=='undefined'&&Jupyter.notebook){"
+                "Jupyter.notebook.metadata.execution_timelines=t;Jupyter.notebook.set_dirty(true);}"
+                "})();")
+
+    def write_ipynb_metadata(self, ipynb_path: str) -> int:
+        """Write ``execution_timelines`` into the metadata of an ``.ipynb`` file on disk (works
+        for every frontend: JupyterLab and VS Code ignore the classic-Notebook JS hook).  Returns
+        the number of records written."""
+        with open(ipynb_path) as f:
+            nb = json.load(f)
+        meta = self.metadata()
+        nb.setdefault("metadata", {})["execution_timelines"] = meta
+        tmp = ipynb_path + ".nbd-tmp"
+        with open(tmp, "w") as f:
+            json.dump(nb, f, indent=1, ensure_ascii=False)
+            f.write("\n")
+        import os
+
+        os.replace(tmp, ipynb_path)
+        return len(meta)
+
     def summary(self, last: int = 20) -> str:
         with self._lock:
             recs = list(self.records)[-last:]

@@ -110,3 +110,19 @@ def test_sampled_generation_reproducible_with_generator():
     a = m.generate(ids, 7, temperature=0.9, top_k=40, generator=torch.Generator().manual_seed(7))
     b = m.generate(ids, 7, temperature=0.9, top_k=40, generator=torch.Generator().manual_seed(7))
     assert torch.equal(a, b) and torch.equal(a[:, :5], ids)
+
+
+def test_generate_refuses_past_the_sliding_window():
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(LlamaConfig.tiny(sliding_window=16)).eval()
+    ids = torch.randint(1, 512, (1, 10))
+    m.generate(ids, 6)  # 16 positions: inside the window
+    with pytest.raises(NotImplementedError):
+        m.generate(ids, 7)
+
+
+def test_returned_cache_has_no_stale_key_bound():
+    m = _models()[0]
+    ids = torch.randint(1, 512, (2, 6), generator=torch.Generator().manual_seed(8))
+    out, cache = m.generate(ids, 4, graph=False, return_cache=True)
+    assert cache.kv_len_max is None

@@ -191,3 +191,23 @@ def test_greedy_advance_matches_torch(V, offset, with_eos):
     assert int(tok[1]) == 7
     if with_eos:
         assert torch.equal(done, want_done)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("family", ["gpt2", "llama"])
+def test_gpu_graphed_sampling_two_new_tokens(family):
+    """Graph capture warms up on the real buffers: with max_new_tokens=2 (one decode step) the
+    warm-up must not advance past ``out`` (sampling path: temperature > 0)."""
+    from nbdistributed_amd.models import GPT2, GPT2Config
+    from nbdistributed_amd.models.llama import LlamaConfig, LlamaForCausalLM
+
+    torch.manual_seed(0)
+    m = (GPT2(GPT2Config(vocab_size=512, n_positions=64, n_embd=128, n_layer=2, n_head=2)) if family == "gpt2"
+         else LlamaForCausalLM(LlamaConfig.tiny()))
+    m = m.to("cuda", torch.bfloat16).eval()
+    ids = torch.randint(1, 512, (3, 20), device="cuda")
+    for n in (2, 3):
+        out = m.generate(ids, n, temperature=0.8, top_k=20, graph=True)
+        torch.cuda.synchronize()
+        assert out.shape == (3, 20 + n) and torch.equal(out[:, :20], ids)
+        assert bool(((out[:, 20:] >= 0) & (out[:, 20:] < 512)).all())

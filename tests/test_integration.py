@@ -161,6 +161,21 @@ def test_sync_status_debug_mode_timeline(nb, tmp_path):
     p = tmp_path / "tl.json"
     sh.run_cell(f"%timeline_save {p}")
     assert p.exists() and (tmp_path / "tl.trace.json").exists()
+    # opt-in notebook-metadata write (reference magic.py:163-283), once on demand
+    import json
+
+    nbp = tmp_path / "nb.ipynb"
+    nbp.write_text(json.dumps({"cells": [], "metadata": {"kernelspec": {"name": "python3"}}, "nbformat": 4,
+                               "nbformat_minor": 5}))
+    cap.take()
+    sh.run_cell(f"%timeline_save {tmp_path / 'tl2.json'} --ipynb {nbp}")
+    assert "execution_timelines" in cap.take()
+    meta = json.loads(nbp.read_text())["metadata"]
+    assert meta["kernelspec"] == {"name": "python3"} and meta["execution_timelines"]
+    rec = next(iter(meta["execution_timelines"].values()))
+    assert {"cell_id", "kind", "duration_s", "per_rank"} <= set(rec)
+    js = core.session.timeline.notebook_metadata_js()
+    assert "Jupyter.notebook.metadata.execution_timelines" in js and rec["cell_id"] in js
     sh.run_cell("%timeline_clear")
     assert "Cleared" in cap.take()
 
@@ -430,3 +445,30 @@ def test_dist_recover_rebuilds_process_group(nb):
     assert "Process group rebuilt on 2 ranks" in cap.take()
     r = sh.run_cell("x = torch.ones(3)\ndist.all_reduce(x)\nint(x.sum())")
     assert r.success and cap.take().count("  6\n") == 2
+
+
+def test_reference_order_programmatic_bringup():
+    """The reference's exact sequence (magic.py:493-504): spawn first, get a port back, bind the
+    CommunicationManager on it afterwards, then send — the first request must not be lost."""
+    from nbdistributed_amd.communication import CommunicationManager
+    from nbdistributed_amd.process_manager import ProcessManager
+
+    streamed = []
+    pm = ProcessManager()
+    port = pm.start_workers(2, "localhost", None, backend="gloo")
+    assert isinstance(port, int) and pm.comm_port == port
+    comm = CommunicationManager(2, port, output_callback=lambda r, t, s: streamed.append((r, t)),
+                                default_timeout=120)
+    try:
+        res = comm.send_to_all("execute", "x = rank * 10\nprint('hello from', rank)\nx")
+        assert res[0]["echo"] == "0" and res[1]["echo"] == "10"
+        assert any("hello from 1" in t for r, t in streamed if r == 1)
+        assert comm.send_to_rank(1, "get_var", "x") == 10
+        assert comm.send_to_ranks([0], "execute", "dist.get_world_size()")[0]["echo"] == "2"
+        st = pm.get_detailed_status(comm)
+        assert all(st[r]["running"] and st[r]["world_size"] == 2 for r in (0, 1))
+    finally:
+        comm.send_to_all("shutdown", timeout=5)
+        comm.shutdown()
+        pm.shutdown()
+    assert not pm.is_running()
