@@ -202,7 +202,7 @@ def test_gpu_graphed_sampling_two_new_tokens(family):
     from nbdistributed_amd.models.llama import LlamaConfig, LlamaForCausalLM
 
     torch.manual_seed(0)
-    m = (GPT2(GPT2Config(vocab_size=512, n_positions=64, n_embd=128, n_layer=2, n_head=2)) if family == "gpt2"
+    m = (GPT2(GPT2Config(vocab_size=512, n_positions=256, n_embd=128, n_layer=2, n_head=2)) if family == "gpt2"
          else LlamaForCausalLM(LlamaConfig.tiny()))
     m = m.to("cuda", torch.bfloat16).eval()
     ids = torch.randint(1, 512, (3, 20), device="cuda")
