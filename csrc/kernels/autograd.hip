@@ -24,15 +24,17 @@
 #include <torch/library.h>
 
 #include "gemm_common.h"
+#include "graddst.h"
 
 namespace nbd {
 namespace gemm {
 void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_km, bool b_kn,
               const c10::optional<at::Tensor>& bias, int64_t epi, const c10::optional<at::Tensor>& aux_in,
-              const c10::optional<at::Tensor>& aux_out, int64_t splits, int64_t tile_hint);
+              const c10::optional<at::Tensor>& aux_out, int64_t splits, int64_t tile_hint, int64_t accum);
 void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor& c1, int64_t epi1,
                    const c10::optional<at::Tensor>& aux_in1, const at::Tensor& a2, const at::Tensor& b2,
-                   const at::Tensor& c2, int64_t epi2, const c10::optional<at::Tensor>& aux_out2, int64_t splits2);
+                   const at::Tensor& c2, int64_t epi2, const c10::optional<at::Tensor>& aux_out2, int64_t splits2,
+                   int64_t accum2);
 }  // namespace gemm
 namespace norm {
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ln_fwd_hip(const at::Tensor& x,
@@ -87,37 +89,94 @@ static Tensor bf16c(const Tensor& t) {
 
 // c = A·B (layouts as gemm.hip), `epi` with its operands; returns (c, aux_out).  The library path
 // (hipBLASLt through at::mm / addmm) serves plain products the plan routes there, and any plain
-// product whose operands are not 16-byte aligned (as ops.gemm.matmul does).
+// product whose operands are not 16-byte aligned (as ops.gemm.matmul does).  `c_out` / `rs_out`:
+// write the product / row sums there (gradient destinations, graddst.h), adding to their contents
+// when `accum` bit 0 / bit 1 is set.
 static std::pair<Tensor, Tensor> run(const Tensor& a, const Tensor& b, bool a_km, bool b_kn, const Prod& p,
                                      int epi = EPI_NONE, const optional<Tensor>& bias = c10::nullopt,
-                                     const optional<Tensor>& aux = c10::nullopt) {
+                                     const optional<Tensor>& aux = c10::nullopt, const Tensor& c_out = Tensor(),
+                                     const Tensor& rs_out = Tensor(), int accum = 0) {
   const int64_t M = a_km ? a.size(1) : a.size(0), N = b_kn ? b.size(1) : b.size(0);
   const bool bias_ok = !bias || (bias->is_contiguous() && aligned(*bias, 8) && bias->scalar_type() == at::kBFloat16);
-  if (epi == EPI_NONE && (p.lib || !aligned(a) || !aligned(b) || !bias_ok)) {
+  const bool out_ok = !c_out.defined() || aligned(c_out);
+  if (epi == EPI_NONE && (p.lib || !aligned(a) || !aligned(b) || !bias_ok || !out_ok)) {
     const Tensor A = a_km ? a.t() : a, B = b_kn ? b : b.t();
+    if (c_out.defined()) {
+      TORCH_CHECK(!bias, "nbd autograd: bias with a destination");
+      if (accum & 1) c_out.view({M, N}).addmm_(A, B);
+      else {
+        Tensor o = c_out.view({M, N});
+        at::mm_out(o, A, B);
+      }
+      return {c_out, Tensor()};
+    }
     return {bias ? at::addmm(*bias, A, B) : at::mm(A, B), Tensor()};
   }
   const int64_t cN = epi == EPI_SWIGLU ? N / 2 : epi == EPI_DSWIGLU ? 2 * N : N;
-  Tensor c = at::empty({M, cN}, a.options());
+  // the 256x256 kernel has no accumulating epilogue: product into a temporary, then add
+  const bool tmp_acc = accum != 0 && (p.tile / 1000 % 1000) == 256;
+  Tensor c = c_out.defined() && !(tmp_acc && (accum & 1)) ? c_out.view({M, cN}) : at::empty({M, cN}, a.options());
   Tensor out;
   if (epi == EPI_GELU) out = at::empty_like(c);
-  if (epi == EPI_ROWSUM) out = at::empty({M}, a.options());
+  if (epi == EPI_ROWSUM) out = rs_out.defined() && !(tmp_acc && (accum & 2)) ? rs_out.view({M}) : at::empty({M}, a.options());
   if (epi == EPI_SWIGLU) out = at::empty({M, N}, a.options());
   gemm_hip(a, b, c, a_km, b_kn, bias, epi, aux, out.defined() ? optional<Tensor>(out) : c10::nullopt, p.splits,
-           p.tile);
+           p.tile, tmp_acc ? 0 : accum);
+  if (tmp_acc) {
+    if (accum & 1) { c_out.view({M, cN}).add_(c); c = c_out.view({M, cN}); }
+    if (accum & 2) { rs_out.view({M}).add_(out); out = rs_out.view({M}); }
+  }
   return {c, out};
+}
+
+// A gradient output: the parameter's registered destination (graddst.h) or a fresh tensor.
+struct GradOut {
+  Tensor t;
+  Tensor param;
+  bool claimed = false, acc = false;
+  int bit(int b) const { return acc ? b : 0; }
+  Tensor done() const { return claimed ? graddst::hand_back(param, t, acc) : t; }
+};
+
+static GradOut grad_out(const Tensor& param, bool want, at::IntArrayRef shape, const at::TensorOptions& opt) {
+  GradOut g;
+  if (!want) return g;
+  if (param.defined()) {
+    g.t = graddst::claim(param, g.acc);
+    g.claimed = g.t.defined();
+    if (g.claimed) {
+      g.param = param;
+      if (!aligned(g.t) || g.t.scalar_type() != opt.dtype().toScalarType()) {  // unusable: normal path
+        g = GradOut();
+      }
+    }
+  }
+  if (!g.claimed) g.t = at::empty(shape, opt);
+  return g;
 }
 
 // dx = dy·W [· act′(aux)], dW = dyᵀ·x [, db = Σ dy] in one grouped launch (gemm_pair_hip)
 static std::tuple<Tensor, Tensor, Tensor> pair(const Tensor& dy, const Tensor& w, const Tensor& x, int epi1,
-                                               const optional<Tensor>& aux1, bool bias_grad, int64_t splits) {
+                                               const optional<Tensor>& aux1, bool bias_grad, int64_t splits,
+                                               const Tensor& bparam = Tensor()) {
   const int64_t M = dy.size(0), N = dy.size(1), K = w.size(1);
   Tensor dx = at::empty({M, epi1 == EPI_DSWIGLU ? 2 * K : K}, dy.options());
-  Tensor dw = at::empty({N, K}, dy.options());
-  Tensor db = bias_grad ? at::empty({N}, dy.options()) : Tensor();
-  gemm_pair_hip(dy, w, dx, epi1, aux1, dy, x, dw, bias_grad ? EPI_ROWSUM : EPI_NONE,
-                bias_grad ? optional<Tensor>(db) : c10::nullopt, splits);
-  return {dx, dw, db};
+  const GradOut dw = grad_out(w, true, {N, K}, dy.options());
+  const GradOut db = grad_out(bparam, bias_grad, {N}, dy.options());
+  gemm_pair_hip(dy, w, dx, epi1, aux1, dy, x, dw.t.view({N, K}), bias_grad ? EPI_ROWSUM : EPI_NONE,
+                bias_grad ? optional<Tensor>(db.t.view({N})) : c10::nullopt, splits, dw.bit(1) | db.bit(2));
+  return {dx, dw.done(), bias_grad ? db.done() : Tensor()};
+}
+
+// dW = dyᵀ·x [, db = Σ dy] as separate products (plan entry `pi`), into the gradient destinations
+static std::pair<Tensor, Tensor> wgrad(const Tensor& dy, const Tensor& x2, const Tensor& w, const Tensor& bparam,
+                                       bool nb, at::IntArrayRef plan, int pi) {
+  const int64_t N = dy.size(1), K = x2.size(1);
+  const GradOut dw = grad_out(w, true, {N, K}, dy.options());
+  const GradOut db = grad_out(bparam, nb, {N}, dy.options());
+  run(dy, x2, true, true, prod(plan, pi), nb ? EPI_ROWSUM : EPI_NONE, c10::nullopt, c10::nullopt, dw.t,
+      nb ? db.t : Tensor(), dw.bit(1) | db.bit(2));
+  return {dw.done(), nb ? db.done() : Tensor()};
 }
 
 static std::vector<int64_t> out_shape(const Tensor& x, int64_t n) {
@@ -131,33 +190,64 @@ static Tensor linear_forward(const Tensor& x2, const Tensor& w, const optional<T
   return run(x2, w, false, false, prod(plan, 0), EPI_NONE, b).first;
 }
 
+// fp32 / fp16 weights (a user's nn.Linear under nbd DDP, parallel/ddp.py): the library GEMMs, with
+// the weight / bias gradients written into their DDP bucket slices like the bf16 path
+static bool lib_dtype(const Tensor& w) { return w.scalar_type() != at::kBFloat16; }
+
 struct LinearFn : public torch::autograd::Function<LinearFn> {
   static Tensor forward(AutogradContext* ctx, const Tensor& x, const Tensor& w, const optional<Tensor>& b,
                         at::IntArrayRef plan) {
     at::AutoDispatchBelowADInplaceOrView guard;
-    const Tensor x2 = bf16c(x).view({-1, x.size(-1)});
-    ctx->save_for_backward({x2, w});
+    const bool lib = lib_dtype(w);
+    const Tensor x2 = lib ? x.reshape({-1, x.size(-1)}).contiguous() : bf16c(x).view({-1, x.size(-1)});
+    ctx->save_for_backward({x2, w, b ? *b : Tensor()});
     ctx->saved_data["plan"] = plan.vec();
     ctx->saved_data["need"] = std::vector<bool>{x.requires_grad(), w.requires_grad(), b && b->requires_grad()};
     ctx->saved_data["xshape"] = x.sizes().vec();
+    if (lib) {
+      const Tensor y = b ? at::addmm(*b, x2, w.t()) : at::mm(x2, w.t());
+      return y.view(out_shape(x, w.size(0)));
+    }
     return linear_forward(x2, w, b, plan).view(out_shape(x, w.size(0)));
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
     const auto saved = ctx->get_saved_variables();
-    const Tensor &x2 = saved[0], &w = saved[1];
+    const Tensor &x2 = saved[0], &w = saved[1], &b = saved[2];
     const auto plan = ctx->saved_data["plan"].toIntVector();
     const auto need = ctx->saved_data["need"].toBoolList();
     const auto xshape = ctx->saved_data["xshape"].toIntVector();
     const bool nx = need[0], nw = need[1], nb = need[2];
-    const Tensor dy = bf16c(grads[0]).view({-1, w.size(0)});
     Tensor dx, dw, db;
+    if (lib_dtype(w)) {
+      const Tensor dy = grads[0].reshape({-1, w.size(0)}).contiguous();
+      if (nx) dx = at::mm(dy, w);
+      if (nw) {
+        const GradOut g = grad_out(w, true, w.sizes(), dy.options());
+        if (g.acc) g.t.addmm_(dy.t(), x2);
+        else {
+          Tensor o = g.t;
+          at::mm_out(o, dy.t(), x2);
+        }
+        dw = g.done();
+      }
+      if (nb) {
+        const GradOut g = grad_out(b, true, {w.size(0)}, dy.options());
+        if (g.acc) g.t.add_(dy.sum(0));
+        else {
+          Tensor o = g.t;
+          at::sum_out(o, dy, {0});
+        }
+        db = g.done();
+      }
+      return {dx.defined() ? dx.view(xshape) : dx, dw, db, Tensor()};
+    }
+    const Tensor dy = bf16c(grads[0]).view({-1, w.size(0)});
     if (nx && nw && plan[9] >= 0) {
-      std::tie(dx, dw, db) = pair(dy, w, x2, EPI_NONE, c10::nullopt, nb, plan[9]);
+      std::tie(dx, dw, db) = pair(dy, w, x2, EPI_NONE, c10::nullopt, nb, plan[9], b);
     } else {
       if (nx) dx = run(dy, w, false, true, prod(plan, 1)).first;
-      if (nw && nb) std::tie(dw, db) = run(dy, x2, true, true, prod(plan, 2), EPI_ROWSUM);
-      else if (nw) dw = run(dy, x2, true, true, prod(plan, 2)).first;
+      if (nw) std::tie(dw, db) = wgrad(dy, x2, w, b, nb, plan, 2);
       else if (nb) db = dy.sum(0, false, at::kFloat).to(dy.scalar_type());
     }
     return {dx.defined() ? dx.view(xshape) : dx, dw, db, Tensor()};
@@ -169,6 +259,10 @@ Tensor linear_ag(const Tensor& x, const Tensor& w, const optional<Tensor>& b, at
 }
 
 Tensor linear_noag(const Tensor& x, const Tensor& w, const optional<Tensor>& b, at::IntArrayRef plan) {
+  if (lib_dtype(w)) {
+    const Tensor x2 = x.reshape({-1, x.size(-1)});
+    return (b ? at::addmm(*b, x2, w.t()) : at::mm(x2, w.t())).view(out_shape(x, w.size(0)));
+  }
   return linear_forward(bf16c(x).view({-1, x.size(-1)}), w, b, plan).view(out_shape(x, w.size(0)));
 }
 
@@ -180,7 +274,7 @@ struct MLPGeluFn : public torch::autograd::Function<MLPGeluFn> {
     const Tensor x2 = bf16c(x).view({-1, x.size(-1)});
     auto [g, pre] = run(x2, w1, false, false, prod(plan, 0), EPI_GELU, b1);
     const Tensor y = run(g, w2, false, false, prod(plan, 1), EPI_NONE, b2).first;
-    ctx->save_for_backward({x2, w1, w2, pre, g});
+    ctx->save_for_backward({x2, w1, w2, pre, g, b1 ? *b1 : Tensor(), b2 ? *b2 : Tensor()});
     ctx->saved_data["plan"] = plan.vec();
     ctx->saved_data["need"] = std::vector<bool>{x.requires_grad(), b1.has_value(), b2.has_value()};
     ctx->saved_data["xshape"] = x.sizes().vec();
@@ -189,7 +283,7 @@ struct MLPGeluFn : public torch::autograd::Function<MLPGeluFn> {
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
     const auto s = ctx->get_saved_variables();
-    const Tensor &x2 = s[0], &w1 = s[1], &w2 = s[2], &pre = s[3], &g = s[4];
+    const Tensor &x2 = s[0], &w1 = s[1], &w2 = s[2], &pre = s[3], &g = s[4], &b1 = s[5], &b2 = s[6];
     const auto plan = ctx->saved_data["plan"].toIntVector();
     const auto need = ctx->saved_data["need"].toBoolList();
     const auto xshape = ctx->saved_data["xshape"].toIntVector();
@@ -197,18 +291,16 @@ struct MLPGeluFn : public torch::autograd::Function<MLPGeluFn> {
     const Tensor dy = bf16c(grads[0]).view({-1, w2.size(0)});
     Tensor dpre, dw2, db2, dx, dw1, db1;
     if (plan[18] >= 0) {
-      std::tie(dpre, dw2, db2) = pair(dy, w2, g, EPI_DGELU, pre, hb2, plan[18]);
+      std::tie(dpre, dw2, db2) = pair(dy, w2, g, EPI_DGELU, pre, hb2, plan[18], b2);
     } else {
       dpre = run(dy, w2, false, true, prod(plan, 2), EPI_DGELU, c10::nullopt, pre).first;
-      if (hb2) std::tie(dw2, db2) = run(dy, g, true, true, prod(plan, 3), EPI_ROWSUM);
-      else dw2 = run(dy, g, true, true, prod(plan, 3)).first;
+      std::tie(dw2, db2) = wgrad(dy, g, w2, b2, hb2, plan, 3);
     }
     if (nx && plan[19] >= 0) {
-      std::tie(dx, dw1, db1) = pair(dpre, w1, x2, EPI_NONE, c10::nullopt, hb1, plan[19]);
+      std::tie(dx, dw1, db1) = pair(dpre, w1, x2, EPI_NONE, c10::nullopt, hb1, plan[19], b1);
     } else {
       if (nx) dx = run(dpre, w1, false, true, prod(plan, 4)).first;
-      if (hb1) std::tie(dw1, db1) = run(dpre, x2, true, true, prod(plan, 5), EPI_ROWSUM);
-      else dw1 = run(dpre, x2, true, true, prod(plan, 5)).first;
+      std::tie(dw1, db1) = wgrad(dpre, x2, w1, b1, hb1, plan, 5);
     }
     return {dx.defined() ? dx.view(xshape) : dx, dw1, db1, dw2, db2, Tensor()};
   }
@@ -253,13 +345,13 @@ struct MLPSwiGLUFn : public torch::autograd::Function<MLPSwiGLUFn> {
       std::tie(dgu, dw_down, unused) = pair(dy, w_down, act, EPI_DSWIGLU, pre, false, plan[18]);
     } else {
       dgu = run(dy, w_down, false, true, prod(plan, 2), EPI_DSWIGLU, c10::nullopt, pre).first;
-      dw_down = run(dy, act, true, true, prod(plan, 3)).first;
+      dw_down = wgrad(dy, act, w_down, Tensor(), false, plan, 3).first;
     }
     if (nx && plan[19] >= 0) {
       std::tie(dx, dw_gu, unused) = pair(dgu, w_gu, x2, EPI_NONE, c10::nullopt, false, plan[19]);
     } else {
       if (nx) dx = run(dgu, w_gu, false, true, prod(plan, 4)).first;
-      dw_gu = run(dgu, x2, true, true, prod(plan, 5)).first;
+      dw_gu = wgrad(dgu, x2, w_gu, Tensor(), false, plan, 5).first;
     }
     return {dx.defined() ? dx.view(xshape) : dx, dw_gu, dw_down, Tensor()};
   }

@@ -193,7 +193,10 @@ static void dispatch_copy(at::ScalarType st_, at::ScalarType dt, const std::vect
 
 static int64_t elem_size(at::ScalarType t) { return (int64_t)c10::elementSize(t); }
 
-void bucket_flatten_hip(at::TensorList tensors, const at::Tensor& bucket, at::IntArrayRef offsets, double scale) {
+// accumulate: bucket[slice] += scale * t (fp32 math) — the local pre-reduce of micro-batch
+// gradients into their bucket (DDP no_sync, parallel/ddp.py), instead of overwriting it
+void bucket_flatten_hip(at::TensorList tensors, const at::Tensor& bucket, at::IntArrayRef offsets, double scale,
+                        bool accumulate) {
   TORCH_CHECK(bucket.is_cuda() && bucket.is_contiguous(), "bucket must be a contiguous GPU tensor");
   TORCH_CHECK((int64_t)tensors.size() == (int64_t)offsets.size(), "tensors/offsets length mismatch");
   if (tensors.empty()) return;
@@ -211,7 +214,8 @@ void bucket_flatten_hip(at::TensorList tensors, const at::Tensor& bucket, at::In
     TORCH_CHECK(offsets[i] >= 0 && offsets[i] + t.numel() <= bucket.numel(), "tensor ", i, " does not fit the bucket");
     items.push_back({t.data_ptr(), base + offsets[i] * es, t.numel()});
   }
-  dispatch_copy(src_t, bucket.scalar_type(), items, (float)scale, false, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+  dispatch_copy(src_t, bucket.scalar_type(), items, (float)scale, accumulate,
+                c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
 }
 
 void bucket_unflatten_hip(const at::Tensor& bucket, at::TensorList tensors, at::IntArrayRef offsets, double scale,

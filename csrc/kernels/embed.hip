@@ -162,15 +162,19 @@ __global__ __launch_bounds__(NT) void partial_kernel(const T* __restrict__ dy, i
   if (cur >= 0) flush(cur);
 }
 
-// one wave per vocabulary row; a lane owns 4-column chunks c = 4·lane + 256·k, k < NCH
+// one wave per gradient row; a lane owns 4-column chunks c = 4·lane + 256·k, k < NCH.  Rows
+// [V, R) (a table padded past the vocabulary) get zeros.  `accumulate`: add into the gradient
+// instead (it already holds another contribution — the tied LM head's, ops/embedding.py), and
+// touch only the rows some token hit.
 template <typename T, int NCH>
 __global__ __launch_bounds__(NT) void rows_kernel(const float* __restrict__ acc, int C, const int* __restrict__ offsets,
-                                                  int V, T* __restrict__ grad) {
+                                                  int V, int R, T* __restrict__ grad, int accumulate) {
   const int lane = threadIdx.x & 63;
   const int64_t v = (int64_t)blockIdx.x * (NT / kWave) + (threadIdx.x >> 6);
-  if (v >= V) return;
-  const int b = offsets[v];
-  const bool hit = offsets[v + 1] > b;
+  if (v >= R) return;
+  const int b = v < V ? offsets[v] : 0;
+  const bool hit = v < V && offsets[v + 1] > b;
+  if (accumulate && !hit) return;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int c = 4 * lane + 256 * k;
@@ -179,6 +183,12 @@ __global__ __launch_bounds__(NT) void rows_kernel(const float* __restrict__ acc,
       if (hit) {
         const float4 a = *reinterpret_cast<const float4*>(acc + (int64_t)b * C + c);
         x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+      }
+      if (accumulate) {
+        float o[4];
+        ld4<T>(grad + v * C + c, o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] += o[e];
       }
       st4<T>(grad + v * C + c, x);
     }
@@ -201,23 +211,26 @@ static void dispatch_nch(int64_t C, F&& f) {
 // ---- token + position embedding forward: out[r] = wte[idx[r]] + wpe[pos[r % T]] ---------------
 // One pass (16 B per lane from each table, fp32 add, one rounding — the same bits as
 // F.embedding(idx, wte) + F.embedding(pos, wpe) in the tables' dtype) instead of two gathers and
-// an add.  Out-of-range ids read as zero rows (F.embedding would raise; the host cannot check
-// without a sync).
+// an add.  Out-of-range ids (outside [0, V): V = the vocabulary, which may be smaller than the
+// table when its rows are padded) read as zero rows and set `err` (F.embedding would raise; the
+// host cannot check without a sync — ops/embedding.py reads the flag lazily and raises there).
 template <typename T>
 __global__ __launch_bounds__(NT) void tokpos_kernel(const int64_t* __restrict__ idx, const int64_t* __restrict__ pos, int T_,
                                                     const T* __restrict__ wte, int V, const T* __restrict__ wpe, int P, int C,
-                                                    int64_t n8, T* __restrict__ out) {
+                                                    int64_t n8, T* __restrict__ out, int* __restrict__ err) {
   const int c8 = C / 8;
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
     const int64_t r = i / c8;
     const int c = (int)(i - r * c8) * 8;
     const int64_t v = idx[r], q = pos[r % T_];
     float a[8], b[8];
-    if (v >= 0 && v < V)
+    if (v >= 0 && v < V) {
       load8<T>(wte + v * C + c, a);
-    else
+    } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] = 0.f;
+      if (err != nullptr && c == 0) atomicOr(err, 1);  // (a vector-memory atomic)
+    }
     if (q >= 0 && q < P)
       load8<T>(wpe + q * C + c, b);
     else
@@ -229,7 +242,8 @@ __global__ __launch_bounds__(NT) void tokpos_kernel(const int64_t* __restrict__ 
   }
 }
 
-at::Tensor embedding_tokpos_hip(const at::Tensor& idx, const at::Tensor& wte, const at::Tensor& pos, const at::Tensor& wpe) {
+at::Tensor embedding_tokpos_hip(const at::Tensor& idx, const at::Tensor& wte, const at::Tensor& pos, const at::Tensor& wpe,
+                                int64_t vocab, const c10::optional<at::Tensor>& err) {
   TORCH_CHECK(idx.is_cuda() && wte.is_cuda() && pos.is_cuda() && wpe.is_cuda(), "embedding_tokpos: GPU tensors expected");
   TORCH_CHECK(idx.scalar_type() == at::kLong && pos.scalar_type() == at::kLong && idx.is_contiguous() && pos.is_contiguous() &&
                   pos.dim() == 1 && pos.numel() > 0 && idx.numel() % pos.numel() == 0,
@@ -238,6 +252,8 @@ at::Tensor embedding_tokpos_hip(const at::Tensor& idx, const at::Tensor& wte, co
                   wte.scalar_type() == wpe.scalar_type(),
               "embedding_tokpos: contiguous [V, C] / [P, C] tables of one dtype");
   const int64_t C = wte.size(1), N = idx.numel();
+  const int64_t V = vocab > 0 ? std::min<int64_t>(vocab, wte.size(0)) : wte.size(0);
+  if (err) TORCH_CHECK(err->is_cuda() && err->scalar_type() == at::kInt && err->numel() >= 1, "embedding_tokpos: int32 error flag");
   TORCH_CHECK(C % 8 == 0 && ((uintptr_t)wte.data_ptr() & 15) == 0 && ((uintptr_t)wpe.data_ptr() & 15) == 0,
               "embedding_tokpos: C % 8 == 0 and 16-B aligned tables");
   std::vector<int64_t> shape(idx.sizes().begin(), idx.sizes().end());
@@ -251,8 +267,9 @@ at::Tensor embedding_tokpos_hip(const at::Tensor& idx, const at::Tensor& wte, co
   auto launch = [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((tokpos_kernel<T>), dim3(blocks), dim3(NT), 0, st, idx.data_ptr<int64_t>(), pos.data_ptr<int64_t>(),
-                       (int)pos.numel(), static_cast<const T*>(wte.data_ptr()), (int)wte.size(0),
-                       static_cast<const T*>(wpe.data_ptr()), (int)wpe.size(0), (int)C, n8, static_cast<T*>(out.data_ptr()));
+                       (int)pos.numel(), static_cast<const T*>(wte.data_ptr()), (int)V,
+                       static_cast<const T*>(wpe.data_ptr()), (int)wpe.size(0), (int)C, n8, static_cast<T*>(out.data_ptr()),
+                       err ? err->data_ptr<int>() : nullptr);
   };
   switch (wte.scalar_type()) {
     case at::kFloat: launch(float{}); break;
@@ -264,7 +281,10 @@ at::Tensor embedding_tokpos_hip(const at::Tensor& idx, const at::Tensor& wte, co
   return out;
 }
 
-at::Tensor embedding_bwd_hip(const at::Tensor& dy, const at::Tensor& idx, int64_t V) {
+// grad_out: write (or with `accumulate`, add) the gradient there — [R, C] with R >= V rows
+// (a vocabulary-padded table, or the tied LM head's gradient slot, graddst.h)
+at::Tensor embedding_bwd_hip(const at::Tensor& dy, const at::Tensor& idx, int64_t V,
+                             const c10::optional<at::Tensor>& grad_out, bool accumulate) {
   TORCH_CHECK(dy.is_cuda() && idx.is_cuda(), "embedding_bwd: GPU tensors expected");
   TORCH_CHECK(dy.dim() == 2 && dy.is_contiguous(), "embedding_bwd: dy must be a contiguous [N, C]");
   TORCH_CHECK(idx.dim() == 1 && idx.is_contiguous() && idx.scalar_type() == at::kLong && idx.size(0) == dy.size(0),
@@ -273,7 +293,17 @@ at::Tensor embedding_bwd_hip(const at::Tensor& dy, const at::Tensor& idx, int64_
   TORCH_CHECK(C % 4 == 0 && C <= 4096, "embedding_bwd: C must be a multiple of 4 and <= 4096");
   TORCH_CHECK(V > 0 && V < (1LL << 31) && N < (1LL << 31), "embedding_bwd: sizes out of range");
   TORCH_CHECK(((uintptr_t)dy.data_ptr() & 15) == 0, "embedding_bwd: dy must be 16-B aligned");
-  at::Tensor grad = at::empty({V, C}, dy.options());
+  at::Tensor grad;
+  if (grad_out) {
+    grad = *grad_out;
+    TORCH_CHECK(grad.dim() == 2 && grad.size(0) >= V && grad.size(1) == C && grad.is_contiguous() &&
+                    grad.scalar_type() == dy.scalar_type() && ((uintptr_t)grad.data_ptr() & 15) == 0,
+                "embedding_bwd: grad_out must be a contiguous, aligned [R >= V, C] tensor of dy's dtype");
+  } else {
+    TORCH_CHECK(!accumulate, "embedding_bwd: accumulate needs grad_out");
+    grad = at::empty({V, C}, dy.options());
+  }
+  const int64_t R = grad.size(0);
   auto io = idx.options().dtype(at::kInt);
   at::Tensor counts = at::zeros({V + 1}, io);  // [V] counts, [V] = out-of-range flag
   at::Tensor cursor = at::zeros({V}, io);
@@ -296,7 +326,7 @@ at::Tensor embedding_bwd_hip(const at::Tensor& dy, const at::Tensor& idx, int64_
   // slots [0, offsets[V]) hold every in-range token; out-of-range ids are flagged and never
   // placed, and partial_kernel stops at offsets[V] (read on the device)
   const dim3 pgrid((unsigned)((N + kSlots * 4 - 1) / (kSlots * 4)));
-  const dim3 rgrid((unsigned)((V + 3) / 4));
+  const dim3 rgrid((unsigned)((R + 3) / 4));
   dispatch_nch(C, [&](auto nch) {
     constexpr int K = decltype(nch)::value;
     auto launch = [&](auto tag) {
@@ -305,7 +335,7 @@ at::Tensor embedding_bwd_hip(const at::Tensor& dy, const at::Tensor& idx, int64_
                          idx.data_ptr<int64_t>(), offsets.data_ptr<int>(), order.data_ptr<int>(), (int)V,
                          acc.data_ptr<float>());
       hipLaunchKernelGGL((rows_kernel<T, K>), rgrid, dim3(NT), 0, st, acc.data_ptr<float>(), (int)C,
-                         offsets.data_ptr<int>(), (int)V, static_cast<T*>(grad.data_ptr()));
+                         offsets.data_ptr<int>(), (int)V, (int)R, static_cast<T*>(grad.data_ptr()), accumulate ? 1 : 0);
     };
     switch (dy.scalar_type()) {
       case at::kFloat: launch(float{}); break;

@@ -257,7 +257,7 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
         if (S > 1)
           p.ws[(int64_t)S * p.M * p.ldc + (int64_t)by * p.M + m] = accb[j][0];
         else
-          p.aux_out[m] = f32_to_bf16(accb[j][0]);
+          p.aux_out[m] = f32_to_bf16((p.accum & 2) ? accb[j][0] + bf16_to_f32(p.aux_out[m]) : accb[j][0]);
       }
     }
   }
@@ -354,6 +354,13 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
       load8<bf16_t>(reinterpret_cast<const bf16_t*>(p.aux_in) + off, h);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= dgelu_tanh(h[e]);
+    } else {
+      if (p.accum & 1) {  // gradient accumulation: c += A·B (one bf16 rounding of the fp32 sum)
+        float o[8];
+        load8<bf16_t>(reinterpret_cast<const bf16_t*>(p.c) + off, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += o[e];
+      }
     }
     store8<bf16_t>(reinterpret_cast<bf16_t*>(p.c) + off, v);
   }
@@ -394,7 +401,7 @@ __global__ __launch_bounds__(64 * W, 2) void pair_kernel(Args p1, int t1, int nb
 // rs_out, the EPI_ROWSUM partials ws[S*slab + s*M + m] are summed into rs_out[m] the same way.
 __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ ws, int splits, int64_t n8, int64_t slab,
                                                      uint16_t* __restrict__ out, int64_t m8,
-                                                     uint16_t* __restrict__ rs_out) {
+                                                     uint16_t* __restrict__ rs_out, int accum) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8 + m8; i += (int64_t)gridDim.x * blockDim.x) {
     const bool rs = i >= n8;
     const float* src = rs ? ws + splits * slab + 8 * (i - n8) : ws + 8 * i;
@@ -407,7 +414,14 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ w
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += w[e];
     }
-    store8<bf16_t>(reinterpret_cast<bf16_t*>(rs ? rs_out : out) + 8 * (rs ? i - n8 : i), v);
+    bf16_t* dst = reinterpret_cast<bf16_t*>(rs ? rs_out : out) + 8 * (rs ? i - n8 : i);
+    if (accum & (rs ? 2 : 1)) {  // gradient accumulation into the destination
+      float o[8];
+      load8<bf16_t>(dst, o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += o[e];
+    }
+    store8<bf16_t>(dst, v);
   }
 }
 
@@ -520,7 +534,7 @@ static Tile pick_tile(int M, int N, int64_t tile_hint) {
 // c = A·B with the layouts above; c is [M][N] bf16 (contiguous).
 void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_km, bool b_kn,
               const c10::optional<at::Tensor>& bias, int64_t epi, const c10::optional<at::Tensor>& aux_in,
-              const c10::optional<at::Tensor>& aux_out, int64_t splits, int64_t tile_hint) {
+              const c10::optional<at::Tensor>& aux_out, int64_t splits, int64_t tile_hint, int64_t accum) {
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "nbd::gemm: 2-D operands");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kBFloat16,
               "nbd::gemm: bf16 operands");
@@ -565,6 +579,8 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   }
   TORCH_CHECK(epi >= EPI_NONE && epi <= EPI_DSWIGLU, "nbd::gemm: epilogue ", epi);
   const Tile t = pick_tile(M, N, tile_hint);
+  TORCH_CHECK(accum == 0 || ((epi == EPI_NONE || epi == EPI_ROWSUM) && !bias && t.bm != 256),
+              "nbd::gemm: accumulation only for plain / row-sum products on the 64-128 tile kernels");
   // per-lane DMA offsets are 32-bit byte offsets within one tile's rows (gemm_common.h Pieces)
   {
     const int64_t ra = a_km ? BK : t.bm, rb = b_kn ? BK : (epi == EPI_SWIGLU ? N / 2 + t.bn : t.bn);
@@ -593,6 +609,7 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   p.ldc = cN;
   p.tiles_m = M / t.bm;
   p.tiles_n = N / t.bn;
+  p.accum = (int)accum;
   const dim3 grid(tiles, S);
   p.c = static_cast<uint16_t*>(c.data_ptr());
   at::Tensor ws;
@@ -614,7 +631,8 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   if (S > 1) {
     const int64_t n8 = (int64_t)M * N / 8, m8 = epi == EPI_ROWSUM ? M / 8 : 0;
     const int blocks = (int)std::min<int64_t>((n8 + m8 + 255) / 256, 2048);
-    hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, p.ws, S, n8, (int64_t)M * N, p.c, m8, p.aux_out);
+    hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, p.ws, S, n8, (int64_t)M * N, p.c, m8, p.aux_out,
+                       p.accum);
     C10_HIP_KERNEL_LAUNCH_CHECK();
   }
 }
@@ -625,7 +643,8 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
 // into aux_out2}, split s2 ways along K2 (fp32 slabs + reduce_kernel).  128x128 tiles only.
 void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor& c1, int64_t epi1,
                    const c10::optional<at::Tensor>& aux_in1, const at::Tensor& a2, const at::Tensor& b2,
-                   const at::Tensor& c2, int64_t epi2, const c10::optional<at::Tensor>& aux_out2, int64_t splits2) {
+                   const at::Tensor& c2, int64_t epi2, const c10::optional<at::Tensor>& aux_out2, int64_t splits2,
+                   int64_t accum2) {
   for (const at::Tensor* x : {&a1, &b1, &c1, &a2, &b2, &c2}) {
     TORCH_CHECK(x->dim() == 2 && x->scalar_type() == at::kBFloat16 && x->is_contiguous() && x->is_cuda() &&
                     reinterpret_cast<uintptr_t>(x->data_ptr()) % 16 == 0,
@@ -675,6 +694,7 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   p2.M = M2; p2.N = N2; p2.K = K2 / S;
   p2.lda = a2.size(1); p2.ldb = b2.size(1); p2.ldc = N2;
   p2.tiles_m = M2 / TB; p2.tiles_n = N2 / TB;
+  p2.accum = (int)accum2;  // the weight-gradient half may accumulate into its destination
   at::Tensor ws;
   if (S > 1) {
     ws = at::empty({(int64_t)S * M2 * N2 + (epi2 == EPI_ROWSUM ? (int64_t)S * M2 : 0)}, a1.options().dtype(at::kFloat));
@@ -712,7 +732,7 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
     const int64_t n8 = (int64_t)M2 * N2 / 8, m8 = epi2 == EPI_ROWSUM ? M2 / 8 : 0;
     const int blocks = (int)std::min<int64_t>((n8 + m8 + 255) / 256, 2048);
     hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, p2.ws, S, n8, (int64_t)M2 * N2, p2.c, m8,
-                       p2.aux_out);
+                       p2.aux_out, p2.accum);
     C10_HIP_KERNEL_LAUNCH_CHECK();
   }
 }

@@ -40,6 +40,8 @@ struct Args {
   int M, N, K;             // K = reduction length handled by one split
   int64_t lda, ldb, ldc;
   int tiles_m, tiles_n;
+  int accum;               // bit 0: c += result (EPI_NONE / EPI_ROWSUM); bit 1: aux_out row sums +=
+                           // (gradient accumulation into a DDP bucket slice: graddst.h)
 };
 
 // ---- swizzles ---------------------------------------------------------------------------------
@@ -180,7 +182,7 @@ __device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, i
 
 // out[i] = Σ_s ws[s][i] as bf16 (fixed order: deterministic); defined in gemm.hip
 __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ ws, int splits, int64_t n8, int64_t slab,
-                              uint16_t* __restrict__ out, int64_t m8, uint16_t* __restrict__ rs_out);
+                              uint16_t* __restrict__ out, int64_t m8, uint16_t* __restrict__ rs_out, int accum);
 
 // gemm256.hip: the 256x256 phase-interleaved kernel for (a_km, b_kn, epi); grid (tiles, splits)
 void launch_gemm256(const Args& p, bool a_km, bool b_kn, int epi, dim3 grid, hipStream_t st, int variant);

@@ -5,7 +5,7 @@
 #include <torch/library.h>
 
 TORCH_LIBRARY(nbd, m) {
-  m.def("bucket_flatten(Tensor[] tensors, Tensor(a!) bucket, int[] offsets, float scale) -> ()");
+  m.def("bucket_flatten(Tensor[] tensors, Tensor(a!) bucket, int[] offsets, float scale, bool accumulate=False) -> ()");
   m.def("bucket_unflatten(Tensor bucket, Tensor(a!)[] tensors, int[] offsets, float scale, bool accumulate) -> ()");
   m.def("local_prereduce(Tensor[] inputs, Tensor(a!) out, float scale) -> ()");
   m.def("tensor_summary(Tensor x) -> Tensor");
@@ -24,8 +24,8 @@ TORCH_LIBRARY(nbd, m) {
   m.def("colsum(Tensor x, ScalarType dtype) -> Tensor");
   m.def("rms_fwd(Tensor x, Tensor? delta, Tensor weight, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("rms_bwd(Tensor x, Tensor dy, Tensor? dres, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
-  m.def("embedding_bwd(Tensor dy, Tensor idx, int V) -> Tensor");
-  m.def("embedding_tokpos(Tensor idx, Tensor wte, Tensor pos, Tensor wpe) -> Tensor");
+  m.def("embedding_bwd(Tensor dy, Tensor idx, int V, Tensor(a!)? grad_out=None, bool accumulate=False) -> Tensor");
+  m.def("embedding_tokpos(Tensor idx, Tensor wte, Tensor pos, Tensor wpe, int vocab=-1, Tensor(a!)? err=None) -> Tensor");
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, int n_rot, int head_dim, bool inverse) -> ()");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");
@@ -33,9 +33,9 @@ TORCH_LIBRARY(nbd, m) {
   m.def("xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor scale, int ignore_index, Tensor(a!) dlogits) -> ()");
   m.def("xent_fused(Tensor(a!) logits, Tensor target, int ignore_index, Tensor scale) -> (Tensor, Tensor)");
   m.def("gemm(Tensor a, Tensor b, Tensor(a!) c, bool a_km, bool b_kn, Tensor? bias, int epi, Tensor? aux_in, "
-        "Tensor(b!)? aux_out, int splits, int tile) -> ()");
+        "Tensor(b!)? aux_out, int splits, int tile, int accum=0) -> ()");
   m.def("gemm_pair(Tensor a1, Tensor b1, Tensor(a!) c1, int epi1, Tensor? aux_in1, Tensor a2, Tensor b2, "
-        "Tensor(b!) c2, int epi2, Tensor(c!)? aux_out2, int splits2) -> ()");
+        "Tensor(b!) c2, int epi2, Tensor(c!)? aux_out2, int splits2, int accum2=0) -> ()");
   // autograd nodes of the fused Linear / MLP paths (autograd.hip); plan = ops/gemm.py native_plan
   m.def("linear_ag(Tensor x, Tensor w, Tensor? b, int[] plan) -> Tensor");
   m.def("mlp_gelu_ag(Tensor x, Tensor w1, Tensor? b1, Tensor w2, Tensor? b2, int[] plan) -> Tensor");

@@ -33,6 +33,16 @@ class GPT2Config:
     fused_attn: bool = True  # GPU bf16: nbd.ops.attention_qkv (HIP flash fwd/bwd) instead of SDPA
     fused_norm: bool = True  # GPU, no autocast: HIP residual-add+LayerNorm and bias-grad kernels
     hip_gemm: bool = True  # GPU bf16 fast path: Linear layers on the HIP MFMA GEMM (GELU fused in its epilogues)
+    # the token table (and the tied LM head) is stored with its rows padded to a multiple of this
+    # from 4096 classes up: zero rows that never receive a gradient, so the LM-head GEMMs run on an
+    # aligned vocabulary (hipBLASLt on 50257 vs 50304 columns: 2.18 vs 1.75 ms per GPT-2 step,
+    # docs/FINDINGS.md §16) with no per-step padded copy of the weight.  1 = no padding.
+    vocab_pad: int = 128
+
+    @property
+    def padded_vocab(self) -> int:
+        v, a = self.vocab_size, max(1, self.vocab_pad)
+        return -(-v // a) * a if v >= 4096 else v
 
     @classmethod
     def small(cls):
@@ -135,17 +145,22 @@ class GPT2(nn.Module):
         super().__init__()
         c = config or GPT2Config()
         self.config = c
-        self.wte = nn.Embedding(c.vocab_size, c.n_embd)
+        Vp = c.padded_vocab
+        self.wte = nn.Embedding(Vp, c.n_embd)
         self.wpe = nn.Embedding(c.n_positions, c.n_embd)
         self.h = nn.ModuleList([Block(c) for _ in range(c.n_layer)])
         self.ln_f = nn.LayerNorm(c.n_embd, bias=c.bias)
-        self.lm_head = nn.Linear(c.n_embd, c.vocab_size, bias=False)
+        self.lm_head = nn.Linear(c.n_embd, Vp, bias=False)
         if c.tie_weights:
             self.lm_head.weight = self.wte.weight
         self.apply(self._init)
         for n, p in self.named_parameters():
             if n.endswith("c_proj.weight"):
                 nn.init.normal_(p, mean=0.0, std=0.02 / math.sqrt(2 * c.n_layer))
+        if Vp != c.vocab_size:
+            with torch.no_grad():  # the pad rows stay zero: no id reaches them, their gradient is 0
+                self.wte.weight[c.vocab_size:].zero_()
+                self.lm_head.weight[c.vocab_size:].zero_()
 
     @staticmethod
     def _init(m: nn.Module) -> None:
@@ -173,7 +188,14 @@ class GPT2(nn.Module):
                 and self.wte.weight.dtype in (torch.bfloat16, torch.float16))
 
     def num_params(self) -> int:
-        return sum(p.numel() for p in self.parameters())
+        """Parameters of the architecture (the vocabulary's pad rows not counted)."""
+        pad = (self.config.padded_vocab - self.config.vocab_size) * self.config.n_embd
+        return sum(p.numel() for p in self.parameters()) - pad * (1 if self.config.tie_weights else 2)
+
+    def _logits(self, h: torch.Tensor) -> torch.Tensor:
+        logits = self.lm_head(h)
+        V = self.config.vocab_size
+        return logits[..., :V] if logits.shape[-1] != V else logits
 
     def _trunk(self, idx: torch.Tensor, cache=None):
         """Final-normed hidden states [B, T, C] (and whether the HIP fast path ran); ``cache``
@@ -184,7 +206,7 @@ class GPT2(nn.Module):
         if self._fast_ok(idx):
             from .. import ops
 
-            x = ops.embedding_tok_pos(idx, self.wte.weight, pos, self.wpe.weight)
+            x = ops.embedding_tok_pos(idx, self.wte.weight, pos, self.wpe.weight, self.config.vocab_size)
         else:
             x = self.wte(idx) + self.wpe(pos)
         if self._fast(x):
@@ -218,12 +240,12 @@ class GPT2(nn.Module):
             if ops.loss.FUSED_XENT:
                 # LM head + loss: one pass over the logits for the loss forward and backward
                 red = "sum" if cp is not None else "mean"
-                return None, self._cp_loss(ops.linear_cross_entropy(h, self.lm_head.weight, targets, reduction=red),
-                                           targets, cp)
-        logits = self.lm_head(h)
+                return None, self._cp_loss(ops.linear_cross_entropy(h, self.lm_head.weight, targets, reduction=red,
+                                                                    vocab=c.vocab_size), targets, cp)
+        logits = self._logits(h)
         loss = None
         if targets is not None:
-            flat, tgt = logits.view(-1, logits.size(-1)), targets.reshape(-1)
+            flat, tgt = logits.reshape(-1, logits.size(-1)), targets.reshape(-1)
             red = "sum" if cp is not None else "mean"
             if self.config.fused_ce and logits.is_cuda:
                 from .. import ops
@@ -249,12 +271,15 @@ class GPT2(nn.Module):
                 ln.eps = hc.layer_norm_epsilon
         m.ln_f.eps = hc.layer_norm_epsilon
         sd = {}
+        Vp = c.padded_vocab
         for k, v in hf_model.state_dict().items():
             k = k[len("transformer."):] if k.startswith("transformer.") else k
             if k.endswith(".attn.bias") or k.endswith(".attn.masked_bias"):
                 continue  # causal-mask buffers of older transformers
             if k.endswith(".weight") and any(f".{n}.weight" in "." + k for n in ("c_attn", "c_proj", "c_fc")):
                 v = v.t()
+            if k in ("wte.weight", "lm_head.weight") and v.shape[0] != Vp:  # zero pad rows
+                v = torch.cat([v, v.new_zeros(Vp - v.shape[0], v.shape[1])])
             sd[k] = v
         missing, unexpected = m.load_state_dict(sd, strict=False)
         missing = [k for k in missing if not (k == "lm_head.weight" and c.tie_weights)]
@@ -283,7 +308,7 @@ class GPT2(nn.Module):
         h, _ = self._trunk(idx, cache)
         B, _, C = h.shape
         last = torch.gather(h, 1, (lengths - 1).view(B, 1, 1).expand(B, 1, C)).squeeze(1)
-        return self.lm_head(last)
+        return self._logits(last)
 
     @torch.no_grad()
     def decode_step(self, tok: torch.Tensor, pos: torch.Tensor, cache) -> torch.Tensor:
@@ -293,7 +318,8 @@ class GPT2(nn.Module):
 
         c = self.config
         if self._fast_ok(tok):
-            x = ops.embedding_tok_pos(tok.view(1, -1), self.wte.weight, pos, self.wpe.weight).view(-1, c.n_embd)
+            x = ops.embedding_tok_pos(tok.view(1, -1), self.wte.weight, pos, self.wpe.weight,
+                                      c.vocab_size).view(-1, c.n_embd)
         else:
             x = self.wte(tok) + self.wpe(pos)
         # five fused kernels per block (ops.linear_small: norm prologue, bias / GELU / residual
@@ -301,7 +327,9 @@ class GPT2(nn.Module):
         for i, blk in enumerate(self.h):
             x = blk.attn.decode(x, blk.ln_1, cache, i, pos)
             x = blk.mlp.decode(x, blk.ln_2)
-        return ops.linear_small(x, self.lm_head.weight, norm=("ln", self.ln_f.weight, self.ln_f.bias, self.ln_f.eps))
+        # the first vocab_size rows of the (padded) table: a contiguous view, no copy
+        w = self.lm_head.weight[:c.vocab_size]
+        return ops.linear_small(x, w, norm=("ln", self.ln_f.weight, self.ln_f.bias, self.ln_f.eps))
 
     def generate(self, idx: torch.Tensor, max_new_tokens: int, **kw) -> torch.Tensor:
         """``generation.generate`` (KV cache, HIP decode attention, graph-captured decode loop)."""

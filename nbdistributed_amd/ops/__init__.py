@@ -6,6 +6,9 @@ op                     what it fuses                                    kernel (
 bucket_flatten (K1)    N grads -> 1 bucket + cast (fp32->bf16) + scale  bucket.hip multi_copy
 bucket_unflatten (K2)  bucket -> N grads + scale (1/world) + cast (+=)  bucket.hip multi_copy
 local_prereduce (K3)   sum of k buffers, fp32 accumulate, scale, cast   bucket.hip prereduce
+prereduce_into_bucket  K3 multi-tensor: bucket slices += grads (no_sync)  bucket.hip multi_copy<ACC>
+graddst                gradient destinations: backward GEMMs write into   graddst.cpp + autograd.hip
+                       DDP bucket slices (accumulating in the epilogue)
 tensor_summary (K4)    count/sum/mean/std/norm/min/max/absmax/nan/inf   summary.hip (MFMA Σx, Σx²)
 adamw_flat (K5)        AdamW step over a DDP bucket: fp32 master/m/v,   optim.hip
                        param cast, optional device clip coefficient
@@ -37,8 +40,9 @@ from __future__ import annotations
 from . import _lib
 from ._lib import _require, load_library, native_available
 from .attention import attention_qkv, flash_attention, flash_supported
+from . import graddst
 from .bucket import (_ref_flatten, _ref_prereduce, _ref_unflatten, bucket_flatten, bucket_unflatten, local_prereduce,
-                     plan_offsets)
+                     plan_offsets, prereduce_into_bucket)
 from .decode import decode_attention, decode_attention_reference, linear_small, linear_small_reference
 from .embedding import embedding, embedding_tok_pos
 from .gemm import gemm_linear, mlp_gelu, mlp_swiglu
@@ -55,7 +59,7 @@ def __getattr__(name):
     raise AttributeError(name)
 
 
-__all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "adamw_flat", "cross_entropy", "linear_cross_entropy",
+__all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "prereduce_into_bucket", "graddst", "adamw_flat", "cross_entropy", "linear_cross_entropy",
            "flash_attention", "attention_qkv", "decode_attention", "decode_attention_reference", "linear_small", "linear_small_reference", "flash_supported", "layer_norm", "add_layer_norm", "linear",
            "colsum", "embedding", "embedding_tok_pos", "gemm_linear", "mlp_gelu", "mlp_swiglu", "rms_norm", "add_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary",
            "tensor_summary_text", "tensor_summary_raw", "plan_offsets", "native_available", "load_library",

@@ -22,10 +22,13 @@ def plan_offsets(numels: Sequence[int], align: int = 64) -> Tuple[List[int], int
 
 # ---------------------------------------------------------------- reference implementations
 
-def _ref_flatten(tensors, bucket, offsets, scale):
+def _ref_flatten(tensors, bucket, offsets, scale, accumulate=False):
     for t, o in zip(tensors, offsets):
         n = t.numel()
-        bucket[o:o + n].copy_((t.reshape(-1).float() * scale).to(bucket.dtype))
+        v = t.reshape(-1).float() * scale
+        if accumulate:
+            v = v + bucket[o:o + n].float()
+        bucket[o:o + n].copy_(v.to(bucket.dtype))
 
 def _ref_unflatten(bucket, tensors, offsets, scale, accumulate):
     for t, o in zip(tensors, offsets):
@@ -42,9 +45,10 @@ def _ref_prereduce(inputs, out, scale):
     out.view(-1).copy_((acc * scale).to(out.dtype))
 
 def bucket_flatten(tensors: Sequence, bucket=None, offsets: Optional[Sequence[int]] = None, dtype=None,
-                   scale: float = 1.0, align: int = 64):
+                   scale: float = 1.0, align: int = 64, accumulate: bool = False):
     """Copy ``tensors`` into one flat ``bucket`` (allocated if None), casting to the bucket's dtype
-    and multiplying by ``scale``.  Returns (bucket, offsets)."""
+    and multiplying by ``scale``; ``accumulate``: add into the bucket's contents instead (fp32 math,
+    one rounding — the local pre-reduce of micro-batch gradients).  Returns (bucket, offsets)."""
     import torch
 
     tensors = list(tensors)
@@ -60,9 +64,9 @@ def bucket_flatten(tensors: Sequence, bucket=None, offsets: Optional[Sequence[in
     flat = [t if t.is_contiguous() else t.contiguous() for t in tensors]
     if bucket.is_cuda:
         _require()
-        torch.ops.nbd.bucket_flatten(flat, bucket, list(offsets), float(scale))
+        torch.ops.nbd.bucket_flatten(flat, bucket, list(offsets), float(scale), bool(accumulate))
     else:
-        _ref_flatten(flat, bucket, offsets, scale)
+        _ref_flatten(flat, bucket, offsets, scale, accumulate)
     return bucket, list(offsets)
 
 def bucket_unflatten(bucket, tensors: Sequence, offsets: Sequence[int], scale: float = 1.0,
@@ -82,6 +86,14 @@ def bucket_unflatten(bucket, tensors: Sequence, offsets: Sequence[int], scale: f
         torch.ops.nbd.bucket_unflatten(bucket, tensors, list(offsets), float(scale), bool(accumulate))
     else:
         _ref_unflatten(bucket, tensors, offsets, scale, accumulate)
+
+def prereduce_into_bucket(tensors: Sequence, bucket, offsets: Sequence[int], scale: float = 1.0) -> None:
+    """K3 in its multi-tensor form: ``bucket[slice_i] += scale * tensors[i]`` for every i, fp32
+    accumulation, one launch per <= 256 tensors.  DDP's ``no_sync`` path sums each micro-batch's
+    gradients into their bucket with it (``parallel/ddp.py``), so the last micro-batch's bucket is
+    the locally pre-reduced gradient and no per-parameter autograd adds run."""
+    bucket_flatten(tensors, bucket, offsets, scale=scale, accumulate=True)
+
 
 def local_prereduce(inputs: Sequence, out=None, scale: float = 1.0, dtype=None):
     """``out = scale * Σ inputs`` with fp32 accumulation.  Returns ``out``."""

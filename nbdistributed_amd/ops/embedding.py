@@ -7,6 +7,57 @@ from ._lib import _require
 
 # NBD_FUSED_EMBED=0: token and position lookups as two gathers + an add (A/B)
 FUSED_EMBED = os.environ.get("NBD_FUSED_EMBED", "1") != "0"
+# out-of-range token ids: the fused lookup kernel raises a device-side flag; it is read back
+# asynchronously every CHECK_EVERY calls (never a sync on the hot path) and raised at the next call
+CHECK_EVERY = max(1, int(os.environ.get("NBD_EMBED_CHECK_EVERY", "8")))
+_ERR: dict = {}
+
+
+def _err_state(device):
+    import torch
+
+    st = _ERR.get(device.index)
+    if st is None:
+        st = _ERR[device.index] = {"flag": torch.zeros(1, dtype=torch.int32, device=device),
+                                   "host": torch.zeros(1, dtype=torch.int32).pin_memory(), "event": None, "n": 0}
+    return st
+
+
+def _raise_ids(st) -> None:
+    st["flag"].zero_()
+    st["host"][0] = 0
+    raise IndexError("embedding: a token id outside [0, vocab) was looked up (F.embedding would raise); "
+                     "detected by the fused HIP lookup's error flag (read back lazily, ops/embedding.py)")
+
+
+def _poll_ids(device) -> "torch.Tensor":  # noqa: F821
+    """The error flag for this call's launch; raises if an earlier launch saw a bad id."""
+    import torch
+
+    st = _err_state(device)
+    if torch.cuda.is_current_stream_capturing():
+        return st["flag"]  # replays set it too; read at the next eager call or check_ids()
+    ev = st["event"]
+    if ev is not None and ev.query():
+        st["event"] = None
+        if int(st["host"][0]):
+            _raise_ids(st)
+    st["n"] += 1
+    if st["event"] is None and st["n"] % CHECK_EVERY == 0:
+        st["host"].copy_(st["flag"], non_blocking=True)
+        st["event"] = torch.cuda.Event()
+        st["event"].record()
+    return st["flag"]
+
+
+def check_ids(device=None) -> None:
+    """Synchronously check the out-of-range-id flag of ``embedding_tok_pos`` (raises IndexError)."""
+    import torch
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    st = _ERR.get(dev.index)
+    if st is not None and int(st["flag"].item()):
+        _raise_ids(st)
 
 
 _EmbFn = None
@@ -44,19 +95,39 @@ def _tokpos_fn():
 
         class _TokPos(torch.autograd.Function):
             @staticmethod
-            def forward(ctx, idx, wte, pos, wpe):
-                ctx.save_for_backward(idx, pos)
-                ctx.shapes = (wte.shape[0], wpe.shape[0])
-                return torch.ops.nbd.embedding_tokpos(idx, wte, pos, wpe)
+            def forward(ctx, idx, wte, pos, wpe, vocab):
+                ctx.save_for_backward(idx, pos, wte)
+                V = vocab if 0 < vocab < wte.shape[0] else wte.shape[0]
+                ctx.shapes = (V, wpe.shape[0])
+                return torch.ops.nbd.embedding_tokpos(idx, wte, pos, wpe, V, _poll_ids(wte.device))
 
             @staticmethod
             def backward(ctx, dy):
-                idx, pos = ctx.saved_tensors
+                from . import graddst
+
+                idx, pos, wte = ctx.saved_tensors
                 V, P = ctx.shapes
                 C = dy.shape[-1]
                 dy2 = dy.reshape(-1, C)
                 dy2 = dy2 if dy2.is_contiguous() else dy2.contiguous()
-                d_wte = torch.ops.nbd.embedding_bwd(dy2, idx.reshape(-1), V) if ctx.needs_input_grad[1] else None
+                d_wte = None
+                if ctx.needs_input_grad[1]:
+                    ids = idx.reshape(-1)
+                    dst = graddst.join(wte)
+                    if dst is not None:
+                        # the tied LM head already wrote this step's gradient into the DDP bucket
+                        # slice: add the rows the tokens hit and contribute nothing else
+                        torch.ops.nbd.embedding_bwd(dy2, ids, V, dst, True)
+                    else:
+                        dst, acc = graddst.claim(wte)
+                        if dst is not None:
+                            torch.ops.nbd.embedding_bwd(dy2, ids, V, dst, acc)
+                            d_wte = graddst.hand_back(wte, dst, acc)
+                        elif V < wte.shape[0]:  # padded table: the pad rows get zeros
+                            d_wte = torch.empty_like(wte)
+                            torch.ops.nbd.embedding_bwd(dy2, ids, V, d_wte, False)
+                        else:
+                            d_wte = torch.ops.nbd.embedding_bwd(dy2, ids, V)
                 d_wpe = None
                 if ctx.needs_input_grad[3]:
                     # positions repeat every T rows: sum the batch first (fp32), then place the T
@@ -64,17 +135,19 @@ def _tokpos_fn():
                     T = pos.numel()
                     s = dy2.view(-1, T, C).sum(0, dtype=torch.float32)
                     d_wpe = torch.zeros(P, C, dtype=torch.float32, device=dy.device).index_add_(0, pos, s).to(dy.dtype)
-                return None, d_wte, None, d_wpe
+                return None, d_wte, None, d_wpe, None
 
         _TokPosFn = _TokPos
     return _TokPosFn
 
 
-def embedding_tok_pos(idx, wte, pos, wpe):
+def embedding_tok_pos(idx, wte, pos, wpe, vocab: int = -1):
     """``F.embedding(idx, wte) + F.embedding(pos, wpe)`` (GPT-2's input: token + learned position
     embeddings, ``idx`` [..., T], ``pos`` [T] of unique positions) in one HIP pass on the GPU; the
     backward sums the batch for the position table and uses the counting-sort kernels for the
-    token table."""
+    token table.  ``vocab`` < ``wte.shape[0]``: rows past it are padding (ids must be < vocab).
+    Out-of-range ids raise IndexError — lazily (a device flag read back without syncing, see
+    ``check_ids``), where F.embedding raises at once."""
     import torch
 
     C = wte.shape[-1]
@@ -82,7 +155,10 @@ def embedding_tok_pos(idx, wte, pos, wpe):
             and wte.dtype == wpe.dtype and wte.dtype in (torch.bfloat16, torch.float16, torch.float32)
             and idx.shape[-1] == pos.numel() and pos.dim() == 1):
         _require()
-        return _tokpos_fn().apply(idx.contiguous(), wte, pos.contiguous(), wpe)
+        return _tokpos_fn().apply(idx.contiguous(), wte, pos.contiguous(), wpe, int(vocab))
+    if 0 < vocab < wte.shape[0]:
+        if not idx.is_cuda and idx.numel() and int(idx.max()) >= vocab:
+            raise IndexError(f"embedding: token id {int(idx.max())} >= vocab {vocab}")
     return embedding(idx, wte) + embedding(pos, wpe)
 
 

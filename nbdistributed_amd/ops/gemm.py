@@ -501,3 +501,33 @@ def _swiglu(gu):
     from .llama import swiglu
 
     return swiglu(gu)
+
+
+# plan for the C++ Linear node's library path (fp32 / fp16 weights): every product on hipBLASLt,
+# no grouped backward launch (the node ignores tiles and splits there)
+_LIB_PLAN = [1, 0, 1, 1, 0, 1, 1, 0, 1, -1]
+
+
+def native_available_or_raise() -> None:
+    """The C++ autograd nodes need the extension: fail loudly on a GPU box without it."""
+    _require()
+
+
+def linear_any(x, weight, bias=None):
+    """``F.linear`` through the C++ Linear autograd node for any GPU dtype: bf16 with 64-granular
+    dims runs the HIP MFMA GEMMs (``gemm_linear``), everything else the library GEMMs.  Either way
+    the weight / bias gradients go to their registered DDP bucket slices (``ops.graddst``) — this
+    is the forward ``parallel.DistributedDataParallel(fused_linear=True)`` gives ``nn.Linear``."""
+    import torch
+
+    if _fast(x, weight) and _native(bias):
+        return gemm_linear(x, weight, bias)
+    # (bf16 shapes the HIP GEMMs cannot tile stay on F.linear: the node's bias-gradient row sums
+    # need the HIP kernel)
+    if (x.is_cuda and x.dtype == weight.dtype and x.dtype in (torch.float32, torch.float16)
+            and (bias is None or bias.dtype == weight.dtype) and NATIVE_AUTOGRAD):
+        _require()
+        return torch.ops.nbd.linear_ag(x, weight, bias, _LIB_PLAN)
+    import torch.nn.functional as F
+
+    return F.linear(x, weight, bias)

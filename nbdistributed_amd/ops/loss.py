@@ -47,14 +47,19 @@ def _xent_fn():
         the [N, V] gradient."""
 
         @staticmethod
-        def forward(ctx, h2, w, target, ignore_index, reduction):
+        def forward(ctx, h2, w, target, ignore_index, reduction, vocab):
             # vocabulary padded to a multiple of VOCAB_ALIGN for the three GEMMs (hipBLASLt: GPT-2's
             # 50257 -> 50304 takes the LM head from 2.18 to 1.75 ms per step, profiles/lmhead_r2.txt):
             # zero weight rows give exactly-zero pad logits, the loss reads only the first V columns
-            # (row stride Vp), so the pad columns stay 0 as gradients and dW's pad rows are dropped
-            V = w.shape[0]
-            Vp = -(-V // VOCAB_ALIGN) * VOCAB_ALIGN if V >= VOCAB_PAD_MIN else V
-            if Vp != V:
+            # (row stride Vp), so the pad columns stay 0 as gradients and dW's pad rows are 0.
+            # A model whose table is already padded (GPT2: rows [vocab, Vp) kept at zero) passes
+            # `vocab` < w.shape[0] and nothing is copied; otherwise the padded copy is made here.
+            V = vocab if vocab > 0 else w.shape[0]
+            if V < w.shape[0]:
+                Vp = w.shape[0]
+            else:
+                Vp = -(-V // VOCAB_ALIGN) * VOCAB_ALIGN if V >= VOCAB_PAD_MIN else V
+            if Vp != w.shape[0]:
                 wp = torch.empty(Vp, w.shape[1], dtype=w.dtype, device=w.device)
                 wp[:V].copy_(w)
                 wp[V:].zero_()
@@ -67,17 +72,32 @@ def _xent_fn():
                 scale = torch.ones(1, dtype=torch.float32, device=h2.device)
             loss_rows, _ = torch.ops.nbd.xent_fused(logits_p[:, :V] if Vp != V else logits_p, target, ignore_index,
                                                     scale)
-            ctx.save_for_backward(h2, wp, logits_p)  # logits now hold d(loss)/d(logits) for grad_out = 1
-            ctx.V = V
+            # logits now hold d(loss)/d(logits) for grad_out = 1
+            ctx.save_for_backward(h2, wp, logits_p, w)
+            ctx.rows = w.shape[0]
+            ctx.copied = wp is not w
             return loss_rows.sum() * scale[0]
 
         @staticmethod
         def backward(ctx, grad):
-            h2, wp, dlogits = ctx.saved_tensors
+            from . import graddst
+
+            h2, wp, dlogits, w = ctx.saved_tensors
             g = grad.to(h2.dtype)
             dh = torch.mm(dlogits, wp).mul_(g) if ctx.needs_input_grad[0] else None
-            dw = torch.mm(dlogits.t(), h2 * g)[:ctx.V] if ctx.needs_input_grad[1] else None
-            return dh, dw, None, None, None
+            dw = None
+            if ctx.needs_input_grad[1]:
+                hg = h2 * g
+                dst, acc = graddst.claim(w) if not ctx.copied else (None, False)
+                if dst is not None:  # straight into the DDP bucket slice (graddst.py)
+                    if acc:
+                        dst.addmm_(dlogits.t(), hg)
+                    else:
+                        torch.mm(dlogits.t(), hg, out=dst)
+                    dw = graddst.hand_back(w, dst, acc)
+                else:
+                    dw = torch.mm(dlogits.t(), hg)[:ctx.rows]
+            return dh, dw, None, None, None, None
 
     _XentFn = (_FusedCrossEntropy, _LinearCrossEntropy)
     return _XentFn
@@ -109,11 +129,13 @@ VOCAB_ALIGN = max(1, int(os.environ.get("NBD_VOCAB_ALIGN", "128")))  # 1 = no pa
 VOCAB_PAD_MIN = 4096
 
 
-def linear_cross_entropy(h, weight, target, ignore_index: int = -100, reduction: str = "mean"):
+def linear_cross_entropy(h, weight, target, ignore_index: int = -100, reduction: str = "mean", vocab: int = -1):
     """``cross_entropy(h @ weight.T, target)`` for an LM head (``h`` [..., C], ``weight`` [V, C]) —
     the loss's forward and backward fused into one pass over the logits on the GPU path (bf16/fp16,
     V ≤ 65,536: one read and one in-place write of the [N, V] logits instead of two reads and a
-    write), the GEMMs on hipBLASLt.  The logits are not returned."""
+    write), the GEMMs on hipBLASLt.  The logits are not returned.  ``vocab`` < ``weight.shape[0]``:
+    the table's rows past ``vocab`` are zero padding (GPT2 keeps its tied table padded to a
+    multiple of 128) — the loss covers the first ``vocab`` classes only."""
     import torch
     import torch.nn.functional as F
 
@@ -121,9 +143,13 @@ def linear_cross_entropy(h, weight, target, ignore_index: int = -100, reduction:
         raise ValueError("linear_cross_entropy: reduction must be 'mean' or 'sum'")
     h2 = h.reshape(-1, h.shape[-1])
     tgt = target.reshape(-1)
+    V = vocab if 0 < vocab < weight.shape[0] else weight.shape[0]
     if not (h.is_cuda and h.dtype in (torch.bfloat16, torch.float16) and weight.dtype == h.dtype
             and weight.shape[0] <= FUSED_MAX_VOCAB and not torch.is_autocast_enabled()):
-        return F.cross_entropy(F.linear(h2, weight).float(), tgt, ignore_index=ignore_index, reduction=reduction)
+        logits = F.linear(h2, weight)
+        if V < weight.shape[0]:
+            logits = logits[:, :V]
+        return F.cross_entropy(logits.float(), tgt, ignore_index=ignore_index, reduction=reduction)
     _require()
     return _xent_fn()[1].apply(h2 if h2.is_contiguous() else h2.contiguous(), weight, tgt.contiguous().long(),
-                               int(ignore_index), reduction)
+                               int(ignore_index), reduction, int(V))

@@ -31,6 +31,18 @@ designed for MI355X + RCCL over xGMI:
   wire as the all-reduce (RCCL's ring all-reduce IS a reduce-scatter + all-gather), 1/world of
   the optimizer work and state.
 
+Gradients as bucket views (``grad_views``, on by default on the GPU when a bucket's dtype is its
+parameters' dtype): every parameter's bucket slice is registered as its gradient's home
+(``ops.graddst``).  The framework's backward nodes — the C++ Linear / MLP nodes (weight and bias
+gradients out of the GEMM epilogues, ``csrc/kernels/autograd.hip``), the LM head and the tied
+token embedding — write straight into it, and ``p.grad`` *is* the slice: no flatten copy before
+the all-reduce (which then averages with ``ReduceOp.AVG``) and no unflatten after it.  Plain
+``nn.Linear`` layers of the wrapped module are routed through the same C++ node
+(``fused_linear``).  Under ``no_sync()`` micro-batches accumulate in place: the GEMMs add into
+the slice in their epilogue (beta = 1) and the remaining gradients are pre-reduced into the
+bucket by K3 (``ops.prereduce_into_bucket``, fp32 accumulate) — no per-parameter autograd adds,
+and the last micro-batch's bucket is the whole local gradient.
+
 Also provides DDP communication hooks for stock ``torch.nn.parallel.DistributedDataParallel``
 (``bf16_compress_hook``) built on the same fused kernels.
 """
@@ -66,20 +78,32 @@ class _Bucket:
     grad_shard: Optional[torch.Tensor] = None
     gather_work: Any = None
     done: Any = None  # side-stream mode: event recorded after this bucket's collective
+    views: Optional[List[torch.Tensor]] = None  # grad_views: each parameter's gradient home
+    partial: bool = False  # no_sync: the bucket holds locally accumulated (unscaled) gradients
+    rest_grads: List[torch.Tensor] = field(default_factory=list)  # gradients not written in place
+    rest_offsets: List[int] = field(default_factory=list)
+    post_div: bool = False  # averaged after the collective (no ReduceOp.AVG on this backend)
 
 
 class DistributedDataParallel(torch.nn.Module):
     def __init__(self, module: torch.nn.Module, process_group=None, bucket_cap_mb: float = 64.0,
                  first_bucket_mb: float = 4.0, comm_dtype: Optional[torch.dtype] = None,
                  broadcast_buffers: bool = True, init_sync: bool = True, align: int = 64,
-                 flat_params: bool = False, grad_mode: str = "unflatten", shard: bool = False):
+                 flat_params: bool = False, grad_mode: str = "unflatten", shard: bool = False,
+                 grad_views: Optional[bool] = None, fused_linear: Optional[bool] = None,
+                 accumulate: str = "bucket"):
         """``flat_params``: re-home each bucket's parameters into one contiguous buffer (the
         nn.Parameters become views) so a flat optimizer (``nbdistributed_amd.optim.FlatAdamW``)
         can update a whole bucket in one pass.  ``grad_mode="bucket"``: leave the averaged
         gradients in the bucket buffers (no unflatten, ``p.grad`` released after the flatten) —
         only for optimizers that read the buckets (FlatAdamW).  ``shard=True``: ZeRO-2 —
         reduce-scatter the buckets, optimizer state and update on this rank's slice only (module
-        docstring); needs ``flat_params=True, grad_mode="bucket"``."""
+        docstring); needs ``flat_params=True, grad_mode="bucket"``.  ``grad_views`` (default: on
+        for GPU modules): gradients live in their bucket slices (module docstring);
+        ``fused_linear`` (default: = grad_views): route ``nn.Linear`` layers through the C++
+        Linear node so their gradients are written in place too.  ``accumulate``: where
+        ``no_sync()`` micro-batches accumulate — ``"bucket"`` (K3 pre-reduce into the bucket,
+        ``p.grad`` released; same-dtype buckets) or ``"grad"`` (in ``p.grad``, torch's semantics)."""
         super().__init__()
         self.module = module
         self.pg = process_group if process_group is not None else dist.group.WORLD
@@ -98,6 +122,10 @@ class DistributedDataParallel(torch.nn.Module):
         if shard and not (flat_params and grad_mode == "bucket"):
             raise ValueError("shard=True needs flat_params=True and grad_mode='bucket' (with FlatAdamW)")
         self.shard = shard
+        if accumulate not in ("bucket", "grad"):
+            raise ValueError("accumulate must be 'bucket' or 'grad'")
+        self.accumulate = accumulate
+        self._sync_pass = True
         self.rank = dist.get_rank(self.pg)
         self._require_sync = True
         self._in_backward = False
@@ -138,12 +166,67 @@ class DistributedDataParallel(torch.nn.Module):
             for b in self.buckets:
                 b.done = torch.cuda.Event()
 
+        # gradients as bucket views (module docstring): same-dtype buckets only (a cast needs a copy)
+        if grad_views is None:
+            grad_views = self.cuda
+        self.grad_views = bool(grad_views) and self.cuda
+        self._avg_ok = self.cuda and dist.get_backend(self.pg) in ("nccl", "rccl")
+        self._n_views = 0
+        if self.grad_views:
+            from ..ops import graddst
+
+            for b in self.buckets:
+                if any(p.dtype != b.buffer.dtype for p in b.params):
+                    continue
+                b.views = [b.buffer[o:o + p.numel()].view_as(p) for p, o in zip(b.params, b.offsets)]
+                for p, v in zip(b.params, b.views):
+                    graddst.register(p, v)
+                self._n_views += len(b.params)
+        self._patched: List[torch.nn.Module] = []
+        if (self.grad_views if fused_linear is None else fused_linear) and self._n_views:
+            self._patch_linears()
+
         self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in self.params]
         if init_sync and self.world > 1:
             self._broadcast_tensors([p.data for p in module.parameters()])
             self._broadcast_tensors(list(module.buffers()))
         self.stats = {"buckets": len(self.buckets), "bucket_numels": [b.numel for b in self.buckets],
-                      "comm_dtype": str(self.comm_dtype)}
+                      "comm_dtype": str(self.comm_dtype), "grad_views": self._n_views,
+                      "fused_linears": len(self._patched)}
+
+    # ------------------------------------------------------------------ gradients in place
+    def _patch_linears(self) -> None:
+        """Route every ``nn.Linear`` whose parameters have bucket views through the C++ Linear
+        autograd node (``torch.ops.nbd.linear_ag``), which writes dW / db into the views."""
+        import types
+
+        from ..ops import gemm as _gemm
+
+        viewed = {id(p) for b in self.buckets if b.views is not None for p in b.params}
+        for m in self.module.modules():
+            if type(m) is not torch.nn.Linear or id(m.weight) not in viewed:
+                continue
+            if m.bias is not None and id(m.bias) not in viewed:
+                continue
+            m.forward = types.MethodType(_fused_linear_forward, m)
+            self._patched.append(m)
+        if self._patched:
+            _gemm.native_available_or_raise()
+
+    def unpatch(self) -> None:
+        """Undo ``fused_linear`` and the gradient-destination registrations."""
+        for m in self._patched:
+            m.__dict__.pop("forward", None)
+        self._patched = []
+        if self._n_views:
+            from ..ops import graddst
+
+            for b in self.buckets:
+                if b.views is not None:
+                    for p in b.params:
+                        graddst.register(p, None)
+                    b.views = None
+            self._n_views = 0
 
     # ------------------------------------------------------------------ planning
     def _plan(self, cap_mb: float, first_mb: float, align: int) -> List[_Bucket]:
@@ -208,13 +291,18 @@ class DistributedDataParallel(torch.nn.Module):
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
             self._joined = True
 
-    def _reduce(self, b: _Bucket):
+    def _reduce(self, b: _Bucket, avg: bool = False):
+        op = dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
         if self.shard:  # ZeRO-2: this rank keeps the averaged gradient of its slice only
-            return dist.reduce_scatter_tensor(b.grad_shard, b.buffer, group=self.pg, async_op=True)
-        return dist.all_reduce(b.buffer, group=self.pg, async_op=True)
+            return dist.reduce_scatter_tensor(b.grad_shard, b.buffer, op=op, group=self.pg, async_op=True)
+        return dist.all_reduce(b.buffer, op=op, group=self.pg, async_op=True)
 
     # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
+        if self._n_views:
+            from ..ops import graddst
+
+            graddst.new_pass()  # each gradient home may be handed out once per backward
         if self.shard:
             # the updated parameter slices of the last step must be back on every rank.  (Per
             # module pre-forward waits would let the first layers start earlier, but the models'
@@ -239,6 +327,7 @@ class DistributedDataParallel(torch.nn.Module):
     # ------------------------------------------------------------------ backward hooks
     def _start_backward(self) -> None:
         self._in_backward = True
+        self._sync_pass = self._require_sync
         self._next_launch = 0
         # Under HIP-graph capture the collectives are issued from the capturing stream itself
         # (ProcessGroupNCCL's own stream becomes a parallel branch of the graph) and every wait
@@ -254,15 +343,54 @@ class DistributedDataParallel(torch.nn.Module):
         torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
 
     def _grad_ready(self, p: torch.nn.Parameter) -> None:
-        if not self._require_sync:
-            return
         if not self._in_backward:
             self._start_backward()
         b = self._bucket_of[id(p)]
         b.pending -= 1
         if b.pending == 0:
             b.ready = True
-            self._launch_ready()
+            if self._sync_pass:
+                self._launch_ready()
+            else:
+                self._prereduce_local(b)
+
+    def _split_in_place(self, b: _Bucket):
+        """(#gradients already in their bucket slice, indices of the other parameters)."""
+        n_in, rest = 0, []
+        for i, p in enumerate(b.params):
+            g = p.grad
+            if b.views is not None and g is not None and g.data_ptr() == b.views[i].data_ptr():
+                n_in += 1
+            else:
+                rest.append(i)
+        return n_in, rest
+
+    def _local_home(self, b: _Bucket) -> bool:
+        """no_sync micro-batches accumulate in this bucket (K3) rather than in ``p.grad``: when its
+        dtype is the parameters' own (no precision lost against autograd's accumulation)."""
+        return self.accumulate == "bucket" and all(p.dtype == b.buffer.dtype for p in b.params)
+
+    def _prereduce_local(self, b: _Bucket) -> None:
+        """no_sync micro-batch: sum this bucket's new gradients into the bucket (K3, fp32
+        accumulate) and release them; gradients written in place already accumulated there."""
+        if not self._local_home(b):
+            return  # plain autograd accumulation into p.grad (torch semantics)
+        _, rest = self._split_in_place(b)
+        arrived = [i for i in rest if b.params[i].grad is not None]
+        if not b.partial:
+            # the first micro-batch defines the bucket: zero the slices of parameters that got no
+            # gradient, overwrite the others (in-place gradients were written by their GEMMs)
+            for i in rest:
+                if b.params[i].grad is None:
+                    o = b.offsets[i]
+                    b.buffer[o:o + b.params[i].numel()].zero_()
+            if arrived:
+                ops.bucket_flatten([b.params[i].grad for i in arrived], b.buffer, [b.offsets[i] for i in arrived])
+        elif arrived:
+            ops.prereduce_into_bucket([b.params[i].grad for i in arrived], b.buffer, [b.offsets[i] for i in arrived])
+        for i in arrived:
+            b.params[i].grad = None
+        b.partial = True
 
     def _launch_ready(self) -> None:
         while self._next_launch < len(self.buckets) and self.buckets[self._next_launch].ready:
@@ -278,8 +406,71 @@ class DistributedDataParallel(torch.nn.Module):
         return grads
 
     def _launch(self, b: _Bucket) -> None:
+        n_in, rest = self._split_in_place(b)
+        if n_in == 0 and not b.partial:
+            self._launch_flat(b)
+            return
+        # some gradients are already in their slices (bucket views), or the bucket holds the
+        # no_sync micro-batches' local sum: the rest are pre-reduced into the bucket unscaled and
+        # the collective averages (ReduceOp.AVG; a divide after it where the backend has no AVG)
+        grads = []
+        for i in rest:
+            p = b.params[i]
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            grads.append(p.grad)
+        offs = [b.offsets[i] for i in rest]
+        b.rest_grads, b.rest_offsets = grads, offs
+        avg = self._avg_ok
+        b.post_div = not avg and self.world > 1
+        unflatten = self.grad_mode == "unflatten"
+
+        def pre():
+            if grads:
+                ops.bucket_flatten(grads, b.buffer, offs, scale=1.0, accumulate=b.partial)
+
+        def post():
+            if b.post_div:
+                (b.grad_shard if self.shard else b.buffer).div_(self.world)
+            if unflatten and grads:
+                ops.bucket_unflatten(b.buffer, grads, offs)
+
+        if self.cuda and self._capturing:
+            pre()
+            b.work = self._reduce(b, avg)  # waited (and post-processed) in _finalize
+        elif self.cuda and not self._side:
+            pre()
+            self._reduce(b, avg).wait()
+            post()
+            b.work = None
+        elif self.cuda:
+            cur = torch.cuda.current_stream(self.device)
+            self.comm_stream.wait_stream(cur)
+            with torch.cuda.stream(self.comm_stream):
+                pre()
+                self._reduce(b, avg).wait()
+                post()
+                if self._per_bucket_wait:
+                    b.done.record(self.comm_stream)
+            for g in grads:
+                g.record_stream(self.comm_stream)
+        else:
+            pre()
+            b.work = self._reduce(b, avg)
+        b.partial = False
+        if not unflatten:
+            for p in b.params:
+                p.grad = None
+            if not self.cuda:
+                b.rest_grads = []
+        b.launched = True
+
+    def _launch_flat(self, b: _Bucket) -> None:
+        """No gradient in place: flatten (pre-divided by the world size) -> all-reduce SUM ->
+        unflatten."""
         grads = self._bucket_grads(b)
         b.grads = grads
+        b.rest_grads, b.rest_offsets, b.post_div = [], [], False
         scale = 1.0 / self.world
         unflatten = self.grad_mode == "unflatten"
         if self.cuda and self._capturing:
@@ -318,6 +509,12 @@ class DistributedDataParallel(torch.nn.Module):
         b.launched = True
 
     def _finalize(self) -> None:
+        if not self._sync_pass:  # no_sync micro-batch: buckets hold the local sums, nothing to send
+            for b in self.buckets:
+                if not b.ready and b.pending < len(b.params):
+                    self._prereduce_local(b)  # (some parameters of it got no gradient)
+            self._in_backward = False
+            return
         # buckets whose params got no gradient this step (unused parameters): zeros
         for b in self.buckets:
             if not b.ready:
@@ -331,16 +528,33 @@ class DistributedDataParallel(torch.nn.Module):
             for b in self.buckets:
                 if b.work is not None:
                     b.work.wait()
+                    if b.post_div:
+                        (b.grad_shard if self.shard else b.buffer).div_(self.world)
                     if self.grad_mode == "unflatten":
-                        ops.bucket_unflatten(b.buffer, b.grads, b.offsets)
+                        if b.grads:
+                            ops.bucket_unflatten(b.buffer, b.grads, b.offsets)
+                        elif b.rest_grads:
+                            ops.bucket_unflatten(b.buffer, b.rest_grads, b.rest_offsets)
         for b in self.buckets:
             b.grads = []
+            b.rest_grads, b.rest_offsets = [], []
             b.work = None
         self._in_backward = False
 
     # ------------------------------------------------------------------ broadcast
     def _broadcast_tensors(self, tensors: List[torch.Tensor]) -> None:
         broadcast_tensors(tensors, src=0, group=self.pg)
+
+
+def _fused_linear_forward(self, x):
+    """``nn.Linear.forward`` through the C++ Linear node (``torch.ops.nbd.linear_ag``): same
+    math (bf16: the HIP GEMMs; fp32 / fp16: the library GEMMs), with dW / db written straight into
+    the DDP bucket slices (``ops.graddst``).  Autocast and CPU inputs keep the stock path."""
+    if not x.is_cuda or torch.is_autocast_enabled() or x.dtype != self.weight.dtype:
+        return torch.nn.functional.linear(x, self.weight, self.bias)
+    from ..ops import gemm as _gemm
+
+    return _gemm.linear_any(x, self.weight, self.bias)
 
 
 def broadcast_tensors(tensors: List[torch.Tensor], src: int = 0, group=None, coalesce_max_bytes: int = 4 << 20) -> None:
