@@ -36,7 +36,8 @@ def _xent_fn():
         def backward(ctx, grad):
             logits, target, lse, denom = ctx.saved_tensors
             scale = (grad.float() / denom).reshape(1)
-            dlogits = logits if ctx.inplace else torch.empty_like(logits)
+            dlogits = logits if ctx.inplace else torch.empty_strided(logits.shape, logits.stride(), dtype=logits.dtype,
+                                                                             device=logits.device)
             torch.ops.nbd.xent_bwd(logits, target, lse, scale, ctx.ignore_index, dlogits)
             return dlogits, None, None, None, None
 

@@ -81,7 +81,7 @@ class FlatAdamW(torch.optim.Optimizer):
             ops.adamw_flat(self._grad(b), self._param_slice(b), st["master"], st["exp_avg"], st["exp_avg_sq"], g["lr"],
                            b1, b2, g["eps"], g["weight_decay"], max(self.step_count, 1), grad_scale_t=self._clip_coef,
                            step_t=self.step_t, lr_t=self.lr_t)
-            if self.sharded:  # rebuild the full bucket from every rank's updated slice
+            if self.sharded and self.ddp.world > 1:  # rebuild the full bucket from every rank's updated slice
                 b.gather_work = dist.all_gather_into_tensor(b.param_flat, self._param_slice(b), group=self.ddp.pg,
                                                             async_op=True)
         if self.sharded and _capturing():
@@ -142,5 +142,5 @@ class FlatAdamW(torch.optim.Optimizer):
                 st[k].copy_(src[k])
         for b, st in zip(self.ddp.buckets, self.flat_state):
             self._param_slice(b).copy_(st["master"].to(b.param_flat.dtype))
-            if self.sharded:
+            if self.sharded and self.ddp.world > 1:
                 dist.all_gather_into_tensor(b.param_flat, self._param_slice(b), group=self.ddp.pg)

@@ -85,6 +85,19 @@ class _Bucket:
     post_div: bool = False  # averaged after the collective (no ReduceOp.AVG on this backend)
 
 
+class _Done:
+    """A collective that had nothing to do (world size 1)."""
+
+    def wait(self, timeout=None) -> bool:
+        return True
+
+    def is_completed(self) -> bool:
+        return True
+
+
+_DONE = _Done()
+
+
 class DistributedDataParallel(torch.nn.Module):
     def __init__(self, module: torch.nn.Module, process_group=None, bucket_cap_mb: float = 64.0,
                  first_bucket_mb: float = 4.0, comm_dtype: Optional[torch.dtype] = None,
@@ -149,8 +162,12 @@ class DistributedDataParallel(torch.nn.Module):
                 b.numel = (b.numel + q - 1) // q * q
                 b.shard = b.numel // self.world
                 b.lo = self.rank * b.shard
-                b.grad_shard = torch.zeros(b.shard, dtype=self.comm_dtype, device=self.device)
             b.buffer = torch.zeros(b.numel, dtype=self.comm_dtype, device=self.device)
+            if shard:
+                # this rank's slice of the bucket itself: the reduce-scatter runs in place
+                # (recv = send + rank·count), no second buffer, and at world 1 it is the whole
+                # bucket with nothing to send
+                b.grad_shard = b.buffer[b.lo:b.lo + b.shard]
             for p in b.params:
                 self._bucket_of[id(p)] = b
         if flat_params:
@@ -292,6 +309,8 @@ class DistributedDataParallel(torch.nn.Module):
             self._joined = True
 
     def _reduce(self, b: _Bucket, avg: bool = False):
+        if self.world == 1 and self.shard:
+            return _DONE  # the slice is the bucket: nothing to scatter (and nothing to gather back)
         op = dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
         if self.shard:  # ZeRO-2: this rank keeps the averaged gradient of its slice only
             return dist.reduce_scatter_tensor(b.grad_shard, b.buffer, op=op, group=self.pg, async_op=True)
