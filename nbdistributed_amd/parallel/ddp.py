@@ -309,8 +309,11 @@ class DistributedDataParallel(torch.nn.Module):
             self._joined = True
 
     def _reduce(self, b: _Bucket, avg: bool = False):
-        if self.world == 1 and self.shard:
-            return _DONE  # the slice is the bucket: nothing to scatter (and nothing to gather back)
+        if self.world == 1:
+            # nothing to exchange (and for ZeRO the slice is the whole bucket).  Not even a no-op
+            # launch: RCCL runs a one-rank ReduceOp.AVG as a full pre-multiply pass over the bucket
+            # (oneRankReduce<FuncPreMulSum>: 190 µs per 48 MB bucket, profiles/gpt2_graph_prof_r3*.md)
+            return _DONE
         op = dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
         if self.shard:  # ZeRO-2: this rank keeps the averaged gradient of its slice only
             return dist.reduce_scatter_tensor(b.grad_shard, b.buffer, op=op, group=self.pg, async_op=True)
