@@ -42,6 +42,7 @@
 #include <torch/library.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "gemm_common.h"
@@ -51,12 +52,15 @@ namespace gemm {
 
 constexpr int NT = 256;
 
+// STAGES >= 100: the ping-pong schedule (gemm_body, below) with a ring of STAGES - 100 buffers
+constexpr int ring_of(int stages) { return stages >= 100 ? stages - 100 : stages; }
+
 template <int BM, int BN, int STAGES, int KS = 1>
 struct Smem {
   static constexpr int BUF = (BM + BN) * BK * 2;      // one A + B K-tile pair
   static constexpr int LDC = BN + 4;                  // fp32 C-tile row stride (+16 B: rows hit distinct banks)
   static constexpr int CT = BM * LDC * 4 + BM * 4;    // fp32 C tile (+ row-sum scratch), reuses the operand buffers
-  static constexpr int PIPE = KS * STAGES * BUF;      // one pipeline per K-split group
+  static constexpr int PIPE = KS * ring_of(STAGES) * BUF;  // one pipeline per K-split group
   static constexpr int BYTES = PIPE > CT ? PIPE : CT;
 };
 
@@ -95,7 +99,7 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
   const int lane = threadIdx.x & 63, wave_all = threadIdx.x >> 6;
   const int kg = wave_all / W, wave = wave_all % W;  // K-split group, wave within the group
   const int wm = wave / WN, wn = wave % WN;
-  uint8_t* smem = smem_all + kg * (STAGES * BUF);   // this group's pipeline buffers
+  uint8_t* smem = smem_all + kg * (ring_of(STAGES) * BUF);  // this group's pipeline buffers
 
   int tm, tn;
   tile_coords<8>(p.tiles_m, p.tiles_n, tm, tn, bx);
@@ -151,7 +155,79 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
     pb.stage(B, p.ldb, EPI == EPI_SWIGLU ? n0 / 2 : n0, (t * KS + kg) * BK, buf + A_BYTES, wave);
   };
 
-  if constexpr (STAGES == 2) {
+  if constexpr (STAGES >= 100) {
+    // Ping-pong (cdna_hip_programming.md §5 256² template's staggered groups, MI355X_MICROARCH.md
+    // "Two waves per SIMD"), one 512-thread workgroup per CU: waves 0-3 (rows 0-63 of the tile)
+    // and 4-7 (rows 64-127) share the SIMDs pairwise (w, w+4) and run one barrier apart, so on
+    // every SIMD one wave issues its 16 MFMAs while its partner reads the next K-tile's
+    // fragments and issues its share of a DMA.  Per group and K-tile t:
+    //   R(t):  fragments of tile t -> registers; DMA of tile t+2 into the buffer tile t-1 used;
+    //          counted vmcnt retires tile t+1 (tile t+2 stays in flight); lgkmcnt(0)
+    //   s_barrier (A_t) — MFMA(t) at priority 1 — s_barrier (B_t)
+    // The lagging group's A_t is the leading group's B_t.  RAW: a wave's wait for tile t+1 comes
+    // before its A_t, and both groups read tile t+1 only after a barrier every wave passed after
+    // that wait.  WAR: tile t+2's DMA (issued in R(t), after the issuer's B_{t-1}) overwrites
+    // tile t-1, whose reads both groups retired before barriers at or before that B_{t-1}.
+    constexpr int S = ring_of(STAGES);
+    static_assert(S == 3 && W == 8 && KS == 1, "ping-pong: 3-buffer ring, 8 waves, no K-split groups");
+    const bool lag = __builtin_amdgcn_readfirstlane(threadIdx.x) >= NTW / 2;
+    stage_tile(0, smem);
+    if (nk > 1) {
+      stage_tile(1, smem + BUF);
+      wait_barrier<NPT>();  // tile 0 landed everywhere
+    } else {
+      wait_barrier<0>();
+    }
+    if (lag) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    s8v af[2][FM], bf[2][FN];
+    auto pp_step = [&](int t, auto cur_c) {
+      constexpr int CUR = decltype(cur_c)::value, NXT2 = (CUR + 2) % S;
+      const uint8_t* cur = smem + CUR * BUF;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int j = 0; j < FM; ++j) af[kk][j] = frag<BM, A_KM>(cur, wm * (BM / WM) + 16 * j, kk, lane);
+#pragma unroll
+        for (int i = 0; i < FN; ++i) bf[kk][i] = frag<BN, B_KN>(cur + A_BYTES, wn * (BN / WN) + 16 * i, kk, lane);
+      }
+      if (t + 2 < nk) {
+        stage_tile(t + 2, smem + NXT2 * BUF);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPT) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[kk][i], af[kk][j], acc[i][j], 0, 0, 0);
+        if constexpr (ROWSUM) {
+          if (do_rs) {
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+              accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[kk][j], accb[j], 0, 0, 0);
+          }
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    for (int t = 0; t < nk; t += S) {
+      pp_step(t, std::integral_constant<int, 0>{});
+      if (t + 1 < nk) pp_step(t + 1, std::integral_constant<int, 1>{});
+      if (t + 2 < nk) pp_step(t + 2, std::integral_constant<int, 2>{});
+    }
+    if (!lag) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else if constexpr (STAGES == 2) {
     stage_tile(0, smem);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -385,7 +461,7 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
 // shapes such as SmolLM2's).  nb1 is rounded up to a multiple of 8 so each half's block ids keep
 // the XCD mapping.
 template <int BM, int BN, int W, int STAGES, int EPI1, int EPI2>
-__global__ __launch_bounds__(64 * W, 2) void pair_kernel(Args p1, int t1, int nb1, Args p2, int t2, int s2) {
+__global__ __launch_bounds__(64 * W, W == 8 ? 2 : 2) void pair_kernel(Args p1, int t1, int nb1, Args p2, int t2, int s2) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<BM, BN, STAGES, 1>::BYTES];
   const int b = blockIdx.x;
   if (b < nb1) {
@@ -458,7 +534,8 @@ static void launch_epi(const Tile& t, const Args& a, dim3 grid, hipStream_t st) 
     if constexpr (!A_KM && !B_KN) NBD_GEMM_CASE(128, 96, 1)
   } while (0);
   if (t.bm == 128 && t.bn == 128 && t.waves == 8 && t.ks == 1) {  // 8 waves: 128x128 only
-    if (t.stages == 3) NBD_GEMM_K(128, 128, 3, 8, 1);
+    if (t.stages == 9) NBD_GEMM_K(128, 128, 103, 8, 1);  // ping-pong, 3-buffer ring
+    else if (t.stages == 3) NBD_GEMM_K(128, 128, 3, 8, 1);
     else NBD_GEMM_K(128, 128, 2, 8, 1);
     return;
   }
@@ -514,9 +591,12 @@ static bool tile_fits(const Tile& t, int M, int N) { return M % t.bm == 0 && N %
 static Tile pick_tile(int M, int N, int64_t tile_hint) {
   if (tile_hint > 0) {
     // hint = ks*10^8 + waves*10^7 + stages*10^6 + BM*1000 + BN (ks 0 -> 1, waves 0 -> 4, stages 0 -> 2)
+    // (stages digit 9: the ping-pong schedule with a 3-buffer ring, 128x128 / 8 waves)
     const int stg = (int)(tile_hint / 1000000 % 10), wv = (int)(tile_hint / 10000000 % 10);
     const int ks = (int)(tile_hint / 100000000);
     Tile t{(int)(tile_hint / 1000 % 1000), (int)(tile_hint % 1000), stg < 2 ? 2 : stg, wv == 8 ? 8 : 4, ks == 2 ? 2 : 1};
+    TORCH_CHECK(t.stages != 9 || (t.bm == 128 && t.bn == 128 && t.waves == 8 && t.ks == 1),
+                "nbd::gemm: the ping-pong schedule is built for 128x128 tiles with 8 waves");
     TORCH_CHECK(tile_fits(t, M, N), "nbd::gemm: tile ", t.bm, "x", t.bn, " does not divide ", M, "x", N);
     return t;
   }
@@ -707,9 +787,14 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(a1.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   const dim3 grid((unsigned)nblocks);
+  // NBD_GEMM_PAIR_PP=1: the 128x128 halves on the ping-pong schedule (one workgroup per CU)
+  const char* pp_env = std::getenv("NBD_GEMM_PAIR_PP");
+  const bool pp = pp_env != nullptr && pp_env[0] == '1';
   auto launch = [&](auto e1, auto e2) {
     constexpr int E1 = decltype(e1)::value, E2 = decltype(e2)::value;
-    if (big)
+    if (big && pp)
+      hipLaunchKernelGGL((pair_kernel<128, 128, 8, 103, E1, E2>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
+    else if (big)
       hipLaunchKernelGGL((pair_kernel<128, 128, 8, 2, E1, E2>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
     else
       hipLaunchKernelGGL((pair_kernel<64, 64, 4, 3, E1, E2>), grid, dim3(256), 0, st, p1, t1, nb1, p2, t2, S);

@@ -293,3 +293,47 @@ def test_gemm_pair_swiglu_backward(M, N, I):
     rel = lambda a, b: float((a.float() - b).abs().max() / b.abs().max())  # noqa: E731
     assert dgu.shape == (M, 2 * I) and rel(dgu, ref) < 2e-2
     assert rel(dw, dy.float().t() @ act.float()) < 1e-2 and db is None
+
+
+@pytest.mark.parametrize("layout", ["fwd", "dgrad", "wgrad"])
+@pytest.mark.parametrize("K", [64, 128, 192, 768])
+def test_gemm_ping_pong_schedule(layout, K):
+    """Tile code 89128128: 128x128, 8 waves, 3-buffer ring, staggered wave groups (one barrier
+    apart) — every ring phase (K = 1, 2, 3 and 12 K-tiles) against the fp32 reference."""
+    a_km, b_kn = {"fwd": (False, False), "dgrad": (False, True), "wgrad": (True, True)}[layout]
+    g = torch.Generator(device="cuda").manual_seed(K)
+    M, N = 256, 384
+    A = (torch.randn(*((K, M) if a_km else (M, K)), device="cuda", generator=g)).to(torch.bfloat16)
+    B = (torch.randn(*((K, N) if b_kn else (N, K)), device="cuda", generator=g)).to(torch.bfloat16)
+    ref = (A.float().t() if a_km else A.float()) @ (B.float() if b_kn else B.float().t())
+    out = G.matmul(A, B, a_km=a_km, b_kn=b_kn, tile=89128128, splits=1)
+    assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    if layout == "fwd":
+        bias = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
+        y, pre = G.matmul(A, B, bias=bias, epi=G.EPI_GELU, tile=89128128, splits=1)
+        rp = ref + bias.float()
+        assert (pre.float() - rp).abs().max().item() < 2e-2 * rp.abs().max().item()
+        ry = torch.nn.functional.gelu(rp, approximate="tanh")
+        assert (y.float() - ry).abs().max().item() < 2e-2 * ry.abs().max().item()
+    if layout == "wgrad":
+        c, rs = G.matmul(A, B, a_km=True, b_kn=True, epi=G.EPI_ROWSUM, tile=89128128, splits=1)
+        assert (rs.float() - A.float().sum(0)).abs().max().item() < 2e-2 * A.float().sum(0).abs().max().item()
+
+
+@pytest.mark.parametrize("dgelu", [False, True])
+def test_gemm_pair_ping_pong(dgelu, monkeypatch):
+    monkeypatch.setenv("NBD_GEMM_PAIR_PP", "1")
+    g = torch.Generator(device="cuda").manual_seed(3)
+    M, N, K = 1024, 384, 256
+    dy = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    aux = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16) if dgelu else None
+    dx, dw, db = G.backward_pair(dy, w, x, G.EPI_DGELU if dgelu else G.EPI_NONE, aux, True)
+    rdx = dy.float() @ w.float()
+    if dgelu:
+        rdx = G._dgelu_ref(rdx, aux)
+    rdw = dy.float().t() @ x.float()
+    assert (dx.float() - rdx.float()).abs().max().item() < 2e-2 * rdx.float().abs().max().item()
+    assert (dw.float() - rdw).abs().max().item() < 2e-2 * rdw.abs().max().item()
+    assert (db.float() - dy.float().sum(0)).abs().max().item() < 2e-2 * dy.float().sum(0).abs().max().item()
