@@ -246,41 +246,70 @@ struct ReduceArgs {
   const void* in[kMaxIn];
 };
 
-template <typename S, typename D>
+// One block per kChunk-element chunk (the block footprint the copy kernels measured best at,
+// copy_bw.hip) and kUnroll 16-B vectors per input per thread in flight before any add: a
+// grid-stride loop over 8-element vectors capped at 2048 blocks reached 4.5 TB/s (4 x bf16 ->
+// bf16, docs/FINDINGS.md §3); the inputs are streamed once (non-temporal loads), the output
+// written once (non-temporal for 16-bit types).
+template <typename S, typename D, int KT>  // KT >= k: the register image of the inputs in flight
 __global__ __launch_bounds__(kThreads) void prereduce_kernel(ReduceArgs a, int k, void* out_, int64_t n, float scale,
                                                              int aligned) {
   D* __restrict__ out = static_cast<D*>(out_);
-  const int64_t tid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int64_t nthreads = (int64_t)gridDim.x * kThreads;
+  const int64_t begin = (int64_t)blockIdx.x * kChunk;
+  const int64_t end = min(begin + kChunk, n);
   if (aligned) {
-    const int64_t nv = n / 8;
-    for (int64_t v = tid; v < nv; v += nthreads) {
-      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      // issue every input's load before the adds: k x 16-32 B in flight per lane
-      float x[kMaxIn][8];
+    constexpr int64_t stride = (int64_t)kThreads * 8;
+    int64_t i = begin + (int64_t)threadIdx.x * 8;
+    for (; i + (kUnroll - 1) * stride + 8 <= end; i += kUnroll * stride) {
+      float acc[kUnroll][8];
 #pragma unroll
-      for (int j = 0; j < kMaxIn; ++j)
-        if (j < k) load8<S>(static_cast<const S*>(a.in[j]) + v * 8, x[j]);
+      for (int u = 0; u < kUnroll; ++u)
 #pragma unroll
-      for (int j = 0; j < kMaxIn; ++j)
+        for (int e = 0; e < 8; ++e) acc[u][e] = 0.f;
+      // every input's loads for both vectors are issued before the adds
+      float x[KT][kUnroll][8];
+#pragma unroll
+      for (int j = 0; j < KT; ++j)
         if (j < k)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) acc[e] += x[j][e];
+          for (int u = 0; u < kUnroll; ++u) load8_nt<S>(static_cast<const S*>(a.in[j]) + i + u * stride, x[j][u]);
+#pragma unroll
+      for (int j = 0; j < KT; ++j)
+        if (j < k)
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[u][e] += x[j][u][e];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[u][e] *= scale;
+        if (sizeof(D) == 2) store8_nt<D>(out + i + u * stride, acc[u]);
+        else store8<D>(out + i + u * stride, acc[u]);
+      }
+    }
+    for (; i + 8 <= end; i += stride) {
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int j = 0; j < k; ++j) {
+        float x[8];
+        load8<S>(static_cast<const S*>(a.in[j]) + i, x);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += x[e];
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] *= scale;
-      if (sizeof(D) == 2) store8_nt<D>(out + v * 8, acc);
-      else store8<D>(out + v * 8, acc);
+      store8<D>(out + i, acc);
     }
-    for (int64_t i = nv * 8 + tid; i < n; i += nthreads) {
-      float s = 0.f;
-      for (int j = 0; j < k; ++j) s += Elem<S>::load(static_cast<const S*>(a.in[j]), i);
-      Elem<D>::store(out, i, s * scale);
+    for (int64_t t = i; t < end && t < i + 8; ++t) {  // < 8 trailing elements (last chunk only)
+      float v = 0.f;
+      for (int j = 0; j < k; ++j) v += Elem<S>::load(static_cast<const S*>(a.in[j]), t);
+      Elem<D>::store(out, t, v * scale);
     }
   } else {
-    for (int64_t i = tid; i < n; i += nthreads) {
-      float s = 0.f;
-      for (int j = 0; j < k; ++j) s += Elem<S>::load(static_cast<const S*>(a.in[j]), i);
-      Elem<D>::store(out, i, s * scale);
+    for (int64_t t = begin + threadIdx.x; t < end; t += kThreads) {
+      float v = 0.f;
+      for (int j = 0; j < k; ++j) v += Elem<S>::load(static_cast<const S*>(a.in[j]), t);
+      Elem<D>::store(out, t, v * scale);
     }
   }
 }
@@ -288,10 +317,13 @@ __global__ __launch_bounds__(kThreads) void prereduce_kernel(ReduceArgs a, int k
 template <typename S, typename D>
 static void launch_prereduce(const ReduceArgs& a, int k, void* out, int64_t n, float scale, int aligned,
                              hipStream_t st) {
-  const int64_t work = aligned ? (n + 7) / 8 : n;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((work + kThreads - 1) / kThreads, 256 * 8));
-  hipLaunchKernelGGL((prereduce_kernel<S, D>), dim3((unsigned)blocks), dim3(kThreads), 0, st, a, k, out, n, scale,
-                     aligned);
+  const int64_t blocks = std::max<int64_t>(1, (n + kChunk - 1) / kChunk);
+  TORCH_CHECK(blocks < (1LL << 31), "local_prereduce: too many elements");
+  const dim3 g((unsigned)blocks), b(kThreads);
+  if (k <= 2) hipLaunchKernelGGL((prereduce_kernel<S, D, 2>), g, b, 0, st, a, k, out, n, scale, aligned);
+  else if (k <= 4) hipLaunchKernelGGL((prereduce_kernel<S, D, 4>), g, b, 0, st, a, k, out, n, scale, aligned);
+  else if (k <= 8) hipLaunchKernelGGL((prereduce_kernel<S, D, 8>), g, b, 0, st, a, k, out, n, scale, aligned);
+  else hipLaunchKernelGGL((prereduce_kernel<S, D, kMaxIn>), g, b, 0, st, a, k, out, n, scale, aligned);
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 

@@ -112,6 +112,35 @@ __device__ __forceinline__ void store8<f16_t>(f16_t* p, const float (&v)[8]) {
   *reinterpret_cast<u32x4*>(p) = w;
 }
 
+// non-temporal loads (a source streamed exactly once)
+template <typename T>
+__device__ __forceinline__ void load8_nt(const T* p, float (&v)[8]);
+template <>
+__device__ __forceinline__ void load8_nt<float>(const float* p, float (&v)[8]) {
+  const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+template <>
+__device__ __forceinline__ void load8_nt<bf16_t>(const bf16_t* p, float (&v)[8]) {
+  const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
+}
+template <>
+__device__ __forceinline__ void load8_nt<f16_t>(const f16_t* p, float (&v)[8]) {
+  const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = f16_to_f32((uint16_t)(w[j] & 0xffffu));
+    v[2 * j + 1] = f16_to_f32((uint16_t)(w[j] >> 16));
+  }
+}
+
 // non-temporal variants (streaming destination: measured +1-3 % on MI355X, copy_bw.hip)
 template <typename T>
 __device__ __forceinline__ void store8_nt(T* p, const float (&v)[8]);
