@@ -37,7 +37,6 @@
 #include <torch/library.h>
 
 #include <cmath>
-#include <cstdlib>
 #include <tuple>
 #include <type_traits>
 
@@ -620,33 +619,18 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
 
 // One launch for both backward passes: blocks [0, nkv) compute dK/dV, the rest dQ — the two
 // are independent, and for short sequences (SmolLM2: T = 128) neither fills the chip alone.
-// `interleave` (causal balance): block ids walk the weight classes heaviest first, each class
-// holding its dK/dV blocks (key block c: 2·(nblk − c) query tiles) and then its dQ blocks (query
-// block nblk − 1 − c: the same count of key tiles) — instead of every dK/dV block before every
-// dQ block, which leaves the heaviest dQ blocks to start last.
 template <bool CAUSAL, bool FD>
 __global__ __launch_bounds__(NT, 2) void bwd_kernel(View q, View k, View v, View dout, View out,
                                                      const float* __restrict__ lse,
                                                      const float* __restrict__ delta, MView dq, MView dk, MView dv,
                                                      int Hq, int Hkv, int T, int nblk, float sc2, float scale,
-                                                     int group, Rope rp, int nkv, int gsplit, int64_t split_stride,
-                                                     int interleave) {
-  const int nq = gridDim.x - nkv;
-  int kind, blk;
-  if (interleave) {
-    const int n1 = nkv / nblk, n2 = nq / nblk;
-    const int c = blockIdx.x / (n1 + n2), r = blockIdx.x % (n1 + n2);
-    kind = r < n1 ? 0 : 1;
-    blk = r < n1 ? c * n1 + r : c * n2 + (r - n1);
-  } else {
-    kind = (int)blockIdx.x < nkv ? 0 : 1;
-    blk = kind == 0 ? (int)blockIdx.x : (int)blockIdx.x - nkv;
-  }
-  if (kind == 0)
-    dkdv_body<CAUSAL, FD>(blk, nkv, q, k, v, dout, out, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale, group, rp,
+                                                     int group, Rope rp, int nkv, int gsplit, int64_t split_stride) {
+  if ((int)blockIdx.x < nkv)
+    dkdv_body<CAUSAL, FD>(blockIdx.x, nkv, q, k, v, dout, out, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale, group, rp,
                       gsplit, split_stride);
   else
-    dq_body<CAUSAL, FD>(blk, nq, q, k, v, dout, out, lse, delta, dq, Hq, T, nblk, sc2, scale, group, rp);
+    dq_body<CAUSAL, FD>(blockIdx.x - nkv, gridDim.x - nkv, q, k, v, dout, out, lse, delta, dq, Hq, T, nblk, sc2, scale,
+                    group, rp);
 }
 
 // dk/dv[b, h, t, :] = Σ_s part[s][b][h][t][:] (fp32 sum of the gsplit partials); 8 elements per thread
@@ -776,13 +760,10 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     dkw = MView{static_cast<uint16_t*>(pk.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
     dvw = MView{static_cast<uint16_t*>(pv.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
   }
-  // NBD_ATTN_BWD_ORDER=0: all dK/dV blocks before the dQ blocks (A/B); default interleaved
-  const char* ord = std::getenv("NBD_ATTN_BWD_ORDER");
-  const int interleave = (ord != nullptr && ord[0] == '0') ? 0 : 1;
 #define NBD_BWD(C_, F_)                                                                                      \
   hipLaunchKernelGGL((bwd_kernel<C_, F_>), dim3((unsigned)(nkv + nq)), dim3(NT), 0, st, qv, kv, vv, dov, ov,   \
                      lse.data_ptr<float>(), dptr, dqv, dkw, dvw, H, Hkv, T, nblk, sc2, (float)scale, group, rp, nkv, \
-                     gsplit, split_stride, interleave)
+                     gsplit, split_stride)
   if (causal) {
     if (fd) NBD_BWD(true, true);
     else NBD_BWD(true, false);
