@@ -90,8 +90,25 @@ def main():
             ts.append(s.elapsed_time(e) * 1e3)
         ts.sort()
         r4 = ts[len(ts) // 2]
+        # which cold operand costs: touch (read) W, h or both right before the GEMM
+        touched = {}
+        for name, pre in (("W", lambda: W.view(-1).max()), ("h", lambda: h.view(-1).max()),
+                          ("W+h", lambda: (W.view(-1).max(), h.view(-1).max()))):
+            tt = []
+            for _ in range(10):
+                g(x)
+                pre()
+                s, e = torch.cuda.Event(True), torch.cuda.Event(True)
+                s.record()
+                real()
+                e.record()
+                e.synchronize()
+                tt.append(s.elapsed_time(e) * 1e3)
+            tt.sort()
+            touched[name] = tt[len(tt) // 2]
         print(f"round {rnd}: random b2b {r1:.1f} us ({flops / r1 / 1e6:.0f} TF/s) | real b2b {r2:.1f} | real after "
-              f"20 graph steps {r3:.1f} | real between graph steps (median of 10) {r4:.1f} us", flush=True)
+              f"20 graph steps {r3:.1f} | real between graph steps (median of 10) {r4:.1f} us | after touching "
+              + ", ".join(f"{k} {v:.1f}" for k, v in touched.items()), flush=True)
     dist.destroy_process_group()
 
 
