@@ -43,7 +43,9 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
+#include <unordered_map>
 
 #include "gemm_common.h"
 
@@ -442,12 +444,41 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
   }
 }
 
+// Warm-up block r of P: one 4-byte load per 128-B line of its share of p.pf — the line lands in
+// the XCD's L2 and the MALL, which is all the next launch needs (its first round of workgroups
+// then hits the MALL instead of waiting on HBM for every K-tile).  Four lines per thread in
+// flight per iteration; the values only feed an empty asm, so nothing is stored.
+template <int NTH>
+__device__ __forceinline__ void warm_lines(const Args& p, int r, int P) {
+  const int64_t per = (p.pf_lines + P - 1) / P;
+  const int64_t lo = (int64_t)r * per, hi = min(p.pf_lines, lo + per);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(p.pf);
+  uint32_t x = 0;
+  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += 4 * NTH) {
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + (int64_t)u * NTH;
+      v[u] = i < hi ? q[i * 32] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x ^= v[u];
+  }
+  asm volatile("" ::"v"(x));
+}
+
 template <int BM, int BN, bool A_KM, bool B_KN, int EPI, int STAGES, int W, int KS>
 __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args p) {
   // one __shared__ array for everything (a second LDS object de-pipelines the glds loop:
   // cdna_hip_programming.md §5 "Projection GEMM" item 4a)
   __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<BM, BN, STAGES, KS>::BYTES];
-  gemm_body<BM, BN, A_KM, B_KN, EPI, STAGES, W, KS>(p, blockIdx.x, blockIdx.y, gridDim.y, smem_all);
+  // warm_blocks is a multiple of 8: the tile blocks keep their XCD (block id mod 8)
+  const int bx = (int)blockIdx.x - p.warm_blocks;
+  if (bx < 0) {
+    if (blockIdx.y == 0) warm_lines<64 * W * KS>(p, blockIdx.x, p.warm_blocks);
+    return;
+  }
+  gemm_body<BM, BN, A_KM, B_KN, EPI, STAGES, W, KS>(p, bx, blockIdx.y, gridDim.y, smem_all);
 }
 
 // A Linear layer's backward as one launch: blocks [0, nb1) compute the input gradient
@@ -463,7 +494,11 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
 template <int BM, int BN, int W, int STAGES, int EPI1, int EPI2>
 __global__ __launch_bounds__(64 * W, W == 8 ? 2 : 2) void pair_kernel(Args p1, int t1, int nb1, Args p2, int t2, int s2) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<BM, BN, STAGES, 1>::BYTES];
-  const int b = blockIdx.x;
+  const int b = (int)blockIdx.x - p1.warm_blocks;  // warm-up blocks first (gemm_kernel)
+  if (b < 0) {
+    warm_lines<64 * W>(p1, blockIdx.x, p1.warm_blocks);
+    return;
+  }
   if (b < nb1) {
     if (b >= t1) return;  // padding to the XCD boundary
     gemm_body<BM, BN, false, true, EPI1, STAGES, W, 1>(p1, b, 0, 1, smem_all);
@@ -584,6 +619,80 @@ static void launch_layout(int epi, const Tile& t, const Args& a, dim3 grid, hipS
   TORCH_CHECK(false, "nbd::gemm: epilogue ", epi, " not built for this layout");
 }
 
+// ---- next-weight warm-up -------------------------------------------------------------------------
+// Inside a training step a weight is cold when its product starts: the activations streamed since
+// its last use evicted it from the L2s and the MALL, and the first round of workgroups (all
+// reading the same weight panels) then waits on HBM for every K-tile.  Measured on the q|k|v
+// forward (8192x2304x768) right after a graphed GPT-2 step: 56 µs cold, 49.5 µs with the weight
+// touched beforehand, 46 µs with weight and input touched, 40-42 µs back to back
+// (benchmarks/gemm_context.py, profiles/gemm_context_r3.txt).  The launches therefore learn the
+// order in which weights are used — keyed by (weight address, direction): forward products
+// (B = W [N][K]) and backward ones (dgrad / pair, B = W as [K][N]) form two different chains —
+// and each launch's first workgroups touch the weight the NEXT launch used the previous time
+// round, so it arrives in the MALL while this product computes.  The weight is held weakly
+// through its storage and re-validated at every lookup: an entry whose storage was freed is
+// dropped, and only bytes inside a live storage are ever read.  NBD_GEMM_WARM=0 disables it.
+namespace warm {
+constexpr int64_t kCapBytes = 8 << 20;  // the first 8 MiB: a product's first-round panels
+struct Next {
+  c10::weak_intrusive_ptr<c10::StorageImpl> storage;
+  int64_t offset, bytes;
+};
+std::mutex g_mu;
+std::unordered_map<uintptr_t, Next> g_next;  // key: weight address | direction
+uintptr_t g_last[64] = {};                   // per device: the previous launch's key
+
+bool enabled() {
+  const char* e = std::getenv("NBD_GEMM_WARM");
+  return e == nullptr || e[0] != '0';
+}
+
+// Record `w` as the weight of this launch and return the next launch's weight to touch
+// (nullptr if none is known).
+const uint8_t* lookup(const at::Tensor& w, bool backward, int64_t& lines) {
+  lines = 0;
+  const int dev = w.get_device();
+  if (dev < 0 || dev >= 64 || !w.has_storage()) return nullptr;
+  const uintptr_t key = reinterpret_cast<uintptr_t>(w.data_ptr()) | (backward ? 1u : 0u);
+  std::lock_guard<std::mutex> lk(g_mu);
+  const uintptr_t prev = g_last[dev];
+  g_last[dev] = key;
+  if (prev != 0 && prev != key) {
+    if (g_next.size() > 4096) {  // forget dead weights (tests create many)
+      for (auto it = g_next.begin(); it != g_next.end();) it = it->second.storage.expired() ? g_next.erase(it) : ++it;
+    }
+    const at::Storage& s = w.storage();
+    const int64_t off = static_cast<const uint8_t*>(w.data_ptr()) - static_cast<const uint8_t*>(s.data());
+    g_next.insert_or_assign(prev, Next{s.getWeakStorageImpl(), off, (int64_t)w.numel() * (int64_t)w.element_size()});
+  }
+  auto it = g_next.find(key);
+  if (it == g_next.end()) return nullptr;
+  c10::intrusive_ptr<c10::StorageImpl> s = it->second.storage.lock();
+  if (!s) {
+    g_next.erase(it);
+    return nullptr;
+  }
+  const int64_t off = it->second.offset, bytes = std::min(it->second.bytes, kCapBytes);
+  if (s->device().index() != dev || off < 0 || off + bytes > (int64_t)s->nbytes() || s->data() == nullptr)
+    return nullptr;
+  const uint8_t* base = static_cast<const uint8_t*>(s->data()) + off;
+  // whole 128-B lines inside [base, base + bytes): the 4-byte load at each line start stays in bounds
+  const uintptr_t first = (reinterpret_cast<uintptr_t>(base) + 127) & ~uintptr_t(127);
+  const uintptr_t end = reinterpret_cast<uintptr_t>(base) + bytes;
+  if (end <= first) return nullptr;
+  lines = (int64_t)((end - first) / 128);
+  return lines > 0 ? reinterpret_cast<const uint8_t*>(first) : nullptr;
+}
+
+// warm-up blocks for `lines` lines at `nth` threads per block: ~4 lines per thread, a multiple of
+// 8 (block ids keep their XCD), at most 64
+int blocks_for(int64_t lines, int nth) {
+  if (lines <= 0) return 0;
+  const int64_t b = (lines + 4LL * nth - 1) / (4LL * nth);
+  return (int)std::min<int64_t>(64, (b + 7) / 8 * 8);
+}
+}  // namespace warm
+
 static bool tile_fits(const Tile& t, int M, int N) { return M % t.bm == 0 && N % t.bn == 0; }
 
 // The largest tile that still gives about one workgroup per CU (256 CUs); a hint (BM*1000+BN)
@@ -690,7 +799,17 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   p.tiles_m = M / t.bm;
   p.tiles_n = N / t.bn;
   p.accum = (int)accum;
-  const dim3 grid(tiles, S);
+  p.pf = nullptr;
+  p.pf_lines = 0;
+  p.warm_blocks = 0;
+  if (!a_km && warm::enabled()) {  // B is a weight (forward / dgrad), not an activation (wgrad)
+    const uint8_t* pf = warm::lookup(b, b_kn, p.pf_lines);
+    if (pf != nullptr && t.bm != 256) {  // (the 256x256 kernel has no warm-up blocks)
+      p.pf = pf;
+      p.warm_blocks = warm::blocks_for(p.pf_lines, 64 * t.waves * t.ks);
+    }
+  }
+  const dim3 grid(tiles + p.warm_blocks, S);
   p.c = static_cast<uint16_t*>(c.data_ptr());
   at::Tensor ws;
   p.ws = nullptr;
@@ -782,7 +901,14 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   }
   const int t1 = p1.tiles_m * p1.tiles_n, t2 = p2.tiles_m * p2.tiles_n;
   const int nb1 = (t1 + 7) / 8 * 8;
-  const int64_t nblocks = (int64_t)nb1 + (int64_t)t2 * S;
+  if (warm::enabled()) {  // b1 = W: the backward chain (next-weight warm-up, above)
+    const uint8_t* pf = warm::lookup(b1, true, p1.pf_lines);
+    if (pf != nullptr) {
+      p1.pf = pf;
+      p1.warm_blocks = warm::blocks_for(p1.pf_lines, big ? 512 : 256);
+    }
+  }
+  const int64_t nblocks = (int64_t)p1.warm_blocks + nb1 + (int64_t)t2 * S;
   TORCH_CHECK(nblocks < (1LL << 31), "nbd::gemm_pair: grid too large");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(a1.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();

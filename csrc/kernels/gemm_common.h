@@ -42,6 +42,11 @@ struct Args {
   int tiles_m, tiles_n;
   int accum;               // bit 0: c += result (EPI_NONE / EPI_ROWSUM); bit 1: aux_out row sums +=
                            // (gradient accumulation into a DDP bucket slice: graddst.h)
+  // weight warm-up (gemm.hip "next-weight warm-up"): blocks [0, warm_blocks) of the launch touch
+  // the pf_lines 128-B lines at pf (the next launch's weight) instead of computing a tile
+  const uint8_t* pf;
+  int64_t pf_lines;
+  int warm_blocks;
 };
 
 // ---- swizzles ---------------------------------------------------------------------------------
