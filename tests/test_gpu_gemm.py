@@ -337,3 +337,36 @@ def test_gemm_pair_ping_pong(dgelu, monkeypatch):
     assert (dx.float() - rdx.float()).abs().max().item() < 2e-2 * rdx.float().abs().max().item()
     assert (dw.float() - rdw).abs().max().item() < 2e-2 * rdw.abs().max().item()
     assert (db.float() - dy.float().sum(0)).abs().max().item() < 2e-2 * dy.float().sum(0).abs().max().item()
+
+
+def test_gemm_next_weight_warm_up(monkeypatch):
+    """The warm-up blocks (gemm.hip namespace warm) only read: results are bit-identical with and
+    without them, for learned forward / backward chains, weights that are views at odd offsets of
+    a larger storage, and after the next weight's storage was freed."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    M, K = 512, 384
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    flat = torch.randn(3 * 384 * K + 40, device="cuda", generator=g).to(torch.bfloat16)
+    w1 = flat[8:8 + 384 * K].view(384, K)  # 16-B aligned, not 128-B aligned
+    w2 = flat[8 + 384 * K:8 + 2 * 384 * K].view(384, K)
+    w3 = torch.randn(256, K, device="cuda", generator=g).to(torch.bfloat16)
+    dy = torch.randn(M, 384, device="cuda", generator=g).to(torch.bfloat16)
+
+    def seq():
+        out = [G.matmul(x, w, splits=1) for w in (w1, w2, w3)]
+        out += [G.matmul(dy, w, b_kn=True, splits=1) for w in (w2, w1)]
+        out += list(G.backward_pair(dy, w1, x, 0, None, True))
+        return out
+
+    monkeypatch.setenv("NBD_GEMM_WARM", "0")
+    ref = seq()
+    monkeypatch.setenv("NBD_GEMM_WARM", "1")
+    for _ in range(3):  # learn, then run with the warm-up blocks in place
+        got = seq()
+        torch.cuda.synchronize()
+        for r, o in zip(ref, got):
+            assert torch.equal(r, o)
+    del w3  # the entry pointing at w3's storage must be dropped, not read
+    torch.cuda.empty_cache()
+    assert torch.equal(G.matmul(x, w2, splits=1), ref[1])
+    torch.cuda.synchronize()
