@@ -157,13 +157,24 @@ constexpr float kKappa = 0.044715f;
 // made the fused epilogue cost as much as a separate elementwise pass)
 __device__ __forceinline__ float sig2(float u) { return __fdividef(1.f, 1.f + __expf(-2.f * u)); }
 __device__ __forceinline__ float sigm(float x) { return __fdividef(1.f, 1.f + __expf(-x)); }
+// The epilogue forms fold the constants: σ(2u) = 1 / (1 + 2^z), z = x·(c1 + c2·x²) with
+// c1 = −2β·log2(e), c2 = −2βκ·log2(e) — 5 VALU + v_exp_f32 + v_rcp_f32 per element (the plain
+// form above compiled to ~9 VALU + the two transcendentals; the GELU / GELU′ epilogues run 25 M
+// of them per c_fc product)
+constexpr float kLog2eF = 1.4426950408889634f;
+constexpr float kGc1 = -2.f * kBeta * kLog2eF, kGc2 = -2.f * kBeta * kKappa * kLog2eF;
+__device__ __forceinline__ float sig2_of(float x, float x2) {  // σ(2u(x)), x2 = x·x
+  const float z = x * fmaf(kGc2, x2, kGc1);
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z));
+}
 __device__ __forceinline__ float gelu_tanh(float x) {  // 0.5x(1 + tanh u) = x·σ(2u)
-  return x * sig2(kBeta * (x + kKappa * x * x * x));
+  return x * sig2_of(x, x * x);
 }
 __device__ __forceinline__ float dgelu_tanh(float x) {  // d gelu / dx = s + 2x·s(1−s)·β(1 + 3κx²), s = σ(2u)
   const float x2 = x * x;
-  const float s = sig2(kBeta * (x + kKappa * x2 * x));
-  return s + 2.f * x * s * (1.f - s) * kBeta * (1.f + 3.f * kKappa * x2);
+  const float s = sig2_of(x, x2);
+  const float w = x * fmaf(6.f * kBeta * kKappa, x2, 2.f * kBeta);  // 2xβ(1 + 3κx²)
+  return fmaf(w, s - s * s, s);
 }
 
 // XCD-aware bijective remap of blockIdx.x (cdna_hip_programming.md §5 "XCD swizzle must be
