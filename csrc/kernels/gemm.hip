@@ -285,6 +285,43 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
   }
 
   // ---- epilogue ------------------------------------------------------------------------------
+  constexpr int CPR = BN / 8;  // 8-column chunks per row
+  if constexpr (EPI == EPI_NONE && KS == 1) {
+    // A plain (+ bias) bf16 result with nothing to add to it: bias added and rounded to bf16 in
+    // registers (the one rounding the fp32 path does too), the bf16 tile staged through LDS —
+    // half the bytes of the fp32 image: 8-B ds_write_b64 at ≈85 B/clk instead of 64 KiB of
+    // ds_write_b128 at ≈79 B/clk per 128x128 tile (MI355X_MICROARCH.md LDS table).
+    if (S == 1 && !(p.accum & 1)) {
+      constexpr int LDB = BN + 8;  // bf16 row stride: 16 rows x 8 B of one write hit distinct banks
+      uint16_t* cb = reinterpret_cast<uint16_t*>(smem_all);
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int n = wn * (BN / WN) + 16 * i + 4 * (lane >> 4);
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (p.bias != nullptr) {
+          const uint2 w = *reinterpret_cast<const uint2*>(p.bias + n0 + n);
+          bv[0] = __uint_as_float(w.x << 16); bv[1] = __uint_as_float(w.x & 0xffff0000u);
+          bv[2] = __uint_as_float(w.y << 16); bv[3] = __uint_as_float(w.y & 0xffff0000u);
+        }
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          const int m = wm * (BM / WM) + 16 * j + (lane & 15);
+          const f4 v = acc[i][j];
+          uint2 w;
+          w.x = (uint32_t)f32_to_bf16(v[0] + bv[0]) | ((uint32_t)f32_to_bf16(v[1] + bv[1]) << 16);
+          w.y = (uint32_t)f32_to_bf16(v[2] + bv[2]) | ((uint32_t)f32_to_bf16(v[3] + bv[3]) << 16);
+          *reinterpret_cast<uint2*>(cb + m * LDB + n) = w;
+        }
+      }
+      __syncthreads();
+      for (int c = threadIdx.x; c < BM * CPR; c += NTW) {
+        const int r = c / CPR, cn = (c % CPR) * 8;
+        const uint4 v = *reinterpret_cast<const uint4*>(cb + r * LDB + cn);
+        *reinterpret_cast<uint4*>(p.c + (int64_t)(m0 + r) * p.ldc + n0 + cn) = v;
+      }
+      return;
+    }
+  }
   // The fp32 tile goes through LDS (the loop's last barrier retired every operand read) so the
   // global traffic is row-contiguous: each thread then owns 8 consecutive columns of a row —
   // 16-B bf16 stores / aux loads, 32-B fp32 slab stores.  acc[i][j] element e = C[m][n] with
@@ -325,7 +362,6 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
     __syncthreads();
   }
 
-  constexpr int CPR = BN / 8;  // 8-column chunks per row
   if constexpr (ROWSUM) {
     // lanes 0..15 hold row m = .. + lane in element 0 (all four elements are equal)
     if (do_rs && kg == 0 && lane < 16) {
