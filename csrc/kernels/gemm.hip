@@ -683,9 +683,10 @@ bool enabled() {
   return e == nullptr || e[0] != '0';
 }
 
-// Record `w` as the weight of this launch and return the next launch's weight to touch
-// (nullptr if none is known).
-const uint8_t* lookup(const at::Tensor& w, bool backward, int64_t& lines) {
+// Record `w` as the weight of this launch (or of a library product announced by
+// gemm_warm_hint; `cap` = how much of it the launch before may warm) and return the next
+// launch's weight to touch (nullptr if none is known).
+const uint8_t* lookup(const at::Tensor& w, bool backward, int64_t& lines, int64_t cap = kCapBytes) {
   lines = 0;
   const int dev = w.get_device();
   if (dev < 0 || dev >= 64 || !w.has_storage()) return nullptr;
@@ -699,7 +700,8 @@ const uint8_t* lookup(const at::Tensor& w, bool backward, int64_t& lines) {
     }
     const at::Storage& s = w.storage();
     const int64_t off = static_cast<const uint8_t*>(w.data_ptr()) - static_cast<const uint8_t*>(s.data());
-    g_next.insert_or_assign(prev, Next{s.getWeakStorageImpl(), off, (int64_t)w.numel() * (int64_t)w.element_size()});
+    const int64_t bytes = std::min<int64_t>((int64_t)w.numel() * (int64_t)w.element_size(), cap);
+    g_next.insert_or_assign(prev, Next{s.getWeakStorageImpl(), off, bytes});
   }
   auto it = g_next.find(key);
   if (it == g_next.end()) return nullptr;
@@ -708,7 +710,7 @@ const uint8_t* lookup(const at::Tensor& w, bool backward, int64_t& lines) {
     g_next.erase(it);
     return nullptr;
   }
-  const int64_t off = it->second.offset, bytes = std::min(it->second.bytes, kCapBytes);
+  const int64_t off = it->second.offset, bytes = it->second.bytes;
   if (s->device().index() != dev || off < 0 || off + bytes > (int64_t)s->nbytes() || s->data() == nullptr)
     return nullptr;
   const uint8_t* base = static_cast<const uint8_t*>(s->data()) + off;
@@ -720,14 +722,22 @@ const uint8_t* lookup(const at::Tensor& w, bool backward, int64_t& lines) {
   return lines > 0 ? reinterpret_cast<const uint8_t*>(first) : nullptr;
 }
 
-// warm-up blocks for `lines` lines at `nth` threads per block: ~4 lines per thread, a multiple of
-// 8 (block ids keep their XCD), at most 64
+// warm-up blocks for `lines` lines at `nth` threads per block: ~4 lines per thread per pass, a
+// multiple of 8 (block ids keep their XCD), at most 128 (a large weight takes several passes)
 int blocks_for(int64_t lines, int nth) {
   if (lines <= 0) return 0;
   const int64_t b = (lines + 4LL * nth - 1) / (4LL * nth);
-  return (int)std::min<int64_t>(64, (b + 7) / 8 * 8);
+  return (int)std::min<int64_t>(128, (b + 7) / 8 * 8);
 }
 }  // namespace warm
+
+// A library product (the LM head's hipBLASLt GEMMs) announces its weight: it joins the learned
+// order, so the HIP launch before it warms up to max_bytes of that weight.  Host-side only.
+void gemm_warm_hint(const at::Tensor& w, bool backward, int64_t max_bytes) {
+  if (!warm::enabled() || !w.is_cuda()) return;
+  int64_t lines = 0;
+  warm::lookup(w, backward, lines, std::max<int64_t>(0, max_bytes));
+}
 
 static bool tile_fits(const Tile& t, int M, int N) { return M % t.bm == 0 && N % t.bn == 0; }
 
@@ -990,4 +1000,9 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
 TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
   m.impl("gemm", &nbd::gemm::gemm_hip);
   m.impl("gemm_pair", &nbd::gemm::gemm_pair_hip);
+}
+
+// bookkeeping only (no device work): a catch-all kernel
+TORCH_LIBRARY_FRAGMENT(nbd, m) {
+  m.def("gemm_warm_hint(Tensor w, bool backward, int max_bytes) -> ()", &nbd::gemm::gemm_warm_hint);
 }

@@ -66,6 +66,11 @@ def _xent_fn():
                 wp[V:].zero_()
             else:
                 wp = w
+                # the table is cold here (the step's activations evicted it since the last
+                # step): the last HIP GEMM launch before this one warms it into the MALL
+                # (csrc/kernels/gemm.hip "next-weight warm-up"; docs/FINDINGS.md §23)
+                if LM_HEAD_WARM_BYTES > 0 and wp.is_cuda and hasattr(torch.ops.nbd, "gemm_warm_hint"):
+                    torch.ops.nbd.gemm_warm_hint(wp, False, LM_HEAD_WARM_BYTES)
             logits_p = torch.mm(h2, wp.t())
             if reduction == "mean":
                 scale = (1.0 / (target != ignore_index).sum().float()).reshape(1)  # inf (-> nan loss) if none
@@ -128,6 +133,11 @@ FUSED_MAX_VOCAB = 256 * 8 * 32  # xent_fused keeps a row in registers: 256 lanes
 # [V, C] weight copy costs one pass over it); the padded width must stay <= FUSED_MAX_VOCAB + 14
 VOCAB_ALIGN = max(1, int(os.environ.get("NBD_VOCAB_ALIGN", "128")))  # 1 = no padding (A/B)
 VOCAB_PAD_MIN = 4096
+# how much of the LM-head table the HIP GEMM launch before the head warms into the MALL
+# (opt-in, NBD_LM_HEAD_WARM_MB=96: measured no faster on the GPT-2 step,
+# profiles/lmhead_warm_ab_r3.txt — hipBLASLt's head is not first-touch bound the way the
+# short-K HIP GEMMs are)
+LM_HEAD_WARM_BYTES = int(float(os.environ.get("NBD_LM_HEAD_WARM_MB", "0")) * (1 << 20))
 
 
 def linear_cross_entropy(h, weight, target, ignore_index: int = -100, reduction: str = "mean", vocab: int = -1):
