@@ -36,7 +36,9 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <tuple>
 #include <type_traits>
 
@@ -657,6 +659,22 @@ __global__ __launch_bounds__(NT) void gqa_reduce_kernel(const uint16_t* __restri
 }
 
 // ============================================================================ host
+// Extra dynamic LDS per workgroup (bytes) from an environment variable, read once: caps the
+// workgroups resident per CU (160 KiB / (static + pad)) so that the hardware dispatcher, not
+// the initial placement, balances the causal grid's unequal workgroups (experiment knob).
+static int lds_pad(const char* name) {
+  const char* e = std::getenv(name);
+  return e == nullptr ? 0 : std::max(0, std::min(131072, std::atoi(e)));
+}
+static int fwd_pad() {
+  static const int v = lds_pad("NBD_ATTN_FWD_LDS_PAD");
+  return v;
+}
+static int bwd_pad() {
+  static const int v = lds_pad("NBD_ATTN_BWD_LDS_PAD");
+  return v;
+}
+
 static View view_of(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.size(3) == D && t.stride(3) == 1, "attn: ", name,
               " must be a [B, H, T, 64] GPU view with a contiguous last dim");
@@ -707,10 +725,10 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::T
   const float sc2 = (float)scale * kLog2e;
   const int group = H / (int)k.size(1);
   if (causal)
-    hipLaunchKernelGGL((fwd_kernel<true>), grid, dim3(NT), 0, st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
+    hipLaunchKernelGGL((fwd_kernel<true>), grid, dim3(NT), fwd_pad(), st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
                        sc2, group, rp);
   else
-    hipLaunchKernelGGL((fwd_kernel<false>), grid, dim3(NT), 0, st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
+    hipLaunchKernelGGL((fwd_kernel<false>), grid, dim3(NT), fwd_pad(), st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
                        sc2, group, rp);
   C10_HIP_KERNEL_LAUNCH_CHECK();
   return {o, lse};
@@ -761,7 +779,7 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     dvw = MView{static_cast<uint16_t*>(pv.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
   }
 #define NBD_BWD(C_, F_)                                                                                      \
-  hipLaunchKernelGGL((bwd_kernel<C_, F_>), dim3((unsigned)(nkv + nq)), dim3(NT), 0, st, qv, kv, vv, dov, ov,   \
+  hipLaunchKernelGGL((bwd_kernel<C_, F_>), dim3((unsigned)(nkv + nq)), dim3(NT), bwd_pad(), st, qv, kv, vv, dov, ov,   \
                      lse.data_ptr<float>(), dptr, dqv, dkw, dvw, H, Hkv, T, nblk, sc2, (float)scale, group, rp, nkv, \
                      gsplit, split_stride)
   if (causal) {

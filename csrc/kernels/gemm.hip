@@ -527,19 +527,28 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
 // interchangeable (128x128 / 8 waves / 2 stages; 64x64 / 4 waves / 3 stages for 64-granular
 // shapes such as SmolLM2's).  nb1 is rounded up to a multiple of 8 so each half's block ids keep
 // the XCD mapping.
+// `first` = blocks of the half dispatched first (rounded up to a multiple of 8 so each half's
+// block ids keep the XCD mapping); wfirst = 1 puts the weight-gradient units first.  The
+// dispatcher hands out blocks in id order as slots free up, so the half with the longer units
+// goes first (longest-processing-time order): a short-unit half dispatched first leaves the
+// long units as a serial tail once it drains (ops/gemm.py pair_plan).
 template <int BM, int BN, int W, int STAGES, int EPI1, int EPI2>
-__global__ __launch_bounds__(64 * W, W == 8 ? 2 : 2) void pair_kernel(Args p1, int t1, int nb1, Args p2, int t2, int s2) {
+__global__ __launch_bounds__(64 * W, W == 8 ? 2 : 2) void pair_kernel(Args p1, int t1, int first, Args p2, int t2, int s2,
+                                                                      int wfirst) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<BM, BN, STAGES, 1>::BYTES];
   const int b = (int)blockIdx.x - p1.warm_blocks;  // warm-up blocks first (gemm_kernel)
   if (b < 0) {
     warm_lines<64 * W>(p1, blockIdx.x, p1.warm_blocks);
     return;
   }
-  if (b < nb1) {
-    if (b >= t1) return;  // padding to the XCD boundary
-    gemm_body<BM, BN, false, true, EPI1, STAGES, W, 1>(p1, b, 0, 1, smem_all);
+  const bool dgrad = wfirst ? b >= first : b < first;
+  if (dgrad) {
+    const int l = wfirst ? b - first : b;
+    if (l >= t1) return;  // padding to the XCD boundary
+    gemm_body<BM, BN, false, true, EPI1, STAGES, W, 1>(p1, l, 0, 1, smem_all);
   } else {
-    const int l = b - nb1;
+    const int l = wfirst ? b : b - first;
+    if (l >= t2 * s2) return;
     gemm_body<BM, BN, true, true, EPI2, STAGES, W, 1>(p2, l % t2, l / t2, s2, smem_all);
   }
 }
@@ -906,7 +915,9 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   // product 2: wgrad layout
   const int K2 = a2.size(0), M2 = a2.size(1), N2 = b2.size(1);
   TORCH_CHECK(b2.size(0) == K2 && c2.size(0) == M2 && c2.size(1) == N2, "nbd::gemm_pair: product 2 shapes");
-  const int S = splits2 > 0 ? (int)splits2 : 1;
+  // splits2 = S | wfirst << 4 (the plan's encoding: ops/gemm.py pair_plan)
+  const int S = (splits2 & 15) > 0 ? (int)(splits2 & 15) : 1;
+  const int wfirst = (int)((splits2 >> 4) & 1);
   const bool big = M1 % 128 == 0 && N1 % 128 == 0 && M2 % 128 == 0 && N2 % 128 == 0;
   const int TB = big ? 128 : 64;
   TORCH_CHECK(M1 % TB == 0 && N1 % TB == 0 && M2 % TB == 0 && N2 % TB == 0 && K1 % BK == 0 && K1 > 0 &&
@@ -946,7 +957,8 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
     p2.ws = ws.data_ptr<float>();
   }
   const int t1 = p1.tiles_m * p1.tiles_n, t2 = p2.tiles_m * p2.tiles_n;
-  const int nb1 = (t1 + 7) / 8 * 8;
+  const int nb1 = (t1 + 7) / 8 * 8, nb2 = (t2 * S + 7) / 8 * 8;
+  const int first = wfirst ? nb2 : nb1;
   if (warm::enabled()) {  // b1 = W: the backward chain (next-weight warm-up, above)
     const uint8_t* pf = warm::lookup(b1, true, p1.pf_lines);
     if (pf != nullptr) {
@@ -954,7 +966,7 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
       p1.warm_blocks = warm::blocks_for(p1.pf_lines, big ? 512 : 256);
     }
   }
-  const int64_t nblocks = (int64_t)p1.warm_blocks + nb1 + (int64_t)t2 * S;
+  const int64_t nblocks = (int64_t)p1.warm_blocks + nb1 + nb2;
   TORCH_CHECK(nblocks < (1LL << 31), "nbd::gemm_pair: grid too large");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(a1.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
@@ -965,11 +977,11 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   auto launch = [&](auto e1, auto e2) {
     constexpr int E1 = decltype(e1)::value, E2 = decltype(e2)::value;
     if (big && pp)
-      hipLaunchKernelGGL((pair_kernel<128, 128, 8, 103, E1, E2>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
+      hipLaunchKernelGGL((pair_kernel<128, 128, 8, 103, E1, E2>), grid, dim3(512), 0, st, p1, t1, first, p2, t2, S, wfirst);
     else if (big)
-      hipLaunchKernelGGL((pair_kernel<128, 128, 8, 2, E1, E2>), grid, dim3(512), 0, st, p1, t1, nb1, p2, t2, S);
+      hipLaunchKernelGGL((pair_kernel<128, 128, 8, 2, E1, E2>), grid, dim3(512), 0, st, p1, t1, first, p2, t2, S, wfirst);
     else
-      hipLaunchKernelGGL((pair_kernel<64, 64, 4, 3, E1, E2>), grid, dim3(256), 0, st, p1, t1, nb1, p2, t2, S);
+      hipLaunchKernelGGL((pair_kernel<64, 64, 4, 3, E1, E2>), grid, dim3(256), 0, st, p1, t1, first, p2, t2, S, wfirst);
   };
   using I0 = std::integral_constant<int, EPI_NONE>;
   using I2 = std::integral_constant<int, EPI_DGELU>;

@@ -33,12 +33,88 @@ EPI_NONE, EPI_GELU, EPI_DGELU, EPI_ROWSUM, EPI_SWIGLU, EPI_DSWIGLU = 0, 1, 2, 3,
 
 def pair_splits(M2: int, N2: int, K2: int, tile: int = 128) -> int:
     """K splits of the weight-gradient half of a grouped backward launch: enough units to cover
-    the CUs (≥ 256 with the input-gradient tiles running alongside), each split ≥ 1024 deep."""
+    the CUs (≥ 256 with the input-gradient tiles running alongside), each split ≥ 1024 deep.
+    (The round-2 rule; ``pair_schedule`` below supersedes it for the launches.)"""
     t2 = (M2 // tile) * (N2 // tile)
     s = 1
     while t2 * s < PAIR_UNITS and s < 8 and K2 % (64 * 2 * s) == 0 and K2 // (2 * s) >= 1024:
         s *= 2
     return s
+
+
+# Grouped-backward dispatch model (pair_schedule): workgroup slots resident at once (2 per CU at
+# 128x128 / 8 waves — 68 KiB of LDS each; 3 at 64x64), per-unit cost in 64-deep K-steps plus a
+# fixed prologue/epilogue, a split-K unit's fp32 slab store, and the reduce kernel's HBM pass.
+_PAIR_SLOTS = {128: 512, 64: 768}
+_UNIT_OVERHEAD = 3.0   # K-steps: pipeline fill + epilogue of one tile
+_SLAB_OVERHEAD = 1.0   # K-steps: fp32 slab instead of a bf16 tile
+_STEP_US = 1.0         # ≈ µs per 128x128x64 K-step with two workgroups per CU (c_fc dgrad: 50.9 µs / 48)
+_HBM_BPUS = 5.0e6      # bytes per µs (reduce kernel)
+# NBD_GEMM_PAIR_SCHED="S:order" forces the split count and the order (0 = input gradient first,
+# 1 = weight gradient first) of every grouped launch; "legacy" = the round-2 rule (pair_splits,
+# input gradient first) — A/B measurements
+_SCHED_ENV = os.environ.get("NBD_GEMM_PAIR_SCHED", "")
+
+
+def _greedy_end(units, slots: int) -> float:
+    """Finish time of `units` (durations, in dispatch order) handed to the earliest-free slot."""
+    import heapq
+
+    h = [0.0] * slots
+    end = 0.0
+    for d in units:
+        t = heapq.heappop(h) + d
+        end = max(end, t)
+        heapq.heappush(h, t)
+    return end
+
+
+# Measured best schedules (S | wfirst << 4) of the workload's grouped launches, keyed by
+# (M, N, K, epi1) for dy [M, N], W [N, K] (benchmarks/pair_sched.py, profiles/pair_sched_r3.txt);
+# the model below covers other shapes (it picks these or schedules within 1-7 % of them)
+_PAIR_TUNED = {
+    (8192, 2304, 768, EPI_NONE): 2 | 16,   # gpt2.c_attn   74.0 us (round-2 rule S=4, input first: 79.0)
+    (8192, 768, 768, EPI_NONE): 8 | 16,    # gpt2.attn.c_proj 35.6 us (38.5)
+    (8192, 3072, 768, EPI_NONE): 4 | 16,   # gpt2.c_fc     92.5 us (S=2, input first: 102.8)
+    (8192, 768, 3072, EPI_DGELU): 2 | 16,  # gpt2.mlp.c_proj 98.9 us (110.7)
+    (2048, 960, 576, EPI_NONE): 2 | 16,    # smollm2.qkv   15.5 us (16.1)
+    (2048, 576, 576, EPI_NONE): 2 | 16,    # smollm2.o_proj 12.9 us (13.4)
+    (2048, 3072, 576, EPI_NONE): 1,        # smollm2.gate_up 25.0 us
+}
+
+
+def pair_schedule(M: int, N: int, K: int, tile: int = 128, epi1: int = EPI_NONE) -> int:
+    """Split count and dispatch order of the grouped backward launch for dy [M, N], W [N, K]
+    (dx = dy·W: (M/t)(K/t) units of N/64 K-steps; dW = dyᵀ·x: (N/t)(K/t)·S units of M/(64 S)),
+    encoded as S | wfirst << 4 (gemm.hip gemm_pair_hip).  The workgroup dispatcher hands out
+    blocks in id order as slots free up, so the finish time is the greedy list schedule of the
+    two halves: chosen by that model over S ∈ {1, 2, 4, 8} and both orders, plus the reduce
+    pass S > 1 costs; measured entries (``_PAIR_TUNED``) first.  GPT-2 small (8192 tokens): the
+    MLP pairs went from S = 2, input gradient first (a 48- or 12-step half, then 64-step
+    weight-gradient units as a serial tail) to weight gradient first (docs/FINDINGS.md §24)."""
+    if _SCHED_ENV == "legacy":
+        return pair_splits(N, K, M, tile)
+    if _SCHED_ENV:
+        s, o = (int(v) for v in _SCHED_ENV.split(":"))
+        return s | (o << 4)
+    hit = _PAIR_TUNED.get((M, N, K, epi1))
+    if hit is not None:
+        return hit
+    slots = _PAIR_SLOTS.get(tile, 512)
+    t1 = (M // tile) * (K // tile)
+    t2 = (N // tile) * (K // tile)
+    best = None
+    for s in (1, 2, 4, 8):
+        if M % (64 * s) or (s > 1 and M // s < 512):
+            continue
+        d1 = [N / 64 + _UNIT_OVERHEAD + (1.0 if epi1 != EPI_NONE else 0.0)] * t1
+        d2 = [M / 64 / s + _UNIT_OVERHEAD + (_SLAB_OVERHEAD if s > 1 else 0.0)] * (t2 * s)
+        red = (s * N * K * 4 + N * K * 2) / _HBM_BPUS / _STEP_US if s > 1 else 0.0
+        for order, units in ((0, d1 + d2), (1, d2 + d1)):
+            t = _greedy_end(units, slots) + red
+            if best is None or t < best[0] - 1e-9:
+                best = (t, s | (order << 4))
+    return best[1] if best else 1
 
 
 def backward_pair(dy2, w, x2, epi1: int = EPI_NONE, aux1=None, bias_grad: bool = False):
@@ -65,7 +141,7 @@ def backward_pair(dy2, w, x2, epi1: int = EPI_NONE, aux1=None, bias_grad: bool =
     dw = torch.empty(N, K, dtype=dy2.dtype, device=dy2.device)
     db = torch.empty(N, dtype=dy2.dtype, device=dy2.device) if bias_grad else None
     torch.ops.nbd.gemm_pair(dy2, w, dx, epi1, aux1, dy2, x2, dw, EPI_ROWSUM if bias_grad else EPI_NONE, db,
-                            pair_splits(N, K, M, tile))
+                            pair_schedule(M, N, K, tile, epi1))
     return dx, dw, db
 
 
@@ -390,13 +466,13 @@ def _prod(a_km: bool, b_kn: bool, M: int, N: int, K: int, epi: int = EPI_NONE, c
     return [1 if prefer_library(a_km, b_kn, M, N, K, epi) else 0, t, s]
 
 
-def _pair_plan(M: int, N: int, K: int) -> int:
-    """Split count of the grouped backward launch for dy [M, N], W [N, K] (``backward_pair``), or
-    -1 when the grouped launch is off."""
+def _pair_plan(M: int, N: int, K: int, epi1: int = EPI_NONE) -> int:
+    """Schedule (S | wfirst << 4) of the grouped backward launch for dy [M, N], W [N, K]
+    (``backward_pair``), or -1 when the grouped launch is off."""
     if not PAIR_BWD:
         return -1
     tile = 128 if M % 128 == 0 and N % 128 == 0 and K % 128 == 0 else 64
-    return pair_splits(N, K, M, tile)
+    return pair_schedule(M, N, K, tile, epi1)
 
 
 def native_plan(kind: str, M: int, H: int, I: int, bias1: bool = False, bias2: bool = False) -> list:
@@ -415,12 +491,12 @@ def native_plan(kind: str, M: int, H: int, I: int, bias1: bool = False, bias2: b
         p = (_prod(False, False, M, I, H, EPI_GELU, can_split=False) + _prod(False, False, M, H, I, can_split=not bias2)
              + _prod(False, True, M, I, H, EPI_DGELU, can_split=False) + _prod(True, True, H, I, M, R if bias2 else EPI_NONE)
              + _prod(False, True, M, H, I) + _prod(True, True, I, H, M, R if bias1 else EPI_NONE)
-             + [_pair_plan(M, H, I), _pair_plan(M, I, H)])
+             + [_pair_plan(M, H, I, EPI_DGELU), _pair_plan(M, I, H)])
     elif kind == "mlp_swiglu":
         p = (_prod(False, False, M, 2 * I, H, EPI_SWIGLU, can_split=False) + _prod(False, False, M, H, I)
              + _prod(False, True, M, I, H, EPI_DSWIGLU, can_split=False) + _prod(True, True, H, I, M)
              + _prod(False, True, M, H, 2 * I) + _prod(True, True, 2 * I, H, M)
-             + [_pair_plan(M, H, I), _pair_plan(M, 2 * I, H)])
+             + [_pair_plan(M, H, I, EPI_DSWIGLU), _pair_plan(M, 2 * I, H)])
     else:
         raise ValueError(kind)
     _PLANS[key] = p

@@ -276,6 +276,28 @@ def test_gemm_pair_matches_separate_products(dgelu, bias_grad, M, N, K):
         assert db is None
 
 
+@pytest.mark.parametrize("sched", [1 | 16, 2, 2 | 16, 4 | 16, 8, 8 | 16])
+@pytest.mark.parametrize("M,N,K", [(2048, 384, 640), (1024, 320, 192)])  # 128- and 64-tile kernels
+def test_gemm_pair_schedules(sched, M, N, K):
+    """Every split count / dispatch order of the grouped launch (S | wfirst << 4, including unit
+    counts that are not multiples of 8: 3x5x2 weight-gradient tiles) = the fp32 reference."""
+    from nbdistributed_amd.ops import gemm as G
+
+    g = torch.Generator(device="cuda").manual_seed(sched + M)
+    dy = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    pre = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    dx = torch.full((M, K), float("nan"), device="cuda", dtype=torch.bfloat16)
+    dw = torch.full((N, K), float("nan"), device="cuda", dtype=torch.bfloat16)
+    db = torch.full((N,), float("nan"), device="cuda", dtype=torch.bfloat16)
+    torch.ops.nbd.gemm_pair(dy, w, dx, G.EPI_DGELU, pre, dy, x, dw, G.EPI_ROWSUM, db, sched)
+    rel = lambda a, b: float((a.float() - b).abs().max() / b.abs().max())  # noqa: E731
+    assert rel(dx, G._dgelu_ref(dy.float() @ w.float(), pre).float()) < 1e-2
+    assert rel(dw, dy.float().t() @ x.float()) < 1e-2
+    assert rel(db, dy.float().sum(0)) < 1e-2
+
+
 @pytest.mark.parametrize("M,N,I", [(2048, 576, 1536), (1024, 512, 1024)])
 def test_gemm_pair_swiglu_backward(M, N, I):
     """Llama MLP backward through the grouped launch: d[g|u] (SwiGLU′ epilogue) + dW_down."""
