@@ -44,11 +44,14 @@ def _median_ms(fn, iters: int) -> float:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only", default="", help="comma-separated shape names")
     a = ap.parse_args()
     assert _lib.load_library(), _lib._load_error
     dev = torch.device("cuda")
     out = {"lib": os.environ.get("NBD_OPS_LIB", "in-tree")}
     for name, B, H, Hkv, T, causal in SHAPES:
+        if a.only and name not in a.only.split(","):
+            continue
         g = torch.Generator(device=dev).manual_seed(0)
         q = torch.randn(B, H, T, 64, device=dev, dtype=torch.bfloat16, generator=g)
         k, v = (torch.randn(B, Hkv, T, 64, device=dev, dtype=torch.bfloat16, generator=g) for _ in range(2))

@@ -48,7 +48,7 @@ def _xent_fn():
         the [N, V] gradient."""
 
         @staticmethod
-        def forward(ctx, h2, w, target, ignore_index, reduction, vocab):
+        def forward(ctx, h2, w, target, ignore_index, reduction, vocab, fuse_dgrad):
             # vocabulary padded to a multiple of VOCAB_ALIGN for the three GEMMs (hipBLASLt: GPT-2's
             # 50257 -> 50304 takes the LM head from 2.18 to 1.75 ms per step, profiles/lmhead_r2.txt):
             # zero weight rows give exactly-zero pad logits, the loss reads only the first V columns
@@ -71,15 +71,36 @@ def _xent_fn():
                 # (csrc/kernels/gemm.hip "next-weight warm-up"; docs/FINDINGS.md §23)
                 if LM_HEAD_WARM_BYTES > 0 and wp.is_cuda and hasattr(torch.ops.nbd, "gemm_warm_hint"):
                     torch.ops.nbd.gemm_warm_hint(wp, False, LM_HEAD_WARM_BYTES)
-            logits_p = torch.mm(h2, wp.t())
             if reduction == "mean":
                 scale = (1.0 / (target != ignore_index).sum().float()).reshape(1)  # inf (-> nan loss) if none
             else:
                 scale = torch.ones(1, dtype=torch.float32, device=h2.device)
-            loss_rows, _ = torch.ops.nbd.xent_fused(logits_p[:, :V] if Vp != V else logits_p, target, ignore_index,
-                                                    scale)
-            # logits now hold d(loss)/d(logits) for grad_out = 1
-            ctx.save_for_backward(h2, wp, logits_p, w)
+            N = h2.shape[0]
+            chunk = LM_HEAD_CHUNK if 0 < LM_HEAD_CHUNK < N else N
+            dh = None
+            if chunk == N:
+                logits_p = torch.mm(h2, wp.t())
+                loss_rows, _ = torch.ops.nbd.xent_fused(logits_p[:, :V] if Vp != V else logits_p, target,
+                                                        ignore_index, scale)
+            else:
+                # row chunks: each chunk's logits are written by its GEMM, turned into dlogits in
+                # place by xent_fused and (fuse_dgrad) read by the input-gradient GEMM while they
+                # are still in the MALL, instead of three HBM round trips of the whole [N, Vp]
+                logits_p = torch.empty(N, Vp, dtype=h2.dtype, device=h2.device)
+                loss_rows = torch.empty(N, dtype=torch.float32, device=h2.device)
+                if fuse_dgrad:
+                    dh = torch.empty_like(h2)
+                for r0 in range(0, N, chunk):
+                    r1 = min(N, r0 + chunk)
+                    lc = logits_p[r0:r1]
+                    torch.mm(h2[r0:r1], wp.t(), out=lc)
+                    lr, _ = torch.ops.nbd.xent_fused(lc[:, :V] if Vp != V else lc, target[r0:r1], ignore_index,
+                                                     scale)
+                    loss_rows[r0:r1] = lr
+                    if dh is not None:
+                        torch.mm(lc, wp, out=dh[r0:r1])
+            # logits now hold d(loss)/d(logits) for grad_out = 1 (and dh = dlogits·W, if fused)
+            ctx.save_for_backward(h2, wp, logits_p, w, dh)
             ctx.rows = w.shape[0]
             ctx.copied = wp is not w
             return loss_rows.sum() * scale[0]
@@ -88,9 +109,11 @@ def _xent_fn():
         def backward(ctx, grad):
             from . import graddst
 
-            h2, wp, dlogits, w = ctx.saved_tensors
+            h2, wp, dlogits, w, dh_fused = ctx.saved_tensors
             g = grad.to(h2.dtype)
-            dh = torch.mm(dlogits, wp).mul_(g) if ctx.needs_input_grad[0] else None
+            dh = None
+            if ctx.needs_input_grad[0]:
+                dh = dh_fused.mul_(g) if dh_fused is not None else torch.mm(dlogits, wp).mul_(g)
             dw = None
             if ctx.needs_input_grad[1]:
                 hg = h2 * g
@@ -103,7 +126,7 @@ def _xent_fn():
                     dw = graddst.hand_back(w, dst, acc)
                 else:
                     dw = torch.mm(dlogits.t(), hg)[:ctx.rows]
-            return dh, dw, None, None, None, None
+            return dh, dw, None, None, None, None, None
 
     _XentFn = (_FusedCrossEntropy, _LinearCrossEntropy)
     return _XentFn
@@ -138,6 +161,9 @@ VOCAB_PAD_MIN = 4096
 # profiles/lmhead_warm_ab_r3.txt — hipBLASLt's head is not first-touch bound the way the
 # short-K HIP GEMMs are)
 LM_HEAD_WARM_BYTES = int(float(os.environ.get("NBD_LM_HEAD_WARM_MB", "0")) * (1 << 20))
+# rows per LM-head chunk (0 = one [N, Vp] GEMM): GEMM -> in-place loss gradient -> input-gradient
+# GEMM per chunk, so a chunk's logits are re-read from the 256 MB MALL rather than from HBM
+LM_HEAD_CHUNK = int(os.environ.get("NBD_LMHEAD_CHUNK", "0"))
 
 
 def linear_cross_entropy(h, weight, target, ignore_index: int = -100, reduction: str = "mean", vocab: int = -1):
@@ -162,5 +188,6 @@ def linear_cross_entropy(h, weight, target, ignore_index: int = -100, reduction:
             logits = logits[:, :V]
         return F.cross_entropy(logits.float(), tgt, ignore_index=ignore_index, reduction=reduction)
     _require()
+    fuse_dgrad = torch.is_grad_enabled() and h.requires_grad
     return _xent_fn()[1].apply(h2 if h2.is_contiguous() else h2.contiguous(), weight, tgt.contiguous().long(),
-                               int(ignore_index), reduction, int(V))
+                               int(ignore_index), reduction, int(V), fuse_dgrad)

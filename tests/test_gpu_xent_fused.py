@@ -44,9 +44,15 @@ def test_xent_fused_op_matches_reference(dev, V, dtype):
     assert bool((work[::7] == 0).all())         # ignored rows: zero gradient
 
 
+@pytest.mark.parametrize("chunk", [0, 128, 200])
 @pytest.mark.parametrize("reduction", ["mean", "sum"])
 @pytest.mark.parametrize("V,C", [(50257, 768), (4000, 256)])
-def test_linear_cross_entropy_autograd(dev, reduction, V, C):
+def test_linear_cross_entropy_autograd(dev, reduction, V, C, chunk, monkeypatch):
+    """chunk > 0: the row-chunked head (GEMM -> in-place loss gradient -> input-gradient GEMM per
+    chunk; 200 leaves a ragged last chunk)."""
+    from nbdistributed_amd.ops import loss as L
+
+    monkeypatch.setattr(L, "LM_HEAD_CHUNK", chunk)
     torch.manual_seed(1)
     N = 512
     h = (torch.randn(N, C, device=dev) * 0.5).to(torch.bfloat16).requires_grad_()
