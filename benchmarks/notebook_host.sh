@@ -14,3 +14,4 @@ for e in NBD_GEMM_WARM=0; do
 done
 timeout -k 10 200 python benchmarks/host_profile.py --model smollm2 --steps 5 >> $o 2>&1
 timeout -k 10 200 python benchmarks/host_profile.py --model smollm2 --steps 5 --cprofile >> $o 2>&1
+bash benchmarks/prof_notebook.sh

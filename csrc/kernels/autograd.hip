@@ -50,6 +50,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rms_fwd_hip(const at::Tensor& x, 
 std::tuple<at::Tensor, at::Tensor> rms_bwd_hip(const at::Tensor& x, const at::Tensor& dy,
                                                const c10::optional<at::Tensor>& dres, const at::Tensor& weight,
                                                const at::Tensor& rstd);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_into(const at::Tensor& x, const at::Tensor& dy,
+                                                           const c10::optional<at::Tensor>& dres,
+                                                           const at::Tensor& weight, const at::Tensor& mean,
+                                                           const at::Tensor& rstd, const at::Tensor& dw_dst,
+                                                           const at::Tensor& db_dst, int accum);
+std::tuple<at::Tensor, at::Tensor> rms_bwd_into(const at::Tensor& x, const at::Tensor& dy,
+                                                const c10::optional<at::Tensor>& dres, const at::Tensor& weight,
+                                                const at::Tensor& rstd, const at::Tensor& dw_dst, int accum);
 }  // namespace norm
 namespace attn {
 std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
@@ -120,6 +128,9 @@ static std::pair<Tensor, Tensor> run(const Tensor& a, const Tensor& b, bool a_km
   if (epi == EPI_GELU) out = at::empty_like(c);
   if (epi == EPI_ROWSUM) out = rs_out.defined() && !(tmp_acc && (accum & 2)) ? rs_out.view({M}) : at::empty({M}, a.options());
   if (epi == EPI_SWIGLU) out = at::empty({M, N}, a.options());
+  // a deferred split-K reduce only when it writes the destinations themselves (not a temporary
+  // that is read right after)
+  const defer::Scope ds(defer::want() && !tmp_acc && c_out.defined() && (epi != EPI_ROWSUM || rs_out.defined()));
   gemm_hip(a, b, c, a_km, b_kn, bias, epi, aux, out.defined() ? optional<Tensor>(out) : c10::nullopt, p.splits,
            p.tile, tmp_acc ? 0 : accum);
   if (tmp_acc) {
@@ -163,6 +174,8 @@ static std::tuple<Tensor, Tensor, Tensor> pair(const Tensor& dy, const Tensor& w
   Tensor dx = at::empty({M, epi1 == EPI_DSWIGLU ? 2 * K : K}, dy.options());
   const GradOut dw = grad_out(w, true, {N, K}, dy.options());
   const GradOut db = grad_out(bparam, bias_grad, {N}, dy.options());
+  // every output of the split-K reduce is a bucket slice: it may be deferred (graddst.h)
+  const defer::Scope ds(dw.claimed && (!bias_grad || db.claimed));
   gemm_pair_hip(dy, w, dx, epi1, aux1, dy, x, dw.t.view({N, K}), bias_grad ? EPI_ROWSUM : EPI_NONE,
                 bias_grad ? optional<Tensor>(db.t.view({N})) : c10::nullopt, splits, dw.bit(1) | db.bit(2));
   return {dx, dw.done(), bias_grad ? db.done() : Tensor()};
@@ -174,6 +187,7 @@ static std::pair<Tensor, Tensor> wgrad(const Tensor& dy, const Tensor& x2, const
   const int64_t N = dy.size(1), K = x2.size(1);
   const GradOut dw = grad_out(w, true, {N, K}, dy.options());
   const GradOut db = grad_out(bparam, nb, {N}, dy.options());
+  const defer::Scope ds(dw.claimed && (!nb || db.claimed));
   run(dy, x2, true, true, prod(plan, pi), nb ? EPI_ROWSUM : EPI_NONE, c10::nullopt, c10::nullopt, dw.t,
       nb ? db.t : Tensor(), dw.bit(1) | db.bit(2));
   return {dw.done(), nb ? db.done() : Tensor()};
@@ -390,8 +404,12 @@ struct RMSFn : public torch::autograd::Function<RMSFn> {
     const bool add = ctx->saved_data["add"].toBool();
     const Tensor ds = add ? grads[0] : Tensor(), dy = add ? grads[1] : grads[0];
     if (!dy.defined()) return {ds, ds, Tensor(), Tensor()};
-    auto [dx, dw] = norm::rms_bwd_hip(sv[0], dy.contiguous(), opt(ds), sv[1], sv[2]);
-    return {dx, add ? dx : Tensor(), dw, Tensor()};
+    // dγ into its bucket slice when DDP registered one (graddst.h); the column sum may be deferred
+    const Tensor& w = sv[1];
+    const GradOut gw = grad_out(w, w.requires_grad(), w.sizes(), w.options());
+    const defer::Scope dsc(gw.claimed);
+    auto [dx, dw] = norm::rms_bwd_into(sv[0], dy.contiguous(), opt(ds), w, sv[2], gw.t, gw.bit(1));
+    return {dx, add ? dx : Tensor(), gw.t.defined() ? gw.done() : dw, Tensor()};
   }
 };
 
@@ -404,6 +422,7 @@ struct LNFn : public torch::autograd::Function<LNFn> {
     const bool add = delta.has_value();
     ctx->save_for_backward({add ? sum : x, w, mean, rstd});
     ctx->saved_data["add"] = add;
+    if (b.requires_grad()) ctx->saved_data["b"] = b;  // (identity only: its gradient's bucket slice)
     if (add) return {sum, y};
     return {y};
   }
@@ -413,8 +432,15 @@ struct LNFn : public torch::autograd::Function<LNFn> {
     const bool add = ctx->saved_data["add"].toBool();
     const Tensor ds = add ? grads[0] : Tensor(), dy = add ? grads[1] : grads[0];
     if (!dy.defined()) return {ds, ds, Tensor(), Tensor(), Tensor()};
-    auto [dx, dw, db] = norm::ln_bwd_hip(sv[0], dy.contiguous(), opt(ds), sv[1], sv[2], sv[3]);
-    return {dx, add ? dx : Tensor(), dw, db, Tensor()};
+    const Tensor& w = sv[1];
+    const GradOut gw = grad_out(w, w.requires_grad(), w.sizes(), w.options());
+    // the bias is not saved: its slice is looked up through the weight's node input (below)
+    const GradOut gb = grad_out(ctx->saved_data.count("b") ? ctx->saved_data["b"].toTensor() : Tensor(), true,
+                                w.sizes(), w.options());
+    const defer::Scope dsc(gw.claimed && gb.claimed);
+    auto [dx, dw, db] = norm::ln_bwd_into(sv[0], dy.contiguous(), opt(ds), w, sv[2], sv[3], gw.t, gb.t,
+                                          gw.bit(1) | gb.bit(2));
+    return {dx, add ? dx : Tensor(), gw.t.defined() ? gw.done() : dw, gb.t.defined() ? gb.done() : db, Tensor()};
   }
 };
 

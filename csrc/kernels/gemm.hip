@@ -42,12 +42,15 @@
 #include <torch/library.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <type_traits>
 #include <unordered_map>
+#include <vector>
 
 #include "gemm_common.h"
+#include "graddst.h"
 
 namespace nbd {
 namespace gemm {
@@ -581,6 +584,17 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ w
   }
 }
 
+// the split-K reduce of a product: queued when the caller's scope asks for it (a weight
+// gradient written into its claimed bucket slice, autograd.hip), else launched now
+static void splitk_reduce(const at::Tensor& ws, int S, int64_t n8, int64_t slab, uint16_t* out, int64_t m8,
+                          uint16_t* rs_out, int accum, hipStream_t st) {
+  if (defer::want() && defer::push_splitk(ws, S, n8, m8, slab, out, rs_out, accum, st)) return;
+  const int blocks = (int)std::min<int64_t>((n8 + m8 + 255) / 256, 2048);
+  hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, ws.data_ptr<float>(), S, n8, slab, out, m8,
+                     rs_out, accum);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
 // ---- host --------------------------------------------------------------------------------------
 struct Tile {
   int bm, bn, stages, waves, ks;
@@ -882,13 +896,9 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   else
     launch_layout<true, true>((int)epi, t, p, grid, st);
   C10_HIP_KERNEL_LAUNCH_CHECK();
-  if (S > 1) {
-    const int64_t n8 = (int64_t)M * N / 8, m8 = epi == EPI_ROWSUM ? M / 8 : 0;
-    const int blocks = (int)std::min<int64_t>((n8 + m8 + 255) / 256, 2048);
-    hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, p.ws, S, n8, (int64_t)M * N, p.c, m8, p.aux_out,
-                       p.accum);
-    C10_HIP_KERNEL_LAUNCH_CHECK();
-  }
+  if (S > 1)
+    splitk_reduce(ws, S, (int64_t)M * N / 8, (int64_t)M * N, p.c, epi == EPI_ROWSUM ? M / 8 : 0, p.aux_out, p.accum,
+                  st);
 }
 
 // A Linear layer's two backward products in one launch (pair_kernel): c1 = a1·b1 in the dgrad
@@ -997,13 +1007,9 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
     else launch(I5{}, I3{});
   }
   C10_HIP_KERNEL_LAUNCH_CHECK();
-  if (S > 1) {
-    const int64_t n8 = (int64_t)M2 * N2 / 8, m8 = epi2 == EPI_ROWSUM ? M2 / 8 : 0;
-    const int blocks = (int)std::min<int64_t>((n8 + m8 + 255) / 256, 2048);
-    hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, p2.ws, S, n8, (int64_t)M2 * N2, p2.c, m8,
-                       p2.aux_out, p2.accum);
-    C10_HIP_KERNEL_LAUNCH_CHECK();
-  }
+  if (S > 1)
+    splitk_reduce(ws, S, (int64_t)M2 * N2 / 8, (int64_t)M2 * N2, p2.c, epi2 == EPI_ROWSUM ? M2 / 8 : 0, p2.aux_out,
+                  p2.accum, st);
 }
 
 }  // namespace gemm

@@ -31,7 +31,13 @@ at::Tensor claim(const at::Tensor& param, bool& acc) {
   auto it = g_map.find(param.unsafeGetTensorImpl());
   if (it == g_map.end()) return at::Tensor();
   Entry& e = it->second;
-  if (e.param.expired() || e.gen == g_gen) return at::Tensor();
+  if (e.param.expired()) return at::Tensor();
+  if (e.gen == g_gen) {
+    // a second use in this pass: the engine adds the contributions before AccumulateGrad, so the
+    // first writer's deferred reduce into the slice must have been issued
+    defer::flush();
+    return at::Tensor();
+  }
   const at::Tensor& g = param.grad();
   if (g.defined()) {
     // accumulate only onto our own slice; any other .grad (set by the user) keeps the normal path
@@ -65,6 +71,7 @@ void set_grad_dest(const at::Tensor& param, const c10::optional<at::Tensor>& dst
 }
 
 void grad_dest_new_pass() {
+  defer::flush();  // nothing should be pending here (DDP flushes at the end of backward)
   std::lock_guard<std::mutex> lk(g_mu);
   ++g_gen;
 }
@@ -85,6 +92,7 @@ at::Tensor grad_dest_join(const at::Tensor& param) {
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_map.find(param.unsafeGetTensorImpl());
   if (it == g_map.end() || it->second.param.expired() || it->second.gen != g_gen) return at::empty({0}, param.options());
+  defer::flush();  // the caller adds into the slice: the first writer's reduce goes first
   return it->second.dst;
 }
 
@@ -94,6 +102,10 @@ std::tuple<at::Tensor, bool> grad_dest_claim(const at::Tensor& param) {
   at::Tensor d = claim(param, acc);
   return {d.defined() ? d : at::empty({0}, param.options()), acc};
 }
+
+void grad_defer_enable(bool on) { defer::set_enabled(on); }
+void grad_defer_flush() { defer::flush(); }
+int64_t grad_defer_pending() { return defer::pending(); }
 
 }  // namespace graddst
 }  // namespace nbd
@@ -105,4 +117,7 @@ TORCH_LIBRARY_FRAGMENT(nbd, m) {
   m.def("grad_dest_count() -> int", &nbd::graddst::grad_dest_count);
   m.def("grad_dest_claim(Tensor param) -> (Tensor, bool)", &nbd::graddst::grad_dest_claim);
   m.def("grad_dest_join(Tensor param) -> Tensor", &nbd::graddst::grad_dest_join);
+  m.def("grad_defer_enable(bool on) -> ()", &nbd::graddst::grad_defer_enable);
+  m.def("grad_defer_flush() -> ()", &nbd::graddst::grad_defer_flush);
+  m.def("grad_defer_pending() -> int", &nbd::graddst::grad_defer_pending);
 }

@@ -27,4 +27,33 @@ at::Tensor claim(const at::Tensor& param, bool& acc);
 at::Tensor hand_back(const at::Tensor& param, const at::Tensor& dst, bool acc);
 
 }  // namespace graddst
+
+// Deferred weight-gradient reductions (defer.hip).  A split-K weight-gradient GEMM writes fp32
+// partial slabs that a second kernel sums into the gradient, a norm backward per-workgroup
+// partial rows; for a small model each such reduce is a ≈5 µs launch (90 + 61 per SmolLM2 step).
+// When the gradient goes to its claimed bucket slice nothing reads it before the bucket is
+// consumed, so the autograd node opens a Scope and the producer queues the reduce instead of
+// launching it; flush() issues every queued reduce in one launch per kind.  DDP flushes before a
+// bucket's collective and at the end of backward (parallel/ddp.py); a second use of a handed-out
+// slice (claim / join) and a new pass flush first.  enabled() is process-wide
+// (torch.ops.nbd.grad_defer_enable; NBD_GRAD_DEFER=0 keeps it off).
+namespace defer {
+bool enabled();
+void set_enabled(bool on);
+bool want();  // enabled and inside a Scope(true) on this thread
+struct Scope {
+  explicit Scope(bool on);
+  ~Scope();
+  bool prev;
+};
+// queue one reduce (reduce_kernel's arguments; `ws` kept alive until the flush); false = launch now
+bool push_splitk(const at::Tensor& ws, int splits, int64_t n8, int64_t m8, int64_t slab, uint16_t* out,
+                 uint16_t* rs_out, int accum, void* stream);
+// queue one norm weight-gradient column sum (norm.hip col_reduce: `part` [nparts][ld] fp32,
+// columns [0, C) -> out0, [C, W) -> out1, bf16); false = launch now
+bool push_colred(const at::Tensor& part, int nparts, int ld, int W, int C, uint16_t* out0, uint16_t* out1, int accum,
+                 void* stream);
+void flush();
+int64_t pending();
+}  // namespace defer
 }  // namespace nbd

@@ -25,6 +25,7 @@
 #include <tuple>
 #include <type_traits>
 
+#include "graddst.h"
 #include "nbd_common.h"
 
 namespace nbd {
@@ -459,8 +460,9 @@ __global__ __launch_bounds__(NT) void colsum_kernel(const T* __restrict__ x, int
 // loads are independent and issued together, the 16 groups are combined in LDS — no serial
 // per-column loop (a one-thread-per-column version spent 18 µs per call, latency-bound).
 template <typename O>
-__global__ __launch_bounds__(NT) void col_reduce_kernel(const float* __restrict__ part, int nparts, int W, int C,
-                                                        O* __restrict__ out0, O* __restrict__ out1) {
+__global__ __launch_bounds__(NT) void col_reduce_kernel(const float* __restrict__ part, int nparts, int ld, int W,
+                                                        int C, O* __restrict__ out0, O* __restrict__ out1,
+                                                        int accum) {
   __shared__ float red[16][17];
   const int cx = threadIdx.x & 15, pg = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cx;
@@ -468,12 +470,12 @@ __global__ __launch_bounds__(NT) void col_reduce_kernel(const float* __restrict_
   if (c < W) {
     int p = pg;
     for (; p + 48 < nparts; p += 64) {
-      a0 += part[(int64_t)p * W + c];
-      a1 += part[(int64_t)(p + 16) * W + c];
-      a2 += part[(int64_t)(p + 32) * W + c];
-      a3 += part[(int64_t)(p + 48) * W + c];
+      a0 += part[(int64_t)p * ld + c];
+      a1 += part[(int64_t)(p + 16) * ld + c];
+      a2 += part[(int64_t)(p + 32) * ld + c];
+      a3 += part[(int64_t)(p + 48) * ld + c];
     }
-    for (; p < nparts; p += 16) a0 += part[(int64_t)p * W + c];
+    for (; p < nparts; p += 16) a0 += part[(int64_t)p * ld + c];
   }
   red[pg][cx] = (a0 + a1) + (a2 + a3);
   __syncthreads();
@@ -481,8 +483,9 @@ __global__ __launch_bounds__(NT) void col_reduce_kernel(const float* __restrict_
     float s = 0.f;
 #pragma unroll
     for (int g = 0; g < 16; ++g) s += red[g][cx];
-    if (c < C) Elem<O>::store(out0, c, s);
-    else Elem<O>::store(out1, c - C, s);
+    // accum bit 0 / 1: add to out0 / out1 (gradient accumulation in a bucket slice)
+    if (c < C) Elem<O>::store(out0, c, (accum & 1) ? s + Elem<O>::load(out0, c) : s);
+    else Elem<O>::store(out1, c - C, (accum & 2) ? s + Elem<O>::load(out1, c - C) : s);
   }
 }
 
@@ -513,18 +516,25 @@ static void dispatch_tw(at::ScalarType t, at::ScalarType w, F&& f) {
 }
 
 template <typename O>
-static void launch_reduce(const at::Tensor& part, int nparts, int W, int C, const at::Tensor& out0,
-                          const at::Tensor& out1, hipStream_t st) {
-  hipLaunchKernelGGL((col_reduce_kernel<O>), dim3((W + 15) / 16), dim3(NT), 0, st, part.data_ptr<float>(), nparts, W,
-                     C, static_cast<O*>(out0.data_ptr()), static_cast<O*>(out1.data_ptr()));
+static void launch_reduce(const at::Tensor& part, int nparts, int ld, int W, int C, const at::Tensor& out0,
+                          const at::Tensor& out1, int accum, hipStream_t st) {
+  hipLaunchKernelGGL((col_reduce_kernel<O>), dim3((W + 15) / 16), dim3(NT), 0, st, part.data_ptr<float>(), nparts, ld,
+                     W, C, static_cast<O*>(out0.data_ptr()), out1.defined() ? static_cast<O*>(out1.data_ptr()) : nullptr,
+                     accum);
 }
-// part [nparts, W] -> out0 = columns [0, C), out1 = columns [C, W) (same dtype)
-static void reduce_into(const at::Tensor& part, int nparts, int W, int C, const at::Tensor& out0,
-                        const at::Tensor& out1, hipStream_t st) {
+// part [nparts][ld] -> out0 = columns [0, C), out1 = columns [C, W) (same dtype; W == C: no out1),
+// adding to out0 / out1 for accum bit 0 / 1.  Queued instead (defer.hip) when the caller's
+// scope says both outputs are claimed bucket slices.
+static void reduce_into(const at::Tensor& part, int nparts, int ld, int W, int C, const at::Tensor& out0,
+                        const at::Tensor& out1, int accum, hipStream_t st) {
+  if (defer::want() && out0.scalar_type() == at::kBFloat16 &&
+      defer::push_colred(part, nparts, ld, W, C, static_cast<uint16_t*>(out0.data_ptr()),
+                         out1.defined() ? static_cast<uint16_t*>(out1.data_ptr()) : nullptr, accum, st))
+    return;
   switch (out0.scalar_type()) {
-    case at::kFloat: launch_reduce<float>(part, nparts, W, C, out0, out1, st); break;
-    case at::kBFloat16: launch_reduce<bf16_t>(part, nparts, W, C, out0, out1, st); break;
-    case at::kHalf: launch_reduce<f16_t>(part, nparts, W, C, out0, out1, st); break;
+    case at::kFloat: launch_reduce<float>(part, nparts, ld, W, C, out0, out1, accum, st); break;
+    case at::kBFloat16: launch_reduce<bf16_t>(part, nparts, ld, W, C, out0, out1, accum, st); break;
+    case at::kHalf: launch_reduce<f16_t>(part, nparts, ld, W, C, out0, out1, accum, st); break;
     default: TORCH_CHECK(false, "norm: unsupported output dtype");
   }
   C10_HIP_KERNEL_LAUNCH_CHECK();
@@ -614,11 +624,13 @@ static void launch_bwd(bool res, const at::Tensor& x, const at::Tensor& dy, cons
                        dxp, pgp, rows, (int)C, rpb);
 }
 
-// returns (dx, dweight, dbias); dx includes dres when given
-std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_hip(const at::Tensor& x, const at::Tensor& dy,
-                                                          const c10::optional<at::Tensor>& dres,
-                                                          const at::Tensor& weight, const at::Tensor& mean,
-                                                          const at::Tensor& rstd) {
+// returns (dx, dweight, dbias); dx includes dres when given.  dw_dst / db_dst (optional): write
+// the weight / bias gradients there (their bucket slices, autograd.hip), adding for accum bit 0 / 1
+std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_into(const at::Tensor& x, const at::Tensor& dy,
+                                                           const c10::optional<at::Tensor>& dres,
+                                                           const at::Tensor& weight, const at::Tensor& mean,
+                                                           const at::Tensor& rstd, const at::Tensor& dw_dst,
+                                                           const at::Tensor& db_dst, int accum) {
   const int64_t C = x.size(-1);
   TORCH_CHECK(C % 4 == 0 && C <= 256 * kMaxCh && C > 0, "ln_bwd: C must be a multiple of 4 and <= 2048");
   check_rows(x, C, "x");
@@ -634,10 +646,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_hip(const at::Tensor& x, c
                   rstd.scalar_type() == at::kFloat,
               "ln_bwd: mean/rstd must be float32 [rows]");
   at::Tensor dx = at::empty_like(x);
-  at::Tensor dw = at::empty({C}, weight.options()), db = at::empty({C}, weight.options());
+  at::Tensor dw = dw_dst.defined() ? dw_dst.view({C}) : at::empty({C}, weight.options());
+  at::Tensor db = db_dst.defined() ? db_dst.view({C}) : at::empty({C}, weight.options());
   const int rpb = bwd_rows_per_block(rows);
   const int nblk = (int)((rows + rpb - 1) / rpb);
-  if (rows == 0) return {dx, dw.zero_(), db.zero_()};
+  if (rows == 0) {
+    if (!(accum & 1)) dw.zero_();
+    if (!(accum & 2)) db.zero_();
+    return {dx, dw, db};
+  }
   auto fo = x.options().dtype(at::kFloat);
   at::Tensor pg = at::empty({nblk, 2 * C}, fo);
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -653,8 +670,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_hip(const at::Tensor& x, c
    });
   });
   C10_HIP_KERNEL_LAUNCH_CHECK();
-  reduce_into(pg, nblk, (int)(2 * C), (int)C, dw, db, st);
+  reduce_into(pg, nblk, (int)(2 * C), (int)(2 * C), (int)C, dw, db, accum, st);
   return {dx, dw, db};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_hip(const at::Tensor& x, const at::Tensor& dy,
+                                                          const c10::optional<at::Tensor>& dres,
+                                                          const at::Tensor& weight, const at::Tensor& mean,
+                                                          const at::Tensor& rstd) {
+  return ln_bwd_into(x, dy, dres, weight, mean, rstd, at::Tensor(), at::Tensor(), 0);
 }
 
 // RMSNorm: y = x · rsqrt(mean(x²) + eps) · g  (optionally on x + delta, returned as xsum)
@@ -701,9 +725,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rms_fwd_hip(const at::Tensor& x, 
   return {y, xsum, rstd};
 }
 
-std::tuple<at::Tensor, at::Tensor> rms_bwd_hip(const at::Tensor& x, const at::Tensor& dy,
-                                               const c10::optional<at::Tensor>& dres, const at::Tensor& weight,
-                                               const at::Tensor& rstd) {
+std::tuple<at::Tensor, at::Tensor> rms_bwd_into(const at::Tensor& x, const at::Tensor& dy,
+                                                const c10::optional<at::Tensor>& dres, const at::Tensor& weight,
+                                                const at::Tensor& rstd, const at::Tensor& dw_dst, int accum) {
   const int64_t C = x.size(-1);
   TORCH_CHECK(C % 4 == 0 && C <= 256 * kMaxCh && C > 0, "rms_bwd: C must be a multiple of 4 and <= 2048");
   check_rows(x, C, "x");
@@ -717,10 +741,13 @@ std::tuple<at::Tensor, at::Tensor> rms_bwd_hip(const at::Tensor& x, const at::Te
   const int64_t rows = x.numel() / C;
   TORCH_CHECK(rstd.numel() == rows && rstd.scalar_type() == at::kFloat, "rms_bwd: rstd must be float32 [rows]");
   at::Tensor dx = at::empty_like(x);
-  at::Tensor dw = at::empty({C}, weight.options()), db = at::empty({C}, weight.options());
+  at::Tensor dw = dw_dst.defined() ? dw_dst.view({C}) : at::empty({C}, weight.options());
   const int rpb = bwd_rows_per_block(rows);
   const int nblk = (int)((rows + rpb - 1) / rpb);
-  if (rows == 0) return {dx, dw.zero_()};
+  if (rows == 0) {
+    if (!(accum & 1)) dw.zero_();
+    return {dx, dw};
+  }
   at::Tensor pg = at::empty({nblk, 2 * C}, x.options().dtype(at::kFloat));
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
@@ -735,8 +762,15 @@ std::tuple<at::Tensor, at::Tensor> rms_bwd_hip(const at::Tensor& x, const at::Te
    });
   });
   C10_HIP_KERNEL_LAUNCH_CHECK();
-  reduce_into(pg, nblk, (int)(2 * C), (int)C, dw, db, st);
+  // the partial rows are [dγ | Σdy] (the kernel is LayerNorm's); RMSNorm sums the first half only
+  reduce_into(pg, nblk, (int)(2 * C), (int)C, (int)C, dw, at::Tensor(), accum & 1, st);
   return {dx, dw};
+}
+
+std::tuple<at::Tensor, at::Tensor> rms_bwd_hip(const at::Tensor& x, const at::Tensor& dy,
+                                               const c10::optional<at::Tensor>& dres, const at::Tensor& weight,
+                                               const at::Tensor& rstd) {
+  return rms_bwd_into(x, dy, dres, weight, rstd, at::Tensor(), 0);
 }
 
 // Σ over rows of a contiguous [..., C] tensor -> [C] in `dtype` (fp32 accumulation)
@@ -768,7 +802,7 @@ at::Tensor colsum_hip(const at::Tensor& x, at::ScalarType dtype) {
     default: TORCH_CHECK(false, "colsum: unsupported dtype ", x.scalar_type());
   }
   C10_HIP_KERNEL_LAUNCH_CHECK();
-  reduce_into(part, nblk, (int)C, (int)C, out, out, st);
+  reduce_into(part, nblk, (int)C, (int)C, (int)C, out, at::Tensor(), 0, st);
   return out;
 }
 

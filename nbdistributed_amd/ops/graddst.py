@@ -54,6 +54,28 @@ def hand_back(param, dst, acc: bool):
     return dst.view(dst.shape)
 
 
+def defer_enable(on: bool) -> None:
+    """Queue the split-K reduces of weight gradients written into their slices (graddst.h
+    ``defer``) instead of launching one per Linear; ``defer_flush`` issues them in one launch."""
+    import torch
+
+    _require()
+    torch.ops.nbd.grad_defer_enable(bool(on))
+
+
+def defer_flush() -> None:
+    """Issue every queued weight-gradient reduce (one launch, on the stream they were queued on)."""
+    import torch
+
+    torch.ops.nbd.grad_defer_flush()
+
+
+def defer_pending() -> int:
+    import torch
+
+    return int(torch.ops.nbd.grad_defer_pending())
+
+
 def join(param):
     """The destination if another node already wrote ``param``'s gradient there in this pass
     (it is still on its way to AccumulateGrad): add into it and return no gradient."""

@@ -49,6 +49,7 @@ Also provides DDP communication hooks for stock ``torch.nn.parallel.DistributedD
 from __future__ import annotations
 
 import contextlib
+import os
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
 
@@ -145,8 +146,6 @@ class DistributedDataParallel(torch.nn.Module):
         self._capturing = False
         self._side = False
         self._next_launch = 0
-        import os
-
         # normal | high | none.  A high-priority stream measured 2.2x slower end to end on
         # MI355X (GPT-2 small DDP step 55 ms vs 25.5 ms, benchmarks/ddp_compare.py).
         mode = os.environ.get("NBD_DDP_COMM_STREAM", "normal")
@@ -202,6 +201,15 @@ class DistributedDataParallel(torch.nn.Module):
         self._patched: List[torch.nn.Module] = []
         if (self.grad_views if fused_linear is None else fused_linear) and self._n_views:
             self._patch_linears()
+        # weight-gradient split-K reduces into the slices are queued and issued in one launch per
+        # flush (before a bucket's collective, at the end of backward) — ops.graddst.defer_enable
+        # (process-wide switch; NBD_GRAD_DEFER=0 turns it off for A/B runs).  Every DDP with slices
+        # flushes, whoever enabled it.
+        self._defer = bool(self._n_views)
+        if self._defer:
+            from ..ops import graddst
+
+            graddst.defer_enable(os.environ.get("NBD_GRAD_DEFER", "1") != "0")
 
         self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in self.params]
         if init_sync and self.world > 1:
@@ -427,7 +435,15 @@ class DistributedDataParallel(torch.nn.Module):
             grads.append(p.grad)
         return grads
 
+    def _flush_deferred(self) -> None:
+        if self._defer:
+            from ..ops import graddst
+
+            graddst.defer_flush()
+
     def _launch(self, b: _Bucket) -> None:
+        if self.world > 1:
+            self._flush_deferred()  # the collective reads the slices: their reduces go first
         n_in, rest = self._split_in_place(b)
         if n_in == 0 and not b.partial:
             self._launch_flat(b)
@@ -531,6 +547,7 @@ class DistributedDataParallel(torch.nn.Module):
         b.launched = True
 
     def _finalize(self) -> None:
+        self._flush_deferred()
         if not self._sync_pass:  # no_sync micro-batch: buckets hold the local sums, nothing to send
             for b in self.buckets:
                 if not b.ready and b.pending < len(b.params):

@@ -174,3 +174,95 @@ def test_ddp_fp32_linear_in_place_matches_torch_ddp(sess):
     r = sess.execute(CODE_LINEAR, render=False)
     assert r.ok, r.errors
     assert r.results[0]["echo"] == "(1, True, True, True)", r.results[0]
+
+
+def test_deferred_splitk_reduce_matches_immediate(dev):
+    """A split-K weight gradient written into its slice is queued (graddst.h ``defer``), summed
+    by one flush launch bit-identically to the immediate reduce; a second use of the slice in the
+    same pass flushes first; a pass start flushes what is left."""
+    from nbdistributed_amd.ops import gemm as G
+    from nbdistributed_amd.ops import graddst
+
+    torch.manual_seed(1)
+    M, N, K = 2048, 576, 576  # SmolLM2 o_proj: the grouped backward splits the weight gradient
+    assert G.pair_schedule(M, N, K, 64) & 15 > 1
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, requires_grad=True)  # the grouped launch
+    lin = torch.nn.Linear(K, N, bias=False, device="cuda", dtype=torch.bfloat16)
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    home = torch.zeros(N * K, device="cuda", dtype=torch.bfloat16)
+    vw = home.view(N, K)
+    graddst.register(lin.weight, vw)
+    try:
+        ref = []
+        for on in (False, True):
+            graddst.defer_enable(on)
+            lin.weight.grad = None
+            home.fill_(7.0)  # stale contents must be overwritten
+            graddst.new_pass()
+            G.linear_any(x, lin.weight).backward(dy)
+            assert lin.weight.grad.data_ptr() == vw.data_ptr()
+            assert graddst.defer_pending() == (1 if on else 0)
+            graddst.defer_flush()
+            assert graddst.defer_pending() == 0
+            ref.append(vw.clone())
+            # accumulate (grad already the slice): the queued reduce adds
+            graddst.new_pass()
+            G.linear_any(x, lin.weight).backward(dy)
+            graddst.new_pass()  # flushes
+            assert graddst.defer_pending() == 0
+            ref.append(vw.clone())
+        assert torch.equal(ref[0], ref[2]) and torch.equal(ref[1], ref[3])
+        assert torch.equal(ref[1], 2 * ref[0])
+        # used twice in one pass: the second claim flushes the first writer's reduce
+        graddst.defer_enable(True)
+        lin.weight.grad = None
+        graddst.new_pass()
+        (G.linear_any(x, lin.weight) + G.linear_any(x, lin.weight)).backward(dy)
+        graddst.defer_flush()
+        assert (lin.weight.grad.float() - 2 * ref[0].float()).abs().max().item() <= 1e-2 * ref[0].float().abs().max().item()
+    finally:
+        graddst.defer_enable(False)
+        graddst.register(lin.weight, None)
+
+
+CODE_DEFER = """
+import copy
+import contextlib
+from nbdistributed_amd.models.llama import LlamaConfig, LlamaForSequenceClassification
+from nbdistributed_amd.models import GPT2, GPT2Config
+from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP
+from nbdistributed_amd.ops import graddst
+res = []
+for kind in ("llama", "gpt2"):
+    torch.manual_seed(5)
+    if kind == "llama":
+        base = LlamaForSequenceClassification(LlamaConfig.smollm2_135m(num_hidden_layers=2)).to(device, torch.bfloat16)
+        ids = torch.randint(1, 49152, (16, 128), generator=torch.Generator().manual_seed(0)).to(device)
+        fwd = lambda m: m(ids, torch.ones_like(ids), torch.zeros(16, dtype=torch.long, device=device))[0]
+    else:
+        base = GPT2(GPT2Config(vocab_size=5000, n_positions=256, n_embd=256, n_layer=2, n_head=4)).to(device, torch.bfloat16)
+        ids = torch.randint(0, 5000, (4, 256), generator=torch.Generator().manual_seed(0)).to(device)
+        fwd = lambda m: m(ids, ids, return_logits=False)[1]
+    m = NbdDDP(copy.deepcopy(base), flat_params=True, grad_mode="bucket")
+    out = []
+    for on in (True, False):
+        graddst.defer_enable(on)
+        for k in (1, 3):
+            for p in m.parameters():
+                p.grad = None
+            for i in range(k):
+                ctx = m.no_sync() if i < k - 1 else contextlib.nullcontext()
+                with ctx:
+                    fwd(m).backward()
+            torch.cuda.synchronize()
+            out.append(torch.cat([b.buffer.float() for b in m.buckets]))
+    graddst.defer_enable(True)
+    res.append(torch.equal(out[0], out[2]) and torch.equal(out[1], out[3]) and graddst.defer_pending() == 0)
+tuple(res)
+"""
+
+
+def test_ddp_deferred_reduces_bit_identical(sess):
+    r = sess.execute(CODE_DEFER, render=False)
+    assert r.ok, r.errors
+    assert r.results[0]["echo"] == "(True, True)", r.results[0]
