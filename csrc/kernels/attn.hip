@@ -766,7 +766,11 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
   const int Hkv = (int)k.size(1), group = H / Hkv;
   const float sc2 = (float)scale * kLog2e;
   // GQA with few key/value workgroups: split each kv head's query-head group over workgroups
-  const int gsplit = (group > 1 && B * Hkv * nblk < 256) ? group : 1;
+  static const int gsplit_env = [] {  // NBD_ATTN_GSPLIT=1: never split (A/B)
+    const char* e = std::getenv("NBD_ATTN_GSPLIT");
+    return e == nullptr ? 0 : std::atoi(e);
+  }();
+  const int gsplit = gsplit_env == 1 ? 1 : (group > 1 && B * Hkv * nblk < 256) ? group : 1;
   const int nkv = B * Hkv * nblk * gsplit, nq = B * H * nblk;
   MView dkw = dkv, dvw = dvv;
   at::Tensor pk, pv;
