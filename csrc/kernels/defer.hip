@@ -9,12 +9,14 @@
 // issues every queued one in a single launch per kind.  Each descriptor is exactly one original
 // launch's work with the same fixed-order sums, so the gradients are bit-identical.
 //
-// Flushes: DDP before a bucket's collective and at the end of backward (parallel/ddp.py), a second
-// use of a handed-out slice and a new pass (graddst.cpp), a change of stream, and by itself once
-// the queue holds kFlushBytes of partials (so a flush reads MALL-warm data).
+// Flushes: at the end of the backward that queued (an autograd-engine callback registered by the
+// first push), DDP before a bucket's collective (parallel/ddp.py), a second use of a handed-out
+// slice and a new pass (graddst.cpp), a change of stream or of graph-capture state, and by itself
+// once the queue holds NBD_GRAD_DEFER_FLUSH_MB of partials (so a flush reads MALL-warm data).
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/csrc/autograd/engine.h>
 
 #include <atomic>
 #include <cstdlib>
@@ -149,8 +151,10 @@ std::vector<Item> q_items;
 int64_t q_bytes = 0;
 hipStream_t q_stream = nullptr;
 int q_device = -1;
+bool q_capturing = false;  // the queued items belong to a HIP-graph capture (or to eager work)
 std::atomic<bool> g_enabled{false};
 thread_local bool t_scope = false;
+bool q_callback = false;  // an end-of-backward flush is registered with the running backward
 
 void launch_split(const std::vector<const Item*>& items) {
   size_t pos = 0;
@@ -219,11 +223,28 @@ bool push(Item&& it, void* stream) {
   std::lock_guard<std::mutex> lk(q_mu);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int dev = it.buf.get_device();
-  if (!q_items.empty() && (st != q_stream || dev != q_device)) flush_locked();  // one stream per queue
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  C10_HIP_CHECK(hipStreamIsCapturing(st, &cs));
+  const bool capturing = cs == hipStreamCaptureStatusActive;
+  // one stream per queue, and never a flush that mixes eager work into a graph capture (the
+  // eager partials would be freed while the graph still reads them)
+  if (!q_items.empty() && (st != q_stream || dev != q_device || capturing != q_capturing)) flush_locked();
   q_stream = st;
   q_device = dev;
+  q_capturing = capturing;
   q_items.push_back(std::move(it));
   q_bytes += bytes;
+  if (!q_callback) {
+    // whoever runs this backward (DDP or not), the queue is flushed when it ends: a gradient in
+    // a slice is never left unfinished after backward() returns.  (Outside a backward pass the
+    // engine refuses the callback: then nothing is deferred.)
+    try {
+      torch::autograd::Engine::get_default_engine().queue_callback([] { flush(); });
+      q_callback = true;
+    } catch (const std::exception&) {
+      flush_locked();
+    }
+  }
   if (q_bytes >= flush_bytes() || (int)q_items.size() >= 4 * kMaxD) flush_locked();
   return true;
 }
@@ -242,6 +263,7 @@ void set_enabled(bool on) {
 void flush() {
   std::lock_guard<std::mutex> lk(q_mu);
   flush_locked();
+  q_callback = false;  // (a later push registers again; a stale registration only flushes an empty queue)
 }
 
 int64_t pending() {

@@ -177,9 +177,10 @@ def test_ddp_fp32_linear_in_place_matches_torch_ddp(sess):
 
 
 def test_deferred_splitk_reduce_matches_immediate(dev):
-    """A split-K weight gradient written into its slice is queued (graddst.h ``defer``), summed
-    by one flush launch bit-identically to the immediate reduce; a second use of the slice in the
-    same pass flushes first; a pass start flushes what is left."""
+    """A split-K weight gradient written into its slice is queued (graddst.h ``defer``) and summed
+    by one flush launch bit-identically to the immediate reduce — the flush registered with the
+    running backward has run when ``backward()`` returns (no DDP here); a second use of the slice
+    in the same pass flushes first."""
     from nbdistributed_amd.ops import gemm as G
     from nbdistributed_amd.ops import graddst
 
@@ -199,16 +200,18 @@ def test_deferred_splitk_reduce_matches_immediate(dev):
             lin.weight.grad = None
             home.fill_(7.0)  # stale contents must be overwritten
             graddst.new_pass()
-            G.linear_any(x, lin.weight).backward(dy)
+            seen = []
+            y = G.linear_any(x, lin.weight)
+            # a hook on the input's gradient runs after the weight node, before backward() returns
+            h = x.register_hook(lambda g: seen.append(graddst.defer_pending()))
+            y.backward(dy)
+            h.remove()
             assert lin.weight.grad.data_ptr() == vw.data_ptr()
-            assert graddst.defer_pending() == (1 if on else 0)
-            graddst.defer_flush()
-            assert graddst.defer_pending() == 0
+            assert seen == [1 if on else 0] and graddst.defer_pending() == 0
             ref.append(vw.clone())
             # accumulate (grad already the slice): the queued reduce adds
             graddst.new_pass()
             G.linear_any(x, lin.weight).backward(dy)
-            graddst.new_pass()  # flushes
             assert graddst.defer_pending() == 0
             ref.append(vw.clone())
         assert torch.equal(ref[0], ref[2]) and torch.equal(ref[1], ref[3])
