@@ -753,7 +753,11 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   const int nblk = T / BLK;
   // short sequences: δ inside the main kernel (each (query head, tile) is swept by <= 2 key blocks)
-  const bool fd = nblk <= 2;
+  static const int fd_env = [] {  // NBD_ATTN_FD=1 / 0: force the fused-δ path on / off (A/B)
+    const char* e = std::getenv("NBD_ATTN_FD");
+    return e == nullptr ? -1 : std::atoi(e);
+  }();
+  const bool fd = fd_env >= 0 ? fd_env == 1 : nblk <= 2;
   at::Tensor delta;
   if (!fd) {
     delta = at::empty({B, H, T}, lse.options());
