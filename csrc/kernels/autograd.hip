@@ -528,6 +528,185 @@ Tensor attn_qkv_noag(const Tensor& qkv, int64_t H, int64_t Hkv, bool causal, dou
   return o.transpose(1, 2).reshape({qkv.size(0), qkv.size(1), -1});
 }
 
+// ------------------------------------------------------------ fused Llama decoder block
+// One autograd node for a whole pre-norm decoder block of the Llama family:
+//   qkv = h·W_qkvᵀ (+b) → causal GQA attention with RoPE → y = a·W_oᵀ (+b)
+//   x1 = x + y, h1 = rms(x1)·γ_post → m = down(silu(g)·u), [g|u] = h1·W_guᵀ
+//   x2 = x1 + m, h2 = rms(x2)·γ_next                                  → returns (x2, h2)
+// The same kernels, in the same order, as the per-op nodes above (Linear, attention, add+RMSNorm,
+// SwiGLU MLP: bit-identical results), but one Python call and one autograd node per block instead
+// of six and five — an eager SmolLM2 step is host-bound (docs/FINDINGS.md §15, §27).  Weight
+// gradients go to their bucket slices (graddst) exactly as in the per-op nodes.
+static std::tuple<Tensor, Tensor, Tensor> linear_bwd_core(const Tensor& dy, const Tensor& x2, const Tensor& w,
+                                                          const Tensor& b, at::IntArrayRef plan, bool nx, bool nw,
+                                                          bool nb) {
+  Tensor dx, dw, db;
+  if (nx && nw && plan[9] >= 0) {
+    std::tie(dx, dw, db) = pair(dy, w, x2, EPI_NONE, c10::nullopt, nb, plan[9], b);
+  } else {
+    if (nx) dx = run(dy, w, false, true, prod(plan, 1)).first;
+    if (nw) std::tie(dw, db) = wgrad(dy, x2, w, b, nb, plan, 2);
+    else if (nb) db = dy.sum(0, false, at::kFloat).to(dy.scalar_type());
+  }
+  return {dx, dw, db};
+}
+
+// (dh, dW_gu, dW_down) of m = down(silu(g)·u), [g|u] = h·W_guᵀ, for dm [M, C]
+static std::tuple<Tensor, Tensor, Tensor> swiglu_bwd_core(const Tensor& dm, const Tensor& x2, const Tensor& w_gu,
+                                                          const Tensor& w_down, const Tensor& pre, const Tensor& act,
+                                                          at::IntArrayRef plan, bool nx) {
+  Tensor dgu, dw_down, dx, dw_gu, unused;
+  if (plan[18] >= 0) {
+    std::tie(dgu, dw_down, unused) = pair(dm, w_down, act, EPI_DSWIGLU, pre, false, plan[18]);
+  } else {
+    dgu = run(dm, w_down, false, true, prod(plan, 2), EPI_DSWIGLU, c10::nullopt, pre).first;
+    dw_down = wgrad(dm, act, w_down, Tensor(), false, plan, 3).first;
+  }
+  if (nx && plan[19] >= 0) {
+    std::tie(dx, dw_gu, unused) = pair(dgu, w_gu, x2, EPI_NONE, c10::nullopt, false, plan[19]);
+  } else {
+    if (nx) dx = run(dgu, w_gu, false, true, prod(plan, 4)).first;
+    dw_gu = wgrad(dgu, x2, w_gu, Tensor(), false, plan, 5).first;
+  }
+  return {dx, dw_gu, dw_down};
+}
+
+// (d sum, dγ) of (s = x + δ, y = rms(s)·γ) for dy and the sum's own gradient ds (may be undefined)
+static std::pair<Tensor, Tensor> rms_bwd_core(const Tensor& s, const Tensor& dy, const Tensor& ds, const Tensor& w,
+                                              const Tensor& rstd) {
+  const GradOut gw = grad_out(w, w.requires_grad(), w.sizes(), w.options());
+  const defer::Scope dsc(gw.claimed);
+  auto [dx, dw] = norm::rms_bwd_into(s, dy.contiguous(), opt(ds), w, rstd, gw.t, gw.bit(1));
+  return {dx, gw.t.defined() ? gw.done() : dw};
+}
+
+static Tensor attn_bwd_core(const Tensor& da, const Tensor& qkv, const Tensor& o, const Tensor& lse, int64_t H,
+                            int64_t Hkv, double scale, const optional<Tensor>& cos, const optional<Tensor>& sin) {
+  const int64_t B = qkv.size(0), T = qkv.size(1), D = qkv.size(2) / (H + 2 * Hkv);
+  auto [q, k, v] = split_qkv(qkv, H, Hkv);
+  Tensor dqkv = at::empty_like(qkv, at::MemoryFormat::Contiguous);
+  auto [dq, dk, dv] = split_qkv(dqkv, H, Hkv);
+  const Tensor dout = da.contiguous().view({B, T, H, D}).transpose(1, 2);
+  attn::attn_bwd_hip(dout, q, k, v, o, lse, true, scale, dq, dk, dv, cos, sin);
+  return dqkv;
+}
+
+// forward of the block; `save` (autograd) receives what the backward needs
+static std::tuple<Tensor, Tensor> llama_block_fwd(const Tensor& x, const Tensor& h, const Tensor& w_qkv,
+                                                  const optional<Tensor>& b_qkv, const Tensor& w_o,
+                                                  const optional<Tensor>& b_o, const Tensor& w_post,
+                                                  const Tensor& w_gu, const Tensor& w_down, const Tensor& w_next,
+                                                  at::IntArrayRef plan_qkv, at::IntArrayRef plan_o,
+                                                  at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv, double scale,
+                                                  double eps, const optional<Tensor>& cos, const optional<Tensor>& sin,
+                                                  AutogradContext* ctx) {
+  const int64_t B = h.size(0), T = h.size(1), C = h.size(2);
+  const Tensor h2 = bf16c(h).view({-1, C});
+  const Tensor qkv = linear_forward(h2, w_qkv, b_qkv, plan_qkv).view({B, T, -1});
+  auto [q, k, v] = split_qkv(qkv, H, Hkv);
+  auto [o, lse] = attn::attn_fwd_hip(q, k, v, true, scale, cos, sin);
+  const Tensor a2 = o.transpose(1, 2).reshape({B * T, -1});  // o is stored [B, T, H, D]: a view
+  const Tensor y = linear_forward(a2, w_o, b_o, plan_o).view({B, T, C});
+  auto [h1, x1, rstd1] = norm::rms_fwd_hip(bf16c(x), y, w_post, eps);
+  const Tensor h1f = h1.view({-1, C});
+  auto [act, pre] = run(h1f, w_gu, false, false, prod(plan_mlp, 0), EPI_SWIGLU);
+  const Tensor m = run(act, w_down, false, false, prod(plan_mlp, 1)).first.view({B, T, C});
+  auto [h_out, x_out, rstd2] = norm::rms_fwd_hip(x1, m, w_next, eps);
+  if (ctx != nullptr) {
+    ctx->save_for_backward({h2, w_qkv, b_qkv ? *b_qkv : Tensor(), qkv, o, lse, w_o, b_o ? *b_o : Tensor(), x1, w_post,
+                            rstd1, h1f, w_gu, w_down, pre, act, x_out, w_next, rstd2, cos ? *cos : Tensor(),
+                            sin ? *sin : Tensor()});
+  }
+  return {x_out, h_out};
+}
+
+struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
+  static variable_list forward(AutogradContext* ctx, const Tensor& x, const Tensor& h, const Tensor& w_qkv,
+                               const optional<Tensor>& b_qkv, const Tensor& w_o, const optional<Tensor>& b_o,
+                               const Tensor& w_post, const Tensor& w_gu, const Tensor& w_down, const Tensor& w_next,
+                               at::IntArrayRef plan_qkv, at::IntArrayRef plan_o, at::IntArrayRef plan_mlp, int64_t H,
+                               int64_t Hkv, double scale, double eps, const optional<Tensor>& cos,
+                               const optional<Tensor>& sin) {
+    at::AutoDispatchBelowADInplaceOrView guard;
+    ctx->set_materialize_grads(false);
+    auto [x_out, h_out] = llama_block_fwd(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o,
+                                          plan_mlp, H, Hkv, scale, eps, cos, sin, ctx);
+    ctx->saved_data["plans"] = std::vector<std::vector<int64_t>>{plan_qkv.vec(), plan_o.vec(), plan_mlp.vec()};
+    ctx->saved_data["H"] = H;
+    ctx->saved_data["Hkv"] = Hkv;
+    ctx->saved_data["scale"] = scale;
+    ctx->saved_data["shape"] = h.sizes().vec();
+    ctx->saved_data["need"] = std::vector<bool>{x.requires_grad(), h.requires_grad()};
+    return {x_out, h_out};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const auto sv = ctx->get_saved_variables();
+    const Tensor &h2 = sv[0], &w_qkv = sv[1], &b_qkv = sv[2], &qkv = sv[3], &o = sv[4], &lse = sv[5], &w_o = sv[6],
+                 &b_o = sv[7], &x1 = sv[8], &w_post = sv[9], &rstd1 = sv[10], &h1f = sv[11], &w_gu = sv[12],
+                 &w_down = sv[13], &pre = sv[14], &act = sv[15], &x_out = sv[16], &w_next = sv[17], &rstd2 = sv[18];
+    const optional<Tensor> cos = sv[19].defined() ? optional<Tensor>(sv[19]) : c10::nullopt;
+    const optional<Tensor> sin = sv[20].defined() ? optional<Tensor>(sv[20]) : c10::nullopt;
+    const auto plans = ctx->saved_data["plans"].to<std::vector<std::vector<int64_t>>>();
+    const int64_t H = ctx->saved_data["H"].toInt(), Hkv = ctx->saved_data["Hkv"].toInt();
+    const double scale = ctx->saved_data["scale"].toDouble();
+    const auto shape = ctx->saved_data["shape"].toIntVector();
+    const auto need = ctx->saved_data["need"].toBoolList();
+    const int64_t C = shape[2];
+    variable_list out(19);
+    const Tensor &dx_out = grads[0], &dh_out = grads[1];
+    // x2 = x1 + m, h2 = rms(x2)·γ_next
+    Tensor g2, dw_next;
+    if (dh_out.defined()) std::tie(g2, dw_next) = rms_bwd_core(x_out, dh_out, dx_out, w_next, rstd2);
+    else g2 = dx_out;
+    if (!g2.defined()) return out;  // neither output reached the loss
+    // m = down(swiglu(h1·W_guᵀ))
+    auto [dh1, dw_gu, dw_down] = swiglu_bwd_core(bf16c(g2).view({-1, C}), h1f, w_gu, w_down, pre, act, plans[2], true);
+    // x1 = x + y, h1 = rms(x1)·γ_post
+    auto [g1, dw_post] = rms_bwd_core(x1, dh1.view(shape), g2, w_post, rstd1);
+    // y = a·W_oᵀ (+b)
+    const Tensor a2 = o.transpose(1, 2).reshape({h2.size(0), -1});
+    auto [da, dw_o, db_o] = linear_bwd_core(bf16c(g1).view({-1, C}), a2, w_o, b_o, plans[1], true,
+                                            w_o.requires_grad(), b_o.defined() && b_o.requires_grad());
+    const Tensor dqkv = attn_bwd_core(da, qkv, o, lse, H, Hkv, scale, cos, sin);
+    auto [dh, dw_qkv, db_qkv] = linear_bwd_core(dqkv.view({h2.size(0), -1}), h2, w_qkv, b_qkv, plans[0], need[1],
+                                                w_qkv.requires_grad(), b_qkv.defined() && b_qkv.requires_grad());
+    out[0] = need[0] ? g1 : Tensor();
+    out[1] = dh.defined() ? dh.view(shape) : dh;
+    out[2] = dw_qkv;
+    out[3] = db_qkv;
+    out[4] = dw_o;
+    out[5] = db_o;
+    out[6] = dw_post;
+    out[7] = dw_gu;
+    out[8] = dw_down;
+    out[9] = dw_next;
+    return out;
+  }
+};
+
+std::tuple<Tensor, Tensor> llama_block_ag(const Tensor& x, const Tensor& h, const Tensor& w_qkv,
+                                          const optional<Tensor>& b_qkv, const Tensor& w_o, const optional<Tensor>& b_o,
+                                          const Tensor& w_post, const Tensor& w_gu, const Tensor& w_down,
+                                          const Tensor& w_next, at::IntArrayRef plan_qkv, at::IntArrayRef plan_o,
+                                          at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv, double scale, double eps,
+                                          const optional<Tensor>& cos, const optional<Tensor>& sin) {
+  auto r = LlamaBlockFn::apply(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp,
+                               H, Hkv, scale, eps, cos, sin);
+  return {r[0], r[1]};
+}
+
+std::tuple<Tensor, Tensor> llama_block_noag(const Tensor& x, const Tensor& h, const Tensor& w_qkv,
+                                            const optional<Tensor>& b_qkv, const Tensor& w_o,
+                                            const optional<Tensor>& b_o, const Tensor& w_post, const Tensor& w_gu,
+                                            const Tensor& w_down, const Tensor& w_next, at::IntArrayRef plan_qkv,
+                                            at::IntArrayRef plan_o, at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv,
+                                            double scale, double eps, const optional<Tensor>& cos,
+                                            const optional<Tensor>& sin) {
+  return llama_block_fwd(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp, H, Hkv,
+                         scale, eps, cos, sin, nullptr);
+}
+
 }  // namespace ag
 }  // namespace nbd
 
@@ -542,6 +721,7 @@ TORCH_LIBRARY_IMPL(nbd, Autograd, m) {
   m.impl("layer_norm_ag", &nbd::ag::layer_norm_ag);
   m.impl("add_layer_norm_ag", &nbd::ag::add_layer_norm_ag);
   m.impl("attn_qkv_ag", &nbd::ag::attn_qkv_ag);
+  m.impl("llama_block_ag", &nbd::ag::llama_block_ag);
 }
 
 TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
@@ -553,4 +733,5 @@ TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
   m.impl("linear_ag", &nbd::ag::linear_noag);
   m.impl("mlp_gelu_ag", &nbd::ag::mlp_gelu_noag);
   m.impl("mlp_swiglu_ag", &nbd::ag::mlp_swiglu_noag);
+  m.impl("llama_block_ag", &nbd::ag::llama_block_noag);
 }

@@ -191,10 +191,21 @@ class LlamaModel(nn.Module):
         # the residual stream: each block's two residual adds are fused with the RMSNorm after them
         h = self.layers[0].input_layernorm(x)
         for i, layer in enumerate(self.layers):
+            nxt = self.layers[i + 1].input_layernorm if i + 1 < len(self.layers) else self.norm
+            at = layer.self_attn
+            # (plain modules only: tensor / context parallelism swap in their own attention / MLP)
+            if (cache is None and type(at) is LlamaAttention and type(layer.mlp) is LlamaMLP
+                    and (at.window is None or T <= at.window)):
+                # the whole block as one autograd node (GPU bf16; None -> the op-by-op path below)
+                r = ops.llama_block(x, h, at.qkv_proj.weight, at.qkv_proj.bias, at.o_proj.weight, at.o_proj.bias,
+                                    layer.post_attention_layernorm.weight, layer.mlp.gate_up_proj.weight,
+                                    layer.mlp.down_proj.weight, nxt.weight, at.H, at.Hkv, c.rms_norm_eps, cos, sin)
+                if r is not None:
+                    x, h = r
+                    continue
             a = layer.self_attn(h, cos, sin) if cache is None else layer.self_attn(h, cos, sin, kv=(cache, i))
             x, h = ops.add_rms_norm(x, a, layer.post_attention_layernorm.weight, c.rms_norm_eps)
             m = layer.mlp(h)
-            nxt = self.layers[i + 1].input_layernorm if i + 1 < len(self.layers) else self.norm
             x, h = ops.add_rms_norm(x, m, nxt.weight, c.rms_norm_eps)
         return h
 

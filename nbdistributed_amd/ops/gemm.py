@@ -607,3 +607,38 @@ def linear_any(x, weight, bias=None):
     import torch.nn.functional as F
 
     return F.linear(x, weight, bias)
+
+
+# fused Llama decoder block (csrc/kernels/autograd.hip LlamaBlockFn): NBD_FUSED_BLOCK=0 runs the
+# per-op nodes instead (same kernels, same results)
+FUSED_BLOCK = os.environ.get("NBD_FUSED_BLOCK", "1") != "0"
+_BLOCK_PLANS: dict = {}
+
+
+def llama_block(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, n_head: int, n_kv: int, eps: float,
+                cos, sin):
+    """One pre-norm Llama decoder block as ONE autograd node: ``x1 = x + o_proj(attn(qkv(h)))``,
+    ``h1 = rms(x1)·γ_post``, ``x2 = x1 + down(swiglu(gate_up(h1)))``, returns ``(x2, rms(x2)·γ_next)``
+    — the per-op path's kernels in the same order, one Python call and one node instead of six and
+    five (the eager SmolLM2 step is host-bound).  None when the block does not fit the fused path
+    (the caller then runs the ops one by one)."""
+    import torch
+
+    if not (FUSED_BLOCK and FUSED_SWIGLU and NATIVE_AUTOGRAD and _fast(h, w_qkv, w_o, w_gu, w_down)
+            and x.dtype == h.dtype and x.shape == h.shape and _native(b_qkv, b_o)):
+        return None
+    B, T, C = h.shape
+    D = w_qkv.shape[0] // (n_head + 2 * n_kv)
+    if not (D == 64 and T % 128 == 0 and n_head % n_kv == 0 and w_post.dtype == w_next.dtype == h.dtype
+            and C % 8 == 0 and C <= 2048 and h.is_contiguous() and x.is_contiguous()):
+        return None
+    M = B * T
+    key = (M, C, w_qkv.shape[0], w_o.shape[1], w_down.shape[1], b_qkv is not None, b_o is not None)
+    plans = _BLOCK_PLANS.get(key)
+    if plans is None:
+        plans = (native_plan("linear", M, w_qkv.shape[0], C, b_qkv is not None),
+                 native_plan("linear", M, C, w_o.shape[1], b_o is not None),
+                 native_plan("mlp_swiglu", M, C, w_down.shape[1]))
+        _BLOCK_PLANS[key] = plans
+    return torch.ops.nbd.llama_block_ag(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plans[0],
+                                        plans[1], plans[2], int(n_head), int(n_kv), D ** -0.5, float(eps), cos, sin)

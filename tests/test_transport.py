@@ -242,6 +242,13 @@ def test_fd_capture_streams_python_and_c_output(tmp_path):
         d = T.Socket(T.DEALER, identity=b"w")
         d.set_int(T.OPT_STREAM_FLUSH_US, 1000)
         d.connect({ep!r})
+        # stream chunks are not queued before the connection is up (the worker streams only after
+        # its READY handshake): wait for the coordinator's ack first
+        d.send([b"HI"])
+        while True:
+            m = d.recv(30)
+            if m is not None and not m.is_event:
+                break
         d.stream_header(1, b"OUT")
         d.stream_header(2, b"ERR")
         d.capture_fds()
@@ -260,6 +267,9 @@ def test_fd_capture_streams_python_and_c_output(tmp_path):
     while time.time() < deadline:
         m = r.recv(1)
         if m is None or m.is_event:
+            continue
+        if m.frames[1] == b"HI":
+            r.send([m.frames[0], b"ACK"])
             continue
         if m.frames[1] == b"DONE":
             break
