@@ -174,6 +174,25 @@ void adamw_flat_hip(const at::Tensor& grad, const at::Tensor& param, const at::T
   }
 }
 
+// Every bucket's update from one call (FlatAdamW.step's fast path): the same per-bucket kernels
+// in bucket order, without a Python round trip and an op dispatch per bucket (an eager small-model
+// step is host-bound: docs/FINDINGS.md §27).
+void adamw_flat_multi_hip(at::TensorList grads, at::TensorList params, at::TensorList masters, at::TensorList exp_avgs,
+                          at::TensorList exp_avg_sqs, double lr, double beta1, double beta2, double eps,
+                          double weight_decay, int64_t step, double grad_scale,
+                          const c10::optional<at::Tensor>& grad_scale_t, const c10::optional<at::Tensor>& step_t,
+                          const c10::optional<at::Tensor>& lr_t) {
+  const size_t n = params.size();
+  TORCH_CHECK(grads.size() == n && masters.size() == n && exp_avgs.size() == n && exp_avg_sqs.size() == n,
+              "adamw_flat_multi: one gradient, master, exp_avg and exp_avg_sq per parameter buffer");
+  for (size_t i = 0; i < n; ++i)
+    adamw_flat_hip(grads[i], params[i], masters[i], exp_avgs[i], exp_avg_sqs[i], lr, beta1, beta2, eps, weight_decay,
+                   step, grad_scale, grad_scale_t, step_t, lr_t);
+}
+
 }  // namespace nbd
 
-TORCH_LIBRARY_IMPL(nbd, CUDA, m) { m.impl("adamw_flat", &nbd::adamw_flat_hip); }
+TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
+  m.impl("adamw_flat", &nbd::adamw_flat_hip);
+  m.impl("adamw_flat_multi", &nbd::adamw_flat_multi_hip);
+}

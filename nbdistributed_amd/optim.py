@@ -13,12 +13,17 @@ the next DDP forward, or ``ddp.wait_params()``) rebuilds the full parameters on 
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
 from . import ops
+
+
+# NBD_ADAMW_MULTI=0: one adamw_flat call per bucket (A/B of the one-call update)
+_MULTI = os.environ.get("NBD_ADAMW_MULTI", "1") != "0"
 
 
 def _capturing() -> bool:
@@ -48,10 +53,15 @@ class FlatAdamW(torch.optim.Optimizer):
         self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev) if capturable else None
         self.flat_state: List[Dict[str, torch.Tensor]] = []
         self.sharded = bool(getattr(ddp, "shard", False))
+        self._multi = None  # (grads, params, masters, exp_avgs, exp_avg_sqs) of the one-call update
         for b in ddp.buckets:
             master = self._param_slice(b).detach().float().clone()
             self.flat_state.append({"master": master, "exp_avg": torch.zeros_like(master),
                                     "exp_avg_sq": torch.zeros_like(master)})
+
+    def _joined_grads(self) -> bool:
+        """No bucket's gradient is still waited on per bucket (``wait_grad`` would be a no-op)."""
+        return getattr(self.ddp, "_joined", True) or getattr(self.ddp, "wait_grad", None) is None
 
     def _param_slice(self, b):
         return b.param_flat[b.lo:b.lo + b.shard] if self.sharded else b.param_flat
@@ -69,6 +79,21 @@ class FlatAdamW(torch.optim.Optimizer):
             self.step_t.add_(1.0)
             if not _capturing():
                 self.lr_t.fill_(float(g["lr"]))
+        if (_MULTI and not self.sharded and self.ddp.buckets[0].param_flat.is_cuda
+                and (self._joined_grads() or getattr(self.ddp, "world", 1) == 1)):
+            # all updates from one call.  (At world 1 there is no collective for a per-bucket wait
+            # to overlap with: one join of the side stream, if any, then every bucket.)
+            if not self._joined_grads():
+                self.ddp.wait_grads()
+            if self._multi is None:
+                self._multi = ([self._grad(b) for b in self.ddp.buckets], [b.param_flat for b in self.ddp.buckets],
+                               [st["master"] for st in self.flat_state], [st["exp_avg"] for st in self.flat_state],
+                               [st["exp_avg_sq"] for st in self.flat_state])
+            torch.ops.nbd.adamw_flat_multi(*self._multi, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                           float(g["weight_decay"]), max(self.step_count, 1), 1.0, self._clip_coef,
+                                           self.step_t, self.lr_t)
+            self._clip_coef = None
+            return loss
         pairs = list(zip(self.ddp.buckets, self.flat_state))
         if self.sharded:
             # a previous step's gathers still reading our slices must finish before the update
