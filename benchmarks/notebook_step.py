@@ -58,7 +58,7 @@ def main():
             fwd = model
         else:
             fwd = NbdDDP(model.to(dev, torch.bfloat16), flat_params=True, grad_mode="bucket")
-            opt = FlatAdamW(fwd, lr=2e-5, capturable=mode == "nbdgraph")
+            opt = FlatAdamW(fwd, lr=2e-5, capturable=mode == "nbdgraph")  # overlap: NBD_ADAMW_OVERLAP
         batches = [(ids[i * a.bs:(i + 1) * a.bs], mask[i * a.bs:(i + 1) * a.bs], labels[i * a.bs:(i + 1) * a.bs])
                    for i in range(8)]
 

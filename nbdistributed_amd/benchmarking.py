@@ -356,7 +356,9 @@ def _nbd_notebook_bench(steps, warm, bs=16, seq=128, mode="reference", small=Fal
         model = _NbdDDP(LlamaForSequenceClassification(lc).to(
             device, torch.bfloat16 if device.type == "cuda" else torch.float32), flat_params=True, grad_mode="bucket")
         graph = mode == "nbd_graph"
-        opt = _FlatAdamW(model, lr=2e-5, capturable=graph)
+        # eager: each bucket updated during backward (FlatAdamW(overlap=True): this step is
+        # host-bound, the GPU has room for the update; one rank only, and never inside a graph)
+        opt = _FlatAdamW(model, lr=2e-5, capturable=graph, overlap=not graph)
         sched = get_linear_schedule_with_warmup(opt, 100, 3 * (n // (bs * world_size)))
         sl = slice(rank * (n // world_size), (rank + 1) * (n // world_size))
         ids, mask, labels = ids[sl].to(device), mask[sl].to(device), labels[sl].to(device)
@@ -398,7 +400,8 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
                            "reference_ms_per_step": REFERENCE_NOTEBOOK_MS_PER_STEP,
                            "reference_samples_per_s": 32 / (REFERENCE_NOTEBOOK_MS_PER_STEP / 1e3)}
     recipes = {"reference": "HF model, fp32, accelerate DDP, torch AdamW (the notebook's recipe)",
-               "nbd": "native Llama (HIP kernels), bf16 params + fp32 master (FlatAdamW), nbd DDP",
+               "nbd": "native Llama (HIP kernels, one autograd node per block), bf16 params + fp32 master "
+                       "(FlatAdamW, buckets updated during backward at world 1), nbd DDP",
                "nbd_graph": "as nbd, whole step captured in one HIP graph (GraphedStep)"}
     modes = ["reference", "nbd"]
     # graph capture with RCCL collectives is verified at world size 1 on this pool; at N > 1 it

@@ -24,6 +24,8 @@ from . import ops
 
 # NBD_ADAMW_MULTI=0: one adamw_flat call per bucket (A/B of the one-call update)
 _MULTI = os.environ.get("NBD_ADAMW_MULTI", "1") != "0"
+# default of FlatAdamW(overlap=None): update each bucket during backward (NBD_ADAMW_OVERLAP=1)
+_OVERLAP = os.environ.get("NBD_ADAMW_OVERLAP", "0") == "1"
 
 
 def _capturing() -> bool:
@@ -36,11 +38,21 @@ class FlatAdamW(torch.optim.Optimizer):
     (the bucket kernels apply one lr / weight decay to the whole model)."""
 
     def __init__(self, ddp, lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 1e-2, capturable: bool = False):
+                 weight_decay: float = 1e-2, capturable: bool = False, overlap: Optional[bool] = None):
         """``capturable=True``: the step counter and lr live in device memory (``step_t``,
         ``lr_t``) so the update can be captured in a HIP graph and replayed
         (:class:`nbdistributed_amd.graphs.GraphedStep` calls :meth:`sync_hyper` before each
-        replay to push the current ``param_groups[0]['lr']``)."""
+        replay to push the current ``param_groups[0]['lr']``).
+
+        ``overlap=True`` (one rank, unsharded, eager): each bucket is updated on a side stream as
+        soon as DDP finalises its gradient during backward, so the memory-bound update runs under
+        the rest of the backward; ``step()`` then only completes the bookkeeping.  It pays where
+        the eager step is host-bound (small models: the GPU idles between launches), not where
+        the GPU is busy (GPT-2 small: 1.7 % slower) and not inside a HIP graph (skipped there).
+        Call ``step()`` once after every synchronising backward (the update happens in that
+        backward).  At world
+        size > 1 it falls back to the update in ``step()`` (the bucket is final only after its
+        collective).  ``None``: ``NBD_ADAMW_OVERLAP=1`` turns it on."""
         if not getattr(ddp, "flat_params", False) or ddp.grad_mode != "bucket":
             raise ValueError("FlatAdamW needs DistributedDataParallel(..., flat_params=True, grad_mode='bucket')")
         super().__init__(list(ddp.params), dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
@@ -54,6 +66,13 @@ class FlatAdamW(torch.optim.Optimizer):
         self.flat_state: List[Dict[str, torch.Tensor]] = []
         self.sharded = bool(getattr(ddp, "shard", False))
         self._multi = None  # (grads, params, masters, exp_avgs, exp_avg_sqs) of the one-call update
+        if overlap is None:
+            overlap = _OVERLAP
+        self.overlap = bool(overlap) and not self.sharded and getattr(ddp, "world", 1) == 1 and dev.type == "cuda"
+        self._updated: List[int] = []  # buckets updated during the current backward (overlap)
+        if self.overlap:
+            self._opt_stream = torch.cuda.Stream(device=dev)
+            ddp._on_bucket_ready = self._update_bucket
         for b in ddp.buckets:
             master = self._param_slice(b).detach().float().clone()
             self.flat_state.append({"master": master, "exp_avg": torch.zeros_like(master),
@@ -69,9 +88,51 @@ class FlatAdamW(torch.optim.Optimizer):
     def _grad(self, b):
         return b.grad_shard if self.sharded else b.buffer
 
+    # ------------------------------------------------------------------ overlap (update in backward)
+    @torch.no_grad()
+    def _update_bucket(self, b) -> None:
+        """DDP callback (``_on_bucket_ready``): bucket ``b``'s gradient is final — update it on the
+        side stream now (inside backward; joined back at the end of backward)."""
+        if _capturing():
+            # not inside a HIP graph: the side-stream branches made the graphed SmolLM2 step 11 %
+            # slower (profiles/adamw_overlap_ab_r3.txt); step() updates the captured step
+            return
+        if self._clip_coef is not None:
+            raise RuntimeError("FlatAdamW(overlap=True) updates during backward: clip_grad_norm_ cannot apply")
+        dev = b.param_flat.device
+        cur = torch.cuda.current_stream(dev)
+        if not self._updated:  # first bucket of this backward: the step's bookkeeping
+            self.step_count += 1
+            if self.capturable:
+                self._opt_stream.wait_stream(cur)
+                with torch.cuda.stream(self._opt_stream):
+                    self.step_t.add_(1.0)
+                    if not _capturing():
+                        self.lr_t.fill_(float(self.param_groups[0]["lr"]))
+            torch.autograd.Variable._execution_engine.queue_callback(self._join)
+        done = getattr(b, "done", None)
+        if getattr(self.ddp, "_side", False) and getattr(self.ddp, "_per_bucket_wait", False) and done is not None:
+            self._opt_stream.wait_event(done)  # the bucket was finished on DDP's comm stream
+        self._opt_stream.wait_stream(cur)
+        g = self.param_groups[0]
+        st = self.flat_state[b.index]
+        b1, b2 = g["betas"]
+        with torch.cuda.stream(self._opt_stream):
+            ops.adamw_flat(self._grad(b), self._param_slice(b), st["master"], st["exp_avg"], st["exp_avg_sq"], g["lr"],
+                           b1, b2, g["eps"], g["weight_decay"], max(self.step_count, 1), step_t=self.step_t,
+                           lr_t=self.lr_t)
+        self._updated.append(b.index)
+
+    def _join(self) -> None:
+        torch.cuda.current_stream(self._opt_stream.device).wait_stream(self._opt_stream)
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        if self.overlap and self._updated:
+            # every bucket was updated during backward (DDP finalises each one, unused ones too)
+            self._updated = []
+            return loss
         g = self.param_groups[0]
         self.step_count += 1
         b1, b2 = g["betas"]

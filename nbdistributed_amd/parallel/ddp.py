@@ -205,6 +205,7 @@ class DistributedDataParallel(torch.nn.Module):
         # flush (before a bucket's collective, at the end of backward) — ops.graddst.defer_enable
         # (process-wide switch; NBD_GRAD_DEFER=0 turns it off for A/B runs).  Every DDP with slices
         # flushes, whoever enabled it.
+        self._on_bucket_ready = None  # FlatAdamW(overlap=True): update a bucket as soon as it is final
         self._defer = bool(self._n_views)
         if self._defer:
             from ..ops import graddst
@@ -442,8 +443,8 @@ class DistributedDataParallel(torch.nn.Module):
             graddst.defer_flush()
 
     def _launch(self, b: _Bucket) -> None:
-        if self.world > 1:
-            self._flush_deferred()  # the collective reads the slices: their reduces go first
+        if self.world > 1 or self._on_bucket_ready is not None:
+            self._flush_deferred()  # the collective / the update reads the slices: their reduces go first
         n_in, rest = self._split_in_place(b)
         if n_in == 0 and not b.partial:
             self._launch_flat(b)
@@ -502,6 +503,8 @@ class DistributedDataParallel(torch.nn.Module):
             if not self.cuda:
                 b.rest_grads = []
         b.launched = True
+        if self._on_bucket_ready is not None:
+            self._on_bucket_ready(b)
 
     def _launch_flat(self, b: _Bucket) -> None:
         """No gradient in place: flatten (pre-divided by the world size) -> all-reduce SUM ->
@@ -545,6 +548,8 @@ class DistributedDataParallel(torch.nn.Module):
             if not self.cuda:
                 b.grads = []
         b.launched = True
+        if self._on_bucket_ready is not None:
+            self._on_bucket_ready(b)
 
     def _finalize(self) -> None:
         self._flush_deferred()

@@ -111,3 +111,44 @@ def test_fused_block_ddp_buckets_bit_identical(sess):
     r = sess.execute("import contextlib\n" + CODE, render=False)
     assert r.ok, r.errors
     assert r.results[0]["echo"] == "(True, True, True)", r.results[0]
+
+
+CODE_OVERLAP = """
+import copy
+from nbdistributed_amd.models.llama import LlamaConfig, LlamaForSequenceClassification
+from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP
+from nbdistributed_amd.optim import FlatAdamW
+from nbdistributed_amd.graphs import GraphedStep
+torch.manual_seed(6)
+base = LlamaForSequenceClassification(LlamaConfig.smollm2_135m(num_hidden_layers=2)).to(device, torch.bfloat16)
+ids = torch.randint(1, 49152, (8, 128), generator=torch.Generator().manual_seed(1)).to(device)
+lab = torch.ones(8, dtype=torch.long, device=device)
+res = []
+for graphed in (False, True):
+    outs = []
+    for overlap in (False, True):
+        m = NbdDDP(copy.deepcopy(base), flat_params=True, grad_mode="bucket", bucket_cap_mb=4.0)
+        o = FlatAdamW(m, lr=1e-3, capturable=graphed, overlap=overlap)
+        def step(x, y):
+            loss = m(x, torch.ones_like(x), y)[0]
+            loss.backward()
+            o.step()
+            o.zero_grad()
+            return loss.detach()
+        call = GraphedStep(step, (ids, lab), warmup=2, optimizers=[o]) if graphed else step
+        for _ in range(4):
+            call(ids, lab)
+        torch.cuda.synchronize()
+        outs.append(torch.cat([b.param_flat.float() for b in m.buckets]))
+        m.unpatch()
+    res.append(torch.equal(outs[0], outs[1]))
+tuple(res)
+"""
+
+
+def test_flat_adamw_overlap_matches_step(sess):
+    """FlatAdamW(overlap=True) (buckets updated on a side stream during backward) leaves exactly
+    the parameters of the update in step(), eager and as a HIP graph."""
+    r = sess.execute(CODE_OVERLAP, render=False)
+    assert r.ok, r.errors
+    assert r.results[0]["echo"] == "(True, True)", r.results[0]
