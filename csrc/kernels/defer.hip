@@ -251,7 +251,9 @@ bool push(Item&& it, void* stream) {
 }  // namespace
 
 bool enabled() { return g_enabled.load(std::memory_order_relaxed); }
-bool want() { return t_scope && enabled(); }
+std::atomic<bool> g_force{false};  // benchmarks: queue every split-K reduce (no scope needed)
+bool want() { return (t_scope || g_force.load(std::memory_order_relaxed)) && enabled(); }
+void set_force(bool on) { g_force.store(on, std::memory_order_relaxed); }
 Scope::Scope(bool on) : prev(t_scope) { t_scope = on; }
 Scope::~Scope() { t_scope = prev; }
 

@@ -105,6 +105,7 @@ std::tuple<at::Tensor, bool> grad_dest_claim(const at::Tensor& param) {
 
 void grad_defer_enable(bool on) { defer::set_enabled(on); }
 void grad_defer_flush() { defer::flush(); }
+void grad_defer_force(bool on) { defer::set_force(on); }
 int64_t grad_defer_pending() { return defer::pending(); }
 
 }  // namespace graddst
@@ -119,5 +120,6 @@ TORCH_LIBRARY_FRAGMENT(nbd, m) {
   m.def("grad_dest_join(Tensor param) -> Tensor", &nbd::graddst::grad_dest_join);
   m.def("grad_defer_enable(bool on) -> ()", &nbd::graddst::grad_defer_enable);
   m.def("grad_defer_flush() -> ()", &nbd::graddst::grad_defer_flush);
+  m.def("grad_defer_force(bool on) -> ()", &nbd::graddst::grad_defer_force);
   m.def("grad_defer_pending() -> int", &nbd::graddst::grad_defer_pending);
 }

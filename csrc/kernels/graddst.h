@@ -40,7 +40,8 @@ at::Tensor hand_back(const at::Tensor& param, const at::Tensor& dst, bool acc);
 namespace defer {
 bool enabled();
 void set_enabled(bool on);
-bool want();  // enabled and inside a Scope(true) on this thread
+bool want();  // enabled and inside a Scope(true) on this thread (or forced)
+void set_force(bool on);  // benchmarks only: treat every split-K reduce as deferrable
 struct Scope {
   explicit Scope(bool on);
   ~Scope();

@@ -80,6 +80,8 @@ _PAIR_TUNED = {
     (2048, 960, 576, EPI_NONE): 2 | 16,    # smollm2.qkv   15.5 us (16.1)
     (2048, 576, 576, EPI_NONE): 2 | 16,    # smollm2.o_proj 12.9 us (13.4)
     (2048, 3072, 576, EPI_NONE): 1,        # smollm2.gate_up 25.0 us
+    (2048, 576, 1536, EPI_DSWIGLU): 1 | 16,  # smollm2.down (+SwiGLU') 18.4-18.7 us (model: S=2 input first 23.4-25.5;
+                                             # profiles/pair_sched_smollm2_r3.txt)
 }
 
 
