@@ -172,7 +172,8 @@ _TUNED = {
     (False, False, 2048, 960, 576): (3064064, 1),  # smollm2.qkv fwd 13.5 us
     (False, True, 2048, 576, 960): (3064064, 1),  # smollm2.qkv dgrad 14.9 us
     (True, True, 960, 576, 2048): (203064064, 1),  # smollm2.qkv wgrad 13.2 us (15.3 one K-group)
-    (False, False, 2048, 576, 576): (2064064, 1),  # smollm2.o_proj fwd 12.6 us
+    (False, False, 2048, 576, 576): (3064064, 1),  # smollm2.o_proj fwd 7.3 us vs 7.9 (2-stage;
+                                                   # profiles/gemm_fwd_smollm2_r3.txt)
     (False, True, 2048, 576, 576): (2064064, 1),  # smollm2.o_proj dgrad 13.0 us
     (True, True, 576, 576, 2048): (203064064, 1),  # smollm2.o_proj wgrad 13.2 us (15.0)
     (False, False, 2048, 3072, 576): (2064128, 1),  # smollm2.gate_up fwd 19.4 us
