@@ -99,12 +99,15 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const T* __restrict__ x, con
   const int64_t row = (int64_t)blockIdx.x * (NT / kWave) + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int64_t base = row * C;
-  float v[NCH][4];
+  float v[NCH][4], g[NCH][4], b[NCH][4];
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int c = 4 * lane + 256 * k;
     if (c < C) {
+      // γ / β first: their latency hides under the row's, not after the reductions
+      load4<W>(gamma + c, g[k]);
+      if (!RMS) load4<W>(beta + c, b[k]);
       load4<T>(x + base + c, v[k]);
       if (RES) {
         float d[4];
@@ -136,11 +139,9 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const T* __restrict__ x, con
   for (int k = 0; k < NCH; ++k) {
     const int c = 4 * lane + 256 * k;
     if (c < C) {
-      float g[4], b[4] = {0.f, 0.f, 0.f, 0.f}, o[4];
-      load4<W>(gamma + c, g);
-      if (!RMS) load4<W>(beta + c, b);
+      float o[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = fmaf((v[k][e] - mean) * rstd, g[e], b[e]);
+      for (int e = 0; e < 4; ++e) o[e] = fmaf((v[k][e] - mean) * rstd, g[k][e], RMS ? 0.f : b[k][e]);
       store4<T>(y + base + c, o);
     }
   }
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, con
             s1 += gy;
             s2 = fmaf(gy, xh, s2);
             ag[k][e] = fmaf(dv[j][k][e], xh, ag[k][e]);
-            ab[k][e] += dv[j][k][e];
+            if (!RMS) ab[k][e] += dv[j][k][e];  // RMSNorm has no β: no Σdy partials
             dv[j][k][e] = gy;
           }
         }
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, con
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           red[0][wave - 1][c + e] = ag[k][e];
-          red[1][wave - 1][c + e] = ab[k][e];
+          if (!RMS) red[1][wave - 1][c + e] = ab[k][e];
         }
     }
   }
@@ -271,10 +272,10 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, con
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             ag[k][e] += red[0][w][c + e];
-            ab[k][e] += red[1][w][c + e];
+            if (!RMS) ab[k][e] += red[1][w][c + e];
           }
-        store4<float>(part_g + (int64_t)blockIdx.x * 2 * C + c, ag[k]);      // [blk][0, C)
-        store4<float>(part_g + (int64_t)blockIdx.x * 2 * C + C + c, ab[k]);  // [blk][C, 2C)
+        store4<float>(part_g + (int64_t)blockIdx.x * 2 * C + c, ag[k]);                // [blk][0, C)
+        if (!RMS) store4<float>(part_g + (int64_t)blockIdx.x * 2 * C + C + c, ab[k]);  // [blk][C, 2C)
       }
     }
   }
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(NT) void ln_bwd16_kernel(const T* __restrict__ x, c
           s1 += gy;
           s2 = fmaf(gy, xh, s2);
           ag[k][e] = fmaf(df[e] * lv, xh, ag[k][e]);
-          ab[k][e] = fmaf(df[e], lv, ab[k][e]);
+          if (!RMS) ab[k][e] = fmaf(df[e], lv, ab[k][e]);
         }
       }
       const float m1 = RMS ? 0.f : hsum(s1) / (float)C, m2 = hsum(s2) / (float)C;
@@ -394,7 +395,7 @@ __global__ __launch_bounds__(NT) void ln_bwd16_kernel(const T* __restrict__ x, c
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       ag[k][e] += __shfl_xor(ag[k][e], 32, kWave);
-      ab[k][e] += __shfl_xor(ab[k][e], 32, kWave);
+      if (!RMS) ab[k][e] += __shfl_xor(ab[k][e], 32, kWave);
     }
   if (wave > 0 && half == 0) {
 #pragma unroll
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(NT) void ln_bwd16_kernel(const T* __restrict__ x, c
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         red[0][wave - 1][8 * hl + 256 * k + e] = ag[k][e];
-        red[1][wave - 1][8 * hl + 256 * k + e] = ab[k][e];
+        if (!RMS) red[1][wave - 1][8 * hl + 256 * k + e] = ab[k][e];
       }
   }
   __syncthreads();
@@ -415,10 +416,10 @@ __global__ __launch_bounds__(NT) void ln_bwd16_kernel(const T* __restrict__ x, c
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           ag[k][e] += red[0][w][c + e];
-          ab[k][e] += red[1][w][c + e];
+          if (!RMS) ab[k][e] += red[1][w][c + e];
         }
       store8<float>(part_g + (int64_t)blockIdx.x * 2 * C + c, ag[k]);
-      store8<float>(part_g + (int64_t)blockIdx.x * 2 * C + C + c, ab[k]);
+      if (!RMS) store8<float>(part_g + (int64_t)blockIdx.x * 2 * C + C + c, ab[k]);
     }
   }
 }

@@ -47,6 +47,35 @@ def test_flash_forward_backward(dev, causal, B, H, T):
         assert _rel(a, b) < 3e-2, (name, _rel(a, b))
 
 
+_GQA_CASES = [(2, 9, 3, 128), (4, 8, 2, 256), (1, 6, 1, 384), (16, 9, 3, 128)]
+
+
+def _gqa_case(dev, B, H, Hkv, T, causal):
+    g = torch.Generator(device="cpu").manual_seed(B * 100 + H * 10 + Hkv + T)
+    q, do = (torch.randn(B, H, T, 64, generator=g).to(dev, torch.bfloat16) for _ in range(2))
+    k, v = (torch.randn(B, Hkv, T, 64, generator=g).to(dev, torch.bfloat16) for _ in range(2))
+    qh, kh, vh = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
+    out = ops.flash_attention(qh, kh, vh, causal=causal, scale=0.125)
+    out.backward(do)
+    torch.cuda.synchronize()
+    return (q, k, v, do), (out, qh.grad, kh.grad, vh.grad)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("B,H,Hkv,T", _GQA_CASES)
+def test_flash_gqa_backward(dev, causal, B, H, Hkv, T):
+    """Grouped-query backward, incl. the query-head groups split over workgroups and summed by
+    gqa_reduce_kernel (B·Hkv·T/128 < 256), against fp32 attention on repeated K/V."""
+    (q, k, v, do), (out, dq, dk, dv) = _gqa_case(dev, B, H, Hkv, T, causal)
+    rep = H // Hkv
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = ref_attn(qr, kr.repeat_interleave(rep, 1), vr.repeat_interleave(rep, 1), causal, 0.125)
+    ref.backward(do.float())
+    assert _rel(out, ref) < 2e-2
+    for name, a, b in (("dq", dq, qr.grad), ("dk", dk, kr.grad), ("dv", dv, vr.grad)):
+        assert _rel(a, b) < 3e-2, (name, _rel(a, b))
+
+
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_deferred_rescale_branch(dev, causal):
     """Scores that grow along the keys, by a different rate per query: some waves rescale O at
