@@ -7,19 +7,21 @@
 // benchmarks/ddp_compare.py flatgraph).  This version only uses caching-allocator memory and
 // fixed launch shapes, so it captures and replays, and it is cheaper:
 //
-//   count    counts[v] = #tokens with id v                (int atomics)
+//   count    counts[v] = #tokens with id v  (int atomics; the lanes of a wave that share its
+//            first id — a padding run — count with one)
 //   scan     offsets = exclusive_scan(counts): per-1024 block scans + block sums, then each block
 //            adds the sum of the blocks before it (two fully parallel launches)
-//   place    slot = offsets[v] + atomicAdd(cursor[v]) ; order[slot] = token position
+//   place    slot = offsets[v] + atomicAdd(cursor[v]) ; order[slot] = token position (same
+//            one-atomic-per-wave rule for the first id, ranked by lane)
 //   partial  one wave per 16 consecutive sorted slots: runs of equal ids are summed in fp32 and
-//            flushed into acc[offsets[v]] (a [N, C] scratch; float atomics only for a run shared
-//            with a neighbouring wave) — a frequent id
-//            (padding!) is spread over many waves instead of one wave looping over hundreds of
-//            occurrences (which took 550 µs per step on the notebook's right-padded batches)
-//   rows     one wave per vocabulary row: cast acc[offsets[v]] (or zeros) into the gradient —
-//            written exactly once, no separate zero-fill.
-// Float atomics make the summation order run-to-run dependent (DDP ranks still agree after the
-// all-reduce).
+//            stored into scratch row max(offsets[v], first slot of the wave) of a [N, C] scratch
+//            — a frequent id (padding!) is spread over many waves instead of one wave looping
+//            over hundreds of occurrences (550 µs per step on the notebook's right-padded
+//            batches), and no float atomics: every scratch row has one writer, none is zeroed
+//   rows     one wave per vocabulary row: the run's rows (one per wave it reached) summed and
+//            cast into the gradient (or zeros) — written exactly once, no separate zero-fill.
+// The order of equal ids inside a run follows the cursor atomics, so the fp32 summation order can
+// differ run to run (DDP ranks still agree after the all-reduce).
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -36,12 +38,29 @@ namespace embed {
 constexpr int NT = 256;
 constexpr int kScanT = 1024;
 
+// the id of the wave's first lane with a valid id (-1 if none): the wave's most likely repeat
+__device__ __forceinline__ int wave_first_id(bool ok, int v) {
+  const uint64_t m = __ballot(ok);
+  if (m == 0) return -1;
+  return __shfl(v, __ffsll((unsigned long long)m) - 1, kWave);
+}
+
 __global__ __launch_bounds__(NT) void count_kernel(const int64_t* __restrict__ idx, int64_t n, int V,
                                                    int* __restrict__ counts, int* __restrict__ bad) {
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-    const int64_t v = idx[i];
-    if (v >= 0 && v < V) atomicAdd(&counts[v], 1);
-    else atomicOr(bad, 1);  // out-of-range id: flagged, never written out of bounds
+  for (int64_t i0 = (int64_t)blockIdx.x * NT; i0 < n; i0 += (int64_t)gridDim.x * NT) {
+    const int64_t i = i0 + threadIdx.x;
+    const int64_t v = i < n ? idx[i] : -1;
+    const bool ok = i < n && v >= 0 && v < V;
+    if (i < n && !ok) atomicOr(bad, 1);  // out-of-range id: flagged, never written out of bounds
+    // lanes holding the wave's first valid id count it with one atomic (a padding run would
+    // otherwise be hundreds of same-address atomics in a row)
+    const int lead = wave_first_id(ok, (int)v);
+    const uint64_t same = __ballot(ok && v == lead);
+    if (ok && v == lead) {
+      if (__lane_id() == (unsigned)(__ffsll((unsigned long long)same) - 1)) atomicAdd(&counts[v], (int)__popcll(same));
+    } else if (ok) {
+      atomicAdd(&counts[v], 1);
+    }
   }
 }
 
@@ -82,9 +101,22 @@ __global__ __launch_bounds__(kScanT) void scan_add_kernel(int* __restrict__ offs
 __global__ __launch_bounds__(NT) void place_kernel(const int64_t* __restrict__ idx, int64_t n, int V,
                                                    const int* __restrict__ offsets, int* __restrict__ cursor,
                                                    int* __restrict__ order) {
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-    const int64_t v = idx[i];
-    if (v >= 0 && v < V) order[offsets[v] + atomicAdd(&cursor[v], 1)] = (int)i;
+  for (int64_t i0 = (int64_t)blockIdx.x * NT; i0 < n; i0 += (int64_t)gridDim.x * NT) {
+    const int64_t i = i0 + threadIdx.x;
+    const int64_t v = i < n ? idx[i] : -1;
+    const bool ok = i < n && v >= 0 && v < V;
+    const int lead = wave_first_id(ok, (int)v);
+    const uint64_t same = __ballot(ok && v == lead);
+    if (ok && v == lead) {  // one cursor atomic for the wave's lanes of the first id, ranked by lane
+      const int first = __ffsll((unsigned long long)same) - 1;
+      int base = 0;
+      if (__lane_id() == (unsigned)first) base = atomicAdd(&cursor[v], (int)__popcll(same));
+      base = __shfl(base, first, kWave);
+      const int rank = (int)__popcll(same & ((1ull << __lane_id()) - 1));
+      order[offsets[v] + base + rank] = (int)i;
+    } else if (ok) {
+      order[offsets[v] + atomicAdd(&cursor[v], 1)] = (int)i;
+    }
   }
 }
 
@@ -137,10 +169,7 @@ __global__ __launch_bounds__(NT) void partial_kernel(const T* __restrict__ dy, i
     my_row = order[s0 + lane];
     my_v = (int)idx[my_row];
   }
-  const int v_first = __builtin_amdgcn_readlane(my_v, 0), v_last = __builtin_amdgcn_readlane(my_v, ns - 1);
-  // the first run started in an earlier wave's slots / the last one goes on past ours
-  const bool shared_first = offsets[v_first] < s0;
-  const bool shared_last = offsets[v_last + 1] > s0 + ns;
+  const int v_first = __builtin_amdgcn_readlane(my_v, 0);
   float run[NCH][4];
   auto zero = [&]() {
 #pragma unroll
@@ -148,20 +177,15 @@ __global__ __launch_bounds__(NT) void partial_kernel(const T* __restrict__ dy, i
 #pragma unroll
       for (int e = 0; e < 4; ++e) run[k][e] = 0.f;
   };
+  // a run's sum over this wave's slots goes to scratch row max(offsets[v], s0): the run's first
+  // slot, or this wave's first slot when the run started in an earlier wave — every row written
+  // by exactly one wave, plain stores, no zero-fill; rows_kernel adds a run's per-wave rows
   auto flush = [&](int v) {
-    float* dst = acc + (int64_t)offsets[v] * C;
-    const bool atomic = (v == v_first && shared_first) || (v == v_last && shared_last);
+    float* dst = acc + (int64_t)max(offsets[v], (int)s0) * C;
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       const int c = 4 * lane + 256 * k;
-      if (c < C) {
-        if (atomic) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) atomicAdd(dst + c + e, run[k][e]);
-        } else {
-          *reinterpret_cast<float4*>(dst + c) = make_float4(run[k][0], run[k][1], run[k][2], run[k][3]);
-        }
-      }
+      if (c < C) *reinterpret_cast<float4*>(dst + c) = make_float4(run[k][0], run[k][1], run[k][2], run[k][3]);
     }
   };
   zero();
@@ -208,7 +232,8 @@ __global__ __launch_bounds__(NT) void rows_kernel(const float* __restrict__ acc,
   const int64_t v = (int64_t)blockIdx.x * (NT / kWave) + (threadIdx.x >> 6);
   if (v >= R) return;
   const int b = v < V ? offsets[v] : 0;
-  const bool hit = v < V && offsets[v + 1] > b;
+  const int e = v < V ? offsets[v + 1] : 0;
+  const bool hit = e > b;
   if (accumulate && !hit) return;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
@@ -218,6 +243,19 @@ __global__ __launch_bounds__(NT) void rows_kernel(const float* __restrict__ acc,
       if (hit) {
         const float4 a = *reinterpret_cast<const float4*>(acc + (int64_t)b * C + c);
         x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+        // a run longer than one wave's slots: one more row per wave it reached (first slots of
+        // those waves), four loads in flight at a time
+        for (int r = (b / kSlots + 1) * kSlots; r < e; r += 4 * kSlots) {
+          float4 y[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            y[u] = r + u * kSlots < e ? *reinterpret_cast<const float4*>(acc + (int64_t)(r + u * kSlots) * C + c)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            x[0] += y[u].x; x[1] += y[u].y; x[2] += y[u].z; x[3] += y[u].w;
+          }
+        }
       }
       if (accumulate) {
         float o[4];
@@ -340,13 +378,14 @@ at::Tensor embedding_bwd_hip(const at::Tensor& dy, const at::Tensor& idx, int64_
   }
   const int64_t R = grad.size(0);
   auto io = idx.options().dtype(at::kInt);
-  at::Tensor counts = at::zeros({V + 1}, io);  // [V] counts, [V] = out-of-range flag
-  at::Tensor cursor = at::zeros({V}, io);
+  at::Tensor cc = at::zeros({2 * V + 1}, io);  // one fill: counts [0, V], flag [V], cursor [V+1, 2V+1)
+  at::Tensor counts = cc.narrow(0, 0, V + 1);
+  at::Tensor cursor = cc.narrow(0, V + 1, V);
   at::Tensor offsets = at::empty({V + 1}, io);
   const int nsb = (int)((V + kScanT - 1) / kScanT);
   at::Tensor bsum = at::empty({nsb}, io);
   at::Tensor order = at::empty({std::max<int64_t>(N, 1)}, io);
-  at::Tensor acc = at::zeros({std::max<int64_t>(N, 1), C}, dy.options().dtype(at::kFloat));
+  at::Tensor acc = at::empty({std::max<int64_t>(N, 1), C}, dy.options().dtype(at::kFloat));  // rows read = rows written
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   const int blocks = (int)std::min<int64_t>((N + NT - 1) / NT + 1, 1024);

@@ -97,12 +97,18 @@ def test_gpt2_fused_path_matches_reference(dev):
         assert _rel(p.grad, q.grad) < 6e-2, n
 
 
+@pytest.mark.parametrize("layout", ["head_repeat", "right_padded"])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("V,C,N", [(50257, 768, 8192), (1024, 256, 512), (7, 64, 1000), (33, 4096, 5)])
-def test_embedding_backward(dev, dt, V, C, N):
+@pytest.mark.parametrize("V,C,N", [(50257, 768, 8192), (1024, 256, 512), (7, 64, 1000), (33, 4096, 5), (49152, 576, 2048)])
+def test_embedding_backward(dev, dt, V, C, N, layout):
     g = torch.Generator(device="cpu").manual_seed(V + N)
     idx = torch.randint(0, V, (N,), generator=g)
-    idx[: N // 4] = idx[0]  # one heavily repeated id
+    if layout == "head_repeat":
+        idx[: N // 4] = idx[0]  # one heavily repeated id
+    else:  # 16 right-padded rows: each row's tail is the pad id 2 (runs across many waves' slots)
+        r = idx.view(16, -1) if N % 16 == 0 else idx.view(1, -1)
+        for i in range(r.shape[0]):
+            r[i, int(torch.randint(1, r.shape[1] + 1, (1,), generator=g)):] = 2 % V
     w = torch.randn(V, C, generator=g).to(dev, dt).requires_grad_(True)
     dy = torch.randn(N, C, generator=g).to(dev, dt)
     ops.embedding(idx.to(dev), w).backward(dy)
