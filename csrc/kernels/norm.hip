@@ -153,12 +153,21 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const T* __restrict__ x, con
 
 // ============================================================================ backward
 constexpr int kBwdRows = 16;  // max rows per workgroup (4 per wave, two at a time)
-constexpr int kRpi = 2;       // rows per wave iteration
+// rows per wave iteration: 2 (ln_bwd_kernel's kRpi), or 1 with 4-row workgroups for small
+// inputs (SmolLM2's 2048 rows: 512 workgroups of one row per wave instead of 256 of two)
 
 // rows per workgroup: 16 for large inputs (GPT-2: 8192 rows -> 512 workgroups), fewer when that
 // would leave the chip under-filled, but at least 8 so all four waves hold rows (SmolLM2 at
 // 16 x 128 tokens: 2048 rows -> 8 per workgroup; with 4, two of the four waves idled and the
 // weight-gradient partial rows doubled)
+static bool small_rows_enabled() {  // NBD_LN_BWD_RPI1=0: keep 8-row workgroups (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("NBD_LN_BWD_RPI1");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 static int bwd_rows_per_block(int64_t rows) {
   static const int forced = [] {  // NBD_LN_BWD_ROWS: A/B override (4 .. 64)
     const char* e = std::getenv("NBD_LN_BWD_ROWS");
@@ -168,10 +177,11 @@ static int bwd_rows_per_block(int64_t rows) {
   if (forced) return forced;
   int r = kBwdRows;
   while (r > 8 && (rows + r - 1) / r < 512) r /= 2;
+  if (r == 8 && (rows + 7) / 8 < 512 && small_rows_enabled()) r = 4;  // one row per wave (kRpi 1)
   return r;
 }
 
-template <typename T, typename W, bool RES, int NCH, bool RMS = false>
+template <typename T, typename W, bool RES, int NCH, bool RMS = false, int kRpi = 2>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                     const T* __restrict__ dres, const W* __restrict__ gamma,
                                                     const float* __restrict__ mean_in,
@@ -617,12 +627,17 @@ static void launch_bwd(bool res, const at::Tensor& x, const at::Tensor& dy, cons
       return;
     }
   }
-  if (res)
-    hipLaunchKernelGGL((ln_bwd_kernel<T, W, true, N, RMS>), dim3(nblk), dim3(NT), 0, st, xp, dyp, dr, wp, mean, rstd,
-                       dxp, pgp, rows, (int)C, rpb);
-  else
-    hipLaunchKernelGGL((ln_bwd_kernel<T, W, false, N, RMS>), dim3(nblk), dim3(NT), 0, st, xp, dyp, dr, wp, mean, rstd,
-                       dxp, pgp, rows, (int)C, rpb);
+  auto go = [&](auto rpi) {
+    constexpr int R = decltype(rpi)::value;
+    if (res)
+      hipLaunchKernelGGL((ln_bwd_kernel<T, W, true, N, RMS, R>), dim3(nblk), dim3(NT), 0, st, xp, dyp, dr, wp, mean,
+                         rstd, dxp, pgp, rows, (int)C, rpb);
+    else
+      hipLaunchKernelGGL((ln_bwd_kernel<T, W, false, N, RMS, R>), dim3(nblk), dim3(NT), 0, st, xp, dyp, dr, wp, mean,
+                         rstd, dxp, pgp, rows, (int)C, rpb);
+  };
+  if (rpb == 4) go(std::integral_constant<int, 1>{});  // 4 rows = one per wave
+  else go(std::integral_constant<int, 2>{});
 }
 
 // returns (dx, dweight, dbias); dx includes dres when given.  dw_dst / db_dst (optional): write
