@@ -47,6 +47,7 @@ def main():
                     help="queue the split-K reduces (defer.hip) and flush once per timed batch, as a "
                          "DDP backward does for small weight gradients")
     ap.add_argument("--only", default="", help="comma-separated shape name prefixes")
+    ap.add_argument("--small-tiles", action="store_true", help="also sweep 64x64 tiles (plan bit 5)")
     a = ap.parse_args()
     ops.load_library()
     if a.deferred:
@@ -72,6 +73,8 @@ def main():
             rdx = G._dswiglu_ref(rdx, aux)
         rdw = dy.float().t() @ x.float()
         scheds = [s | (o << 4) for s in (1, 2, 4, 8) if M % (64 * s) == 0 and M // s >= 256 for o in (0, 1)]
+        if tile == 128 and a.small_tiles:  # bit 5: the 64x64 pair kernel on a 128-divisible shape
+            scheds += [sc | 32 for sc in scheds]
         pick = G.pair_schedule(M, N, K, tile, epi)
 
         def run(sc):
@@ -94,7 +97,7 @@ def main():
         for sc in scheds:
             t = min(times[sc])
             mark = (" <- model" if sc == pick else "") + (" <- best" if sc == best else "")
-            print(f"   S={sc & 15} {'wgrad' if sc >> 4 else 'dgrad'}-first  {t:7.1f} us "
+            print(f"   S={sc & 15} {'wgrad' if (sc >> 4) & 1 else 'dgrad'}-first{' 64x64' if sc & 32 else ''}  {t:7.1f} us "
                   f"{flops / t / 1e6:5.0f} TF/s  [{' '.join(f'{v:.1f}' for v in times[sc])}]{mark}", flush=True)
 
 

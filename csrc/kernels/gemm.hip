@@ -925,10 +925,11 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   // product 2: wgrad layout
   const int K2 = a2.size(0), M2 = a2.size(1), N2 = b2.size(1);
   TORCH_CHECK(b2.size(0) == K2 && c2.size(0) == M2 && c2.size(1) == N2, "nbd::gemm_pair: product 2 shapes");
-  // splits2 = S | wfirst << 4 (the plan's encoding: ops/gemm.py pair_plan)
+  // splits2 = S | wfirst << 4 | small << 5 (the plan's encoding: ops/gemm.py pair_plan)
   const int S = (splits2 & 15) > 0 ? (int)(splits2 & 15) : 1;
   const int wfirst = (int)((splits2 >> 4) & 1);
-  const bool big = M1 % 128 == 0 && N1 % 128 == 0 && M2 % 128 == 0 && N2 % 128 == 0;
+  const bool small = (splits2 >> 5) & 1;  // bit 5: 64x64 tiles even where 128x128 would fit
+  const bool big = !small && M1 % 128 == 0 && N1 % 128 == 0 && M2 % 128 == 0 && N2 % 128 == 0;
   const int TB = big ? 128 : 64;
   TORCH_CHECK(M1 % TB == 0 && N1 % TB == 0 && M2 % TB == 0 && N2 % TB == 0 && K1 % BK == 0 && K1 > 0 &&
                   K2 % (BK * S) == 0 && K2 > 0,
