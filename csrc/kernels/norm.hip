@@ -146,7 +146,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const T* __restrict__ x, con
     }
   }
   if (lane == 0) {
-    mean_out[row] = mean;
+    if (!RMS) mean_out[row] = mean;  // RMSNorm: no mean (nullptr)
     rstd_out[row] = rstd;
   }
 }
@@ -713,7 +713,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rms_fwd_hip(const at::Tensor& x, 
   at::Tensor y = at::empty_like(x);
   at::Tensor xsum = res ? at::empty_like(x) : at::Tensor();
   auto fo = x.options().dtype(at::kFloat);
-  at::Tensor mean = at::empty({rows}, fo), rstd = at::empty({rows}, fo);
+  at::Tensor rstd = at::empty({rows}, fo);
   if (rows == 0) return {y, xsum, rstd};
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
@@ -728,12 +728,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rms_fwd_hip(const at::Tensor& x, 
     if (res)
       hipLaunchKernelGGL((ln_fwd_kernel<T, W, true, N, true>), grid, dim3(NT), 0, st,
                          static_cast<const T*>(x.data_ptr()), dp, sp, static_cast<const W*>(weight.data_ptr()),
-                         nullptr, static_cast<T*>(y.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
+                         nullptr, static_cast<T*>(y.data_ptr()), nullptr, rstd.data_ptr<float>(), rows,
                          (int)C, (float)eps);
     else
       hipLaunchKernelGGL((ln_fwd_kernel<T, W, false, N, true>), grid, dim3(NT), 0, st,
                          static_cast<const T*>(x.data_ptr()), dp, sp, static_cast<const W*>(weight.data_ptr()),
-                         nullptr, static_cast<T*>(y.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
+                         nullptr, static_cast<T*>(y.data_ptr()), nullptr, rstd.data_ptr<float>(), rows,
                          (int)C, (float)eps);
    });
   });
