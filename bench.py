@@ -23,6 +23,7 @@ import socket
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -57,16 +58,24 @@ def coordinator_main(a) -> int:
     from nbdistributed_amd.session import Session
 
     sess = Session(writer=lambda s: sys.stderr.write(s))
+
+    def write(res, partial):
+        res = dict(res)
+        res["init_ready"] = {r: sess.ready[r].get("init_s") for r in sess.ready}
+        res["device"] = sess.ready.get(0, {}).get("gpu_name")
+        res["rccl_version"] = sess.ready.get(0, {}).get("rccl_version")
+        res["partial"] = partial
+        tmp = a.out + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(res, f)
+        os.replace(tmp, a.out)  # rank 0 reads whole files only
+
     try:
         sess.attach(a.world, bind=a.endpoint, token=None, startup_timeout=900)
         res = run_all(sess, a.steps, a.warmup, allreduce=not a.no_allreduce, sweep=a.sweep, ar_bytes=a.ar_bytes,
                       ddp=not a.no_ddp, ddp_steps=a.ddp_steps, bcast=not a.no_bcast,
-                      notebook=not a.no_notebook)
-        res["init_ready"] = {r: sess.ready[r].get("init_s") for r in sess.ready}
-        res["device"] = sess.ready[0].get("gpu_name")
-        res["rccl_version"] = sess.ready[0].get("rccl_version")
-        with open(a.out, "w") as f:
-            json.dump(res, f)
+                      notebook=not a.no_notebook, checkpoint=lambda out: write(out, True))
+        write(res, False)
         return 0
     finally:
         sess.shutdown(graceful=True)
@@ -76,6 +85,49 @@ def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+# bench.py must print its line well inside the driver's 600 s limit: past this many seconds from
+# start, rank 0 stops the coordinator and prints what has been measured so far
+HARD_DEADLINE_S = float(os.environ.get("NBD_BENCH_HARD_S", "540"))
+_T0 = time.monotonic()
+
+
+class _Emitter:
+    """Prints the one JSON result line exactly once, from whichever thread gets there first."""
+
+    def __init__(self, out_path, world, a):
+        self.out_path, self.world, self.a = out_path, world, a
+        # the real stdout, kept aside before the worker redirects fd 1 into the control plane
+        self.fd = os.dup(1)
+        self.lock = threading.Lock()
+        self.done = False
+
+    def emit(self, why=None) -> bool:
+        with self.lock:
+            if self.done:
+                return True
+            try:
+                with open(self.out_path) as f:
+                    res = json.load(f)
+            except (OSError, ValueError):
+                return False
+            from nbdistributed_amd.benchmarking import result_line
+
+            line = result_line(res, self.world, self.a.steps, self.a.warmup)
+            line["device"] = res.get("device")
+            line["rccl_version"] = res.get("rccl_version")
+            if res.get("partial") or why:
+                line["partial"] = True
+                line["partial_reason"] = why or "coordinator ended before the last phase"
+            sys.stdout.flush()
+            os.write(self.fd, (json.dumps(line) + "\n").encode())
+            self.done = True
+            try:
+                os.unlink(self.out_path)
+            except OSError:
+                pass
+            return True
 
 
 def main(argv=None) -> int:
@@ -118,6 +170,25 @@ def main(argv=None) -> int:
     from nbdistributed_amd.worker import worker_from_env
 
     w = worker_from_env(endpoint, backend="auto", token=None, capture=True)
+    w.exit_on_disconnect = True  # the coordinator is bench.py's own child: when it ends, so do we
+    emitter = _Emitter(out_path, world, a) if rank == 0 else None
+    if child is not None:
+        def _watch():
+            # hard deadline: stop the coordinator (the workers see it disconnect and return from
+            # run()); if this process is still stuck after a grace period (e.g. inside a
+            # collective), print what was measured and leave
+            while child.poll() is None and time.monotonic() - _T0 < HARD_DEADLINE_S:
+                time.sleep(0.5)
+            if child.poll() is None:
+                print(f"[bench] hard deadline {HARD_DEADLINE_S:.0f}s: stopping the coordinator", file=sys.stderr,
+                      flush=True)
+                child.kill()
+                time.sleep(float(os.environ.get("NBD_BENCH_GRACE_S", "30")))
+                if emitter.emit("hard deadline"):
+                    sys.stdout.flush()
+                    os._exit(0)
+
+        threading.Thread(target=_watch, name="nbd-bench-deadline", daemon=True).start()
     rc = 0
     try:
         w.connect()
@@ -127,19 +198,15 @@ def main(argv=None) -> int:
     finally:
         w.shutdown()  # restores fd 1/2
     if child is not None:
-        rc = child.wait(timeout=600)
-        if rc != 0 or not os.path.exists(out_path):
-            print(f"coordinator failed (exit {rc})", file=sys.stderr)
+        try:
+            rc = child.wait(timeout=max(5.0, HARD_DEADLINE_S + 40.0 - (time.monotonic() - _T0)))
+        except subprocess.TimeoutExpired:
+            child.kill()
+            rc = -9
+        if not emitter.emit(None if rc == 0 else f"coordinator exit {rc}"):
+            print(f"coordinator failed (exit {rc}) before measuring anything", file=sys.stderr)
             return rc or 1
-        from nbdistributed_amd.benchmarking import result_line
-
-        with open(out_path) as f:
-            res = json.load(f)
-        os.unlink(out_path)
-        line = result_line(res, world, a.steps, a.warmup)
-        line["device"] = res.get("device")
-        line["rccl_version"] = res.get("rccl_version")
-        print(json.dumps(line), flush=True)
+        return 0
     return rc
 
 

@@ -688,52 +688,93 @@ static void launch_layout(int epi, const Tile& t, const Args& a, dim3 grid, hipS
 // order in which weights are used — keyed by (weight address, direction): forward products
 // (B = W [N][K]) and backward ones (dgrad / pair, B = W as [K][N]) form two different chains —
 // and each launch's first workgroups touch the weight the NEXT launch used the previous time
-// round, so it arrives in the MALL while this product computes.  The weight is held weakly
-// through its storage and re-validated at every lookup: an entry whose storage was freed is
-// dropped, and only bytes inside a live storage are ever read.  NBD_GEMM_WARM=0 disables it.
+// round, so it arrives in the MALL while this product computes.
+//
+// Safety and stability rules:
+// * the order is learned per HIP stream (a graph's capture stream, the default stream and a side
+//   stream never splice their launch sequences together);
+// * a link prev -> next is used only once it has been observed on two consecutive occurrences
+//   of prev (a one-off transition — the last product of one model followed by the first of
+//   another, or of a different cell — is never acted upon);
+// * the weight is held weakly through its storage and re-validated at every eager lookup: only
+//   bytes inside a live storage are ever read;
+// * under stream capture the pointer is frozen into the graph, so the looked-up storage is also
+//   kept alive STRONGLY until the capturer takes the references (gemm_warm_take_refs, called by
+//   graphs.GraphedStep which holds them for the graph's lifetime).
+// NBD_GEMM_WARM=0 disables it.
 namespace warm {
 constexpr int64_t kCapBytes = 8 << 20;  // the first 8 MiB: a product's first-round panels
+struct Target {
+  c10::weak_intrusive_ptr<c10::StorageImpl> storage{c10::intrusive_ptr<c10::StorageImpl>()};  // null: expired
+  int64_t offset = 0, bytes = 0;
+  uintptr_t key = 0;
+};
 struct Next {
-  c10::weak_intrusive_ptr<c10::StorageImpl> storage;
-  int64_t offset, bytes;
+  Target confirmed;     // acted upon
+  Target cand;          // last observed successor
+  int count = 0;        // consecutive observations of cand
+  bool has_confirmed = false;
 };
 std::mutex g_mu;
-std::unordered_map<uintptr_t, Next> g_next;  // key: weight address | direction
-uintptr_t g_last[64] = {};                   // per device: the previous launch's key
+std::unordered_map<uintptr_t, Next> g_next;         // key: weight address | direction
+std::unordered_map<uintptr_t, uintptr_t> g_last;     // per (device, stream): the previous launch's key
+std::vector<c10::intrusive_ptr<c10::StorageImpl>> g_capture_refs;  // warmed during capture
 
 bool enabled() {
   const char* e = std::getenv("NBD_GEMM_WARM");
   return e == nullptr || e[0] != '0';
 }
 
-// Record `w` as the weight of this launch (or of a library product announced by
-// gemm_warm_hint; `cap` = how much of it the launch before may warm) and return the next
-// launch's weight to touch (nullptr if none is known).
-const uint8_t* lookup(const at::Tensor& w, bool backward, int64_t& lines, int64_t cap = kCapBytes) {
+static bool capturing(hipStream_t st) {
+  hipStreamCaptureStatus s = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &s) != hipSuccess) return true;  // unknown: behave as under capture
+  return s != hipStreamCaptureStatusNone;
+}
+
+// Record `w` as the weight of this launch on stream `st` (or of a library product announced by
+// gemm_warm_hint; `cap` = how much of it the launch before may warm) and return the next launch's
+// weight to touch (nullptr if none is confirmed).
+const uint8_t* lookup(const at::Tensor& w, bool backward, hipStream_t st, int64_t& lines, int64_t cap = kCapBytes) {
   lines = 0;
   const int dev = w.get_device();
-  if (dev < 0 || dev >= 64 || !w.has_storage()) return nullptr;
+  if (dev < 0 || !w.has_storage()) return nullptr;
   const uintptr_t key = reinterpret_cast<uintptr_t>(w.data_ptr()) | (backward ? 1u : 0u);
+  const uintptr_t skey = reinterpret_cast<uintptr_t>(st) ^ (uintptr_t)dev;
+  const bool cap_mode = capturing(st);
   std::lock_guard<std::mutex> lk(g_mu);
-  const uintptr_t prev = g_last[dev];
-  g_last[dev] = key;
+  uintptr_t& last = g_last[skey];
+  const uintptr_t prev = last;
+  last = key;
   if (prev != 0 && prev != key) {
     if (g_next.size() > 4096) {  // forget dead weights (tests create many)
-      for (auto it = g_next.begin(); it != g_next.end();) it = it->second.storage.expired() ? g_next.erase(it) : ++it;
+      for (auto it = g_next.begin(); it != g_next.end();)
+        it = it->second.cand.storage.expired() && it->second.confirmed.storage.expired() ? g_next.erase(it) : ++it;
     }
     const at::Storage& s = w.storage();
-    const int64_t off = static_cast<const uint8_t*>(w.data_ptr()) - static_cast<const uint8_t*>(s.data());
-    const int64_t bytes = std::min<int64_t>((int64_t)w.numel() * (int64_t)w.element_size(), cap);
-    g_next.insert_or_assign(prev, Next{s.getWeakStorageImpl(), off, bytes});
+    Target t;
+    t.storage = s.getWeakStorageImpl();
+    t.offset = static_cast<const uint8_t*>(w.data_ptr()) - static_cast<const uint8_t*>(s.data());
+    t.bytes = std::min<int64_t>((int64_t)w.numel() * (int64_t)w.element_size(), cap);
+    t.key = key;
+    Next& n = g_next[prev];
+    if (n.count > 0 && n.cand.key == key && !n.cand.storage.expired()) {
+      if (++n.count >= 2) {
+        n.confirmed = t;
+        n.has_confirmed = true;
+      }
+    } else {
+      n.cand = t;
+      n.count = 1;
+    }
   }
   auto it = g_next.find(key);
-  if (it == g_next.end()) return nullptr;
-  c10::intrusive_ptr<c10::StorageImpl> s = it->second.storage.lock();
+  if (it == g_next.end() || !it->second.has_confirmed) return nullptr;
+  c10::intrusive_ptr<c10::StorageImpl> s = it->second.confirmed.storage.lock();
   if (!s) {
-    g_next.erase(it);
+    it->second.has_confirmed = false;
     return nullptr;
   }
-  const int64_t off = it->second.offset, bytes = it->second.bytes;
+  const int64_t off = it->second.confirmed.offset, bytes = it->second.confirmed.bytes;
   if (s->device().index() != dev || off < 0 || off + bytes > (int64_t)s->nbytes() || s->data() == nullptr)
     return nullptr;
   const uint8_t* base = static_cast<const uint8_t*>(s->data()) + off;
@@ -742,7 +783,9 @@ const uint8_t* lookup(const at::Tensor& w, bool backward, int64_t& lines, int64_
   const uintptr_t end = reinterpret_cast<uintptr_t>(base) + bytes;
   if (end <= first) return nullptr;
   lines = (int64_t)((end - first) / 128);
-  return lines > 0 ? reinterpret_cast<const uint8_t*>(first) : nullptr;
+  if (lines <= 0) return nullptr;
+  if (cap_mode) g_capture_refs.push_back(std::move(s));  // frozen into the graph: keep it alive
+  return reinterpret_cast<const uint8_t*>(first);
 }
 
 // warm-up blocks for `lines` lines at `nth` threads per block: ~4 lines per thread per pass, a
@@ -759,7 +802,34 @@ int blocks_for(int64_t lines, int nth) {
 void gemm_warm_hint(const at::Tensor& w, bool backward, int64_t max_bytes) {
   if (!warm::enabled() || !w.is_cuda()) return;
   int64_t lines = 0;
-  warm::lookup(w, backward, lines, std::max<int64_t>(0, max_bytes));
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  warm::lookup(w, backward, st, lines, std::max<int64_t>(0, max_bytes));
+}
+
+// The storages whose bytes captured launches warm (one tensor aliasing each): the graph's owner
+// keeps them for the graph's lifetime.  Clears the pending list.
+std::vector<at::Tensor> gemm_warm_take_refs() {
+  std::vector<c10::intrusive_ptr<c10::StorageImpl>> refs;
+  {
+    std::lock_guard<std::mutex> lk(warm::g_mu);
+    refs.swap(warm::g_capture_refs);
+  }
+  std::vector<at::Tensor> out;
+  out.reserve(refs.size());
+  for (auto& s : refs) {
+    at::Tensor t = at::empty({0}, at::TensorOptions().dtype(at::kByte).device(s->device()));
+    t.set_(at::Storage(std::move(s)));
+    out.push_back(std::move(t));
+  }
+  return out;
+}
+
+// Forget every learned link (tests; a notebook that wants a clean slate).
+void gemm_warm_reset() {
+  std::lock_guard<std::mutex> lk(warm::g_mu);
+  warm::g_next.clear();
+  warm::g_last.clear();
 }
 
 static bool tile_fits(const Tile& t, int M, int N) { return M % t.bm == 0 && N % t.bn == 0; }
@@ -872,7 +942,7 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   p.pf_lines = 0;
   p.warm_blocks = 0;
   if (!a_km && warm::enabled()) {  // B is a weight (forward / dgrad), not an activation (wgrad)
-    const uint8_t* pf = warm::lookup(b, b_kn, p.pf_lines);
+    const uint8_t* pf = warm::lookup(b, b_kn, st, p.pf_lines);
     if (pf != nullptr && t.bm != 256) {  // (the 256x256 kernel has no warm-up blocks)
       p.pf = pf;
       p.warm_blocks = warm::blocks_for(p.pf_lines, 64 * t.waves * t.ks);
@@ -970,8 +1040,10 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   const int t1 = p1.tiles_m * p1.tiles_n, t2 = p2.tiles_m * p2.tiles_n;
   const int nb1 = (t1 + 7) / 8 * 8, nb2 = (t2 * S + 7) / 8 * 8;
   const int first = wfirst ? nb2 : nb1;
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(a1.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   if (warm::enabled()) {  // b1 = W: the backward chain (next-weight warm-up, above)
-    const uint8_t* pf = warm::lookup(b1, true, p1.pf_lines);
+    const uint8_t* pf = warm::lookup(b1, true, st, p1.pf_lines);
     if (pf != nullptr) {
       p1.pf = pf;
       p1.warm_blocks = warm::blocks_for(p1.pf_lines, big ? 512 : 256);
@@ -979,8 +1051,6 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   }
   const int64_t nblocks = (int64_t)p1.warm_blocks + nb1 + nb2;
   TORCH_CHECK(nblocks < (1LL << 31), "nbd::gemm_pair: grid too large");
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(a1.device());
-  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   const dim3 grid((unsigned)nblocks);
   // NBD_GEMM_PAIR_PP=1: the 128x128 halves on the ping-pong schedule (one workgroup per CU)
   const char* pp_env = std::getenv("NBD_GEMM_PAIR_PP");
@@ -1024,4 +1094,6 @@ TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
 // bookkeeping only (no device work): a catch-all kernel
 TORCH_LIBRARY_FRAGMENT(nbd, m) {
   m.def("gemm_warm_hint(Tensor w, bool backward, int max_bytes) -> ()", &nbd::gemm::gemm_warm_hint);
+  m.def("gemm_warm_take_refs() -> Tensor[]", &nbd::gemm::gemm_warm_take_refs);
+  m.def("gemm_warm_reset() -> ()", &nbd::gemm::gemm_warm_reset);
 }

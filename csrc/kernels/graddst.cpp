@@ -56,8 +56,20 @@ at::Tensor hand_back(const at::Tensor& param, const at::Tensor& dst, bool acc) {
 }
 
 // ---- ops -----------------------------------------------------------------------------------------
+namespace {
+// entries whose parameter died still pin their bucket view (and so the whole bucket buffer):
+// drop them whenever the registry changes
+void purge_expired_locked() {
+  for (auto it = g_map.begin(); it != g_map.end();) {
+    if (it->second.param.expired()) it = g_map.erase(it);
+    else ++it;
+  }
+}
+}  // namespace
+
 void set_grad_dest(const at::Tensor& param, const c10::optional<at::Tensor>& dst) {
   std::lock_guard<std::mutex> lk(g_mu);
+  purge_expired_locked();
   const c10::TensorImpl* key = param.unsafeGetTensorImpl();
   if (!dst || !dst->defined()) {
     g_map.erase(key);
@@ -78,10 +90,7 @@ void grad_dest_new_pass() {
 
 int64_t grad_dest_count() {
   std::lock_guard<std::mutex> lk(g_mu);
-  for (auto it = g_map.begin(); it != g_map.end();) {
-    if (it->second.param.expired()) it = g_map.erase(it);
-    else ++it;
-  }
+  purge_expired_locked();
   return (int64_t)g_map.size();
 }
 

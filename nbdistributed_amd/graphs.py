@@ -53,6 +53,19 @@ def _drain_collective_watchdog(poll_s: float = 0.35) -> None:
         time.sleep(poll_s)
 
 
+def _take_warm_refs():
+    """Tensors aliasing every storage that GEMM launches captured since the last call warm up
+    (``torch.ops.nbd.gemm_warm_take_refs``); empty without the native extension."""
+    try:
+        from .ops import _lib
+
+        if not _lib.native_available():
+            return []
+        return list(torch.ops.nbd.gemm_warm_take_refs())
+    except (AttributeError, RuntimeError):
+        return []
+
+
 class GraphedStep:
     """``step = GraphedStep(fn, example_args, optimizers=[opt])``; ``out = step(*args)``.
 
@@ -85,8 +98,12 @@ class GraphedStep:
         # thread_local: only this thread's calls are checked during capture — ProcessGroupNCCL's
         # watchdog thread keeps querying its events meanwhile, which "global" mode turns into a
         # hipErrorStreamCaptureUnsupported abort (seen intermittently on this stack)
+        _take_warm_refs()  # (drop references left by an earlier capture that nobody took)
         with torch.cuda.graph(self.graph, pool=pool, capture_error_mode="thread_local"):
             self.static_out = fn(*self.static_args)
+        # the captured GEMMs' next-weight warm-up reads (csrc/kernels/gemm.hip, namespace warm)
+        # are frozen pointers into those weights' storages: hold them as long as the graph
+        self._warm_refs = _take_warm_refs()
         torch.cuda.synchronize()
 
     def _sync_hyper(self) -> None:

@@ -68,7 +68,8 @@ class FlatAdamW(torch.optim.Optimizer):
         self._multi = None  # (grads, params, masters, exp_avgs, exp_avg_sqs) of the one-call update
         if overlap is None:
             overlap = _OVERLAP
-        self.overlap = bool(overlap) and not self.sharded and getattr(ddp, "world", 1) == 1 and dev.type == "cuda"
+        self.overlap = (bool(overlap) and not self.sharded and not getattr(ddp, "_collectives", False)
+                        and dev.type == "cuda")
         self._updated: List[int] = []  # buckets updated during the current backward (overlap)
         if self.overlap:
             self._opt_stream = torch.cuda.Stream(device=dev)
@@ -141,7 +142,7 @@ class FlatAdamW(torch.optim.Optimizer):
             if not _capturing():
                 self.lr_t.fill_(float(g["lr"]))
         if (_MULTI and not self.sharded and self.ddp.buckets[0].param_flat.is_cuda
-                and (self._joined_grads() or getattr(self.ddp, "world", 1) == 1)):
+                and (self._joined_grads() or not getattr(self.ddp, "_collectives", False))):
             # all updates from one call.  (At world 1 there is no collective for a per-bucket wait
             # to overlap with: one join of the side stream, if any, then every bucket.)
             if not self._joined_grads():
@@ -167,7 +168,7 @@ class FlatAdamW(torch.optim.Optimizer):
             ops.adamw_flat(self._grad(b), self._param_slice(b), st["master"], st["exp_avg"], st["exp_avg_sq"], g["lr"],
                            b1, b2, g["eps"], g["weight_decay"], max(self.step_count, 1), grad_scale_t=self._clip_coef,
                            step_t=self.step_t, lr_t=self.lr_t)
-            if self.sharded and self.ddp.world > 1:  # rebuild the full bucket from every rank's updated slice
+            if self.sharded and self.ddp._collectives:  # rebuild the full bucket from every rank's updated slice
                 b.gather_work = dist.all_gather_into_tensor(b.param_flat, self._param_slice(b), group=self.ddp.pg,
                                                             async_op=True)
         if self.sharded and _capturing():
@@ -186,6 +187,12 @@ class FlatAdamW(torch.optim.Optimizer):
         comes from the one-pass summary kernel (``ops.tensor_summary_raw``, float64 partials) over
         each averaged bucket; the clip coefficient stays on the device and is applied inside the
         next ``step()`` — no host synchronisation.  Returns the total norm (device tensor)."""
+        if self.overlap:
+            # the buckets were already updated during backward, unclipped: refuse loudly, and
+            # leave no coefficient behind for a later step
+            self._clip_coef = None
+            raise RuntimeError("FlatAdamW(overlap=True) applies each bucket's update during backward, before "
+                               "clip_grad_norm_ can run; construct it with overlap=False to clip gradients")
         sq = None
         if hasattr(self.ddp, "wait_grads"):
             self.ddp.wait_grads()
@@ -228,5 +235,5 @@ class FlatAdamW(torch.optim.Optimizer):
                 st[k].copy_(src[k])
         for b, st in zip(self.ddp.buckets, self.flat_state):
             self._param_slice(b).copy_(st["master"].to(b.param_flat.dtype))
-            if self.sharded and self.ddp.world > 1:
+            if self.sharded and self.ddp._collectives:
                 dist.all_gather_into_tensor(b.param_flat, self._param_slice(b), group=self.ddp.pg)

@@ -6,7 +6,7 @@ from .backend import abort_process_group, init_data_plane, rccl_version, registe
 
 __all__ = ["abort_process_group", "init_data_plane", "rccl_version", "register_rccl_backend", "resolve_backend",
            "DistributedDataParallel", "bf16_compress_hook", "allreduce_hook", "broadcast_params", "broadcast_tensors",
-           "tensor", "sequence", "expert", "pipeline", "pipeline_step", "MoE", "parallelize_gpt2", "parallelize_llama", "ColumnParallelLinear", "RowParallelLinear", "ulysses_attention", "context", "ring_attention", "mesh", "ParallelMesh"]
+           "tensor", "sequence", "expert", "pipeline", "pipeline_step", "MoE", "parallelize_gpt2", "parallelize_llama", "ColumnParallelLinear", "RowParallelLinear", "ulysses_attention", "context", "ring_attention", "mesh", "ParallelMesh", "p2p", "batch_isend_irecv"]
 
 
 def __getattr__(name):
@@ -15,7 +15,11 @@ def __getattr__(name):
         from . import ddp
 
         return getattr(ddp, name)
-    if name in ("tensor", "sequence", "expert", "pipeline", "context", "mesh"):
+    if name == "batch_isend_irecv":
+        from . import p2p
+
+        return p2p.batch_isend_irecv
+    if name in ("tensor", "sequence", "expert", "pipeline", "context", "mesh", "p2p"):
         import importlib
 
         return importlib.import_module(f".{name}", __name__)

@@ -30,6 +30,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from .p2p import batch_isend_irecv
 from .sequence import _rank, _size
 
 
@@ -178,7 +179,7 @@ class _Ring:
         ops = []
         for a, b in zip(send, recv):
             ops += [dist.P2POp(dist.isend, a, self.nxt, self.group), dist.P2POp(dist.irecv, b, self.prv, self.group)]
-        return dist.batch_isend_irecv(ops), recv, dev, send
+        return batch_isend_irecv(ops), recv, dev, send
 
     @staticmethod
     def finish(handle):

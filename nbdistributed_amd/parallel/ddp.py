@@ -50,6 +50,8 @@ from __future__ import annotations
 
 import contextlib
 import os
+import types
+import weakref
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
 
@@ -105,7 +107,7 @@ class DistributedDataParallel(torch.nn.Module):
                  broadcast_buffers: bool = True, init_sync: bool = True, align: int = 64,
                  flat_params: bool = False, grad_mode: str = "unflatten", shard: bool = False,
                  grad_views: Optional[bool] = None, fused_linear: Optional[bool] = None,
-                 accumulate: str = "bucket"):
+                 accumulate: str = "bucket", force_collectives: Optional[bool] = None):
         """``flat_params``: re-home each bucket's parameters into one contiguous buffer (the
         nn.Parameters become views) so a flat optimizer (``nbdistributed_amd.optim.FlatAdamW``)
         can update a whole bucket in one pass.  ``grad_mode="bucket"``: leave the averaged
@@ -117,11 +119,20 @@ class DistributedDataParallel(torch.nn.Module):
         ``fused_linear`` (default: = grad_views): route ``nn.Linear`` layers through the C++
         Linear node so their gradients are written in place too.  ``accumulate``: where
         ``no_sync()`` micro-batches accumulate — ``"bucket"`` (K3 pre-reduce into the bucket,
-        ``p.grad`` released; same-dtype buckets) or ``"grad"`` (in ``p.grad``, torch's semantics)."""
+        ``p.grad`` released; same-dtype buckets) or ``"grad"`` (in ``p.grad``, torch's semantics).
+        ``force_collectives`` (default: ``NBD_DDP_FORCE_COLLECTIVES=1``): issue the real
+        collectives even at world size 1 — every code path of a multi-GPU run (per-bucket
+        flushes, side-stream collectives and events, in-place reduce-scatter / all-gather, RCCL
+        inside a captured graph) then runs, and can be timed and profiled, on one GPU."""
         super().__init__()
+        self._token = object()  # ownership of registrations / patches shared with newer DDPs
         self.module = module
         self.pg = process_group if process_group is not None else dist.group.WORLD
         self.world = dist.get_world_size(self.pg)
+        if force_collectives is None:
+            force_collectives = os.environ.get("NBD_DDP_FORCE_COLLECTIVES", "0") == "1"
+        # the multi-rank code path: collectives issued (always at world > 1; forced at world 1)
+        self._collectives = self.world > 1 or bool(force_collectives)
         self.broadcast_buffers = broadcast_buffers
         self.params = [p for p in module.parameters() if p.requires_grad]
         if not self.params:
@@ -197,6 +208,7 @@ class DistributedDataParallel(torch.nn.Module):
                 b.views = [b.buffer[o:o + p.numel()].view_as(p) for p, o in zip(b.params, b.offsets)]
                 for p, v in zip(b.params, b.views):
                     graddst.register(p, v)
+                    _GRAD_OWNER[id(p)] = self._token
                 self._n_views += len(b.params)
         self._patched: List[torch.nn.Module] = []
         if (self.grad_views if fused_linear is None else fused_linear) and self._n_views:
@@ -212,8 +224,21 @@ class DistributedDataParallel(torch.nn.Module):
 
             graddst.defer_enable(os.environ.get("NBD_GRAD_DEFER", "1") != "0")
 
-        self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in self.params]
-        if init_sync and self.world > 1:
+        # the hooks reach this object through a weak reference, so a DDP that the notebook drops
+        # (re-running the cell that wraps the same module) is collected; its finalizer removes
+        # the hooks, its gradient-destination registrations and its patched forwards — unless a
+        # newer DDP on the same module has taken them over (ownership token)
+        wself = weakref.ref(self)
+
+        def _hook(p, _w=wself):
+            s = _w()
+            if s is not None:
+                s._grad_ready(p)
+
+        self._hooks = [p.register_post_accumulate_grad_hook(_hook) for p in self.params]
+        self._finalizer = weakref.finalize(self, _release, self._token, self._hooks, list(self._patched),
+                                           [p for b in self.buckets if b.views is not None for p in b.params])
+        if init_sync and self._collectives:
             self._broadcast_tensors([p.data for p in module.parameters()])
             self._broadcast_tensors(list(module.buffers()))
         self.stats = {"buckets": len(self.buckets), "bucket_numels": [b.numel for b in self.buckets],
@@ -224,8 +249,6 @@ class DistributedDataParallel(torch.nn.Module):
     def _patch_linears(self) -> None:
         """Route every ``nn.Linear`` whose parameters have bucket views through the C++ Linear
         autograd node (``torch.ops.nbd.linear_ag``), which writes dW / db into the views."""
-        import types
-
         from ..ops import gemm as _gemm
 
         viewed = {id(p) for b in self.buckets if b.views is not None for p in b.params}
@@ -235,24 +258,20 @@ class DistributedDataParallel(torch.nn.Module):
             if m.bias is not None and id(m.bias) not in viewed:
                 continue
             m.forward = types.MethodType(_fused_linear_forward, m)
+            m._nbd_ddp_owner = self._token
             self._patched.append(m)
         if self._patched:
             _gemm.native_available_or_raise()
 
     def unpatch(self) -> None:
-        """Undo ``fused_linear`` and the gradient-destination registrations."""
-        for m in self._patched:
-            m.__dict__.pop("forward", None)
+        """Undo ``fused_linear`` and the gradient-destination registrations (those still owned
+        by this DDP); also runs when the DDP object is garbage-collected."""
+        params = [p for b in self.buckets if b.views is not None for p in b.params]
+        _release(self._token, [], self._patched, params)
         self._patched = []
-        if self._n_views:
-            from ..ops import graddst
-
-            for b in self.buckets:
-                if b.views is not None:
-                    for p in b.params:
-                        graddst.register(p, None)
-                    b.views = None
-            self._n_views = 0
+        for b in self.buckets:
+            b.views = None
+        self._n_views = 0
 
     # ------------------------------------------------------------------ planning
     def _plan(self, cap_mb: float, first_mb: float, align: int) -> List[_Bucket]:
@@ -318,7 +337,7 @@ class DistributedDataParallel(torch.nn.Module):
             self._joined = True
 
     def _reduce(self, b: _Bucket, avg: bool = False):
-        if self.world == 1:
+        if not self._collectives:
             # nothing to exchange (and for ZeRO the slice is the whole bucket).  Not even a no-op
             # launch: RCCL runs a one-rank ReduceOp.AVG as a full pre-multiply pass over the bucket
             # (oneRankReduce<FuncPreMulSum>: 190 µs per 48 MB bucket, profiles/gpt2_graph_prof_r3*.md)
@@ -340,7 +359,7 @@ class DistributedDataParallel(torch.nn.Module):
             # fused paths read weights without calling their modules' forward, so the hooks
             # would not fire: all buckets are waited here.)
             self._wait_gathers(self.buckets)
-        if self._require_sync and self.broadcast_buffers and self.world > 1:
+        if self._require_sync and self.broadcast_buffers and self._collectives:
             bufs = [b for b in self.module.buffers() if b.is_floating_point() or b.dtype in (torch.int64, torch.int32)]
             if bufs:
                 self._broadcast_tensors(bufs)
@@ -402,8 +421,16 @@ class DistributedDataParallel(torch.nn.Module):
         return self.accumulate == "bucket" and all(p.dtype == b.buffer.dtype for p in b.params)
 
     def _prereduce_local(self, b: _Bucket) -> None:
-        """no_sync micro-batch: sum this bucket's new gradients into the bucket (K3, fp32
-        accumulate) and release them; gradients written in place already accumulated there."""
+        """no_sync micro-batch: fold this bucket's new gradients into the bucket.
+
+        Bucket with gradient views: after every micro-batch each ``p.grad`` IS its slice, so the
+        next micro-batch accumulates in place (the GEMM epilogues claim the slice with
+        ``acc=True``; autograd's AccumulateGrad adds into a defined ``.grad`` in place).  A
+        gradient that still arrives elsewhere — a weight used twice in one pass, whose
+        contributions the engine sums out of place — was computed as ``old .grad + new``, i.e.
+        it already contains the slice: it OVERWRITES the slice (adding it would count the earlier
+        micro-batches twice).  Bucket without views: the new gradients are summed into the bucket
+        (K3, fp32 accumulate) and released."""
         if not self._local_home(b):
             return  # plain autograd accumulation into p.grad (torch semantics)
         _, rest = self._split_in_place(b)
@@ -415,12 +442,19 @@ class DistributedDataParallel(torch.nn.Module):
                 if b.params[i].grad is None:
                     o = b.offsets[i]
                     b.buffer[o:o + b.params[i].numel()].zero_()
-            if arrived:
-                ops.bucket_flatten([b.params[i].grad for i in arrived], b.buffer, [b.offsets[i] for i in arrived])
-        elif arrived:
-            ops.prereduce_into_bucket([b.params[i].grad for i in arrived], b.buffer, [b.offsets[i] for i in arrived])
-        for i in arrived:
-            b.params[i].grad = None
+        overwrite = not b.partial or b.views is not None
+        if arrived:
+            gs, offs = [b.params[i].grad for i in arrived], [b.offsets[i] for i in arrived]
+            if overwrite:
+                ops.bucket_flatten(gs, b.buffer, offs)
+            else:
+                ops.prereduce_into_bucket(gs, b.buffer, offs)
+        if b.views is not None:
+            for p, v in zip(b.params, b.views):
+                p.grad = v  # the running sum: later micro-batches accumulate into it in place
+        else:
+            for i in arrived:
+                b.params[i].grad = None
         b.partial = True
 
     def _launch_ready(self) -> None:
@@ -443,7 +477,7 @@ class DistributedDataParallel(torch.nn.Module):
             graddst.defer_flush()
 
     def _launch(self, b: _Bucket) -> None:
-        if self.world > 1 or self._on_bucket_ready is not None:
+        if self._collectives or self._on_bucket_ready is not None:
             self._flush_deferred()  # the collective / the update reads the slices: their reduces go first
         n_in, rest = self._split_in_place(b)
         if n_in == 0 and not b.partial:
@@ -461,12 +495,16 @@ class DistributedDataParallel(torch.nn.Module):
         offs = [b.offsets[i] for i in rest]
         b.rest_grads, b.rest_offsets = grads, offs
         avg = self._avg_ok
-        b.post_div = not avg and self.world > 1
+        b.post_div = not avg and self._collectives
         unflatten = self.grad_mode == "unflatten"
+
+        # a partial bucket with views: every arrival was computed on top of its slice (see
+        # _prereduce_local) and replaces it; without views the arrivals are new and add up
+        acc_rest = b.partial and b.views is None
 
         def pre():
             if grads:
-                ops.bucket_flatten(grads, b.buffer, offs, scale=1.0, accumulate=b.partial)
+                ops.bucket_flatten(grads, b.buffer, offs, scale=1.0, accumulate=acc_rest)
 
         def post():
             if b.post_div:
@@ -588,6 +626,31 @@ class DistributedDataParallel(torch.nn.Module):
     # ------------------------------------------------------------------ broadcast
     def _broadcast_tensors(self, tensors: List[torch.Tensor]) -> None:
         broadcast_tensors(tensors, src=0, group=self.pg)
+
+
+# id(param) -> token of the DDP whose bucket slice is its registered gradient home
+_GRAD_OWNER: Dict[int, object] = {}
+
+
+def _release(token, hooks, patched, params) -> None:
+    """Undo one DDP's hooks, patched ``nn.Linear`` forwards and gradient-destination
+    registrations, leaving alone whatever a newer DDP on the same module has taken over."""
+    for h in hooks:
+        h.remove()
+    for m in patched:
+        if m.__dict__.get("_nbd_ddp_owner") is token:
+            m.__dict__.pop("forward", None)
+            m.__dict__.pop("_nbd_ddp_owner", None)
+    mine = [p for p in params if _GRAD_OWNER.get(id(p)) is token]
+    if mine:
+        try:
+            from ..ops import graddst
+
+            for p in mine:
+                graddst.register(p, None)
+                _GRAD_OWNER.pop(id(p), None)
+        except Exception:  # noqa: BLE001 - interpreter shutdown: the registry dies with the process
+            pass
 
 
 def _fused_linear_forward(self, x):

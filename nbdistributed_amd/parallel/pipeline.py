@@ -23,6 +23,8 @@ from typing import Callable, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
+from .p2p import batch_isend_irecv
+
 
 def _size(group) -> int:
     return dist.get_world_size(group) if dist.is_initialized() else 1
@@ -48,7 +50,7 @@ class _P2P:
 
     def _run(self, ops):
         if ops:
-            for w in dist.batch_isend_irecv(ops):
+            for w in batch_isend_irecv(ops):
                 w.wait()
 
     def exchange(self, send_to=None, send=None, recv_from=None):

@@ -161,6 +161,9 @@ class Session:
         self.timeline = Timeline(self.cfg.timeline_capacity)
         self.gpu_ids: Optional[List[Optional[int]]] = None
         self.default_timeout: Optional[float] = None
+        # optional absolute deadline (time.monotonic()): no request waits past it (benchmarks
+        # that must hand in their result before an outer time limit)
+        self.deadline: Optional[float] = None
         self.attached = False
         self.started_at: Optional[float] = None
         self.init_s: Optional[float] = None
@@ -267,6 +270,13 @@ class Session:
             raise RuntimeError("No distributed workers running. Use %dist_init first.")
         return self.comm
 
+    def _effective_timeout(self, timeout: Optional[float]) -> Optional[float]:
+        t = timeout if timeout is not None else self.default_timeout
+        if self.deadline is not None:
+            left = max(0.0, self.deadline - time.monotonic())
+            t = left if t is None else min(t, left)
+        return t
+
     def all_ranks(self) -> List[int]:
         return list(range(self.num_processes))
 
@@ -275,6 +285,7 @@ class Session:
                 ns_delta: bool = False, timeout: Optional[float] = None, kind: str = "distributed",
                 raise_on_error: bool = True, show_header: bool = True) -> CellResult:
         comm = self._require()
+        timeout = self._effective_timeout(timeout)
         ranks = self.all_ranks() if ranks is None else list(ranks)
         flags = (P.F_NS_DELTA if ns_delta and 0 in ranks else 0) | (0 if echo else P.F_NO_ECHO)
         t0 = time.perf_counter()
@@ -359,7 +370,7 @@ class Session:
     # ------------------------------------------------------------------ other requests
     def sync(self, timeout: Optional[float] = None) -> Dict[int, Any]:
         comm = self._require()
-        return comm.send_to_ranks(self.alive_ranks(), "sync", {}, timeout=timeout)
+        return comm.send_to_ranks(self.alive_ranks(), "sync", {}, timeout=self._effective_timeout(timeout))
 
     def alive_ranks(self) -> List[int]:
         comm = self._require()

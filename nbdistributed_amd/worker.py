@@ -134,6 +134,9 @@ class DistributedWorker:
         self.ns = self.executor.ns
         self.sock: Optional[Socket] = None
         self.console_err = sys.__stderr__
+        # a spawned worker ends with its coordinator; an attached one (torchrun) waits for a new
+        # one unless its launcher says otherwise (bench.py: the coordinator is its child)
+        self.exit_on_disconnect = not attach
 
     # ------------------------------------------------------------------ bootstrap
     def connect(self) -> None:
@@ -574,7 +577,7 @@ class DistributedWorker:
                     break  # the coordinator died without telling us
                 continue
             if m.is_event:
-                if m.event in (EV_DISCONNECTED, EV_HEARTBEAT_TIMEOUT) and not self.attach:
+                if m.event in (EV_DISCONNECTED, EV_HEARTBEAT_TIMEOUT) and self.exit_on_disconnect:
                     break
                 continue
             try:

@@ -134,3 +134,30 @@ def test_world1_reports_no_bandwidth():
 def test_magic_path_cells(sess):
     r = B.bench_cells_magic(sess, steps=5, warmup=2)
     assert r["p50_ms"] > 0 and r["ide_sync"] is True and r["rendered_bytes"] > 0
+
+
+def _run_bench(env_extra, timeout=240):
+    env = dict(os.environ, **env_extra)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "1"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd="/tmp", env=env)
+    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
+    return res, lines
+
+
+def test_bench_line_survives_a_phase_past_the_global_deadline():
+    """A phase that hangs past the bench's global budget is interrupted and recorded; the JSON
+    line (with the measured cell p50) is still printed, exactly once."""
+    res, lines = _run_bench({"NBD_BENCH_FAULT_HANG": "600", "NBD_BENCH_DEADLINE_S": "25"})
+    assert res.returncode == 0 and len(lines) == 1, res.stdout[-2000:] + res.stderr[-3000:]
+    d = json.loads(lines[0])
+    assert d["value"] > 0 and d["aborted_phase"] == "fault_hang"
+
+
+def test_bench_line_survives_the_hard_deadline():
+    """Past the hard deadline rank 0 kills the coordinator and, still stuck in the cell, prints
+    the checkpointed result itself."""
+    res, lines = _run_bench({"NBD_BENCH_FAULT_HANG": "600", "NBD_BENCH_DEADLINE_S": "400",
+                             "NBD_BENCH_HARD_S": "30", "NBD_BENCH_GRACE_S": "3"})
+    assert res.returncode == 0 and len(lines) == 1, res.stdout[-2000:] + res.stderr[-3000:]
+    d = json.loads(lines[0])
+    assert d["value"] > 0 and d["partial"] is True
