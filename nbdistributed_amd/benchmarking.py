@@ -356,8 +356,11 @@ def _nbd_notebook_bench(steps, warm, bs=16, seq=128, mode="reference", small=Fal
     n = bs * world_size * (steps + warm + 2)
     ids, mask, labels = synthetic_mrpc(n=n, seq_len=seq, vocab=over.get("vocab_size", 49152))
     model = smollm2_135m_classifier(**over)
-    if mode == "reference":       # the notebook's recipe: fp32, accelerate-prepared torch DDP
+    if mode in ("reference", "reference_native"):  # the notebook's loop: accelerate-prepared torch DDP
         from accelerate import Accelerator
+        if mode == "reference_native":  # + the one-line swap: native Llama, fp32 master, bf16 compute
+            from nbdistributed_amd.models import native
+            model = native(model.to(device))
         acc = Accelerator(cpu=device.type == "cpu")
         opt = torch.optim.AdamW(model.parameters(), lr=2e-5)
         dl = DataLoader(TensorDataset(ids, mask, labels), batch_size=bs, shuffle=True)
@@ -424,10 +427,12 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
                            "reference_ms_per_step": REFERENCE_NOTEBOOK_MS_PER_STEP,
                            "reference_samples_per_s": 32 / (REFERENCE_NOTEBOOK_MS_PER_STEP / 1e3)}
     recipes = {"reference": "HF model, fp32, accelerate DDP, torch AdamW (the notebook's recipe)",
+               "reference_native": "the notebook's accelerate loop unchanged except model = nbd.models.native(model): "
+                                   "native Llama, fp32 master weights + torch AdamW, bf16 compute on the fused HIP path",
                "nbd": "native Llama (HIP kernels, one autograd node per block), bf16 params + fp32 master "
                        "(FlatAdamW, buckets updated during backward at world 1), nbd DDP",
                "nbd_graph": "as nbd, whole step captured in one HIP graph (GraphedStep)"}
-    modes = ["reference", "nbd"]
+    modes = ["reference", "reference_native", "nbd"]
     # graph capture with RCCL collectives is verified at world size 1 on this pool; at N > 1 it
     # runs only on request, so a capture problem cannot cost the driver its result line
     if n == 1 or os.environ.get("NBD_BENCH_GRAPH_MULTI") == "1":
@@ -453,7 +458,11 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
     # same-recipe comparisons only: the fp32 HF arm and the bf16 native arms differ in precision
     # and model implementation, so no cross-recipe "speedup" is printed
     out["reference_vs_native_note"] = ("'reference' = HF fp32 model through accelerate (the notebook as written); "
-                                       "'nbd*' = native bf16 Llama + FlatAdamW; different recipes, not a like-for-like speedup")
+                                       "'reference_native' = the same loop with the one-line model swap (bf16 compute, "
+                                       "fp32 master weights: the recipe of Accelerator(mixed_precision='bf16')); "
+                                       "'nbd*' = native bf16 Llama + FlatAdamW (bf16 params, fp32 master in the optimizer)")
+    if "reference" in out and "reference_native" in out:
+        out["reference_native_speedup_same_loop"] = out["reference"]["ms_per_step"] / out["reference_native"]["ms_per_step"]
     return out
 
 

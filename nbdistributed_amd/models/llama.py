@@ -21,7 +21,7 @@ supported).
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Any, Dict, Optional
+from typing import Any, Dict, NamedTuple, Optional
 
 import torch
 import torch.nn as nn
@@ -104,6 +104,47 @@ class LlamaConfig:
                    sliding_window=window, rope_scaling=scaling)
 
 
+class SequenceClassifierOutput(NamedTuple):
+    """``(loss, logits)`` that also reads like HF's output object: ``out.loss``, ``out.logits``."""
+    loss: Optional[torch.Tensor]
+    logits: torch.Tensor
+
+
+class CausalLMOutput(NamedTuple):
+    """``(loss, logits)`` with HF-style attribute access (``logits`` None when not returned)."""
+    loss: Optional[torch.Tensor]
+    logits: Optional[torch.Tensor]
+
+
+class _CastGroup(torch.autograd.Function):
+    """Mixed precision for fp32 master parameters: one fused HIP pass
+    (``nbd::bucket_flatten``) casts a group of parameters into one flat compute-dtype buffer, and
+    the backward casts their gradients back into one flat fp32 buffer — two launches per group
+    instead of two per parameter (what per-op autocast would issue).  The model casts one decoder
+    layer per group, so under DDP each layer's fp32 gradients are ready as soon as that layer's
+    backward is done (bucket all-reduces keep overlapping backward)."""
+
+    @staticmethod
+    def forward(ctx, dtype, *ps):
+        offs, total = ops.plan_offsets([p.numel() for p in ps])
+        buf = torch.empty(total, dtype=dtype, device=ps[0].device)
+        torch.ops.nbd.bucket_flatten(list(ps), buf, offs, 1.0, False)
+        ctx.meta = ([p.shape for p in ps], offs, total, ps[0].dtype)
+        return tuple(buf[o:o + p.numel()].view(p.shape) for p, o in zip(ps, offs))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        shapes, offs, total, dt = ctx.meta
+        have = [i for i, g in enumerate(gs) if g is not None]
+        out = [None] * len(gs)
+        if have:
+            buf = torch.empty(total, dtype=dt, device=gs[have[0]].device)
+            torch.ops.nbd.bucket_flatten([gs[i].contiguous() for i in have], buf, [offs[i] for i in have], 1.0, False)
+            for i in have:
+                out[i] = buf[offs[i]:offs[i] + shapes[i].numel()].view(shapes[i])
+        return (None, *out)
+
+
 class RMSNorm(nn.Module):
     def __init__(self, n: int, eps: float):
         super().__init__()
@@ -174,6 +215,26 @@ class LlamaModel(nn.Module):
         self.layers = nn.ModuleList([LlamaDecoderLayer(c) for _ in range(c.num_hidden_layers)])
         self.norm = RMSNorm(c.hidden_size, c.rms_norm_eps)
         self._rope: Dict[Any, tuple] = {}
+        # fp32 parameters computed in this dtype on the fused GPU path (``native()``): the
+        # parameters stay fp32 for the optimizer, each layer is cast once per forward
+        self.compute_dtype: Optional[torch.dtype] = None
+
+    def cast_dtype(self, input_ids) -> Optional[torch.dtype]:
+        """The dtype the fp32 parameters are cast to for this forward, or None (run as stored).
+        Only where the whole stack takes the fused per-block path."""
+        cd = self.compute_dtype
+        if cd is None or not input_ids.is_cuda or self.embed_tokens.weight.dtype != torch.float32:
+            return None
+        c = self.config
+        if c.head_dim != 64 or input_ids.shape[1] % 128 or not ops.native_available():
+            return None
+        for layer in self.layers:
+            at = layer.self_attn
+            if type(at) is not LlamaAttention or type(layer.mlp) is not LlamaMLP:
+                return None
+            if at.window is not None and input_ids.shape[1] > at.window:
+                return None
+        return cd
 
     def rope(self, T: int, device) -> tuple:
         key = (str(device), T)
@@ -187,6 +248,9 @@ class LlamaModel(nn.Module):
         c = self.config
         T = input_ids.shape[1]
         cos, sin = self.rope(T, input_ids.device)
+        cd = self.cast_dtype(input_ids) if cache is None else None
+        if cd is not None:
+            return self._forward_cast(input_ids, cd, cos, sin)
         x = ops.embedding(input_ids, self.embed_tokens.weight)
         # the residual stream: each block's two residual adds are fused with the RMSNorm after them
         h = self.layers[0].input_layernorm(x)
@@ -209,6 +273,40 @@ class LlamaModel(nn.Module):
             x, h = ops.add_rms_norm(x, m, nxt.weight, c.rms_norm_eps)
         return h
 
+    def _forward_cast(self, input_ids, cd, cos, sin):
+        """fp32 parameters, ``cd`` compute: the embedding gathers fp32 rows (no table cast) and
+        casts them; each block's weights — with the NEXT norm's weight, so every parameter is
+        cast exactly once — go through one fused cast (``_CastGroup``)."""
+        c = self.config
+        x = ops.embedding(input_ids, self.embed_tokens.weight).to(cd)
+        (w_in,) = _CastGroup.apply(cd, self.layers[0].input_layernorm.weight)
+        h = ops.rms_norm(x, w_in, c.rms_norm_eps)
+        for i, layer in enumerate(self.layers):
+            nxt = self.layers[i + 1].input_layernorm if i + 1 < len(self.layers) else self.norm
+            at, mlp = layer.self_attn, layer.mlp
+            ps = [at.qkv_proj.weight, at.o_proj.weight, layer.post_attention_layernorm.weight,
+                  mlp.gate_up_proj.weight, mlp.down_proj.weight, nxt.weight]
+            if at.qkv_proj.bias is not None:
+                ps.append(at.qkv_proj.bias)
+            if at.o_proj.bias is not None:
+                ps.append(at.o_proj.bias)
+            ws = _CastGroup.apply(cd, *ps)
+            w_qkv, w_o, w_post, w_gu, w_down, w_next = ws[:6]
+            extra = list(ws[6:])
+            b_qkv = extra.pop(0) if at.qkv_proj.bias is not None else None
+            b_o = extra.pop(0) if at.o_proj.bias is not None else None
+            r = ops.llama_block(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, at.H, at.Hkv,
+                                c.rms_norm_eps, cos, sin)
+            if r is None:  # (cast_dtype() checked the conditions: not expected)
+                qkv = ops.gemm_linear(h, w_qkv, b_qkv)
+                a = ops.gemm_linear(ops.attention_qkv(qkv, at.H, causal=True, n_kv_head=at.Hkv, rope=(cos, sin)),
+                                    w_o, b_o)
+                x, h = ops.add_rms_norm(x, a, w_post, c.rms_norm_eps)
+                x, h = ops.add_rms_norm(x, ops.mlp_swiglu(h, w_gu, w_down), w_next, c.rms_norm_eps)
+            else:
+                x, h = r
+        return h
+
 
 class _LlamaPreTrained(nn.Module):
     def _init_weights(self) -> None:
@@ -222,7 +320,10 @@ class _LlamaPreTrained(nn.Module):
 
 class LlamaForSequenceClassification(_LlamaPreTrained):
     """HF ``LlamaForSequenceClassification`` semantics: score the rightmost non-pad token;
-    cross-entropy loss when ``labels`` are given.  Returns (loss, logits)."""
+    cross-entropy loss when ``labels`` are given.  Returns ``SequenceClassifierOutput`` —
+    a ``(loss, logits)`` tuple with ``.loss`` / ``.logits``, so a notebook written against the HF
+    model (``out = model(input_ids=..., attention_mask=..., labels=...)``; ``out.loss``) runs
+    unchanged on it."""
 
     def __init__(self, c: LlamaConfig):
         super().__init__()
@@ -231,7 +332,8 @@ class LlamaForSequenceClassification(_LlamaPreTrained):
         self.score = nn.Linear(c.hidden_size, c.num_labels, bias=False)
         self._init_weights()
 
-    def forward(self, input_ids, attention_mask=None, labels=None):
+    def forward(self, input_ids, attention_mask=None, labels=None, **hf_kwargs):
+        _check_hf_kwargs(hf_kwargs)
         h = self.model(input_ids)
         B, T, C = h.shape
         if self.config.pad_token_id is None:
@@ -241,11 +343,12 @@ class LlamaForSequenceClassification(_LlamaPreTrained):
             last = (torch.arange(T, device=h.device, dtype=torch.int32) * nonpad).argmax(-1)
         # gather (backward = scatter-add: no sort, graph-safe) instead of advanced indexing
         pooled = torch.gather(h, 1, last.view(B, 1, 1).expand(B, 1, C)).squeeze(1)
-        logits = self.score(pooled)
+        w = self.score.weight
+        logits = self.score(pooled) if w.dtype == pooled.dtype else F.linear(pooled, w.to(pooled.dtype))
         loss = None
         if labels is not None:
             loss = F.cross_entropy(logits.float(), labels.view(-1))
-        return loss, logits
+        return SequenceClassifierOutput(loss, logits)
 
 
 class LlamaForCausalLM(_LlamaPreTrained):
@@ -282,7 +385,7 @@ class LlamaForCausalLM(_LlamaPreTrained):
                 from ..parallel.context import context_loss
 
                 loss = context_loss(loss, (tgt != -100).sum(), cp[0])
-        return loss, (logits if return_logits else None)
+        return CausalLMOutput(loss, logits if return_logits else None)
 
     # ------------------------------------------------------------------ generation (generation.py)
     def kv_layout(self):
@@ -352,9 +455,22 @@ def hf_to_nbd_state_dict(sd: Dict[str, torch.Tensor], c: LlamaConfig) -> Dict[st
     return out
 
 
-def from_hf(hf_model) -> nn.Module:
+# keyword arguments an HF call may pass that change nothing here
+_HF_NEUTRAL = {"return_dict": (True, None), "output_attentions": (False, None), "output_hidden_states": (False, None),
+               "use_cache": (False, None, True), "token_type_ids": (None,), "position_ids": (None,)}
+
+
+def _check_hf_kwargs(kw) -> None:
+    for k, v in kw.items():
+        if k not in _HF_NEUTRAL or not any(v is x or (x is not None and v == x) for x in _HF_NEUTRAL[k]):
+            raise TypeError(f"nbd Llama: unsupported argument {k}={v!r}")
+
+
+def from_hf(hf_model, compute_dtype: Optional[torch.dtype] = None) -> nn.Module:
     """Build the equivalent nbd model from an instantiated HF Llama sequence-classification or
-    causal-LM model (weights copied)."""
+    causal-LM model (weights copied, same dtype and device).  ``compute_dtype`` (e.g. bf16) with
+    fp32 weights: keep the fp32 parameters (the optimizer's master copy) and run the fused HIP
+    path in that dtype (mixed precision, one cast per decoder layer — ``LlamaModel.compute_dtype``)."""
     c = LlamaConfig.from_hf(hf_model.config)
     cls = LlamaForSequenceClassification if hasattr(hf_model, "score") else LlamaForCausalLM
     m = cls(c)
@@ -363,8 +479,23 @@ def from_hf(hf_model) -> nn.Module:
     missing = [k for k in missing if not (k == "lm_head.weight" and c.tie_word_embeddings)]
     if missing or unexpected:
         raise ValueError(f"from_hf: missing {missing}, unexpected {unexpected}")
-    return m.to(next(hf_model.parameters()).dtype)
+    p0 = next(hf_model.parameters())
+    m = m.to(device=p0.device, dtype=p0.dtype)
+    m.train(hf_model.training)
+    if compute_dtype is not None and compute_dtype != p0.dtype:
+        m.model.compute_dtype = compute_dtype
+    return m
+
+
+def native(hf_model, compute_dtype: Optional[torch.dtype] = torch.bfloat16) -> nn.Module:
+    """The one-line swap for a notebook written against HF transformers: call it on the HF
+    Llama / SmolLM2 / Qwen2 / Mistral model BEFORE creating the optimizer and
+    ``accelerator.prepare``.  The returned module takes the same keyword arguments, returns
+    outputs with ``.loss`` / ``.logits``, keeps the HF parameters' dtype (fp32 master weights for
+    ``torch.optim.AdamW``) and computes in ``compute_dtype`` on the fused HIP path (bf16 by
+    default: the same mixed-precision recipe as ``Accelerator(mixed_precision="bf16")``)."""
+    return from_hf(hf_model, compute_dtype=compute_dtype)
 
 
 __all__ = ["LlamaConfig", "LlamaModel", "LlamaForSequenceClassification", "LlamaForCausalLM", "RMSNorm",
-           "from_hf", "hf_to_nbd_state_dict"]
+           "from_hf", "native", "hf_to_nbd_state_dict", "SequenceClassifierOutput", "CausalLMOutput"]

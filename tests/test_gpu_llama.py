@@ -176,3 +176,40 @@ def test_attention_with_fused_rope_matches_separate_rope(dev, Hkv):
     torch.cuda.synchronize()
     assert _rel(y1, y2) < 1e-2, _rel(y1, y2)
     assert _rel(a.grad, b.grad) < 2e-2, _rel(a.grad, b.grad)
+
+
+def test_native_swap_bf16_compute_fp32_master(dev):
+    """``nbd.models.native(hf_fp32)`` on the GPU: fp32 parameters, bf16 fused compute (one cast
+    per layer), loss/logits close to the fp32 HF model, fp32 gradients on every parameter,
+    and one torch AdamW step moves the fp32 weights."""
+    transformers = pytest.importorskip("transformers")
+    import nbdistributed_amd as nbd
+    from nbdistributed_amd.models import SMOLLM2_135M
+
+    cfg = dict(SMOLLM2_135M)
+    cfg.update(num_hidden_layers=2, vocab_size=4096)
+    torch.manual_seed(0)
+    hf = transformers.LlamaForSequenceClassification(
+        transformers.LlamaConfig(num_labels=2, pad_token_id=0, **cfg)).to(dev)
+    m = nbd.models.native(hf)
+    assert m.model.compute_dtype == torch.bfloat16
+    assert all(p.dtype == torch.float32 and p.is_cuda for p in m.parameters())
+    ids, mask, labels = _batch(dev)
+    assert m.model.cast_dtype(ids) == torch.bfloat16
+    out = m(input_ids=ids, attention_mask=mask, labels=labels)
+    ref = hf(input_ids=ids, attention_mask=mask, labels=labels)
+    assert out.logits.dtype == torch.bfloat16
+    assert _rel(out.logits.float(), ref.logits) < 5e-2, (out.logits, ref.logits)
+    assert abs(float(out.loss) - float(ref.loss)) < 3e-2
+    out.loss.backward()
+    ref.loss.backward()
+    grads = {n: p.grad for n, p in m.named_parameters()}
+    assert all(g is not None and g.dtype == torch.float32 for g in grads.values()), \
+        [n for n, g in grads.items() if g is None or g.dtype != torch.float32]
+    hg = dict(hf.named_parameters())
+    assert _rel(grads["model.norm.weight"], hg["model.norm.weight"].grad) < 0.1
+    assert _rel(grads["model.embed_tokens.weight"], hg["model.embed_tokens.weight"].grad) < 0.1
+    w0 = m.model.layers[0].mlp.down_proj.weight.detach().clone()
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+    opt.step()
+    assert not torch.equal(w0, m.model.layers[0].mlp.down_proj.weight)

@@ -73,3 +73,26 @@ def test_tied_lm_head_and_param_count():
     m = LlamaForCausalLM(LlamaConfig.smollm2_135m())
     assert m.lm_head.weight is m.model.embed_tokens.weight
     assert sum(p.numel() for p in m.parameters()) == 134_515_008  # SmolLM2-135M
+
+
+def test_native_swap_has_hf_outputs_and_signature():
+    """``nbd.models.native(hf)``: same keyword call, ``out.loss`` / ``out.logits``, fp32 master
+    parameters kept (CPU: the plain-math path)."""
+    import nbdistributed_amd as nbd
+
+    torch.manual_seed(0)
+    c = LlamaConfig.tiny(rope_theta=100000.0)
+    hf = transformers.LlamaForSequenceClassification(_hf_config(c, num_labels=2)).eval()
+    ours = nbd.models.native(hf).eval()
+    assert all(p.dtype == torch.float32 for p in ours.parameters())
+    ids, mask = _batch()
+    labels = torch.tensor([0, 1, 1])
+    ref = hf(input_ids=ids, attention_mask=mask, labels=labels)
+    out = ours(input_ids=ids, attention_mask=mask, labels=labels, return_dict=True)
+    assert torch.allclose(out.logits, ref.logits, atol=2e-5, rtol=1e-4)
+    assert abs(float(out.loss) - float(ref.loss)) < 1e-5
+    loss, logits = out  # still a (loss, logits) tuple
+    assert loss is out.loss and logits is out.logits
+    assert ours(input_ids=ids, attention_mask=mask).loss is None
+    with pytest.raises(TypeError):
+        ours(input_ids=ids, output_attentions=True)

@@ -10,10 +10,12 @@ from nbdistributed_amd.utils.fakeshell import HeadlessShell
 NB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "00_accelerate_mi355x.ipynb")
 
 
-def test_example_notebook_runs_end_to_end(monkeypatch):
+@pytest.mark.parametrize("hf_only", [False, True], ids=["native-swap", "hf-as-written"])
+def test_example_notebook_runs_end_to_end(monkeypatch, hf_only):
     pytest.importorskip("transformers")
     pytest.importorskip("accelerate")
     monkeypatch.setenv("NBD_NOTEBOOK_TINY", "1")
+    monkeypatch.setenv("NBD_NOTEBOOK_HF", "1" if hf_only else "0")
     cells = [c for c in json.load(open(NB))["cells"] if c["cell_type"] == "code"]
     sh = HeadlessShell()
     core = sh.load_extension()
