@@ -342,7 +342,9 @@ class DistributedDataParallel(torch.nn.Module):
             # launch: RCCL runs a one-rank ReduceOp.AVG as a full pre-multiply pass over the bucket
             # (oneRankReduce<FuncPreMulSum>: 190 µs per 48 MB bucket, profiles/gpt2_graph_prof_r3*.md)
             return _DONE
-        op = dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
+        # (forced at world 1: the average over one rank is the sum — RCCL would run AVG as a
+        # separate pre-multiply pass over the bucket there, an artefact no N-GPU run has)
+        op = dist.ReduceOp.AVG if avg and self.world > 1 else dist.ReduceOp.SUM
         if self.shard:  # ZeRO-2: this rank keeps the averaged gradient of its slice only
             return dist.reduce_scatter_tensor(b.grad_shard, b.buffer, op=op, group=self.pg, async_op=True)
         return dist.all_reduce(b.buffer, op=op, group=self.pg, async_op=True)
