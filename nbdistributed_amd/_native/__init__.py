@@ -100,6 +100,10 @@ def _torch_build_flags() -> tuple:
     inc = cpp_extension.include_paths()
     libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    import sysconfig
+
+    # Python.h: ddp_hooks.cpp calls back into the interpreter (symbols resolve in the host process)
+    inc = list(inc) + [sysconfig.get_paths()["include"]]
     cflags = [f"-I{p}" for p in inc] + [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H"]
     ldflags = [f"-L{libdir}", f"-Wl,-rpath,{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-lc10_hip", "-ltorch_hip"]
     return cflags, ldflags

@@ -107,7 +107,8 @@ class DistributedDataParallel(torch.nn.Module):
                  broadcast_buffers: bool = True, init_sync: bool = True, align: int = 64,
                  flat_params: bool = False, grad_mode: str = "unflatten", shard: bool = False,
                  grad_views: Optional[bool] = None, fused_linear: Optional[bool] = None,
-                 accumulate: str = "bucket", force_collectives: Optional[bool] = None):
+                 accumulate: str = "bucket", force_collectives: Optional[bool] = None,
+                 cpp_hooks: Optional[bool] = None):
         """``flat_params``: re-home each bucket's parameters into one contiguous buffer (the
         nn.Parameters become views) so a flat optimizer (``nbdistributed_amd.optim.FlatAdamW``)
         can update a whole bucket in one pass.  ``grad_mode="bucket"``: leave the averaged
@@ -123,7 +124,10 @@ class DistributedDataParallel(torch.nn.Module):
         ``force_collectives`` (default: ``NBD_DDP_FORCE_COLLECTIVES=1``): issue the real
         collectives even at world size 1 — every code path of a multi-GPU run (per-bucket
         flushes, side-stream collectives and events, in-place reduce-scatter / all-gather, RCCL
-        inside a captured graph) then runs, and can be timed and profiled, on one GPU."""
+        inside a captured graph) then runs, and can be timed and profiled, on one GPU.
+        ``cpp_hooks`` (default: on for GPU modules, ``NBD_DDP_CPP_HOOKS=0`` turns it off): count
+        bucket readiness in C++ hooks (``csrc/kernels/ddp_hooks.cpp``) instead of one Python hook
+        per parameter."""
         super().__init__()
         self._token = object()  # ownership of registrations / patches shared with newer DDPs
         self.module = module
@@ -229,15 +233,32 @@ class DistributedDataParallel(torch.nn.Module):
         # the hooks, its gradient-destination registrations and its patched forwards — unless a
         # newer DDP on the same module has taken them over (ownership token)
         wself = weakref.ref(self)
+        self._hooks = []
+        self._hook_handle = None
+        self._hook_buckets = [self._bucket_of[id(p)].index for p in self.params]
+        if cpp_hooks is None:
+            cpp_hooks = self.cuda and os.environ.get("NBD_DDP_CPP_HOOKS", "1") != "0"
+        if cpp_hooks and ops.native_available():
+            # bucket readiness counted in C++ (csrc/kernels/ddp_hooks.cpp): Python is entered
+            # once at the first gradient of a pass and once per completed bucket, not once per
+            # parameter (the eager step is host-bound)
+            def _on_bucket(i, _w=wself):
+                s = _w()
+                if s is not None:
+                    s._bucket_event(i)
 
-        def _hook(p, _w=wself):
-            s = _w()
-            if s is not None:
-                s._grad_ready(p)
+            self._hook_cb = _on_bucket
+            self._hook_handle = int(torch.ops.nbd.ddp_hooks_install(self.params, self._hook_buckets, id(_on_bucket)))
+        else:
+            def _hook(p, _w=wself):
+                s = _w()
+                if s is not None:
+                    s._grad_ready(p)
 
-        self._hooks = [p.register_post_accumulate_grad_hook(_hook) for p in self.params]
+            self._hooks = [p.register_post_accumulate_grad_hook(_hook) for p in self.params]
         self._finalizer = weakref.finalize(self, _release, self._token, self._hooks, list(self._patched),
-                                           [p for b in self.buckets if b.views is not None for p in b.params])
+                                           [p for b in self.buckets if b.views is not None for p in b.params],
+                                           self._hook_handle, list(self.params))
         if init_sync and self._collectives:
             self._broadcast_tensors([p.data for p in module.parameters()])
             self._broadcast_tensors(list(module.buffers()))
@@ -267,7 +288,7 @@ class DistributedDataParallel(torch.nn.Module):
         """Undo ``fused_linear`` and the gradient-destination registrations (those still owned
         by this DDP); also runs when the DDP object is garbage-collected."""
         params = [p for b in self.buckets if b.views is not None for p in b.params]
-        _release(self._token, [], self._patched, params)
+        _release(self._token, [], self._patched, params)  # (the bucket hooks stay: DDP still counts)
         self._patched = []
         for b in self.buckets:
             b.views = None
@@ -351,6 +372,12 @@ class DistributedDataParallel(torch.nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
+        if self._hook_handle is not None and torch.is_grad_enabled():
+            # a new pass (also after a backward that raised); hooks a user registered since
+            # replaced ours: wrap theirs again
+            self._rearm()
+            if torch.ops.nbd.ddp_hooks_intact(self._hook_handle, self.params) != len(self.params):
+                torch.ops.nbd.ddp_hooks_reattach(self._hook_handle, self.params, self._hook_buckets)
         if self._n_views:
             from ..ops import graddst
 
@@ -393,6 +420,20 @@ class DistributedDataParallel(torch.nn.Module):
             b.ready = b.launched = False
             b.work = None
         torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+
+    def _bucket_event(self, i: int) -> None:
+        """C++ hook callback: ``i = -1`` first gradient of a pass, else bucket ``i`` complete."""
+        if not self._in_backward:
+            self._start_backward()
+        if i < 0:
+            return
+        b = self.buckets[i]
+        b.pending = 0
+        b.ready = True
+        if self._sync_pass:
+            self._launch_ready()
+        else:
+            self._prereduce_local(b)
 
     def _grad_ready(self, p: torch.nn.Parameter) -> None:
         if not self._in_backward:
@@ -594,10 +635,14 @@ class DistributedDataParallel(torch.nn.Module):
     def _finalize(self) -> None:
         self._flush_deferred()
         if not self._sync_pass:  # no_sync micro-batch: buckets hold the local sums, nothing to send
+            if self._hook_handle is not None and not all(b.ready for b in self.buckets):
+                for b, n in zip(self.buckets, torch.ops.nbd.ddp_hooks_pending(self._hook_handle)):
+                    b.pending = int(n)
             for b in self.buckets:
                 if not b.ready and b.pending < len(b.params):
                     self._prereduce_local(b)  # (some parameters of it got no gradient)
             self._in_backward = False
+            self._rearm()
             return
         # buckets whose params got no gradient this step (unused parameters): zeros
         for b in self.buckets:
@@ -624,6 +669,11 @@ class DistributedDataParallel(torch.nn.Module):
             b.rest_grads, b.rest_offsets = [], []
             b.work = None
         self._in_backward = False
+        self._rearm()
+
+    def _rearm(self) -> None:
+        if self._hook_handle is not None:
+            torch.ops.nbd.ddp_hooks_rearm(self._hook_handle)
 
     # ------------------------------------------------------------------ broadcast
     def _broadcast_tensors(self, tensors: List[torch.Tensor]) -> None:
@@ -634,11 +684,16 @@ class DistributedDataParallel(torch.nn.Module):
 _GRAD_OWNER: Dict[int, object] = {}
 
 
-def _release(token, hooks, patched, params) -> None:
+def _release(token, hooks, patched, params, hook_handle=None, all_params=()) -> None:
     """Undo one DDP's hooks, patched ``nn.Linear`` forwards and gradient-destination
     registrations, leaving alone whatever a newer DDP on the same module has taken over."""
     for h in hooks:
         h.remove()
+    if hook_handle is not None:
+        try:
+            torch.ops.nbd.ddp_hooks_remove(hook_handle, list(all_params))
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
     for m in patched:
         if m.__dict__.get("_nbd_ddp_owner") is token:
             m.__dict__.pop("forward", None)

@@ -169,3 +169,36 @@ res
     r = sess.execute(code, render=False)
     for rank in (0, 1):
         assert r.results[rank]["echo"] == "[True, True, True, True, True, True]", r.results[rank]
+
+
+def test_cpp_bucket_hooks_match_torch_ddp(sess):
+    """Bucket readiness counted by the C++ post-accumulate hooks (csrc/kernels/ddp_hooks.cpp):
+    same gradients as torch DDP with an unused parameter and no_sync accumulation; a hook the
+    user registers later still fires and DDP keeps working; a dropped DDP removes its hooks."""
+    code = """
+import gc
+ours_c = NbdDDP(copy.deepcopy(base), bucket_cap_mb=0.01, first_bucket_mb=0.005, cpp_hooks=True)
+assert ours_c._hook_handle is not None and not ours_c._hooks
+ok = []
+for accum in (1, 3, 1):
+    gr = run(ref, accum)
+    go = run(ours_c, accum)
+    ok += [(b is None or float(b.abs().max()) == 0.0) if a is None else bool(torch.allclose(a, b, atol=1e-6, rtol=1e-5))
+           for a, b in zip(gr, go)]
+seen = []
+h = ours_c.module.a.weight.register_post_accumulate_grad_hook(lambda p: seen.append(1))
+gr, go = run(ref, 1), run(ours_c, 1)
+ok += [bool(torch.allclose(a, b, atol=1e-6, rtol=1e-5)) for a, b in zip(gr, go) if a is not None]
+intact = int(torch.ops.nbd.ddp_hooks_intact(ours_c._hook_handle, ours_c.params)) == len(ours_c.params)
+h.remove()
+handle, params = ours_c._hook_handle, ours_c.params
+del ours_c
+gc.collect()
+gone = int(torch.ops.nbd.ddp_hooks_intact(handle, params)) == 0
+(all(ok), seen == [1], intact, gone)
+"""
+    sess.execute(SETUP, render=False)
+    sess.execute(STEP, render=False)  # defines run()
+    r = sess.execute(code, render=False)
+    for rank in (0, 1):
+        assert r.results[rank]["output"] == "(True, True, True, True)", r.results[rank]
