@@ -156,6 +156,38 @@ def bench_prereduce(res, dev):
     t_torch = timeit(torch_pre)
     res["prereduce_4x_bf16"] = {"numel": n, "hip_ms": t_hip, "torch_ms": t_torch, "hip_GBps": byts / t_hip / 1e6,
                                 "torch_GBps": byts / t_torch / 1e6, "speedup": t_torch / t_hip}
+    del xs, out
+    # K3 on DDP's no_sync path (parallel/ddp.py _prereduce_local, buckets without gradient views):
+    # one micro-batch's bf16 gradients summed into a 64 MiB bf16 bucket (fp32 math, one rounding),
+    # GPT-2 block shapes filling the bucket; bytes = gradients read + bucket read + bucket written
+    d = 768
+    block = [(d,), (d,), (d, 3 * d), (3 * d,), (d, d), (d,), (d,), (d,), (d, 4 * d), (4 * d,), (4 * d, d), (d,)]
+    shapes, numel = [], 0
+    while True:
+        for s in block:
+            k = 1
+            for x in s:
+                k *= x
+            if (numel + k) * 2 > (64 << 20):
+                break
+            shapes.append(s)
+            numel += k
+        else:
+            continue
+        break
+    grads = [torch.randn(s, device=dev, dtype=torch.bfloat16) for s in shapes]
+    offs, total = ops.plan_offsets([g.numel() for g in grads])
+    bucket = torch.zeros(total, device=dev, dtype=torch.bfloat16)
+    t_acc = timeit(lambda: ops.prereduce_into_bucket(grads, bucket, offs))
+
+    def torch_acc():
+        for g, o in zip(grads, offs):
+            bucket[o:o + g.numel()].add_(g.view(-1))
+
+    t_torch = timeit(torch_acc)
+    res["nosync_prereduce_64MiB"] = {"tensors": len(grads), "numel": numel, "hip_ms": t_acc, "torch_ms": t_torch,
+                                     "hip_GBps": numel * 6 / t_acc / 1e6, "torch_GBps": numel * 6 / t_torch / 1e6,
+                                     "speedup": t_torch / t_acc}
 
 
 def bench_summary(res, dev):

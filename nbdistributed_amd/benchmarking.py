@@ -293,6 +293,62 @@ def bench_cells_magic(session, steps: int, warmup: int, code: str = "1 + 1") -> 
             "rendered_bytes": rendered[0]}
 
 
+IPYTHON_PY = "/opt/conda/bin/python3.9"  # IPython 7.29, no torch: a kernel that never imports torch
+
+IPYTHON_KERNEL = """
+import io, json, statistics, sys, time
+sys.path.insert(0, {root!r})
+from IPython.core.interactiveshell import InteractiveShell
+sh = InteractiveShell.instance()
+sh.run_cell("%load_ext nbdistributed_amd")
+res = {{}}
+for n in {ranks!r}:
+    r = sh.run_cell("%dist_init -n " + str(n) + " --backend gloo --python {py}")
+    assert r.error_in_exec is None, r.error_in_exec
+    real = sys.stdout
+    for code, key in (("1 + 1", "auto"), ("%%distributed\\n1 + 1", "explicit"), ("%%rank [0]\\n1 + 1", "rank0")):
+        lat = []
+        for i in range({warm} + {steps}):
+            sys.stdout = io.StringIO()     # the renderer's output, as a frontend would receive it
+            t = time.perf_counter()
+            r = sh.run_cell(code, store_history=True)
+            dt = time.perf_counter() - t
+            sys.stdout = real
+            assert r.error_in_exec is None, r.error_in_exec
+            if i >= {warm}:
+                lat.append(dt * 1e3)
+        lat.sort()
+        res.setdefault(str(n), {{}})[key] = {{"p50_ms": statistics.median(lat), "p90_ms": lat[int(0.9 * (len(lat) - 1))],
+                                           "min_ms": lat[0], "steps": len(lat)}}
+    sh.run_cell("%dist_shutdown")
+print("RESULT " + json.dumps(res))
+"""
+
+
+def bench_cells_ipython(ranks: List[int], steps: int = 200, warmup: int = 20, timeout_s: float = 300.0,
+                        worker_python: Optional[str] = None) -> Dict[str, Any]:
+    """The trivial cell through a REAL IPython ``InteractiveShell.run_cell`` (input transformers,
+    auto mode -> ``%%distributed``, cell-magic dispatch, run-cell events, history) on the
+    torch-less IPython interpreter, with CPU/gloo workers of the PyTorch interpreter — the control
+    plane as a Jupyter kernel drives it (the GPU plays no part in a trivial cell's round trip).
+    Returns {ranks: {auto|explicit|rank0: {p50_ms, ...}}}; raises if no IPython is installed."""
+    import json as _json
+    import subprocess
+    import textwrap
+
+    if not os.path.exists(IPYTHON_PY):
+        raise FileNotFoundError(f"no IPython interpreter at {IPYTHON_PY}")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent(IPYTHON_KERNEL.format(root=root, ranks=list(ranks), py=worker_python or sys.executable,
+                                                 warm=warmup, steps=steps))
+    env = {k: v for k, v in os.environ.items() if k not in ("PYTHONPATH", "PYTHONHOME")}
+    p = subprocess.run([IPYTHON_PY, "-c", code], capture_output=True, text=True, env=env, timeout=timeout_s)
+    line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]
+    if p.returncode != 0 or not line:
+        raise RuntimeError(f"real-IPython cell bench failed ({p.returncode}): {(p.stdout + p.stderr)[-600:]}")
+    return _json.loads(line[0][7:])
+
+
 WORLD_CHECK = "(dist.get_world_size(), dist.get_backend(), rank)"
 
 
@@ -596,6 +652,16 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
         if "p50_ms" in out["cell_magic"]:
             _log(f"magic-path cell p50 {out['cell_magic']['p50_ms']:.3f} ms")
         ckpt(out)
+        if os.path.exists(IPYTHON_PY) and os.environ.get("NBD_BENCH_IPYTHON", "1") != "0":
+            _log(f"phase 1c: trivial cells through a real IPython kernel ({n} gloo worker(s))")
+            _phase(session, out, "cell_ipython",
+                   lambda: bench_cells_ipython([n], steps=max(steps, 50), warmup=warmup,
+                                               timeout_s=max(30.0, min(240.0, deadline - time.monotonic() - 5.0))),
+                   phase_timeout_s, deadline, 30.0)
+            ci = out["cell_ipython"].get(str(n), {}).get("auto") if isinstance(out["cell_ipython"], dict) else None
+            if ci:
+                _log(f"real-IPython cell p50 {ci['p50_ms']:.3f} ms")
+            ckpt(out)
         hang = os.environ.get("NBD_BENCH_FAULT_HANG")
         if hang:  # fault injection (tests): a cell that outlives the budget must not cost the line
             _phase(session, out, "fault_hang",
@@ -691,6 +757,17 @@ def result_line(res: Dict[str, Any], n: int, steps: int, warmup: int) -> Dict[st
                                    f"{cm.get('ide_sync')} namespace delta + renderer (default settings)")
     elif cm:
         line["cell_magic_error"] = cm.get("error") or cm.get("skipped")
+    ci = res.get("cell_ipython") or {}
+    if isinstance(ci, dict) and str(n) in ci:
+        d = ci[str(n)]
+        line["cell_ipython_p50_ms"] = round(d["auto"]["p50_ms"], 4)
+        line["cell_ipython_explicit_p50_ms"] = round(d["explicit"]["p50_ms"], 4)
+        line["cell_ipython_rank0_p50_ms"] = round(d["rank0"]["p50_ms"], 4)
+        line["cell_ipython_note"] = ("plain cell through a real IPython 7.29 InteractiveShell.run_cell (auto mode, "
+                                     "ide_sync, renderer; torch-less kernel) with CPU/gloo workers: the control "
+                                     "plane as a Jupyter kernel drives it")
+    elif ci and ("error" in ci or "skipped" in ci):
+        line["cell_ipython_error"] = ci.get("error") or ci.get("skipped")
     wd = res.get("world") or {}
     if "per_rank" in wd:
         line["rccl_world_size"] = {str(r): v["world_size"] for r, v in wd["per_rank"].items()}

@@ -67,6 +67,11 @@ class WorkerProc:
         return self.proc.poll() is None
 
 
+# torchrun's per-process variables (the workers get their own RANK / WORLD_SIZE / MASTER_*)
+_LAUNCHER_VARS = {"RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                  "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"}
+
+
 class ProcessManager:
     """Spawns and supervises the local worker processes."""
 
@@ -133,7 +138,11 @@ class ProcessManager:
         self.comm_endpoint = comm_endpoint
         plan = self.plan_gpus(num_processes, gpu_ids)
         gpus = [g for g in plan if g is not None]
-        env_base = dict(os.environ)
+        # a kernel that itself runs under torchrun / torchelastic (e.g. bench.py's coordinator)
+        # must not hand its launcher's rendezvous to the workers: TORCHELASTIC_USE_AGENT_STORE
+        # would make rank 0 join the agent's store as a client instead of hosting its own, and
+        # every rank would wait forever
+        env_base = {k: v for k, v in os.environ.items() if k not in _LAUNCHER_VARS and not k.startswith("TORCHELASTIC_")}
         if extra_env:
             env_base.update(extra_env)
         if gpus:
