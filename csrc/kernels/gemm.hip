@@ -60,9 +60,9 @@ constexpr int NT = 256;
 // STAGES >= 100: the ping-pong schedule (gemm_body, below) with a ring of STAGES - 100 buffers
 constexpr int ring_of(int stages) { return stages >= 100 ? stages - 100 : stages; }
 
-template <int BM, int BN, int STAGES, int KS = 1, int BKT = BK>
+template <int BM, int BN, int STAGES, int KS = 1>
 struct Smem {
-  static constexpr int BUF = (BM + BN) * BKT * 2;     // one A + B K-tile pair
+  static constexpr int BUF = (BM + BN) * BK * 2;      // one A + B K-tile pair
   static constexpr int LDC = BN + 4;                  // fp32 C-tile row stride (+16 B: rows hit distinct banks)
   static constexpr int CT = BM * LDC * 4 + BM * 4;    // fp32 C tile (+ row-sum scratch), reuses the operand buffers
   static constexpr int PIPE = KS * ring_of(STAGES) * BUF;  // one pipeline per K-split group
@@ -93,18 +93,13 @@ __device__ __forceinline__ void wait_barrier() {
 // The kernel body as a device function: `bx` = tile index (before the XCD remap), `by` = split
 // index, `S` = number of splits, `smem_all` = the launch's single LDS object.  gemm_kernel runs one
 // product per launch; pair_kernel (below) runs two independent products in one grid.
-// BKT = K-tile depth: 64 (two 16x16x32 k-steps per tile), or 32 — one k-step per tile, the tiles
-// half the bytes, so a 4-deep ring with three tiles in flight fits two 128x128 workgroups per CU
-// (STAGES = 4: counted vmcnt across the barriers instead of the 2-stage loop's vmcnt(0) drain).
-template <int BM, int BN, bool A_KM, bool B_KN, int EPI, int STAGES, int W, int KS, int BKT = BK>
+template <int BM, int BN, bool A_KM, bool B_KN, int EPI, int STAGES, int W, int KS>
 __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, uint8_t* smem_all) {
   constexpr int NTW = 64 * W * KS, WM = 2, WN = W / 2;
   constexpr int FM = BM / (16 * WM), FN = BN / (16 * WN);  // 16-wide fragments per wave along m / n
-  using SM = Smem<BM, BN, STAGES, KS, BKT>;
-  constexpr int A_BYTES = BM * BKT * 2, BUF = SM::BUF, LDC = SM::LDC;
-  constexpr int NPT = (BM + BN) * BKT / (512 * W);  // glds per thread per K-tile
-  constexpr int KK = BKT / 32;                      // 16x16x32 k-steps per K-tile
-  static_assert(BKT == BK || (STAGES >= 3 && STAGES < 100), "32-deep K-tiles: the counted ring only");
+  using SM = Smem<BM, BN, STAGES, KS>;
+  constexpr int A_BYTES = BM * BK * 2, BUF = SM::BUF, LDC = SM::LDC;
+  constexpr int NPT = (BM + BN) / (8 * W);  // glds per thread per K-tile
 
   const int lane = threadIdx.x & 63, wave_all = threadIdx.x >> 6;
   const int kg = wave_all / W, wave = wave_all % W;  // K-split group, wave within the group
@@ -136,15 +131,15 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;  // bf16 1.0
 
-  const int nk = p.K / BKT / KS;  // K-tiles of this group: t_global = t * KS + kg
+  const int nk = p.K / BK / KS;  // K-tiles of this group: t_global = t * KS + kg
   auto compute = [&](const uint8_t* cur) {
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
+    for (int kk = 0; kk < 2; ++kk) {
       s8v af[FM], bf[FN];
 #pragma unroll
-      for (int j = 0; j < FM; ++j) af[j] = frag<BM, A_KM, BKT>(cur, wm * (BM / WM) + 16 * j, kk, lane);
+      for (int j = 0; j < FM; ++j) af[j] = frag<BM, A_KM>(cur, wm * (BM / WM) + 16 * j, kk, lane);
 #pragma unroll
-      for (int i = 0; i < FN; ++i) bf[i] = frag<BN, B_KN, BKT>(cur + A_BYTES, wn * (BN / WN) + 16 * i, kk, lane);
+      for (int i = 0; i < FN; ++i) bf[i] = frag<BN, B_KN>(cur + A_BYTES, wn * (BN / WN) + 16 * i, kk, lane);
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -158,11 +153,11 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
     }
   };
   // DMA addressing: per-lane 32-bit offsets computed once, a scalar base per K-step
-  const Pieces<BM, A_KM, W, BKT> pa(p.lda, wave, lane);
-  const Pieces<BN, B_KN, W, BKT> pb(p.ldb, wave, lane, EPI == EPI_SWIGLU ? (int64_t)(p.N / 2) : 0);
+  const Pieces<BM, A_KM, W> pa(p.lda, wave, lane);
+  const Pieces<BN, B_KN, W> pb(p.ldb, wave, lane, EPI == EPI_SWIGLU ? (int64_t)(p.N / 2) : 0);
   auto stage_tile = [&](int t, uint8_t* buf) {
-    pa.stage(A, p.lda, m0, (t * KS + kg) * BKT, buf, wave);
-    pb.stage(B, p.ldb, EPI == EPI_SWIGLU ? n0 / 2 : n0, (t * KS + kg) * BKT, buf + A_BYTES, wave);
+    pa.stage(A, p.lda, m0, (t * KS + kg) * BK, buf, wave);
+    pb.stage(B, p.ldb, EPI == EPI_SWIGLU ? n0 / 2 : n0, (t * KS + kg) * BK, buf + A_BYTES, wave);
   };
 
   if constexpr (STAGES >= 100) {
@@ -540,10 +535,10 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
 // dispatcher hands out blocks in id order as slots free up, so the half with the longer units
 // goes first (longest-processing-time order): a short-unit half dispatched first leaves the
 // long units as a serial tail once it drains (ops/gemm.py pair_plan).
-template <int BM, int BN, int W, int STAGES, int EPI1, int EPI2, int BKT = BK>
+template <int BM, int BN, int W, int STAGES, int EPI1, int EPI2>
 __global__ __launch_bounds__(64 * W, W == 8 ? 2 : 2) void pair_kernel(Args p1, int t1, int first, Args p2, int t2, int s2,
                                                                       int wfirst) {
-  __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<BM, BN, STAGES, 1, BKT>::BYTES];
+  __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<BM, BN, STAGES, 1>::BYTES];
   const int b = (int)blockIdx.x - p1.warm_blocks;  // warm-up blocks first (gemm_kernel)
   if (b < 0) {
     warm_lines<64 * W>(p1, blockIdx.x, p1.warm_blocks);
@@ -553,11 +548,11 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : 2) void pair_kernel(Args p1, i
   if (dgrad) {
     const int l = wfirst ? b - first : b;
     if (l >= t1) return;  // padding to the XCD boundary
-    gemm_body<BM, BN, false, true, EPI1, STAGES, W, 1, BKT>(p1, l, 0, 1, smem_all);
+    gemm_body<BM, BN, false, true, EPI1, STAGES, W, 1>(p1, l, 0, 1, smem_all);
   } else {
     const int l = wfirst ? b : b - first;
     if (l >= t2 * s2) return;
-    gemm_body<BM, BN, true, true, EPI2, STAGES, W, 1, BKT>(p2, l % t2, l / t2, s2, smem_all);
+    gemm_body<BM, BN, true, true, EPI2, STAGES, W, 1>(p2, l % t2, l / t2, s2, smem_all);
   }
 }
 
@@ -1057,19 +1052,13 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   const int64_t nblocks = (int64_t)p1.warm_blocks + nb1 + nb2;
   TORCH_CHECK(nblocks < (1LL << 31), "nbd::gemm_pair: grid too large");
   const dim3 grid((unsigned)nblocks);
-  // NBD_GEMM_PAIR_PP=1: the 128x128 halves on the ping-pong schedule (one workgroup per CU);
-  // NBD_GEMM_PAIR_BK32=1: 32-deep K-tiles in a 4-stage counted-vmcnt ring (two workgroups per CU)
+  // NBD_GEMM_PAIR_PP=1: the 128x128 halves on the ping-pong schedule (one workgroup per CU)
   const char* pp_env = std::getenv("NBD_GEMM_PAIR_PP");
-  const char* bk_env = std::getenv("NBD_GEMM_PAIR_BK32");
-  const int pair_var = (pp_env != nullptr && pp_env[0] == '1') ? 1 : (bk_env != nullptr && bk_env[0] == '1') ? 2 : 0;
-  const bool pp = pair_var == 1, bk32 = pair_var == 2;
+  const bool pp = pp_env != nullptr && pp_env[0] == '1';
   auto launch = [&](auto e1, auto e2) {
     constexpr int E1 = decltype(e1)::value, E2 = decltype(e2)::value;
     if (big && pp)
       hipLaunchKernelGGL((pair_kernel<128, 128, 8, 103, E1, E2>), grid, dim3(512), 0, st, p1, t1, first, p2, t2, S, wfirst);
-    else if (big && bk32)
-      hipLaunchKernelGGL((pair_kernel<128, 128, 8, 4, E1, E2, 32>), grid, dim3(512), 0, st, p1, t1, first, p2, t2, S,
-                         wfirst);
     else if (big)
       hipLaunchKernelGGL((pair_kernel<128, 128, 8, 2, E1, E2>), grid, dim3(512), 0, st, p1, t1, first, p2, t2, S, wfirst);
     else

@@ -51,16 +51,6 @@ struct Args {
 
 // ---- swizzles ---------------------------------------------------------------------------------
 __device__ __forceinline__ int row_swz(int r) { return (r >> 1) & 7; }  // 16-B chunk XOR, row image
-// 32-deep K-tiles (64-B rows, 4 chunks per row; the counted-vmcnt 4-stage ring of gemm.hip):
-// chunk ^ g((r >> 2) & 3) with g = {0, 2, 3, 1} — the 16 lanes of each ds_read_b128 group (rows
-// {0-3, 12-15} at chunk c and rows {4-11} at chunk c^1, per 16-row fragment) then hit the 16
-// distinct 16-B slots of the 256-B bank row (a plain (r >> 2) XOR leaves a 2-way conflict)
-__device__ __forceinline__ int row_swz32(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
-template <int BKT>
-__device__ __forceinline__ int row_swz_k(int r) {
-  if constexpr (BKT == 32) return row_swz32(r);
-  else return row_swz(r);
-}
 template <int R>
 __device__ __forceinline__ int tr_swz(int k) {  // 8-B slot XOR, tr image with R-element rows
   if constexpr (R >= 128)
@@ -110,11 +100,9 @@ __device__ __forceinline__ void glds16s(const uint16_t* sbase_, uint32_t voff, u
 // image [R][64] (16-B chunk ^ row_swz(row)), tr image [64][R] (16-B chunk ^ tr_swz(k)/2); R1 >= 0: rows R/2.. come from global rows r1.. (SwiGLU's
 // up half), given as an element offset from the tile's first row.  stage() adds the uniform
 // tile / K-step base.  Offsets must fit 32 bits: rows * ld * 2 bytes (asserted on the host).
-template <int R, bool TR, int W, int BKT = 64>
+template <int R, bool TR, int W>
 struct Pieces {
-  static_assert(BKT == 64 || BKT == 32, "K-tile depth");
-  static constexpr int N = R * BKT / (512 * W);  // 1-KiB wave-pieces of an R x BKT image per wave
-  static_assert(N >= 1, "fewer image pieces than waves");
+  static constexpr int N = R / (8 * W);
   uint32_t off[N];
   __device__ __forceinline__ Pieces(int64_t ld, int wave, int lane, int64_t split_rows = 0) {
 #pragma unroll
@@ -122,10 +110,9 @@ struct Pieces {
       const int byte = (i * W + wave) * 1024 + lane * 16;
       int64_t e;
       if constexpr (!TR) {
-        constexpr int RB = 2 * BKT, CPR = BKT / 8;  // row bytes, 16-B chunks per row
-        const int r = byte / RB, pc = (byte >> 4) % CPR;
+        const int r = byte >> 7, pc = (byte >> 4) & 7;
         const int64_t row = (split_rows != 0 && r >= R / 2) ? split_rows + r - R / 2 : r;
-        e = row * ld + 8 * (pc ^ row_swz_k<BKT>(r));
+        e = row * ld + 8 * (pc ^ row_swz(r));
       } else {
         constexpr int RB = 2 * R;
         const int k = byte / RB, pc = (byte % RB) >> 4;
@@ -144,11 +131,11 @@ struct Pieces {
 
 // 16x16x32 operand fragment (lane l: rows/cols r0 + (l&15), k = 32kk + 8(l>>4) + 0..7) from an
 // LDS image with R rows (row image [R][64], 128-B rows) or R columns (tr image [64][R]).
-template <int R, bool TR, int BKT = 64>
+template <int R, bool TR>
 __device__ __forceinline__ s8v frag(const uint8_t* img, int r0, int kk, int lane) {
   if constexpr (!TR) {
     const int r = r0 + (lane & 15), c = (lane >> 4) + 4 * kk;
-    return *reinterpret_cast<const s8v*>(img + r * (2 * BKT) + ((c ^ row_swz_k<BKT>(r)) << 4));
+    return *reinterpret_cast<const s8v*>(img + r * 128 + ((c ^ row_swz(r)) << 4));
   } else {
     constexpr int RB = 2 * R;
     const int i = lane & 15, g = lane >> 4;

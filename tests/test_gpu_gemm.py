@@ -393,28 +393,3 @@ def test_gemm_next_weight_warm_up(monkeypatch):
     assert torch.equal(G.matmul(x, w2, splits=1), ref[1])
     torch.cuda.synchronize()
 
-
-@pytest.mark.parametrize("dgelu", [False, True])
-@pytest.mark.parametrize("M,N,K", [(1024, 384, 256), (8192, 768, 3072), (2048, 384, 640)])
-def test_gemm_pair_bk32_ring(dgelu, M, N, K, monkeypatch):
-    """NBD_GEMM_PAIR_BK32=1: the grouped backward's 128x128 halves with 32-deep K-tiles in a 4-stage
-    counted-vmcnt ring (64-B row images, row_swz32) = the fp32 reference, every split count."""
-    monkeypatch.setenv("NBD_GEMM_PAIR_BK32", "1")
-    g = torch.Generator(device="cuda").manual_seed(M + K)
-    dy = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
-    w = (torch.randn(N, K, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
-    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
-    aux = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16) if dgelu else None
-    rdx = dy.float() @ w.float()
-    if dgelu:
-        rdx = G._dgelu_ref(rdx, aux).float()
-    rdw = dy.float().t() @ x.float()
-    for sched in (1, 2 | 16, 4 | 16):
-        dx = torch.full((M, K), float("nan"), device="cuda", dtype=torch.bfloat16)
-        dw = torch.full((N, K), float("nan"), device="cuda", dtype=torch.bfloat16)
-        db = torch.full((N,), float("nan"), device="cuda", dtype=torch.bfloat16)
-        torch.ops.nbd.gemm_pair(dy, w, dx, G.EPI_DGELU if dgelu else G.EPI_NONE, aux, dy, x, dw, G.EPI_ROWSUM, db,
-                                sched)
-        assert (dx.float() - rdx).abs().max().item() < 2e-2 * rdx.abs().max().item(), sched
-        assert (dw.float() - rdw).abs().max().item() < 2e-2 * rdw.abs().max().item(), sched
-        assert (db.float() - dy.float().sum(0)).abs().max().item() < 2e-2 * dy.float().sum(0).abs().max().item()
