@@ -150,19 +150,30 @@ def _max_over_ranks(res) -> float:
     return max(vals)
 
 
+def _graph_arms(n: int) -> bool:
+    """Graphed arms at this world size: always at N = 1; at N > 1 unless NBD_BENCH_GRAPH_MULTI=0
+    (RCCL inside the captured step is exercised at world 1 with real collectives, the
+    ``collective_path`` arms; the graphed arms run after the eager ones and results are kept
+    arm by arm, so a capture problem at N > 1 cannot cost the measured numbers)."""
+    return n == 1 or os.environ.get("NBD_BENCH_GRAPH_MULTI", "1") != "0"
+
+
 def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 1024, compare_torch: bool = True,
               linear_rows: int = 8192, config: str = "small", linear_dim: int = 4096,
-              force_collectives: bool = True) -> Dict[str, Any]:
+              force_collectives: bool = True, out: Optional[Dict[str, Any]] = None, tick=None) -> Dict[str, Any]:
     """BASELINE configs 4 and 5 as notebook cells: DDP steps timed inside each worker (max over
     ranks).  GPT-2 small, synthetic tokens.  Primary number: bf16 parameters living in the DDP
     buckets, fp32 master weights and moments in ``FlatAdamW`` (fused HIP AdamW per bucket).  Also
     reported: fp32 params + bf16 autocast + torch fused AdamW through nbd DDP (``amp_*``) and
-    through torch DDP (``torch_ddp_*``)."""
+    through torch DDP (``torch_ddp_*``).  ``out`` is filled arm by arm (``tick()`` after each), so
+    a later arm that fails or times out leaves the earlier ones measured."""
     n = session.world_size
+    out = {} if out is None else out
+    tick = tick or (lambda: None)
     session.execute(AR_SETUP, render=False)
     session.execute(DDP_SETUP, render=False)
-    out: Dict[str, Any] = {"model": f"gpt2-{config}", "per_gpu_batch": B, "seq_len": T,
-                           "global_batch": B * n, "steps": steps, "warmup": warmup}
+    out.update({"model": f"gpt2-{config}", "per_gpu_batch": B, "seq_len": T, "global_batch": B * n, "steps": steps,
+                "warmup": warmup})
     # primary: bf16 params re-homed into the DDP buckets + FlatAdamW (fp32 master/moments, one
     # fused HIP kernel per bucket reading the all-reduced bucket); secondary: fp32 params +
     # autocast + torch fused AdamW through nbd DDP (bf16 wire)
@@ -173,29 +184,7 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
                ms_per_step=ms, tokens_per_s=toks, tokens_per_s_per_gpu=toks / n)
     if config == "small":  # 6·N·tokens FLOPs over the 2.5 PFLOP/s dense bf16 peak per GPU
         out["mfu"] = 6 * 124_439_808 * toks / (2.5e15 * n)
-    if n == 1 or os.environ.get("NBD_BENCH_GRAPH_MULTI") == "1":  # see bench_notebook
-        r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flatgraph', {config!r})", render=False)
-        gms = _max_over_ranks(r)
-        out.update(graph_ms_per_step=gms, graph_tokens_per_s=n * B * T / (gms / 1e3),
-                   graph_recipe="as the primary recipe, whole step captured in one HIP graph (GraphedStep)")
-    if n == 1 and force_collectives:
-        # the world > 1 code path on this one GPU: every bucket's all-reduce (reduce-scatter +
-        # all-gather for ZeRO-2) issued on RCCL from the DDP side stream / inside the graph, with
-        # the per-bucket flushes and events of a multi-GPU run — what an N-GPU rank executes
-        cp: Dict[str, Any] = {"note": "NBD_DDP_FORCE_COLLECTIVES semantics at world size 1: real RCCL "
-                                      "collectives per bucket (a one-rank ring moves no bytes)"}
-        for key, impl in (("ms_per_step", "flat"), ("graph_ms_per_step", "flatgraph"), ("zero2_ms_per_step", "zero")):
-            try:
-                r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, {impl!r}, {config!r}, force=True)",
-                                    render=False)
-                cp[key] = _max_over_ranks(r)
-            except Exception as e:  # noqa: BLE001 - recorded, the other arms still run
-                cp[key.replace("ms_per_step", "error")] = f"{type(e).__name__}: {e}"[:400]
-                if isinstance(e, TimeoutError):
-                    raise
-        if "ms_per_step" in cp:
-            cp["vs_no_collectives"] = cp["ms_per_step"] / ms
-        out["collective_path"] = cp
+    tick()
     try:  # ZeRO-2: reduce-scattered gradients, optimizer on this rank's slice, parameter all-gather
         r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'zero', {config!r})", render=False)
         zms = _max_over_ranks(r)
@@ -203,6 +192,9 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
                    zero2_recipe="as the primary recipe with DistributedDataParallel(shard=True) (ZeRO-2)")
     except Exception as e:  # noqa: BLE001 - recorded, the other recipes still run
         out["zero2_error"] = f"{type(e).__name__}: {e}"[:400]
+        if isinstance(e, TimeoutError):
+            raise
+    tick()
     r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'nbd', {config!r})", render=False)
     ams = _max_over_ranks(r)
     out.update(amp_ms_per_step=ams, amp_tokens_per_s=n * B * T / (ams / 1e3))
@@ -214,12 +206,44 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
                    speedup_vs_torch_ddp=tms / ams,
                    speedup_vs_torch_ddp_note="amp_ms_per_step vs torch_ddp_ms_per_step (same recipe)",
                    recipe_speedup_vs_torch_ddp=tms / ms)
+    tick()
     r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'nbd', {linear_dim})", render=False)
     lin = {"rows": linear_rows, "dim": linear_dim, "ms_per_step": _max_over_ranks(r)}
+    out["linear4096"] = lin
     if compare_torch:
         r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'torch', {linear_dim})", render=False)
         lin["torch_ddp_ms_per_step"] = _max_over_ranks(r)
-    out["linear4096"] = lin
+    tick()
+    if _graph_arms(n):
+        try:
+            r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flatgraph', {config!r})", render=False)
+            gms = _max_over_ranks(r)
+            out.update(graph_ms_per_step=gms, graph_tokens_per_s=n * B * T / (gms / 1e3),
+                       graph_recipe="as the primary recipe, whole step captured in one HIP graph (GraphedStep)")
+        except Exception as e:  # noqa: BLE001
+            out["graph_error"] = f"{type(e).__name__}: {e}"[:400]
+            if isinstance(e, TimeoutError):
+                raise
+        tick()
+    if n == 1 and force_collectives:
+        # the world > 1 code path on this one GPU: every bucket's all-reduce (reduce-scatter +
+        # all-gather for ZeRO-2) issued on RCCL from the DDP side stream / inside the graph, with
+        # the per-bucket flushes and events of a multi-GPU run — what an N-GPU rank executes
+        cp: Dict[str, Any] = {"note": "NBD_DDP_FORCE_COLLECTIVES semantics at world size 1: real RCCL "
+                                      "collectives per bucket (a one-rank ring moves no bytes)"}
+        out["collective_path"] = cp
+        for key, impl in (("ms_per_step", "flat"), ("graph_ms_per_step", "flatgraph"), ("zero2_ms_per_step", "zero")):
+            try:
+                r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, {impl!r}, {config!r}, force=True)",
+                                    render=False)
+                cp[key] = _max_over_ranks(r)
+            except Exception as e:  # noqa: BLE001 - recorded, the other arms still run
+                cp[key.replace("ms_per_step", "error")] = f"{type(e).__name__}: {e}"[:400]
+                if isinstance(e, TimeoutError):
+                    raise
+            tick()
+        if "ms_per_step" in cp:
+            cp["vs_no_collectives"] = cp["ms_per_step"] / ms
     return out
 
 
@@ -471,17 +495,19 @@ REFERENCE_NOTEBOOK_MS_PER_STEP = 126.6  # 1 epoch = 14.56 s / 115 s
 
 
 def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = False,
-                   force_collectives: bool = True) -> Dict[str, Any]:
+                   force_collectives: bool = True, out: Optional[Dict[str, Any]] = None, tick=None) -> Dict[str, Any]:
     """The reference's own measured workload (SmolLM2-135M-cls fine-tune, 126.6
     ms/step, ≈252 samples/s on 2 GPUs) as notebook cells, max over ranks."""
     n = session.world_size
+    out = {} if out is None else out
+    tick = tick or (lambda: None)
     session.execute(AR_SETUP, render=False)
     session.execute(DDP_SETUP, render=False)
     session.execute(NOTEBOOK_SETUP, render=False)
-    out: Dict[str, Any] = {"model": "SmolLM2-135M sequence classifier (random init)", "per_gpu_batch": 16,
-                           "seq_len": 128, "data": "synthetic MRPC-shaped",
-                           "reference_ms_per_step": REFERENCE_NOTEBOOK_MS_PER_STEP,
-                           "reference_samples_per_s": 32 / (REFERENCE_NOTEBOOK_MS_PER_STEP / 1e3)}
+    out.update({"model": "SmolLM2-135M sequence classifier (random init)", "per_gpu_batch": 16,
+                "seq_len": 128, "data": "synthetic MRPC-shaped",
+                "reference_ms_per_step": REFERENCE_NOTEBOOK_MS_PER_STEP,
+                "reference_samples_per_s": 32 / (REFERENCE_NOTEBOOK_MS_PER_STEP / 1e3)})
     recipes = {"reference": "HF model, fp32, accelerate DDP, torch AdamW (the notebook's recipe)",
                "reference_native": "the notebook's accelerate loop unchanged except model = nbd.models.native(model): "
                                    "native Llama, fp32 master weights + torch AdamW, bf16 compute on the fused HIP path",
@@ -489,17 +515,22 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
                        "(FlatAdamW, buckets updated during backward at world 1), nbd DDP",
                "nbd_graph": "as nbd, whole step captured in one HIP graph (GraphedStep)"}
     modes = ["reference", "reference_native", "nbd"]
-    # graph capture with RCCL collectives is verified at world size 1 on this pool; at N > 1 it
-    # runs only on request, so a capture problem cannot cost the driver its result line
-    if n == 1 or os.environ.get("NBD_BENCH_GRAPH_MULTI") == "1":
+    if _graph_arms(n):  # last of the main arms (bench_ddp's _graph_arms note)
         modes.append("nbd_graph")
     for mode in modes:
-        r = session.execute(f"_nbd_notebook_bench({steps}, {warmup}, mode={mode!r}, small={small})", render=False)
+        try:
+            r = session.execute(f"_nbd_notebook_bench({steps}, {warmup}, mode={mode!r}, small={small})", render=False)
+        except Exception as e:  # noqa: BLE001 - recorded, the other arms still run
+            out[mode] = {"error": f"{type(e).__name__}: {e}"[:400]}
+            if isinstance(e, TimeoutError):
+                raise
+            continue
         ms = _max_over_ranks(r)
         out[mode] = {"ms_per_step": ms, "samples_per_s": n * 16 / (ms / 1e3), "recipe": recipes[mode]}
+        tick()
     if n == 1 and force_collectives:  # the N-GPU code path on one GPU (see bench_ddp)
         for mode, base in (("nbd_collective_path", "nbd"), ("nbd_graph_collective_path", "nbd_graph")):
-            if base not in out:
+            if "ms_per_step" not in out.get(base, {}):
                 continue
             try:
                 r = session.execute(f"_nbd_notebook_bench({steps}, {warmup}, mode={base!r}, small={small}, force=True)",
@@ -511,13 +542,14 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
                 out[mode] = {"error": f"{type(e).__name__}: {e}"[:400]}
                 if isinstance(e, TimeoutError):
                     raise
+            tick()
     # same-recipe comparisons only: the fp32 HF arm and the bf16 native arms differ in precision
     # and model implementation, so no cross-recipe "speedup" is printed
     out["reference_vs_native_note"] = ("'reference' = HF fp32 model through accelerate (the notebook as written); "
                                        "'reference_native' = the same loop with the one-line model swap (bf16 compute, "
                                        "fp32 master weights: the recipe of Accelerator(mixed_precision='bf16')); "
                                        "'nbd*' = native bf16 Llama + FlatAdamW (bf16 params, fp32 master in the optimizer)")
-    if "reference" in out and "reference_native" in out:
+    if "ms_per_step" in out.get("reference", {}) and "ms_per_step" in out.get("reference_native", {}):
         out["reference_native_speedup_same_loop"] = out["reference"]["ms_per_step"] / out["reference_native"]["ms_per_step"]
     return out
 
@@ -599,7 +631,11 @@ def _phase(session, out: Dict[str, Any], name: str, fn, timeout_s: float, deadli
     try:
         out[name] = fn()
     except Exception as e:  # noqa: BLE001 - recorded in the result line
-        out[name] = {"error": f"{type(e).__name__}: {e}"[:800]}
+        part = out.get(name)
+        if isinstance(part, dict) and part:  # arms measured before the failure stay
+            part["error"] = f"{type(e).__name__}: {e}"[:800]
+        else:
+            out[name] = {"error": f"{type(e).__name__}: {e}"[:800]}
         _log(f"phase {name} failed: {type(e).__name__}: {str(e)[:300]}")
         if isinstance(e, TimeoutError):
             out["aborted"] = name
@@ -689,17 +725,21 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
             ckpt(out)
         if ddp and gpu:
             _log("phase 4: DDP steps (GPT-2 small bf16 config 5, Linear 4096 config 4)")
-            _phase(session, out, "ddp", lambda: bench_ddp(session, steps=ddp_steps), phase_timeout_s, deadline, 60.0)
+            out["ddp"] = {}
+            _phase(session, out, "ddp", lambda: bench_ddp(session, steps=ddp_steps, out=out["ddp"], tick=lambda: ckpt(out)),
+                   phase_timeout_s, deadline, 60.0)
             d = out["ddp"]
             if "ms_per_step" in d:
                 _log(f"gpt2 ddp {d['ms_per_step']:.2f} ms/step {d['tokens_per_s']:.0f} tok/s")
             ckpt(out)
         if notebook and gpu:
             _log("phase 5: reference notebook workload (SmolLM2-135M-cls, bs16, seq128)")
-            _phase(session, out, "notebook", lambda: bench_notebook(session, steps=ddp_steps), phase_timeout_s,
-                   deadline, 60.0)
+            out["notebook"] = {}
+            _phase(session, out, "notebook",
+                   lambda: bench_notebook(session, steps=ddp_steps, out=out["notebook"], tick=lambda: ckpt(out)),
+                   phase_timeout_s, deadline, 60.0)
             nb = out["notebook"]
-            if "reference" in nb:
+            if "ms_per_step" in nb.get("reference", {}) and "ms_per_step" in nb.get("nbd", {}):
                 _log(f"notebook fp32 {nb['reference']['ms_per_step']:.2f} ms/step, nbd {nb['nbd']['ms_per_step']:.2f}")
             ckpt(out)
         return out
