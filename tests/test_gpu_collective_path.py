@@ -222,3 +222,47 @@ os.environ["NBD_GEMM_WARM"] = "1"
 def test_gemm_warmup_is_capture_safe(sess):
     out = _echo(sess.execute(CODE_WARM, render=False))
     assert out == "(True, True, True, True)", out
+
+
+CODE_LIFETIME = """
+import gc
+from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP
+from nbdistributed_amd.optim import FlatAdamW
+from nbdistributed_amd.ops import graddst
+torch.manual_seed(0)
+net = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.GELU(), torch.nn.Linear(512, 256)).to(device, torch.bfloat16)
+x = torch.randn(64, 256, device=device, dtype=torch.bfloat16)
+counts = []
+for i in range(4):   # a notebook re-running the cell that wraps the same module
+    d = NbdDDP(net, flat_params=True, grad_mode="bucket")
+    d(x).float().square().mean().backward()
+    counts.append(graddst.count())
+    patched = sum("forward" in m.__dict__ for m in net.modules())
+    del d
+    gc.collect()
+after = graddst.count()
+unpatched = sum("forward" in m.__dict__ for m in net.modules())
+# FlatAdamW(overlap=True) updates during backward: clipping afterwards must refuse, and leave no
+# stale coefficient behind (the next step still runs)
+d = NbdDDP(net, flat_params=True, grad_mode="bucket")
+o = FlatAdamW(d, lr=1e-3, overlap=True)
+d(x).float().square().mean().backward()
+try:
+    o.clip_grad_norm_(1.0)
+    clip = "no error"
+except RuntimeError:
+    clip = "refused"
+o.step(); o.zero_grad()
+d(x).float().square().mean().backward()
+o.step()
+torch.cuda.synchronize()
+(counts, after, patched, unpatched, clip, o._clip_coef is None)
+"""
+
+
+def test_ddp_lifetime_and_overlap_clip(sess):
+    """Re-creating DDP on the same module keeps one set of gradient-destination registrations
+    (the dropped DDP's finalizer removes its own), and FlatAdamW(overlap=True) refuses
+    clip_grad_norm_ without leaving a stale coefficient."""
+    out = _echo(sess.execute(CODE_LIFETIME, render=False))
+    assert out == "([4, 4, 4, 4], 0, 2, 0, 'refused', True)", out
