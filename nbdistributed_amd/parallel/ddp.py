@@ -372,6 +372,11 @@ class DistributedDataParallel(torch.nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
+        if self._in_backward and torch._C._current_graph_task_id() == -1:
+            # a backward that raised never reached _finalize: this forward starts a new pass
+            self._in_backward = False
+            for b in self.buckets:
+                b.work, b.grads, b.rest_grads, b.rest_offsets = None, [], [], []
         if self._hook_handle is not None and torch.is_grad_enabled():
             # a new pass (also after a backward that raised); hooks a user registered since
             # replaced ours: wrap theirs again

@@ -202,3 +202,41 @@ gone = int(torch.ops.nbd.ddp_hooks_intact(handle, params)) == 0
     r = sess.execute(code, render=False)
     for rank in (0, 1):
         assert r.results[rank]["output"] == "(True, True, True, True)", r.results[rank]
+
+
+def test_cpp_bucket_hook_callback_error_reaches_backward():
+    """A failure inside the bucket callback (called from the C++ hook on the autograd engine's
+    thread) surfaces as an exception from backward(), and the DDP is usable afterwards."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from nbdistributed_amd import ops
+    from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP
+
+    if not ops.native_available():
+        pytest.skip("native ops unavailable")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29641")
+    own = not dist.is_initialized()
+    if own:
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        m = NbdDDP(torch.nn.Linear(8, 4), cpp_hooks=True)
+        orig = m._bucket_event
+
+        def boom(i):
+            if i >= 0:
+                raise ValueError("injected")
+            orig(i)
+
+        m._bucket_event = boom
+        with pytest.raises(RuntimeError, match="injected"):
+            m(torch.randn(3, 8)).sum().backward()
+        m._bucket_event = orig
+        m(torch.randn(3, 8)).sum().backward()  # rearmed by forward: works again
+        assert all(p.grad is not None for p in m.module.parameters())
+    finally:
+        if own:
+            dist.destroy_process_group()
