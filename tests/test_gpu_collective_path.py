@@ -232,15 +232,17 @@ from nbdistributed_amd.ops import graddst
 torch.manual_seed(0)
 net = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.GELU(), torch.nn.Linear(512, 256)).to(device, torch.bfloat16)
 x = torch.randn(64, 256, device=device, dtype=torch.bfloat16)
+gc.collect()
+c0 = graddst.count()  # registrations of other cells' models still alive in this worker
 counts = []
 for i in range(4):   # a notebook re-running the cell that wraps the same module
     d = NbdDDP(net, flat_params=True, grad_mode="bucket")
     d(x).float().square().mean().backward()
-    counts.append(graddst.count())
+    counts.append(graddst.count() - c0)
     patched = sum("forward" in m.__dict__ for m in net.modules())
     del d
     gc.collect()
-after = graddst.count()
+after = graddst.count() - c0
 unpatched = sum("forward" in m.__dict__ for m in net.modules())
 # FlatAdamW(overlap=True) updates during backward: clipping afterwards must refuse, and leave no
 # stale coefficient behind (the next step still runs)
