@@ -8,6 +8,7 @@ fp32      : HF model, fp32 params, torch AdamW (the notebook's recipe, minus acc
 bf16flat  : HF model, bf16 params in nbd DDP buckets (world 1) + FlatAdamW
 nbd       : native Llama (models/llama.py, HIP kernels), bf16 flat DDP + FlatAdamW
 nbdgraph  : nbd captured once into a HIP graph (nbdistributed_amd.graphs) and replayed
+nbdbg     : nbd eager with one HIP graph per decoder block's forward (ops.block_graphs)
 """
 from __future__ import annotations
 
@@ -45,7 +46,7 @@ def main():
     ids, mask, labels = ids.to(dev), mask.to(dev), labels.to(dev)
     for mode in a.modes.split(","):
         torch.manual_seed(42)
-        native = mode in ("nbd", "nbdgraph")
+        native = mode in ("nbd", "nbdgraph", "nbdbg")
         if native:
             from nbdistributed_amd.models.llama import LlamaConfig, LlamaForSequenceClassification
 
@@ -72,6 +73,10 @@ def main():
             opt.zero_grad(set_to_none=True)
             return loss.detach()
 
+        from nbdistributed_amd import ops
+
+        if native:
+            ops.block_graphs(mode == "nbdbg")
         if mode == "nbdgraph":
             from nbdistributed_amd.graphs import GraphedStep
 
@@ -86,7 +91,8 @@ def main():
             loss = call(*batches[i % 8])
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t) / a.steps * 1e3
-        print(f"{mode:9s} {ms:8.2f} ms/step  {a.bs / ms * 1e3:8.1f} samples/s  loss {float(loss.detach()):.4f}",
+        extra = f"  {ops.block_graphs_stats()}" if mode == "nbdbg" else ""
+        print(f"{mode:9s} {ms:8.2f} ms/step  {a.bs / ms * 1e3:8.1f} samples/s  loss {float(loss.detach()):.4f}{extra}",
               flush=True)
         del model, opt, fwd
         torch.cuda.empty_cache()

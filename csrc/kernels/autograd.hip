@@ -20,8 +20,19 @@
 // _LayerNorm / _AddLayerNorm) and attention from a packed q|k|v projection (ops/attention.py
 // _FlashAttentionQKV).
 #include <ATen/ATen.h>
+#include <ATen/hip/HIPGraph.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/GradMode.h>
 #include <torch/csrc/autograd/custom_function.h>
 #include <torch/library.h>
+
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+#include <unordered_map>
 
 #include "gemm_common.h"
 #include "graddst.h"
@@ -59,6 +70,9 @@ std::tuple<at::Tensor, at::Tensor> rms_bwd_into(const at::Tensor& x, const at::T
                                                 const c10::optional<at::Tensor>& dres, const at::Tensor& weight,
                                                 const at::Tensor& rstd, const at::Tensor& dw_dst, int accum);
 }  // namespace norm
+namespace gemm {
+std::vector<at::Tensor> gemm_warm_take_refs();
+}  // namespace gemm
 namespace attn {
 std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                                 bool causal, double scale, const c10::optional<at::Tensor>& rope_cos,
@@ -599,7 +613,7 @@ static std::tuple<Tensor, Tensor> llama_block_fwd(const Tensor& x, const Tensor&
                                                   at::IntArrayRef plan_qkv, at::IntArrayRef plan_o,
                                                   at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv, double scale,
                                                   double eps, const optional<Tensor>& cos, const optional<Tensor>& sin,
-                                                  AutogradContext* ctx) {
+                                                  std::vector<Tensor>* save) {
   const int64_t B = h.size(0), T = h.size(1), C = h.size(2);
   const Tensor h2 = bf16c(h).view({-1, C});
   const Tensor qkv = linear_forward(h2, w_qkv, b_qkv, plan_qkv).view({B, T, -1});
@@ -612,12 +626,215 @@ static std::tuple<Tensor, Tensor> llama_block_fwd(const Tensor& x, const Tensor&
   auto [act, pre] = run(h1f, w_gu, false, false, prod(plan_mlp, 0), EPI_SWIGLU);
   const Tensor m = run(act, w_down, false, false, prod(plan_mlp, 1)).first.view({B, T, C});
   auto [h_out, x_out, rstd2] = norm::rms_fwd_hip(x1, m, w_next, eps);
-  if (ctx != nullptr) {
-    ctx->save_for_backward({h2, w_qkv, b_qkv ? *b_qkv : Tensor(), qkv, o, lse, w_o, b_o ? *b_o : Tensor(), x1, w_post,
-                            rstd1, h1f, w_gu, w_down, pre, act, x_out, w_next, rstd2, cos ? *cos : Tensor(),
-                            sin ? *sin : Tensor()});
+  if (save != nullptr) {
+    *save = {h2, w_qkv, b_qkv ? *b_qkv : Tensor(), qkv, o, lse, w_o, b_o ? *b_o : Tensor(), x1, w_post,
+             rstd1, h1f, w_gu, w_down, pre, act, x_out, w_next, rstd2, cos ? *cos : Tensor(), sin ? *sin : Tensor()};
   }
   return {x_out, h_out};
+}
+
+// ---- one HIP graph per decoder block for the EAGER step (opt-in: NBD_BLOCK_GRAPHS=1 or
+// torch.ops.nbd.llama_block_graphs(1)).  The block's forward — seven kernels plus allocations,
+// ≈70 µs of issuing-thread time on SmolLM2 (docs/FINDINGS.md §27) — is captured once per
+// (block, shape) after two eager calls and then replayed: one graph launch instead of seven
+// kernel launches.  The graph writes its activations into static memory (its private pool), so:
+//  * the block's inputs are copied into static buffers, except when they ARE another block
+//    graph's outputs (the residual stream between consecutive graphed blocks needs no copy);
+//  * the static memory may be replayed into only once the previous pass's autograd node has let
+//    go of it: a token among the node's saved tensors clears `armed` when backward releases the
+//    saved tensors (or the node dies).  A forward while the block is armed (a second forward
+//    before backward, retain_graph) runs eagerly, as does any call whose weights, RoPE tables or
+//    aliased input moved, or that comes inside another capture (graphs.GraphedStep);
+//  * the returned tensors alias that memory: they hold this pass's values until the block's next
+//    replay (a caller keeping block outputs across steps must clone them).
+// Same kernels, same order: bit-identical to the eager block (tests/test_gpu_llama_block.py).
+namespace bg {
+struct Graph {
+  std::unique_ptr<at::cuda::CUDAGraph> g;
+  Tensor x_in, h_in;                   // static inputs
+  bool x_alias = false, h_alias = false;  // ...that are another block graph's outputs
+  std::vector<const void*> ptrs;       // weights, RoPE tables at capture
+  std::vector<int64_t> sig;            // their shapes and the block's scalars
+  std::vector<Tensor> saved;           // llama_block_fwd's saved list (static; weight slots empty)
+  Tensor x_out, h_out;
+  std::vector<Tensor> warm_refs;       // storages the captured GEMM warm-ups read
+  std::atomic<bool> armed{false};
+};
+struct Slot {
+  int eager = 0, captures = 0, misses = 0;
+  bool off = false;
+  std::shared_ptr<Graph> g;
+};
+using Key = std::tuple<const void*, int64_t, int64_t, int64_t>;  // (W_qkv, B, T, device)
+std::mutex g_mu;
+std::map<Key, Slot> g_slots;
+std::unordered_map<const void*, std::weak_ptr<Graph>> g_outs;  // a graph's output address -> graph
+std::atomic<int> g_mode{-1};                                    // -1: not read from the env yet
+std::atomic<int64_t> g_stat[3];                                 // captures, replays, eager calls
+
+bool enabled() {
+  int m = g_mode.load(std::memory_order_relaxed);
+  if (m < 0) {
+    const char* e = std::getenv("NBD_BLOCK_GRAPHS");
+    m = e != nullptr && e[0] == '1';
+    g_mode.store(m, std::memory_order_relaxed);
+  }
+  return m == 1;
+}
+
+bool stream_capturing() {
+  hipStreamCaptureStatus s = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(), &s) != hipSuccess) return true;
+  return s != hipStreamCaptureStatusNone;
+}
+
+// x is the output `which` of a live block graph (so it stays put while that graph lives)
+bool is_graph_output(const Tensor& x) {
+  auto it = g_outs.find(x.data_ptr());
+  if (it == g_outs.end()) return false;
+  auto gr = it->second.lock();
+  if (!gr) return false;
+  const Tensor& o = gr->x_out.data_ptr() == x.data_ptr() ? gr->x_out : gr->h_out;
+  return o.sizes() == x.sizes() && o.strides() == x.strides() && o.scalar_type() == x.scalar_type();
+}
+
+// a CPU scalar whose release (backward done with the saved tensors, or the node gone) disarms
+Tensor token(const std::shared_ptr<Graph>& gr) {
+  static int64_t dummy = 0;
+  std::weak_ptr<Graph> w = gr;
+  return at::from_blob(
+      &dummy, {1},
+      [w](void*) {
+        if (auto g = w.lock()) g->armed.store(false, std::memory_order_release);
+      },
+      at::TensorOptions().dtype(at::kLong));
+}
+}  // namespace bg
+
+// saved-list slots holding the call's weights / RoPE tables (the node's gradient targets)
+constexpr int kBlockWeightSlots[] = {1, 2, 6, 7, 9, 12, 13, 17, 19, 20};
+
+// Replay (or capture, then replay) the block's graph for this call; nullptr = run it eagerly.
+static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, const Tensor& w_qkv,
+                                              const optional<Tensor>& b_qkv, const Tensor& w_o,
+                                              const optional<Tensor>& b_o, const Tensor& w_post, const Tensor& w_gu,
+                                              const Tensor& w_down, const Tensor& w_next, at::IntArrayRef plan_qkv,
+                                              at::IntArrayRef plan_o, at::IntArrayRef plan_mlp, int64_t H,
+                                              int64_t Hkv, double scale, double eps, const optional<Tensor>& cos,
+                                              const optional<Tensor>& sin) {
+  using namespace bg;
+  if (stream_capturing()) return nullptr;  // inside a whole-step capture: the outer graph takes it
+  const Tensor* ts[] = {&w_qkv, b_qkv ? &*b_qkv : nullptr, &w_o, b_o ? &*b_o : nullptr, &w_post, &w_gu,
+                        &w_down, &w_next, cos ? &*cos : nullptr, sin ? &*sin : nullptr};
+  std::vector<const void*> ptrs;
+  std::vector<int64_t> sig{H, Hkv, (int64_t)(scale * 1e9), (int64_t)(eps * 1e12), (int64_t)x.scalar_type()};
+  for (const Tensor* t : ts) {
+    ptrs.push_back(t != nullptr ? t->data_ptr() : nullptr);
+    if (t != nullptr) sig.insert(sig.end(), t->sizes().begin(), t->sizes().end());
+    sig.push_back(-1);
+  }
+  for (at::IntArrayRef p : {plan_qkv, plan_o, plan_mlp}) sig.insert(sig.end(), p.begin(), p.end());
+  const Key key{w_qkv.data_ptr(), h.size(0), h.size(1), h.get_device()};
+  std::shared_ptr<Graph> gr;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Slot& s = g_slots[key];
+    if (s.off) return nullptr;
+    if (s.g && (s.g->ptrs != ptrs || s.g->sig != sig)) s.g.reset(), s.eager = 0;  // weights moved
+    if (s.g) {
+      Graph& G = *s.g;
+      const bool inputs_ok = (!G.x_alias || x.data_ptr() == G.x_in.data_ptr()) &&
+                             (!G.h_alias || h.data_ptr() == G.h_in.data_ptr());
+      if (!inputs_ok) {  // the block before ran eagerly this time; twice in a row: capture anew
+        if (++s.misses >= 2) s.g.reset(), s.eager = 0, s.misses = 0;
+        ++g_stat[2];
+        return nullptr;
+      }
+      if (G.armed.exchange(true, std::memory_order_acq_rel)) {  // last pass still holds the memory
+        ++g_stat[2];
+        return nullptr;
+      }
+      s.misses = 0;
+      gr = s.g;
+    } else if (++s.eager < 3) {
+      ++g_stat[2];
+      return nullptr;
+    } else if (++s.captures > 4) {
+      s.off = true;
+      return nullptr;
+    }
+  }
+  auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA();
+  if (gr) {
+    if (!gr->x_alias && x.data_ptr() != gr->x_in.data_ptr()) gr->x_in.copy_(x);
+    if (!gr->h_alias && h.data_ptr() != gr->h_in.data_ptr()) gr->h_in.copy_(h);
+    gr->g->replay();
+    ++g_stat[1];
+    return gr;
+  }
+  // capture on a side stream, then replay once on the caller's stream (capturing runs nothing)
+  auto G = std::make_shared<Graph>();
+  G->ptrs = std::move(ptrs);
+  G->sig = std::move(sig);
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    G->x_alias = x.is_contiguous() && is_graph_output(x);
+    G->h_alias = h.is_contiguous() && is_graph_output(h);
+  }
+  // (variable_data: the graph must not hold the caller's autograd history — an aliased input is
+  // the previous block's output, whose node would keep this pass's AccumulateGrad nodes alive)
+  G->x_in = G->x_alias ? x.variable_data() : at::empty_like(x, at::MemoryFormat::Contiguous).copy_(x);
+  G->h_in = G->h_alias ? h.variable_data() : at::empty_like(h, at::MemoryFormat::Contiguous).copy_(h);
+  auto side = c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, x.get_device());
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  C10_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+  C10_HIP_CHECK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
+  C10_HIP_CHECK(hipEventRecord(ev_in, cur.stream()));
+  C10_HIP_CHECK(hipStreamWaitEvent(side.stream(), ev_in, 0));
+  std::vector<Tensor> save;
+  std::string err;
+  {
+    const c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(side);
+    G->g = std::make_unique<at::cuda::CUDAGraph>();
+    G->g->capture_begin(at::cuda::graph_pool_handle(), hipStreamCaptureModeThreadLocal);
+    try {
+      std::tie(G->x_out, G->h_out) = llama_block_fwd(G->x_in, G->h_in, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down,
+                                                     w_next, plan_qkv, plan_o, plan_mlp, H, Hkv, scale, eps, cos,
+                                                     sin, &save);
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    try {
+      G->g->capture_end();
+    } catch (const std::exception& e) {
+      if (err.empty()) err = e.what();
+    }
+  }
+  C10_HIP_CHECK(hipEventRecord(ev_out, side.stream()));
+  C10_HIP_CHECK(hipStreamWaitEvent(cur.stream(), ev_out, 0));
+  C10_HIP_CHECK(hipEventDestroy(ev_in));
+  C10_HIP_CHECK(hipEventDestroy(ev_out));
+  G->warm_refs = gemm::gemm_warm_take_refs();
+  if (!err.empty()) {
+    TORCH_WARN_ONCE("nbd: a decoder block's HIP graph capture failed (", err, "); the block runs eagerly");
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_slots[key].off = true;
+    return nullptr;
+  }
+  for (int i : kBlockWeightSlots) save[i] = Tensor();
+  G->saved = std::move(save);
+  G->armed.store(true, std::memory_order_release);
+  G->g->replay();
+  ++g_stat[0];
+  ++g_stat[1];
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto it = g_outs.begin(); it != g_outs.end();) it = it->second.expired() ? g_outs.erase(it) : std::next(it);
+  g_outs[G->x_out.data_ptr()] = G;
+  g_outs[G->h_out.data_ptr()] = G;
+  Slot& s = g_slots[key];
+  s.g = G;
+  s.misses = 0;
+  return G;
 }
 
 struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
@@ -626,11 +843,29 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
                                const Tensor& w_post, const Tensor& w_gu, const Tensor& w_down, const Tensor& w_next,
                                at::IntArrayRef plan_qkv, at::IntArrayRef plan_o, at::IntArrayRef plan_mlp, int64_t H,
                                int64_t Hkv, double scale, double eps, const optional<Tensor>& cos,
-                               const optional<Tensor>& sin) {
+                               const optional<Tensor>& sin, bool graph) {
     at::AutoDispatchBelowADInplaceOrView guard;
     ctx->set_materialize_grads(false);
-    auto [x_out, h_out] = llama_block_fwd(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o,
-                                          plan_mlp, H, Hkv, scale, eps, cos, sin, ctx);
+    std::vector<Tensor> save;
+    Tensor x_out, h_out;
+    std::shared_ptr<bg::Graph> gr;
+    if (graph)
+      gr = block_graph(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp, H, Hkv,
+                       scale, eps, cos, sin);
+    if (gr) {
+      save = gr->saved;
+      const Tensor none;
+      const Tensor* ts[] = {&w_qkv, b_qkv ? &*b_qkv : &none, &w_o, b_o ? &*b_o : &none, &w_post, &w_gu,
+                            &w_down, &w_next, cos ? &*cos : &none, sin ? &*sin : &none};
+      for (size_t i = 0; i < std::size(kBlockWeightSlots); ++i) save[kBlockWeightSlots[i]] = *ts[i];
+      save.push_back(bg::token(gr));
+      x_out = at::alias(gr->x_out);
+      h_out = at::alias(gr->h_out);
+    } else {
+      std::tie(x_out, h_out) = llama_block_fwd(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv,
+                                               plan_o, plan_mlp, H, Hkv, scale, eps, cos, sin, &save);
+    }
+    ctx->save_for_backward(save);
     ctx->saved_data["plans"] = std::vector<std::vector<int64_t>>{plan_qkv.vec(), plan_o.vec(), plan_mlp.vec()};
     ctx->saved_data["H"] = H;
     ctx->saved_data["Hkv"] = Hkv;
@@ -653,7 +888,7 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
     const auto shape = ctx->saved_data["shape"].toIntVector();
     const auto need = ctx->saved_data["need"].toBoolList();
     const int64_t C = shape[2];
-    variable_list out(19);
+    variable_list out(20);
     const Tensor &dx_out = grads[0], &dh_out = grads[1];
     // x2 = x1 + m, h2 = rms(x2)·γ_next
     Tensor g2, dw_next;
@@ -691,8 +926,9 @@ std::tuple<Tensor, Tensor> llama_block_ag(const Tensor& x, const Tensor& h, cons
                                           const Tensor& w_next, at::IntArrayRef plan_qkv, at::IntArrayRef plan_o,
                                           at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv, double scale, double eps,
                                           const optional<Tensor>& cos, const optional<Tensor>& sin) {
+  const bool graph = bg::enabled() && c10::GradMode::is_enabled() && x.is_cuda();
   auto r = LlamaBlockFn::apply(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp,
-                               H, Hkv, scale, eps, cos, sin);
+                               H, Hkv, scale, eps, cos, sin, graph);
   return {r[0], r[1]};
 }
 
@@ -705,6 +941,29 @@ std::tuple<Tensor, Tensor> llama_block_noag(const Tensor& x, const Tensor& h, co
                                             const optional<Tensor>& sin) {
   return llama_block_fwd(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp, H, Hkv,
                          scale, eps, cos, sin, nullptr);
+}
+
+// Per-block graphs: mode 1 on, 0 off, -1 query; returns the previous setting.
+int64_t llama_block_graphs(int64_t mode) {
+  const int64_t prev = bg::enabled() ? 1 : 0;
+  if (mode >= 0) bg::g_mode.store(mode == 1 ? 1 : 0, std::memory_order_relaxed);
+  return prev;
+}
+
+// Drop every captured block graph (their static memory goes once no autograd node holds it).
+void llama_block_graphs_reset() {
+  std::map<bg::Key, bg::Slot> slots;
+  std::lock_guard<std::mutex> lk(bg::g_mu);
+  slots.swap(bg::g_slots);
+  bg::g_outs.clear();
+}
+
+// [captures, replays, eager calls in graph mode, live graphs]
+std::vector<int64_t> llama_block_graphs_stats() {
+  std::lock_guard<std::mutex> lk(bg::g_mu);
+  int64_t live = 0;
+  for (const auto& kv : bg::g_slots) live += kv.second.g != nullptr;
+  return {bg::g_stat[0].load(), bg::g_stat[1].load(), bg::g_stat[2].load(), live};
 }
 
 }  // namespace ag
@@ -734,4 +993,11 @@ TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
   m.impl("mlp_gelu_ag", &nbd::ag::mlp_gelu_noag);
   m.impl("mlp_swiglu_ag", &nbd::ag::mlp_swiglu_noag);
   m.impl("llama_block_ag", &nbd::ag::llama_block_noag);
+}
+
+// bookkeeping only (no device work): catch-all kernels
+TORCH_LIBRARY_FRAGMENT(nbd, m) {
+  m.def("llama_block_graphs(int mode) -> int", &nbd::ag::llama_block_graphs);
+  m.def("llama_block_graphs_reset() -> ()", &nbd::ag::llama_block_graphs_reset);
+  m.def("llama_block_graphs_stats() -> int[]", &nbd::ag::llama_block_graphs_stats);
 }

@@ -16,6 +16,7 @@ Requirements (checked by construction, as for any CUDA/HIP graph):
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Any, Callable, Iterable, Sequence
 
 import torch
@@ -66,6 +67,26 @@ def _take_warm_refs():
         return []
 
 
+@contextlib.contextmanager
+def _suspend_block_graphs():
+    """The per-block graphs of the eager Llama step (ops.block_graphs) off while a whole step is
+    warmed up and captured: inside the capture the blocks are part of the outer graph anyway, and
+    block graphs made during the warm-up would only hold static memory nobody replays."""
+    prev = None
+    try:
+        from .ops import _lib
+
+        if _lib._loaded:
+            prev = int(torch.ops.nbd.llama_block_graphs(0))
+    except (AttributeError, RuntimeError):
+        prev = None
+    try:
+        yield
+    finally:
+        if prev is not None:
+            torch.ops.nbd.llama_block_graphs(prev)
+
+
 class GraphedStep:
     """``step = GraphedStep(fn, example_args, optimizers=[opt])``; ``out = step(*args)``.
 
@@ -83,6 +104,10 @@ class GraphedStep:
         self.optimizers = list(optimizers)
         self.static_args = [_clone_static(a) for a in example_args]
         self.replays = 0
+        with _suspend_block_graphs():
+            self._warm_and_capture(fn, warmup, pool)
+
+    def _warm_and_capture(self, fn, warmup, pool) -> None:
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream()
         side.wait_stream(cur)

@@ -20,6 +20,7 @@ supported).
 """
 from __future__ import annotations
 
+import weakref
 from dataclasses import dataclass
 from typing import Any, Dict, NamedTuple, Optional
 
@@ -205,6 +206,13 @@ class LlamaDecoderLayer(nn.Module):
         self.mlp = LlamaMLP(c)
 
 
+def _drop_block_graphs() -> None:
+    try:
+        ops.block_graphs_reset()
+    except Exception:  # interpreter shutdown
+        pass
+
+
 class LlamaModel(nn.Module):
     """Decoder stack; ``forward`` returns the final-normed hidden states [B, T, C]."""
 
@@ -218,6 +226,8 @@ class LlamaModel(nn.Module):
         # fp32 parameters computed in this dtype on the fused GPU path (``native()``): the
         # parameters stay fp32 for the optimizer, each layer is cast once per forward
         self.compute_dtype: Optional[torch.dtype] = None
+        # per-block HIP graphs (ops.block_graphs) hold static activations: drop them with the model
+        weakref.finalize(self, _drop_block_graphs)
 
     def cast_dtype(self, input_ids) -> Optional[torch.dtype]:
         """The dtype the fp32 parameters are cast to for this forward, or None (run as stored).

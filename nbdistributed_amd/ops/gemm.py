@@ -13,6 +13,7 @@ to PyTorch (hipBLASLt on ROCm) with identical semantics.
 from __future__ import annotations
 
 import os
+from typing import Optional
 
 from ._lib import _require
 
@@ -645,3 +646,36 @@ def llama_block(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, n_he
         _BLOCK_PLANS[key] = plans
     return torch.ops.nbd.llama_block_ag(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plans[0],
                                         plans[1], plans[2], int(n_head), int(n_kv), D ** -0.5, float(eps), cos, sin)
+
+
+def block_graphs(enable: Optional[bool] = None) -> bool:
+    """Per-block HIP graphs for the EAGER Llama step (``csrc/kernels/autograd.hip`` namespace
+    ``bg``; off by default, ``NBD_BLOCK_GRAPHS=1`` turns it on at start).  Each fused decoder
+    block's forward is captured once per (block, shape) after two eager calls and replayed from
+    then on — one graph launch for its seven kernels.  The block's outputs then live in static
+    memory: they keep this pass's values until that block's next forward, so a caller keeping
+    block outputs across steps must clone them.  Bit-identical to the eager block.
+    ``enable=None`` queries; returns the previous setting."""
+    import torch
+
+    _require()
+    return bool(torch.ops.nbd.llama_block_graphs(-1 if enable is None else int(bool(enable))))
+
+
+def block_graphs_reset() -> None:
+    """Drop every captured block graph (a LlamaModel being garbage-collected does this)."""
+    from . import _lib
+
+    if _lib._loaded:
+        import torch
+
+        torch.ops.nbd.llama_block_graphs_reset()
+
+
+def block_graphs_stats() -> dict:
+    """Counters of the per-block graphs: captures, replays, eager calls in graph mode, live graphs."""
+    import torch
+
+    _require()
+    c, r, e, n = torch.ops.nbd.llama_block_graphs_stats()
+    return {"captures": c, "replays": r, "eager": e, "live": n}

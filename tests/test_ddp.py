@@ -4,6 +4,7 @@ import pytest
 from nbdistributed_amd.session import Session
 
 SETUP = """
+import contextlib
 import copy
 import torch.nn as nn
 from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP

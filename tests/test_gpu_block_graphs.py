@@ -1,0 +1,160 @@
+"""GPU: per-block HIP graphs for the eager Llama step (ops.block_graphs, csrc/kernels/autograd.hip
+namespace ``bg``).  The graphed block runs the eager block's kernels in the same order, so every
+loss, gradient and updated parameter must be bit-identical to graphs off — across optimizer steps
+(weights change in place under the graph), with DDP bucket gradients and no_sync accumulation, a
+second forward before backward (the block is still armed: eager), and inside a whole-step
+GraphedStep capture (the outer graph takes the blocks)."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from nbdistributed_amd import ops  # noqa: E402
+
+
+@pytest.fixture
+def dev(require_gpu):
+    assert ops.native_available(), ops._load_error
+    prev = ops.block_graphs()
+    ops.block_graphs_reset()
+    yield torch.device("cuda")
+    ops.block_graphs(prev)
+    ops.block_graphs_reset()
+
+
+def _model(dev, layers=3, seed=0):
+    from nbdistributed_amd.models.llama import LlamaConfig, LlamaForSequenceClassification
+
+    torch.manual_seed(seed)
+    return LlamaForSequenceClassification(LlamaConfig.smollm2_135m(num_hidden_layers=layers)).to(dev, torch.bfloat16)
+
+
+def _batches(dev, n=4, bs=4, T=128):
+    g = torch.Generator(device=dev).manual_seed(1)
+    return [(torch.randint(1, 49152, (bs, T), device=dev, generator=g), torch.randint(0, 2, (bs,), device=dev, generator=g))
+            for _ in range(n)]
+
+
+def _train(m, batches, graphs: bool, steps=6):
+    ops.block_graphs(graphs)
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, foreach=False)
+    losses = []
+    for i in range(steps):
+        ids, lab = batches[i % len(batches)]
+        loss = m(ids, torch.ones_like(ids), lab)[0]
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        losses.append(loss.detach())
+    torch.cuda.synchronize()
+    return torch.stack(losses), torch.cat([p.detach().float().flatten() for p in m.parameters()])
+
+
+def test_block_graphs_bit_identical_across_steps(dev):
+    base = _model(dev)
+    batches = _batches(dev)
+    l0, p0 = _train(copy.deepcopy(base), batches, False)
+    s0 = ops.block_graphs_stats()
+    l1, p1 = _train(copy.deepcopy(base), batches, True)
+    s1 = ops.block_graphs_stats()
+    assert torch.equal(l0, l1), (l0, l1)
+    assert torch.equal(p0, p1)
+    # 3 blocks: two eager calls each, one capture each, then replays (the capturing call replays too)
+    assert s1["captures"] - s0["captures"] == 3, s1
+    assert s1["replays"] - s0["replays"] == 3 * 4, s1
+    assert s1["live"] == 3, s1
+
+
+def test_block_graphs_second_forward_before_backward(dev):
+    """Two forwards before one backward: the second finds every block armed (its static memory
+    still holds the first pass) and runs eagerly; the summed gradients match graphs off."""
+    base = _model(dev, layers=2, seed=3)
+    (a, la), (b, lb) = _batches(dev, n=2)
+
+    def grads(graphs):
+        ops.block_graphs(graphs)
+        m = copy.deepcopy(base)
+        for _ in range(3):  # warm + capture
+            m(a, torch.ones_like(a), la)[0].backward()
+        for p in m.parameters():
+            p.grad = None
+        e0 = ops.block_graphs_stats()["eager"]
+        out_a = m(a, torch.ones_like(a), la)
+        out_b = m(b, torch.ones_like(b), lb)
+        (out_a[0] + out_b[0]).backward()
+        torch.cuda.synchronize()
+        return (torch.cat([p.grad.float().flatten() for p in m.parameters()]), out_a[1].float(), out_b[1].float(),
+                ops.block_graphs_stats()["eager"] - e0)
+
+    g0, a0, b0, _ = grads(False)
+    g1, a1, b1, eager = grads(True)
+    assert torch.equal(a0, a1) and torch.equal(b0, b1)
+    assert torch.equal(g0, g1)
+    assert eager == 2  # the second forward's two blocks
+
+
+def test_block_graphs_ddp_buckets_and_no_sync(dev):
+    from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP
+    from nbdistributed_amd.parallel.backend import init_data_plane
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        import os
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        init_data_plane("rccl", 0, 1, dev)
+    base = _model(dev, layers=2, seed=5)
+    batches = _batches(dev, n=2, bs=8)
+
+    def run(graphs):
+        ops.block_graphs(graphs)
+        m = NbdDDP(copy.deepcopy(base), flat_params=True, grad_mode="bucket")
+        outs = []
+        for k in (1, 2, 1, 2):
+            for p in m.parameters():
+                p.grad = None
+            for i in range(k):
+                ids, lab = batches[i]
+                with (m.no_sync() if i < k - 1 else torch.enable_grad()):
+                    m(ids, torch.ones_like(ids), lab)[0].backward()
+            torch.cuda.synchronize()
+            outs.append(torch.cat([b.buffer.float() for b in m.buckets]))
+        m.unpatch()
+        return outs
+
+    o0, o1 = run(False), run(True)
+    assert all(torch.equal(x, y) for x, y in zip(o0, o1))
+    assert ops.block_graphs_stats()["replays"] > 0
+
+
+def test_block_graphs_inside_whole_step_capture(dev):
+    """Under graphs.GraphedStep the blocks run inside the outer capture (no nested capture)."""
+    from nbdistributed_amd.graphs import GraphedStep
+
+    base = _model(dev, layers=2, seed=7)
+    batches = _batches(dev, n=1)
+
+    def run(graphs):
+        ops.block_graphs(graphs)
+        m = copy.deepcopy(base)
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-3, capturable=True, foreach=False)
+
+        def step(x, y):
+            loss = m(x, torch.ones_like(x), y)[0]
+            loss.backward()
+            opt.step()
+            opt.zero_grad(set_to_none=False)
+            return loss.detach()
+
+        call = GraphedStep(step, batches[0], warmup=3, optimizers=[opt])
+        ls = torch.stack([call(*batches[0]).clone() for _ in range(5)])  # (static output)
+        torch.cuda.synchronize()
+        return ls, torch.cat([p.detach().float().flatten() for p in m.parameters()])
+
+    l0, p0 = run(False)
+    l1, p1 = run(True)
+    assert len(set(l0.tolist())) > 1  # the parameters move between replays
+    assert torch.equal(l0, l1) and torch.equal(p0, p1)
