@@ -8,7 +8,8 @@ fp32      : HF model, fp32 params, torch AdamW (the notebook's recipe, minus acc
 bf16flat  : HF model, bf16 params in nbd DDP buckets (world 1) + FlatAdamW
 nbd       : native Llama (models/llama.py, HIP kernels), bf16 flat DDP + FlatAdamW
 nbdgraph  : nbd captured once into a HIP graph (nbdistributed_amd.graphs) and replayed
-nbdbg     : nbd eager with one HIP graph per decoder block's forward (ops.block_graphs)
+nbdbg     : nbd eager with one HIP graph per decoder block's forward (ops.block_graphs(1))
+nbdbg2    : nbdbg with each block's backward graphed too (ops.block_graphs(2))
 """
 from __future__ import annotations
 
@@ -46,7 +47,7 @@ def main():
     ids, mask, labels = ids.to(dev), mask.to(dev), labels.to(dev)
     for mode in a.modes.split(","):
         torch.manual_seed(42)
-        native = mode in ("nbd", "nbdgraph", "nbdbg")
+        native = mode in ("nbd", "nbdgraph", "nbdbg", "nbdbg2")
         if native:
             from nbdistributed_amd.models.llama import LlamaConfig, LlamaForSequenceClassification
 
@@ -76,7 +77,7 @@ def main():
         from nbdistributed_amd import ops
 
         if native:
-            ops.block_graphs(mode == "nbdbg")
+            ops.block_graphs({"nbdbg": 1, "nbdbg2": 2}.get(mode, 0))
         if mode == "nbdgraph":
             from nbdistributed_amd.graphs import GraphedStep
 
@@ -91,7 +92,7 @@ def main():
             loss = call(*batches[i % 8])
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t) / a.steps * 1e3
-        extra = f"  {ops.block_graphs_stats()}" if mode == "nbdbg" else ""
+        extra = f"  {ops.block_graphs_stats()}" if mode.startswith("nbdbg") else ""
         print(f"{mode:9s} {ms:8.2f} ms/step  {a.bs / ms * 1e3:8.1f} samples/s  loss {float(loss.detach()):.4f}{extra}",
               flush=True)
         del model, opt, fwd

@@ -28,6 +28,7 @@
 #include <torch/library.h>
 
 #include <atomic>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -647,8 +648,25 @@ static std::tuple<Tensor, Tensor> llama_block_fwd(const Tensor& x, const Tensor&
 //    aliased input moved, or that comes inside another capture (graphs.GraphedStep);
 //  * the returned tensors alias that memory: they hold this pass's values until the block's next
 //    replay (a caller keeping block outputs across steps must clone them).
-// Same kernels, same order: bit-identical to the eager block (tests/test_gpu_llama_block.py).
+// The backward of a graph-forwarded block is captured too (its first graphed backward) when every
+// weight gradient goes to a DDP bucket slice (graddst.h): the claims made during the capture are
+// recorded, and a replay first checks that each parameter's destination (and whether it
+// accumulates, no_sync) is still the captured one — peek(), no side effects — then claims them
+// (the pass bookkeeping) and hands the slices back as the weight gradients.  One backward graph per
+// accumulate pattern; deferred reductions queued inside are flushed inside.  Without bucket slices
+// (plain training) the backward stays eager: a graph's weight gradients would be static memory
+// that AccumulateGrad keeps as .grad.
+// Same kernels, same order: bit-identical to the eager block (tests/test_gpu_block_graphs.py).
 namespace bg {
+struct Bwd {
+  std::unique_ptr<at::cuda::CUDAGraph> g;
+  Tensor dx_in, dh_in;                    // static inputs (the incoming gradients)
+  bool dx_alias = false, dh_alias = false;  // ...that are another block graph's outputs
+  Tensor g1, dh;                          // static outputs: the gradients of x and h
+  std::vector<graddst::ClaimRecord> claims;  // in capture order
+  std::vector<int> slot;                  // the node output each claim's slice is returned as
+  std::vector<Tensor> warm_refs;
+};
 struct Graph {
   std::unique_ptr<at::cuda::CUDAGraph> g;
   Tensor x_in, h_in;                   // static inputs
@@ -659,6 +677,20 @@ struct Graph {
   Tensor x_out, h_out;
   std::vector<Tensor> warm_refs;       // storages the captured GEMM warm-ups read
   std::atomic<bool> armed{false};
+  int64_t id = 0;
+  std::map<int, std::shared_ptr<Bwd>> bwd;  // key: accumulate mask | need bits
+  int bwd_captures = 0;
+  bool bwd_off = false;
+  // the static output at `p` (forward or backward), or nullptr
+  const Tensor* output_at(const void* p) const {
+    if (x_out.defined() && x_out.data_ptr() == p) return &x_out;
+    if (h_out.defined() && h_out.data_ptr() == p) return &h_out;
+    for (const auto& kv : bwd) {
+      if (kv.second->g1.defined() && kv.second->g1.data_ptr() == p) return &kv.second->g1;
+      if (kv.second->dh.defined() && kv.second->dh.data_ptr() == p) return &kv.second->dh;
+    }
+    return nullptr;
+  }
 };
 struct Slot {
   int eager = 0, captures = 0, misses = 0;
@@ -669,18 +701,24 @@ using Key = std::tuple<const void*, int64_t, int64_t, int64_t>;  // (W_qkv, B, T
 std::mutex g_mu;
 std::map<Key, Slot> g_slots;
 std::unordered_map<const void*, std::weak_ptr<Graph>> g_outs;  // a graph's output address -> graph
+std::unordered_map<int64_t, std::weak_ptr<Graph>> g_by_id;      // for the backward
+int64_t g_next_id = 1;
 std::atomic<int> g_mode{-1};                                    // -1: not read from the env yet
-std::atomic<int64_t> g_stat[3];                                 // captures, replays, eager calls
+// forward captures, replays, eager calls; backward captures, replays, eager calls
+std::atomic<int64_t> g_stat[6];
 
-bool enabled() {
+// 0 off, 1 forward graphs, 2 forward and backward graphs (NBD_BLOCK_GRAPHS)
+int mode() {
   int m = g_mode.load(std::memory_order_relaxed);
   if (m < 0) {
     const char* e = std::getenv("NBD_BLOCK_GRAPHS");
-    m = e != nullptr && e[0] == '1';
+    m = e != nullptr && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
     g_mode.store(m, std::memory_order_relaxed);
   }
-  return m == 1;
+  return m;
 }
+bool enabled() { return mode() >= 1; }
+bool bwd_enabled() { return mode() >= 2; }
 
 bool stream_capturing() {
   hipStreamCaptureStatus s = hipStreamCaptureStatusNone;
@@ -688,14 +726,47 @@ bool stream_capturing() {
   return s != hipStreamCaptureStatusNone;
 }
 
-// x is the output `which` of a live block graph (so it stays put while that graph lives)
+// x is an output of a live block graph (so it stays put while that graph lives); under g_mu
 bool is_graph_output(const Tensor& x) {
+  if (!x.is_contiguous()) return false;
   auto it = g_outs.find(x.data_ptr());
   if (it == g_outs.end()) return false;
   auto gr = it->second.lock();
   if (!gr) return false;
-  const Tensor& o = gr->x_out.data_ptr() == x.data_ptr() ? gr->x_out : gr->h_out;
-  return o.sizes() == x.sizes() && o.strides() == x.strides() && o.scalar_type() == x.scalar_type();
+  const Tensor* o = gr->output_at(x.data_ptr());
+  return o != nullptr && o->numel() == x.numel() && o->scalar_type() == x.scalar_type();
+}
+
+// Capture `body` into `g` on a side stream ordered after the caller's stream, which then waits
+// for it.  Returns the error ("" = captured).
+std::string capture(at::cuda::CUDAGraph& g, const std::function<void()>& body) {
+  auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA();
+  auto side = c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, cur.device_index());
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  C10_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+  C10_HIP_CHECK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
+  C10_HIP_CHECK(hipEventRecord(ev_in, cur.stream()));
+  C10_HIP_CHECK(hipStreamWaitEvent(side.stream(), ev_in, 0));
+  std::string err;
+  {
+    const c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(side);
+    g.capture_begin(at::cuda::graph_pool_handle(), hipStreamCaptureModeThreadLocal);
+    try {
+      body();
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    try {
+      g.capture_end();
+    } catch (const std::exception& e) {
+      if (err.empty()) err = e.what();
+    }
+  }
+  C10_HIP_CHECK(hipEventRecord(ev_out, side.stream()));
+  C10_HIP_CHECK(hipStreamWaitEvent(cur.stream(), ev_out, 0));
+  C10_HIP_CHECK(hipEventDestroy(ev_in));
+  C10_HIP_CHECK(hipEventDestroy(ev_out));
+  return err;
 }
 
 // a CPU scalar whose release (backward done with the saved tensors, or the node gone) disarms
@@ -764,7 +835,6 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
       return nullptr;
     }
   }
-  auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA();
   if (gr) {
     if (!gr->x_alias && x.data_ptr() != gr->x_in.data_ptr()) gr->x_in.copy_(x);
     if (!gr->h_alias && h.data_ptr() != gr->h_in.data_ptr()) gr->h_in.copy_(h);
@@ -778,42 +848,20 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
   G->sig = std::move(sig);
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    G->x_alias = x.is_contiguous() && is_graph_output(x);
-    G->h_alias = h.is_contiguous() && is_graph_output(h);
+    G->x_alias = is_graph_output(x);
+    G->h_alias = is_graph_output(h);
   }
   // (variable_data: the graph must not hold the caller's autograd history — an aliased input is
   // the previous block's output, whose node would keep this pass's AccumulateGrad nodes alive)
   G->x_in = G->x_alias ? x.variable_data() : at::empty_like(x, at::MemoryFormat::Contiguous).copy_(x);
   G->h_in = G->h_alias ? h.variable_data() : at::empty_like(h, at::MemoryFormat::Contiguous).copy_(h);
-  auto side = c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, x.get_device());
-  hipEvent_t ev_in = nullptr, ev_out = nullptr;
-  C10_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
-  C10_HIP_CHECK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
-  C10_HIP_CHECK(hipEventRecord(ev_in, cur.stream()));
-  C10_HIP_CHECK(hipStreamWaitEvent(side.stream(), ev_in, 0));
   std::vector<Tensor> save;
-  std::string err;
-  {
-    const c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(side);
-    G->g = std::make_unique<at::cuda::CUDAGraph>();
-    G->g->capture_begin(at::cuda::graph_pool_handle(), hipStreamCaptureModeThreadLocal);
-    try {
-      std::tie(G->x_out, G->h_out) = llama_block_fwd(G->x_in, G->h_in, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down,
-                                                     w_next, plan_qkv, plan_o, plan_mlp, H, Hkv, scale, eps, cos,
-                                                     sin, &save);
-    } catch (const std::exception& e) {
-      err = e.what();
-    }
-    try {
-      G->g->capture_end();
-    } catch (const std::exception& e) {
-      if (err.empty()) err = e.what();
-    }
-  }
-  C10_HIP_CHECK(hipEventRecord(ev_out, side.stream()));
-  C10_HIP_CHECK(hipStreamWaitEvent(cur.stream(), ev_out, 0));
-  C10_HIP_CHECK(hipEventDestroy(ev_in));
-  C10_HIP_CHECK(hipEventDestroy(ev_out));
+  G->g = std::make_unique<at::cuda::CUDAGraph>();
+  const std::string err = capture(*G->g, [&] {
+    std::tie(G->x_out, G->h_out) = llama_block_fwd(G->x_in, G->h_in, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down,
+                                                   w_next, plan_qkv, plan_o, plan_mlp, H, Hkv, scale, eps, cos, sin,
+                                                   &save);
+  });
   G->warm_refs = gemm::gemm_warm_take_refs();
   if (!err.empty()) {
     TORCH_WARN_ONCE("nbd: a decoder block's HIP graph capture failed (", err, "); the block runs eagerly");
@@ -829,12 +877,179 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
   ++g_stat[1];
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto it = g_outs.begin(); it != g_outs.end();) it = it->second.expired() ? g_outs.erase(it) : std::next(it);
+  for (auto it = g_by_id.begin(); it != g_by_id.end();) it = it->second.expired() ? g_by_id.erase(it) : std::next(it);
   g_outs[G->x_out.data_ptr()] = G;
   g_outs[G->h_out.data_ptr()] = G;
+  G->id = g_next_id++;
+  g_by_id[G->id] = G;
   Slot& s = g_slots[key];
   s.g = G;
   s.misses = 0;
   return G;
+}
+
+// The block's backward into `out` (the node's 20 outputs).
+static void block_bwd(const std::vector<Tensor>& sv, const std::vector<std::vector<int64_t>>& plans, int64_t H,
+                      int64_t Hkv, double scale, const std::vector<int64_t>& shape, bool need_x, bool need_h,
+                      const Tensor& dx_out, const Tensor& dh_out, variable_list& out) {
+  const Tensor &h2 = sv[0], &w_qkv = sv[1], &b_qkv = sv[2], &qkv = sv[3], &o = sv[4], &lse = sv[5], &w_o = sv[6],
+               &b_o = sv[7], &x1 = sv[8], &w_post = sv[9], &rstd1 = sv[10], &h1f = sv[11], &w_gu = sv[12],
+               &w_down = sv[13], &pre = sv[14], &act = sv[15], &x_out = sv[16], &w_next = sv[17], &rstd2 = sv[18];
+  const optional<Tensor> cos = sv[19].defined() ? optional<Tensor>(sv[19]) : c10::nullopt;
+  const optional<Tensor> sin = sv[20].defined() ? optional<Tensor>(sv[20]) : c10::nullopt;
+  const int64_t C = shape[2];
+  // x2 = x1 + m, h2 = rms(x2)·γ_next
+  Tensor g2, dw_next;
+  if (dh_out.defined()) std::tie(g2, dw_next) = rms_bwd_core(x_out, dh_out, dx_out, w_next, rstd2);
+  else g2 = dx_out;
+  if (!g2.defined()) return;  // neither output reached the loss
+  // m = down(swiglu(h1·W_guᵀ))
+  auto [dh1, dw_gu, dw_down] = swiglu_bwd_core(bf16c(g2).view({-1, C}), h1f, w_gu, w_down, pre, act, plans[2], true);
+  // x1 = x + y, h1 = rms(x1)·γ_post
+  auto [g1, dw_post] = rms_bwd_core(x1, dh1.view(shape), g2, w_post, rstd1);
+  // y = a·W_oᵀ (+b)
+  const Tensor a2 = o.transpose(1, 2).reshape({h2.size(0), -1});
+  auto [da, dw_o, db_o] = linear_bwd_core(bf16c(g1).view({-1, C}), a2, w_o, b_o, plans[1], true,
+                                          w_o.requires_grad(), b_o.defined() && b_o.requires_grad());
+  const Tensor dqkv = attn_bwd_core(da, qkv, o, lse, H, Hkv, scale, cos, sin);
+  auto [dh, dw_qkv, db_qkv] = linear_bwd_core(dqkv.view({h2.size(0), -1}), h2, w_qkv, b_qkv, plans[0], need_h,
+                                              w_qkv.requires_grad(), b_qkv.defined() && b_qkv.requires_grad());
+  out[0] = need_x ? g1 : Tensor();
+  out[1] = dh.defined() ? dh.view(shape) : dh;
+  out[2] = dw_qkv;
+  out[3] = db_qkv;
+  out[4] = dw_o;
+  out[5] = db_o;
+  out[6] = dw_post;
+  out[7] = dw_gu;
+  out[8] = dw_down;
+  out[9] = dw_next;
+}
+
+// The block's backward as a HIP graph (see namespace bg); false = run it eagerly.
+static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
+                            const std::vector<std::vector<int64_t>>& plans, int64_t H, int64_t Hkv, double scale,
+                            const std::vector<int64_t>& shape, bool need_x, bool need_h, const Tensor& dx_out,
+                            const Tensor& dh_out, variable_list& out) {
+  using namespace bg;
+  if (G.bwd_off || !dh_out.defined() || bg::stream_capturing()) return false;
+  for (const Tensor* t : {&dx_out, &dh_out})
+    if (t->defined() && (!t->is_contiguous() || t->scalar_type() != at::kBFloat16 ||
+                         t->numel() != shape[0] * shape[1] * shape[2]))
+      return false;
+  const bool has_dx = dx_out.defined();  // (the last block's residual output reaches no loss)
+  // the parameters whose gradients this node returns: every one needs a bucket slice
+  constexpr int kSlot[] = {2, 3, 4, 5, 6, 7, 8, 9};  // node outputs of sv[1, 2, 6, 7, 9, 12, 13, 17]
+  const Tensor* ps[] = {&sv[1], &sv[2], &sv[6], &sv[7], &sv[9], &sv[12], &sv[13], &sv[17]};
+  Tensor dst[8];
+  bool acc[8] = {};
+  int mask = 0;
+  for (int i = 0; i < 8; ++i) {
+    if (!ps[i]->defined() || !ps[i]->requires_grad()) continue;
+    dst[i] = graddst::peek(*ps[i], acc[i]);
+    if (!dst[i].defined()) return false;
+    mask |= (int)acc[i] << i;
+  }
+  const int key = mask | (int)need_x << 8 | (int)need_h << 9 | (int)has_dx << 10;
+  auto param_index = [&](const c10::TensorImpl* impl) {
+    for (int i = 0; i < 8; ++i)
+      if (ps[i]->defined() && ps[i]->unsafeGetTensorImpl() == impl) return i;
+    return -1;
+  };
+  auto it = G.bwd.find(key);
+  if (it != G.bwd.end()) {
+    Bwd& B = *it->second;
+    bool ok = (!has_dx || !B.dx_alias || dx_out.data_ptr() == B.dx_in.data_ptr()) &&
+              (!B.dh_alias || dh_out.data_ptr() == B.dh_in.data_ptr());
+    for (const auto& c : B.claims) {
+      const int i = param_index(c.param);
+      ok = ok && i >= 0 && dst[i].data_ptr() == c.dst && acc[i] == c.acc;
+    }
+    if (!ok) {
+      G.bwd.erase(it);  // destinations moved: capture anew next time
+      return false;
+    }
+    if (has_dx && !B.dx_alias && dx_out.data_ptr() != B.dx_in.data_ptr()) B.dx_in.copy_(dx_out);
+    if (!B.dh_alias && dh_out.data_ptr() != B.dh_in.data_ptr()) B.dh_in.copy_(dh_out);
+    for (const auto& c : B.claims) {  // the pass bookkeeping of the captured claims
+      const int i = param_index(c.param);
+      bool a = false;
+      const Tensor d = graddst::claim(*ps[i], a);
+      TORCH_CHECK(d.defined() && d.data_ptr() == c.dst && a == c.acc, "nbd: block graph claim changed");
+    }
+    B.g->replay();
+    out[0] = need_x ? at::alias(B.g1) : Tensor();
+    out[1] = need_h ? at::alias(B.dh) : Tensor();
+    for (size_t k = 0; k < B.claims.size(); ++k) {
+      const int i = param_index(B.claims[k].param);
+      if (B.slot[k] >= 0) out[B.slot[k]] = graddst::hand_back(*ps[i], dst[i], B.claims[k].acc);
+    }
+    return true;
+  }
+  if (G.bwd_captures >= 4) {
+    G.bwd_off = true;
+    return false;
+  }
+  ++G.bwd_captures;
+  defer::flush();  // reductions queued by eager nodes before this one stay out of the graph
+  auto B = std::make_shared<Bwd>();
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    B->dx_alias = has_dx && is_graph_output(dx_out);
+    B->dh_alias = is_graph_output(dh_out);
+  }
+  if (has_dx)
+    B->dx_in = B->dx_alias ? dx_out.variable_data() : at::empty_like(dx_out, at::MemoryFormat::Contiguous).copy_(dx_out);
+  B->dh_in = B->dh_alias ? dh_out.variable_data() : at::empty_like(dh_out, at::MemoryFormat::Contiguous).copy_(dh_out);
+  B->g = std::make_unique<at::cuda::CUDAGraph>();
+  variable_list o(20);
+  graddst::record_claims(&B->claims);
+  const std::string err = capture(*B->g, [&] {
+    block_bwd(sv, plans, H, Hkv, scale, shape, need_x, need_h, B->dx_in, B->dh_in, o);
+    defer::flush();  // this node's deferred reductions go into its graph
+  });
+  graddst::record_claims(nullptr);
+  B->warm_refs = gemm::gemm_warm_take_refs();
+  if (!err.empty()) G.bwd_off = true;
+  TORCH_CHECK(err.empty(), "nbd: a decoder block's backward graph capture failed: ", err);
+  // every weight gradient must be its claimed slice (else it would be static graph memory)
+  B->slot.assign(B->claims.size(), -1);
+  bool valid = true;
+  for (int i = 0; i < 8; ++i) {
+    const Tensor& g = o[kSlot[i]];
+    if (!g.defined()) continue;
+    int found = -1;
+    for (size_t k = 0; k < B->claims.size(); ++k)
+      if (B->claims[k].dst == g.data_ptr() && B->claims[k].param == ps[i]->unsafeGetTensorImpl()) found = (int)k;
+    if (found < 0) valid = false;
+    else B->slot[found] = kSlot[i];
+  }
+  B->g->replay();
+  ++g_stat[3];
+  if (!valid) {  // this call: private copies of the non-slice gradients; later calls: eager
+    G.bwd_off = true;
+    for (int i = 0; i < 8; ++i) {
+      Tensor& g = o[kSlot[i]];
+      bool claimed = false;
+      for (const auto& c : B->claims) claimed = claimed || (g.defined() && c.dst == g.data_ptr());
+      if (g.defined() && !claimed) g = g.clone();
+    }
+    out = o;
+    for (int k : {0, 1})
+      if (out[k].defined()) out[k] = out[k].clone();
+    return true;
+  }
+  B->g1 = o[0].defined() ? o[0].view(shape) : Tensor();
+  B->dh = o[1].defined() ? o[1].view(shape) : Tensor();
+  out = o;
+  out[0] = B->g1.defined() ? at::alias(B->g1) : Tensor();
+  out[1] = B->dh.defined() ? at::alias(B->dh) : Tensor();
+  G.bwd[key] = B;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto self = g_by_id.count(G.id) ? g_by_id[G.id] : std::weak_ptr<Graph>();
+  if (B->g1.defined()) g_outs[B->g1.data_ptr()] = self;
+  if (B->dh.defined()) g_outs[B->dh.data_ptr()] = self;
+  return true;
 }
 
 struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
@@ -861,6 +1076,7 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
       save.push_back(bg::token(gr));
       x_out = at::alias(gr->x_out);
       h_out = at::alias(gr->h_out);
+      if (bg::bwd_enabled()) ctx->saved_data["bg"] = gr->id;
     } else {
       std::tie(x_out, h_out) = llama_block_fwd(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv,
                                                plan_o, plan_mlp, H, Hkv, scale, eps, cos, sin, &save);
@@ -877,45 +1093,26 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
     const auto sv = ctx->get_saved_variables();
-    const Tensor &h2 = sv[0], &w_qkv = sv[1], &b_qkv = sv[2], &qkv = sv[3], &o = sv[4], &lse = sv[5], &w_o = sv[6],
-                 &b_o = sv[7], &x1 = sv[8], &w_post = sv[9], &rstd1 = sv[10], &h1f = sv[11], &w_gu = sv[12],
-                 &w_down = sv[13], &pre = sv[14], &act = sv[15], &x_out = sv[16], &w_next = sv[17], &rstd2 = sv[18];
-    const optional<Tensor> cos = sv[19].defined() ? optional<Tensor>(sv[19]) : c10::nullopt;
-    const optional<Tensor> sin = sv[20].defined() ? optional<Tensor>(sv[20]) : c10::nullopt;
     const auto plans = ctx->saved_data["plans"].to<std::vector<std::vector<int64_t>>>();
     const int64_t H = ctx->saved_data["H"].toInt(), Hkv = ctx->saved_data["Hkv"].toInt();
     const double scale = ctx->saved_data["scale"].toDouble();
     const auto shape = ctx->saved_data["shape"].toIntVector();
     const auto need = ctx->saved_data["need"].toBoolList();
-    const int64_t C = shape[2];
     variable_list out(20);
-    const Tensor &dx_out = grads[0], &dh_out = grads[1];
-    // x2 = x1 + m, h2 = rms(x2)·γ_next
-    Tensor g2, dw_next;
-    if (dh_out.defined()) std::tie(g2, dw_next) = rms_bwd_core(x_out, dh_out, dx_out, w_next, rstd2);
-    else g2 = dx_out;
-    if (!g2.defined()) return out;  // neither output reached the loss
-    // m = down(swiglu(h1·W_guᵀ))
-    auto [dh1, dw_gu, dw_down] = swiglu_bwd_core(bf16c(g2).view({-1, C}), h1f, w_gu, w_down, pre, act, plans[2], true);
-    // x1 = x + y, h1 = rms(x1)·γ_post
-    auto [g1, dw_post] = rms_bwd_core(x1, dh1.view(shape), g2, w_post, rstd1);
-    // y = a·W_oᵀ (+b)
-    const Tensor a2 = o.transpose(1, 2).reshape({h2.size(0), -1});
-    auto [da, dw_o, db_o] = linear_bwd_core(bf16c(g1).view({-1, C}), a2, w_o, b_o, plans[1], true,
-                                            w_o.requires_grad(), b_o.defined() && b_o.requires_grad());
-    const Tensor dqkv = attn_bwd_core(da, qkv, o, lse, H, Hkv, scale, cos, sin);
-    auto [dh, dw_qkv, db_qkv] = linear_bwd_core(dqkv.view({h2.size(0), -1}), h2, w_qkv, b_qkv, plans[0], need[1],
-                                                w_qkv.requires_grad(), b_qkv.defined() && b_qkv.requires_grad());
-    out[0] = need[0] ? g1 : Tensor();
-    out[1] = dh.defined() ? dh.view(shape) : dh;
-    out[2] = dw_qkv;
-    out[3] = db_qkv;
-    out[4] = dw_o;
-    out[5] = db_o;
-    out[6] = dw_post;
-    out[7] = dw_gu;
-    out[8] = dw_down;
-    out[9] = dw_next;
+    if (ctx->saved_data.count("bg")) {  // graph-forwarded: the backward may be a graph too
+      std::shared_ptr<bg::Graph> gr;
+      {
+        std::lock_guard<std::mutex> lk(bg::g_mu);
+        auto it = bg::g_by_id.find(ctx->saved_data["bg"].toInt());
+        if (it != bg::g_by_id.end()) gr = it->second.lock();
+      }
+      if (gr && block_bwd_graph(*gr, sv, plans, H, Hkv, scale, shape, need[0], need[1], grads[0], grads[1], out)) {
+        ++bg::g_stat[4];
+        return out;
+      }
+      ++bg::g_stat[5];
+    }
+    block_bwd(sv, plans, H, Hkv, scale, shape, need[0], need[1], grads[0], grads[1], out);
     return out;
   }
 };
@@ -943,10 +1140,10 @@ std::tuple<Tensor, Tensor> llama_block_noag(const Tensor& x, const Tensor& h, co
                          scale, eps, cos, sin, nullptr);
 }
 
-// Per-block graphs: mode 1 on, 0 off, -1 query; returns the previous setting.
+// Per-block graphs: mode 0 off, 1 forward, 2 forward and backward, -1 query; returns the previous mode.
 int64_t llama_block_graphs(int64_t mode) {
-  const int64_t prev = bg::enabled() ? 1 : 0;
-  if (mode >= 0) bg::g_mode.store(mode == 1 ? 1 : 0, std::memory_order_relaxed);
+  const int64_t prev = bg::mode();
+  if (mode >= 0) bg::g_mode.store((int)std::min<int64_t>(mode, 2), std::memory_order_relaxed);
   return prev;
 }
 
@@ -958,12 +1155,13 @@ void llama_block_graphs_reset() {
   bg::g_outs.clear();
 }
 
-// [captures, replays, eager calls in graph mode, live graphs]
+// [captures, replays, eager calls, live graphs, backward captures, replays, eager calls]
 std::vector<int64_t> llama_block_graphs_stats() {
   std::lock_guard<std::mutex> lk(bg::g_mu);
   int64_t live = 0;
   for (const auto& kv : bg::g_slots) live += kv.second.g != nullptr;
-  return {bg::g_stat[0].load(), bg::g_stat[1].load(), bg::g_stat[2].load(), live};
+  return {bg::g_stat[0].load(), bg::g_stat[1].load(), bg::g_stat[2].load(), live,
+          bg::g_stat[3].load(), bg::g_stat[4].load(), bg::g_stat[5].load()};
 }
 
 }  // namespace ag

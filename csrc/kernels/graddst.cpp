@@ -23,7 +23,12 @@ std::unordered_map<const c10::TensorImpl*, Entry> g_map;
 uint64_t g_gen = 1;
 }  // namespace
 
-at::Tensor claim(const at::Tensor& param, bool& acc) {
+thread_local std::vector<ClaimRecord>* t_log = nullptr;
+
+void record_claims(std::vector<ClaimRecord>* log) { t_log = log; }
+
+// claim() with `take` = hand it out (pass bookkeeping, flush on a second use); peek() without
+static at::Tensor lookup(const at::Tensor& param, bool& acc, bool take) {
   acc = false;
   if (!param.defined() || !param.requires_grad() || !param.is_leaf()) return at::Tensor();
   std::lock_guard<std::mutex> lk(g_mu);
@@ -35,7 +40,7 @@ at::Tensor claim(const at::Tensor& param, bool& acc) {
   if (e.gen == g_gen) {
     // a second use in this pass: the engine adds the contributions before AccumulateGrad, so the
     // first writer's deferred reduce into the slice must have been issued
-    defer::flush();
+    if (take) defer::flush();
     return at::Tensor();
   }
   const at::Tensor& g = param.grad();
@@ -45,9 +50,18 @@ at::Tensor claim(const at::Tensor& param, bool& acc) {
       return at::Tensor();
     acc = true;
   }
-  e.gen = g_gen;
+  if (take) e.gen = g_gen;
   return e.dst;
 }
+
+at::Tensor claim(const at::Tensor& param, bool& acc) {
+  at::Tensor d = lookup(param, acc, true);
+  if (t_log != nullptr && param.defined())
+    t_log->push_back({param.unsafeGetTensorImpl(), d.defined() ? d.data_ptr() : nullptr, acc});
+  return d;
+}
+
+at::Tensor peek(const at::Tensor& param, bool& acc) { return lookup(param, acc, false); }
 
 at::Tensor hand_back(const at::Tensor& param, const at::Tensor& dst, bool acc) {
   // AccumulateGrad steals a gradient only while .grad is unset; the slice already holds the sum

@@ -16,6 +16,8 @@
 #pragma once
 #include <ATen/ATen.h>
 
+#include <vector>
+
 namespace nbd {
 namespace graddst {
 
@@ -25,6 +27,18 @@ at::Tensor claim(const at::Tensor& param, bool& acc);
 
 // The tensor to return from backward for a gradient written into `dst` (claimed with `acc`).
 at::Tensor hand_back(const at::Tensor& param, const at::Tensor& dst, bool acc);
+
+// What claim() would return for `param` now, without handing it out (no pass bookkeeping, no
+// flush): the per-block backward graphs (autograd.hip) check their captured destinations with it.
+at::Tensor peek(const at::Tensor& param, bool& acc);
+
+// Claims made on this thread while a log is set are appended to it (nullptr stops recording).
+struct ClaimRecord {
+  const c10::TensorImpl* param;
+  const void* dst;  // nullptr: no destination (the writer allocated)
+  bool acc;
+};
+void record_claims(std::vector<ClaimRecord>* log);
 
 }  // namespace graddst
 

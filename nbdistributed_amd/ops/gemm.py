@@ -13,7 +13,6 @@ to PyTorch (hipBLASLt on ROCm) with identical semantics.
 from __future__ import annotations
 
 import os
-from typing import Optional
 
 from ._lib import _require
 
@@ -648,18 +647,19 @@ def llama_block(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, n_he
                                         plans[1], plans[2], int(n_head), int(n_kv), D ** -0.5, float(eps), cos, sin)
 
 
-def block_graphs(enable: Optional[bool] = None) -> bool:
+def block_graphs(enable=None) -> int:
     """Per-block HIP graphs for the EAGER Llama step (``csrc/kernels/autograd.hip`` namespace
     ``bg``; off by default, ``NBD_BLOCK_GRAPHS=1`` turns it on at start).  Each fused decoder
     block's forward is captured once per (block, shape) after two eager calls and replayed from
     then on — one graph launch for its seven kernels.  The block's outputs then live in static
     memory: they keep this pass's values until that block's next forward, so a caller keeping
-    block outputs across steps must clone them.  Bit-identical to the eager block.
-    ``enable=None`` queries; returns the previous setting."""
+    block outputs across steps must clone them.  ``enable=2`` (``NBD_BLOCK_GRAPHS=2``) graphs the
+    backward too where every weight gradient goes to a DDP bucket slice.  Bit-identical to the
+    eager block.  ``enable=None`` queries; True = 1; returns the previous mode (0, 1, 2)."""
     import torch
 
     _require()
-    return bool(torch.ops.nbd.llama_block_graphs(-1 if enable is None else int(bool(enable))))
+    return int(torch.ops.nbd.llama_block_graphs(-1 if enable is None else int(enable)))
 
 
 def block_graphs_reset() -> None:
@@ -673,9 +673,11 @@ def block_graphs_reset() -> None:
 
 
 def block_graphs_stats() -> dict:
-    """Counters of the per-block graphs: captures, replays, eager calls in graph mode, live graphs."""
+    """Counters of the per-block graphs: forward captures, replays, eager calls in graph mode, live
+    graphs; backward captures, replays (captures included) and eager backwards of graphed forwards."""
     import torch
 
     _require()
-    c, r, e, n = torch.ops.nbd.llama_block_graphs_stats()
-    return {"captures": c, "replays": r, "eager": e, "live": n}
+    c, r, e, n, bc, br, be = torch.ops.nbd.llama_block_graphs_stats()
+    return {"captures": c, "replays": r, "eager": e, "live": n, "bwd_captures": bc, "bwd_replays": br,
+            "bwd_eager": be}

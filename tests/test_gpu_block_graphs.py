@@ -37,7 +37,7 @@ def _batches(dev, n=4, bs=4, T=128):
             for _ in range(n)]
 
 
-def _train(m, batches, graphs: bool, steps=6):
+def _train(m, batches, graphs: int, steps=6):
     ops.block_graphs(graphs)
     opt = torch.optim.AdamW(m.parameters(), lr=1e-3, foreach=False)
     losses = []
@@ -52,13 +52,17 @@ def _train(m, batches, graphs: bool, steps=6):
     return torch.stack(losses), torch.cat([p.detach().float().flatten() for p in m.parameters()])
 
 
-def test_block_graphs_bit_identical_across_steps(dev):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_block_graphs_bit_identical_across_steps(dev, mode):
+    """Plain training (no DDP slices): mode 2 keeps the backward eager (its weight gradients would
+    be static graph memory)."""
     base = _model(dev)
     batches = _batches(dev)
-    l0, p0 = _train(copy.deepcopy(base), batches, False)
+    l0, p0 = _train(copy.deepcopy(base), batches, 0)
     s0 = ops.block_graphs_stats()
-    l1, p1 = _train(copy.deepcopy(base), batches, True)
+    l1, p1 = _train(copy.deepcopy(base), batches, mode)
     s1 = ops.block_graphs_stats()
+    assert s1["bwd_replays"] == s0["bwd_replays"]
     assert torch.equal(l0, l1), (l0, l1)
     assert torch.equal(p0, p1)
     # 3 blocks: two eager calls each, one capture each, then replays (the capturing call replays too)
@@ -95,7 +99,10 @@ def test_block_graphs_second_forward_before_backward(dev):
     assert eager == 2  # the second forward's two blocks
 
 
-def test_block_graphs_ddp_buckets_and_no_sync(dev):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_block_graphs_ddp_buckets_and_no_sync(dev, mode):
+    """DDP bucket gradients (graddst slices), alternating plain and no_sync-accumulated steps: in
+    mode 2 the backward graphs replay with both accumulate patterns."""
     from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP
     from nbdistributed_amd.parallel.backend import init_data_plane
     import torch.distributed as dist
@@ -125,9 +132,15 @@ def test_block_graphs_ddp_buckets_and_no_sync(dev):
         m.unpatch()
         return outs
 
-    o0, o1 = run(False), run(True)
+    o0 = run(0)
+    s0 = ops.block_graphs_stats()
+    o1 = run(mode)
+    s1 = ops.block_graphs_stats()
     assert all(torch.equal(x, y) for x, y in zip(o0, o1))
-    assert ops.block_graphs_stats()["replays"] > 0
+    assert s1["replays"] > s0["replays"]
+    if mode == 2:  # (k=2 passes: the no_sync pass accumulates, a second backward variant)
+        assert s1["bwd_replays"] - s0["bwd_replays"] >= 4, s1
+        assert s1["bwd_captures"] - s0["bwd_captures"] >= 2, s1
 
 
 def test_block_graphs_inside_whole_step_capture(dev):
