@@ -1,0 +1,7 @@
+#!/bin/bash
+# eager (no overlap) vs eager + per-block forward graphs vs whole-step graph, 5 interleaved rounds
+set -o pipefail
+mkdir -p gpurun_out
+for r in 1 2 3 4 5; do
+  timeout -k 10 240 python -u benchmarks/notebook_step.py --modes nbd,nbdbg,nbdgraph --steps 60 --warm 8 || exit $?
+done > gpurun_out/bg_ab5n.txt 2>&1

@@ -1,102 +1,77 @@
 #!/usr/bin/env python3
-"""Timeline view of a rocprofv3 kernel trace: GPU busy vs idle (launch gaps) over the last N
-steps, and device time by kernel family.
+"""GPU busy vs idle time per training step from a rocprofv3 kernel trace: is an eager step
+host-bound (the GPU waits for launches), and in which part of the step?
 
-    python benchmarks/trace_gaps.py PROF_DIR [--marker SUBSTR] [--steps 5] [--out FILE.md]
+    python benchmarks/trace_gaps.py PROF_DIR [--marker adamw] [--steps 10]
 
-A "step" boundary is each launch of the kernel whose name contains --marker (default: the AdamW
-kernel, launched once per bucket: the first of each consecutive run counts).
+Steps are delimited by the optimizer kernels (the last kernel whose name matches --marker before
+a gap, i.e. the end of each step's update).  For the last --steps steps it prints wall time,
+the union of kernel intervals (busy), idle time, and idle time split into thirds of the step
+(forward-ish / early backward / late backward + update), plus the largest gaps with the kernels
+around them.
 """
 from __future__ import annotations
 
 import argparse
-import csv
-import glob
 import os
 import re
-from collections import defaultdict
+import sys
 
-FAMILIES = [
-    ("gemm (nbd)", r"nbd::gemm::gemm_kernel|nbd::gemm::g256|nbd::gemm::pair_kernel"),
-    ("gemm (hipBLASLt)", r"^Cijk_|^Custom_Cijk"),
-    ("gemm split-K reduce", r"nbd::gemm::reduce_kernel"),
-    ("attention", r"nbd::attn::"),
-    ("layer/rms norm", r"nbd::norm::"),
-    ("cross-entropy", r"xent"),
-    ("optimizer", r"adamw|nbd::optim"),
-    ("embedding", r"nbd::embed::"),
-    ("bucket / copy", r"nbd::multi_copy|bucket|copyBuffer|fillBuffer"),
-    ("rccl", r"ncclDevKernel|rccl|nccl"),
-    ("torch elementwise", r"at::native::"),
-]
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from trace_seq import load, short  # noqa: E402
 
 
-def family(name: str) -> str:
-    for fam, pat in FAMILIES:
-        if re.search(pat, name):
-            return fam
-    return "other"
-
-
-def main():
+def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("prof_dir")
-    ap.add_argument("--marker", default="adamw_flat_kernel")
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--out", default=None)
+    ap.add_argument("--marker", default="adamw")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--top", type=int, default=8)
     a = ap.parse_args()
-    path = glob.glob(os.path.join(a.prof_dir, "**", "*kernel_trace.csv"), recursive=True)[0]
-    rows = []
-    for r in csv.DictReader(open(path)):
-        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
-    rows.sort()
-    # step boundaries: first marker kernel of each run of marker kernels
-    starts = []
-    prev_marker = False
-    for i, (s, e, n) in enumerate(rows):
-        m = a.marker in n
-        if m and not prev_marker:
-            starts.append(i)
-        prev_marker = m
-    if len(starts) < a.steps + 1:
-        raise SystemExit(f"only {len(starts)} step markers found")
-    lo, hi = starts[-a.steps - 1], starts[-1]
-    sel = rows[lo:hi]
-    span = sel[-1][1] - sel[0][0]
-    # busy = union of kernel intervals
-    busy = 0
-    cur_s, cur_e = sel[0][0], sel[0][1]
+    rows = load(a.prof_dir)
+    pat = re.compile(a.marker, re.I)
+    # step ends: the last marker kernel of each run of marker kernels
+    ends = [i for i in range(len(rows) - 1) if pat.search(rows[i][2]) and not pat.search(rows[i + 1][2])]
+    if pat.search(rows[-1][2]):
+        ends.append(len(rows) - 1)
+    assert len(ends) > a.steps, f"only {len(ends)} steps found"
+    ends = ends[-(a.steps + 1):]
+    tot_wall = tot_busy = 0.0
+    thirds = [0.0, 0.0, 0.0]
     gaps = []
-    for s, e, n in sel[1:]:
-        if s > cur_e:
-            busy += cur_e - cur_s
-            gaps.append((s - cur_e, n))
-            cur_s, cur_e = s, e
-        else:
-            cur_e = max(cur_e, e)
-    busy += cur_e - cur_s
-    fam = defaultdict(float)
-    for s, e, n in sel:
-        fam[family(n)] += (e - s)
-    steps = a.steps
-    lines = [f"# GPU timeline over the last {steps} steps ({os.path.basename(a.prof_dir)})", "",
-             f"* kernels per step: {len(sel) / steps:.0f}",
-             f"* span per step: {span / steps / 1e6:.3f} ms; GPU busy (union of kernels) {busy / steps / 1e6:.3f} ms "
-             f"({100 * busy / span:.1f} %); idle {(span - busy) / steps / 1e6:.3f} ms in {len(gaps) / steps:.0f} gaps",
-             f"* gaps > 5 us per step: {sum(1 for g, _ in gaps if g > 5000) / steps:.1f} "
-             f"({sum(g for g, _ in gaps if g > 5000) / steps / 1e3:.1f} us)", "",
-             "| family | ms / step | % of kernel time |", "|---|---|---|"]
-    tot = sum(fam.values())
-    for k, v in sorted(fam.items(), key=lambda kv: -kv[1]):
-        lines.append(f"| {k} | {v / steps / 1e6:.3f} | {100 * v / tot:.1f} |")
-    lines += ["", "Largest gaps (before kernel):", ""]
-    for g, n in sorted(gaps, reverse=True)[:10]:
-        lines.append(f"* {g / 1e3:.1f} us before `{n[:100]}`")
-    text = "\n".join(lines) + "\n"
-    print(text)
-    if a.out:
-        with open(a.out, "w") as f:
-            f.write(text)
+    for s in range(a.steps):
+        lo, hi = ends[s] + 1, ends[s + 1]
+        t0, t1 = rows[ends[s]][1], rows[hi][1]
+        wall = t1 - t0
+        busy = 0
+        cur_s, cur_e = None, None
+        prev_end = t0
+        for i in range(lo, hi + 1):
+            st, en, name = rows[i]
+            if st > prev_end:
+                g = st - prev_end
+                frac = (prev_end - t0) / wall
+                thirds[min(2, int(frac * 3))] += g
+                gaps.append((g, rows[i - 1][2], name, frac))
+            if cur_s is None or st > cur_e:
+                if cur_s is not None:
+                    busy += cur_e - cur_s
+                cur_s, cur_e = st, en
+            else:
+                cur_e = max(cur_e, en)
+            prev_end = max(prev_end, en)
+        busy += cur_e - cur_s
+        tot_wall += wall
+        tot_busy += busy
+    n = a.steps
+    print(f"steps {n}: wall {tot_wall / n / 1e6:.3f} ms  busy {tot_busy / n / 1e6:.3f} ms  "
+          f"idle {(tot_wall - tot_busy) / n / 1e6:.3f} ms  (idle by thirds of the step: "
+          + " / ".join(f"{t / n / 1e6:.3f}" for t in thirds) + " ms)")
+    gaps.sort(reverse=True)
+    print(f"largest gaps (µs, position in step, kernel before -> after):")
+    for g, before, after, frac in gaps[:a.top]:
+        print(f"  {g / 1e3:8.1f}  {frac:4.2f}  {short(before)[:50]} -> {short(after)[:50]}")
 
 
 if __name__ == "__main__":

@@ -461,6 +461,10 @@ def _nbd_notebook_bench(steps, warm, bs=16, seq=128, mode="reference", small=Fal
             device, torch.bfloat16 if device.type == "cuda" else torch.float32), flat_params=True, grad_mode="bucket",
             force_collectives=bool(force))
         graph = mode == "nbd_graph"
+        blockg = mode == "nbd_block_graphs" and device.type == "cuda"
+        if blockg:  # eager, each decoder block's forward replayed from its own HIP graph
+            from nbdistributed_amd import ops as _ops
+            _prev_bg = _ops.block_graphs(1)
         # eager: each bucket updated during backward (FlatAdamW(overlap=True): this step is
         # host-bound, the GPU has room for the update; without collectives only, and never
         # inside a graph — with collectives FlatAdamW falls back to the update in step())
@@ -483,7 +487,11 @@ def _nbd_notebook_bench(steps, warm, bs=16, seq=128, mode="reference", small=Fal
             out = run(ids[i:i + bs], mask[i:i + bs], labels[i:i + bs])
             sched.step()
             return out
-    ms, loss = _nbd_time_steps(step, steps, warm)
+    try:
+        ms, loss = _nbd_time_steps(step, steps, warm)
+    finally:
+        if mode == "nbd_block_graphs" and device.type == "cuda":
+            _ops.block_graphs(_prev_bg)
     del model, opt
     gc.collect()
     if device.type == "cuda":
@@ -513,8 +521,10 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
                                    "native Llama, fp32 master weights + torch AdamW, bf16 compute on the fused HIP path",
                "nbd": "native Llama (HIP kernels, one autograd node per block), bf16 params + fp32 master "
                        "(FlatAdamW, buckets updated during backward at world 1), nbd DDP",
+               "nbd_block_graphs": "as nbd (eager), each decoder block's forward replayed from its own HIP graph "
+                                   "(ops.block_graphs(1))",
                "nbd_graph": "as nbd, whole step captured in one HIP graph (GraphedStep)"}
-    modes = ["reference", "reference_native", "nbd"]
+    modes = ["reference", "reference_native", "nbd", "nbd_block_graphs"]
     if _graph_arms(n):  # last of the main arms (bench_ddp's _graph_arms note)
         modes.append("nbd_graph")
     for mode in modes:
