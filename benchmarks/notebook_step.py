@@ -87,12 +87,16 @@ def main():
         for i in range(a.warm):
             call(*batches[i % 8])
         torch.cuda.synchronize()
+        if os.environ.get("NBD_HOST_TIMING") == "1" and native:
+            torch.ops.nbd.host_timing(True)
         t = time.perf_counter()
         for i in range(a.steps):
             loss = call(*batches[i % 8])
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t) / a.steps * 1e3
         extra = f"  {ops.block_graphs_stats()}" if mode.startswith("nbdbg") else ""
+        if os.environ.get("NBD_HOST_TIMING") == "1" and native:
+            extra += "\n" + torch.ops.nbd.host_timing(True)
         print(f"{mode:9s} {ms:8.2f} ms/step  {a.bs / ms * 1e3:8.1f} samples/s  loss {float(loss.detach()):.4f}{extra}",
               flush=True)
         del model, opt, fwd

@@ -28,8 +28,12 @@
 #include <torch/library.h>
 
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <sstream>
 #include <functional>
 #include <map>
+#include <optional>
 #include <memory>
 #include <mutex>
 #include <tuple>
@@ -91,6 +95,37 @@ using torch::autograd::AutogradContext;
 using torch::autograd::variable_list;
 using namespace nbd::gemm;
 
+// ---- host-time breakdown of the block nodes (NBD_HOST_TIMING=1; torch.ops.nbd.host_timing) --
+namespace ht {
+enum Id { FWD, BWD, UNPACK, RMS_NEXT, SWIGLU, RMS_POST, LIN_O, ATTN, LIN_QKV, GEMM_CALL, PAIR_CALL, ATTN_CALL,
+          CLAIM, ALLOC, kN };
+const char* const kNames[kN] = {"block fwd (node)", "block bwd (node)", "  bwd: saved unpack", "  bwd: rms next",
+                                "  bwd: swiglu", "  bwd: rms post", "  bwd: linear o", "  bwd: attention",
+                                "  bwd: linear qkv", "gemm_hip call", "gemm_pair_hip call", "attn_bwd_hip call",
+                                "grad_out (claim+alloc)", "unused"};
+std::atomic<int64_t> g_ns[kN], g_cnt[kN];
+bool on() {
+  static const bool e = [] {
+    const char* v = std::getenv("NBD_HOST_TIMING");
+    return v != nullptr && v[0] == '1';
+  }();
+  return e;
+}
+struct Scope {
+  int id;
+  bool active;
+  std::chrono::steady_clock::time_point t0;
+  explicit Scope(int i) : id(i), active(on()) {
+    if (active) t0 = std::chrono::steady_clock::now();
+  }
+  ~Scope() {
+    if (!active) return;
+    g_ns[id] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    ++g_cnt[id];
+  }
+};
+}  // namespace ht
+
 struct Prod {
   bool lib;
   int64_t tile, splits;
@@ -146,8 +181,11 @@ static std::pair<Tensor, Tensor> run(const Tensor& a, const Tensor& b, bool a_km
   // a deferred split-K reduce only when it writes the destinations themselves (not a temporary
   // that is read right after)
   const defer::Scope ds(defer::want() && !tmp_acc && c_out.defined() && (epi != EPI_ROWSUM || rs_out.defined()));
-  gemm_hip(a, b, c, a_km, b_kn, bias, epi, aux, out.defined() ? optional<Tensor>(out) : c10::nullopt, p.splits,
-           p.tile, tmp_acc ? 0 : accum);
+  {
+    const ht::Scope hs(ht::GEMM_CALL);
+    gemm_hip(a, b, c, a_km, b_kn, bias, epi, aux, out.defined() ? optional<Tensor>(out) : c10::nullopt, p.splits,
+             p.tile, tmp_acc ? 0 : accum);
+  }
   if (tmp_acc) {
     if (accum & 1) { c_out.view({M, cN}).add_(c); c = c_out.view({M, cN}); }
     if (accum & 2) { rs_out.view({M}).add_(out); out = rs_out.view({M}); }
@@ -165,6 +203,7 @@ struct GradOut {
 };
 
 static GradOut grad_out(const Tensor& param, bool want, at::IntArrayRef shape, const at::TensorOptions& opt) {
+  const ht::Scope hs(ht::CLAIM);
   GradOut g;
   if (!want) return g;
   if (param.defined()) {
@@ -191,8 +230,11 @@ static std::tuple<Tensor, Tensor, Tensor> pair(const Tensor& dy, const Tensor& w
   const GradOut db = grad_out(bparam, bias_grad, {N}, dy.options());
   // every output of the split-K reduce is a bucket slice: it may be deferred (graddst.h)
   const defer::Scope ds(dw.claimed && (!bias_grad || db.claimed));
-  gemm_pair_hip(dy, w, dx, epi1, aux1, dy, x, dw.t.view({N, K}), bias_grad ? EPI_ROWSUM : EPI_NONE,
-                bias_grad ? optional<Tensor>(db.t.view({N})) : c10::nullopt, splits, dw.bit(1) | db.bit(2));
+  {
+    const ht::Scope hs(ht::PAIR_CALL);
+    gemm_pair_hip(dy, w, dx, epi1, aux1, dy, x, dw.t.view({N, K}), bias_grad ? EPI_ROWSUM : EPI_NONE,
+                  bias_grad ? optional<Tensor>(db.t.view({N})) : c10::nullopt, splits, dw.bit(1) | db.bit(2));
+  }
   return {dx, dw.done(), bias_grad ? db.done() : Tensor()};
 }
 
@@ -602,7 +644,10 @@ static Tensor attn_bwd_core(const Tensor& da, const Tensor& qkv, const Tensor& o
   Tensor dqkv = at::empty_like(qkv, at::MemoryFormat::Contiguous);
   auto [dq, dk, dv] = split_qkv(dqkv, H, Hkv);
   const Tensor dout = da.contiguous().view({B, T, H, D}).transpose(1, 2);
-  attn::attn_bwd_hip(dout, q, k, v, o, lse, true, scale, dq, dk, dv, cos, sin);
+  {
+    const ht::Scope hs(ht::ATTN_CALL);
+    attn::attn_bwd_hip(dout, q, k, v, o, lse, true, scale, dq, dk, dv, cos, sin);
+  }
   return dqkv;
 }
 
@@ -900,20 +945,43 @@ static void block_bwd(const std::vector<Tensor>& sv, const std::vector<std::vect
   const int64_t C = shape[2];
   // x2 = x1 + m, h2 = rms(x2)·γ_next
   Tensor g2, dw_next;
-  if (dh_out.defined()) std::tie(g2, dw_next) = rms_bwd_core(x_out, dh_out, dx_out, w_next, rstd2);
-  else g2 = dx_out;
+  {
+    const ht::Scope hs(ht::RMS_NEXT);
+    if (dh_out.defined()) std::tie(g2, dw_next) = rms_bwd_core(x_out, dh_out, dx_out, w_next, rstd2);
+    else g2 = dx_out;
+  }
   if (!g2.defined()) return;  // neither output reached the loss
   // m = down(swiglu(h1·W_guᵀ))
-  auto [dh1, dw_gu, dw_down] = swiglu_bwd_core(bf16c(g2).view({-1, C}), h1f, w_gu, w_down, pre, act, plans[2], true);
+  Tensor dh1, dw_gu, dw_down;
+  {
+    const ht::Scope hs(ht::SWIGLU);
+    std::tie(dh1, dw_gu, dw_down) = swiglu_bwd_core(bf16c(g2).view({-1, C}), h1f, w_gu, w_down, pre, act, plans[2], true);
+  }
   // x1 = x + y, h1 = rms(x1)·γ_post
-  auto [g1, dw_post] = rms_bwd_core(x1, dh1.view(shape), g2, w_post, rstd1);
+  Tensor g1, dw_post;
+  {
+    const ht::Scope hs(ht::RMS_POST);
+    std::tie(g1, dw_post) = rms_bwd_core(x1, dh1.view(shape), g2, w_post, rstd1);
+  }
   // y = a·W_oᵀ (+b)
-  const Tensor a2 = o.transpose(1, 2).reshape({h2.size(0), -1});
-  auto [da, dw_o, db_o] = linear_bwd_core(bf16c(g1).view({-1, C}), a2, w_o, b_o, plans[1], true,
-                                          w_o.requires_grad(), b_o.defined() && b_o.requires_grad());
-  const Tensor dqkv = attn_bwd_core(da, qkv, o, lse, H, Hkv, scale, cos, sin);
-  auto [dh, dw_qkv, db_qkv] = linear_bwd_core(dqkv.view({h2.size(0), -1}), h2, w_qkv, b_qkv, plans[0], need_h,
-                                              w_qkv.requires_grad(), b_qkv.defined() && b_qkv.requires_grad());
+  Tensor da, dw_o, db_o;
+  {
+    const ht::Scope hs(ht::LIN_O);
+    const Tensor a2 = o.transpose(1, 2).reshape({h2.size(0), -1});
+    std::tie(da, dw_o, db_o) = linear_bwd_core(bf16c(g1).view({-1, C}), a2, w_o, b_o, plans[1], true,
+                                               w_o.requires_grad(), b_o.defined() && b_o.requires_grad());
+  }
+  Tensor dqkv;
+  {
+    const ht::Scope hs(ht::ATTN);
+    dqkv = attn_bwd_core(da, qkv, o, lse, H, Hkv, scale, cos, sin);
+  }
+  Tensor dh, dw_qkv, db_qkv;
+  {
+    const ht::Scope hs(ht::LIN_QKV);
+    std::tie(dh, dw_qkv, db_qkv) = linear_bwd_core(dqkv.view({h2.size(0), -1}), h2, w_qkv, b_qkv, plans[0], need_h,
+                                                   w_qkv.requires_grad(), b_qkv.defined() && b_qkv.requires_grad());
+  }
   out[0] = need_x ? g1 : Tensor();
   out[1] = dh.defined() ? dh.view(shape) : dh;
   out[2] = dw_qkv;
@@ -1059,6 +1127,7 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
                                at::IntArrayRef plan_qkv, at::IntArrayRef plan_o, at::IntArrayRef plan_mlp, int64_t H,
                                int64_t Hkv, double scale, double eps, const optional<Tensor>& cos,
                                const optional<Tensor>& sin, bool graph) {
+    const ht::Scope hs(ht::FWD);
     at::AutoDispatchBelowADInplaceOrView guard;
     ctx->set_materialize_grads(false);
     std::vector<Tensor> save;
@@ -1092,12 +1161,15 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const ht::Scope hs_total(ht::BWD);
+    std::optional<ht::Scope> hs_unpack(std::in_place, ht::UNPACK);
     const auto sv = ctx->get_saved_variables();
     const auto plans = ctx->saved_data["plans"].to<std::vector<std::vector<int64_t>>>();
     const int64_t H = ctx->saved_data["H"].toInt(), Hkv = ctx->saved_data["Hkv"].toInt();
     const double scale = ctx->saved_data["scale"].toDouble();
     const auto shape = ctx->saved_data["shape"].toIntVector();
     const auto need = ctx->saved_data["need"].toBoolList();
+    hs_unpack.reset();
     variable_list out(20);
     if (ctx->saved_data.count("bg")) {  // graph-forwarded: the backward may be a graph too
       std::shared_ptr<bg::Graph> gr;
@@ -1138,6 +1210,19 @@ std::tuple<Tensor, Tensor> llama_block_noag(const Tensor& x, const Tensor& h, co
                                             const optional<Tensor>& sin) {
   return llama_block_fwd(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp, H, Hkv,
                          scale, eps, cos, sin, nullptr);
+}
+
+// The NBD_HOST_TIMING breakdown: per section calls and mean µs; `reset` clears the counters.
+std::string host_timing(bool reset) {
+  std::ostringstream os;
+  for (int i = 0; i < ht::kN - 1; ++i) {
+    const int64_t n = ht::g_cnt[i].load(), ns = ht::g_ns[i].load();
+    if (n == 0) continue;
+    os << ht::kNames[i] << ": " << n << " calls, " << (double)ns / n / 1e3 << " us/call\n";
+  }
+  if (reset)
+    for (int i = 0; i < ht::kN; ++i) ht::g_ns[i] = 0, ht::g_cnt[i] = 0;
+  return os.str();
 }
 
 // Per-block graphs: mode 0 off, 1 forward, 2 forward and backward, -1 query; returns the previous mode.
@@ -1198,4 +1283,5 @@ TORCH_LIBRARY_FRAGMENT(nbd, m) {
   m.def("llama_block_graphs(int mode) -> int", &nbd::ag::llama_block_graphs);
   m.def("llama_block_graphs_reset() -> ()", &nbd::ag::llama_block_graphs_reset);
   m.def("llama_block_graphs_stats() -> int[]", &nbd::ag::llama_block_graphs_stats);
+  m.def("host_timing(bool reset) -> str", &nbd::ag::host_timing);
 }
