@@ -27,6 +27,7 @@
 #include <torch/csrc/autograd/custom_function.h>
 #include <torch/library.h>
 
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
@@ -934,7 +935,7 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
 }
 
 // The block's backward into `out` (the node's 20 outputs).
-static void block_bwd(const std::vector<Tensor>& sv, const std::vector<std::vector<int64_t>>& plans, int64_t H,
+static void block_bwd(const std::vector<Tensor>& sv, const std::array<at::IntArrayRef, 3>& plans, int64_t H,
                       int64_t Hkv, double scale, const std::vector<int64_t>& shape, bool need_x, bool need_h,
                       const Tensor& dx_out, const Tensor& dh_out, variable_list& out) {
   const Tensor &h2 = sv[0], &w_qkv = sv[1], &b_qkv = sv[2], &qkv = sv[3], &o = sv[4], &lse = sv[5], &w_o = sv[6],
@@ -996,7 +997,7 @@ static void block_bwd(const std::vector<Tensor>& sv, const std::vector<std::vect
 
 // The block's backward as a HIP graph (see namespace bg); false = run it eagerly.
 static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
-                            const std::vector<std::vector<int64_t>>& plans, int64_t H, int64_t Hkv, double scale,
+                            const std::array<at::IntArrayRef, 3>& plans, int64_t H, int64_t Hkv, double scale,
                             const std::vector<int64_t>& shape, bool need_x, bool need_h, const Tensor& dx_out,
                             const Tensor& dh_out, variable_list& out) {
   using namespace bg;
@@ -1151,12 +1152,12 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
                                                plan_o, plan_mlp, H, Hkv, scale, eps, cos, sin, &save);
     }
     ctx->save_for_backward(save);
-    ctx->saved_data["plans"] = std::vector<std::vector<int64_t>>{plan_qkv.vec(), plan_o.vec(), plan_mlp.vec()};
-    ctx->saved_data["H"] = H;
-    ctx->saved_data["Hkv"] = Hkv;
-    ctx->saved_data["scale"] = scale;
-    ctx->saved_data["shape"] = h.sizes().vec();
-    ctx->saved_data["need"] = std::vector<bool>{x.requires_grad(), h.requires_grad()};
+    std::vector<int64_t> meta{H, Hkv, x.requires_grad(), h.requires_grad(), h.size(0), h.size(1), h.size(2),
+                              (int64_t)plan_qkv.size(), (int64_t)plan_o.size(), (int64_t)plan_mlp.size()};
+    meta.reserve(meta.size() + plan_qkv.size() + plan_o.size() + plan_mlp.size());
+    for (at::IntArrayRef p : {plan_qkv, plan_o, plan_mlp}) meta.insert(meta.end(), p.begin(), p.end());
+    ctx->saved_data["m"] = std::move(meta);
+    ctx->saved_data["s"] = scale;
     return {x_out, h_out};
   }
 
@@ -1164,11 +1165,16 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
     const ht::Scope hs_total(ht::BWD);
     std::optional<ht::Scope> hs_unpack(std::in_place, ht::UNPACK);
     const auto sv = ctx->get_saved_variables();
-    const auto plans = ctx->saved_data["plans"].to<std::vector<std::vector<int64_t>>>();
-    const int64_t H = ctx->saved_data["H"].toInt(), Hkv = ctx->saved_data["Hkv"].toInt();
-    const double scale = ctx->saved_data["scale"].toDouble();
-    const auto shape = ctx->saved_data["shape"].toIntVector();
-    const auto need = ctx->saved_data["need"].toBoolList();
+    // [H, Hkv, need x, need h, B, T, C, |plan_qkv|, |plan_o|, |plan_mlp|, plans...] (one IValue)
+    const std::vector<int64_t> m = ctx->saved_data["m"].toIntVector();
+    const double scale = ctx->saved_data["s"].toDouble();
+    const int64_t H = m[0], Hkv = m[1];
+    const bool need[2] = {m[2] != 0, m[3] != 0};
+    const std::vector<int64_t> shape{m[4], m[5], m[6]};
+    const int64_t* pp = m.data() + 10;
+    const std::array<at::IntArrayRef, 3> plans{at::IntArrayRef(pp, (size_t)m[7]),
+                                               at::IntArrayRef(pp + m[7], (size_t)m[8]),
+                                               at::IntArrayRef(pp + m[7] + m[8], (size_t)m[9])};
     hs_unpack.reset();
     variable_list out(20);
     if (ctx->saved_data.count("bg")) {  // graph-forwarded: the backward may be a graph too
