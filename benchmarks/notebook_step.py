@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--warm", type=int, default=5)
     ap.add_argument("--bs", type=int, default=16)
     ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--phases", action="store_true",
+                    help="eager modes: per-phase host time vs GPU time (HIP events) of forward / backward / step")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29541")
@@ -64,14 +66,28 @@ def main():
         batches = [(ids[i * a.bs:(i + 1) * a.bs], mask[i * a.bs:(i + 1) * a.bs], labels[i * a.bs:(i + 1) * a.bs])
                    for i in range(8)]
 
+        marks = []  # (--phases) per step: [(host s, event)] at start / after fwd / bwd / optimizer
+
+        def mark():
+            if a.phases and mode != "nbdgraph":
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                marks[-1].append((time.perf_counter(), e))
+
         def step(x, m, y):
+            if a.phases and mode != "nbdgraph":
+                marks.append([])
+            mark()
             if native:
                 loss = fwd(x, m, y)[0]
             else:
                 loss = fwd(input_ids=x, attention_mask=m, labels=y).loss
+            mark()
             loss.backward()
+            mark()
             opt.step()
             opt.zero_grad(set_to_none=True)
+            mark()
             return loss.detach()
 
         from nbdistributed_amd import ops
@@ -87,6 +103,7 @@ def main():
         for i in range(a.warm):
             call(*batches[i % 8])
         torch.cuda.synchronize()
+        marks.clear()
         if os.environ.get("NBD_HOST_TIMING") == "1" and native:
             torch.ops.nbd.host_timing(True)
         t = time.perf_counter()
@@ -95,6 +112,17 @@ def main():
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t) / a.steps * 1e3
         extra = f"  {ops.block_graphs_stats()}" if mode.startswith("nbdbg") else ""
+        if marks:  # host enqueue time vs GPU time per phase; GPU idle = the step's GPU span minus busy
+            names = ("forward", "backward", "optimizer")
+            host = [0.0] * 3
+            gpu = [0.0] * 3
+            for mk in marks:
+                for j in range(3):
+                    host[j] += (mk[j + 1][0] - mk[j][0]) * 1e3
+                    gpu[j] += mk[j][1].elapsed_time(mk[j + 1][1])
+            n = len(marks)
+            extra += "\n  phases (host enqueue ms / GPU span ms): " + ", ".join(
+                f"{nm} {h / n:.2f} / {g / n:.2f}" for nm, h, g in zip(names, host, gpu))
         if os.environ.get("NBD_HOST_TIMING") == "1" and native:
             extra += "\n" + torch.ops.nbd.host_timing(True)
         print(f"{mode:9s} {ms:8.2f} ms/step  {a.bs / ms * 1e3:8.1f} samples/s  loss {float(loss.detach()):.4f}{extra}",

@@ -699,7 +699,8 @@ static std::tuple<Tensor, Tensor> llama_block_fwd(const Tensor& x, const Tensor&
 // recorded, and a replay first checks that each parameter's destination (and whether it
 // accumulates, no_sync) is still the captured one — peek(), no side effects — then claims them
 // (the pass bookkeeping) and hands the slices back as the weight gradients.  One backward graph per
-// accumulate pattern; deferred reductions queued inside are flushed inside.  Without bucket slices
+// accumulate pattern; the deferred reductions of the capture are recorded and queued after each
+// replay, so they join the backward's single flush.  Without bucket slices
 // (plain training) the backward stays eager: a graph's weight gradients would be static memory
 // that AccumulateGrad keeps as .grad.
 // Same kernels, same order: bit-identical to the eager block (tests/test_gpu_block_graphs.py).
@@ -712,6 +713,7 @@ struct Bwd {
   std::vector<graddst::ClaimRecord> claims;  // in capture order
   std::vector<int> slot;                  // the node output each claim's slice is returned as
   std::vector<Tensor> warm_refs;
+  std::shared_ptr<void> deferred;          // its deferred reductions (defer::record_begin)
 };
 struct Graph {
   std::unique_ptr<at::cuda::CUDAGraph> g;
@@ -1047,6 +1049,7 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
       TORCH_CHECK(d.defined() && d.data_ptr() == c.dst && a == c.acc, "nbd: block graph claim changed");
     }
     B.g->replay();
+    defer::replay(B.deferred, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
     out[0] = need_x ? at::alias(B.g1) : Tensor();
     out[1] = need_h ? at::alias(B.dh) : Tensor();
     for (size_t k = 0; k < B.claims.size(); ++k) {
@@ -1072,12 +1075,27 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
   B->dh_in = B->dh_alias ? dh_out.variable_data() : at::empty_like(dh_out, at::MemoryFormat::Contiguous).copy_(dh_out);
   B->g = std::make_unique<at::cuda::CUDAGraph>();
   variable_list o(20);
-  graddst::record_claims(&B->claims);
-  const std::string err = capture(*B->g, [&] {
-    block_bwd(sv, plans, H, Hkv, scale, shape, need_x, need_h, B->dx_in, B->dh_in, o);
-    defer::flush();  // this node's deferred reductions go into its graph
-  });
-  graddst::record_claims(nullptr);
+  std::string err;
+  {
+    // (RAII: an exception must not leave this thread recording claims or deferred reductions)
+    struct Recording {
+      explicit Recording(std::vector<graddst::ClaimRecord>* log) {
+        graddst::record_claims(log);
+        defer::record_begin();  // this node's deferred reductions: queued after each replay
+      }
+      ~Recording() {
+        if (!ended) defer::record_end();
+        graddst::record_claims(nullptr);
+      }
+      std::shared_ptr<void> end() {
+        ended = true;
+        return defer::record_end();
+      }
+      bool ended = false;
+    } rec(&B->claims);
+    err = capture(*B->g, [&] { block_bwd(sv, plans, H, Hkv, scale, shape, need_x, need_h, B->dx_in, B->dh_in, o); });
+    B->deferred = rec.end();
+  }
   B->warm_refs = gemm::gemm_warm_take_refs();
   if (!err.empty()) G.bwd_off = true;
   TORCH_CHECK(err.empty(), "nbd: a decoder block's backward graph capture failed: ", err);
@@ -1094,6 +1112,7 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
     else B->slot[found] = kSlot[i];
   }
   B->g->replay();
+  defer::replay(B->deferred, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
   ++g_stat[3];
   if (!valid) {  // this call: private copies of the non-slice gradients; later calls: eager
     G.bwd_off = true;

@@ -217,9 +217,15 @@ void flush_locked() {
   q_bytes = 0;
 }
 
+thread_local std::vector<Item>* t_record = nullptr;  // record_begin(): queued for replays instead
+
 bool push(Item&& it, void* stream) {
   const int64_t bytes = (int64_t)it.buf.numel() * (int64_t)it.buf.element_size();
   if (bytes > max_item_bytes()) return false;
+  if (t_record != nullptr) {
+    t_record->push_back(std::move(it));
+    return true;
+  }
   std::lock_guard<std::mutex> lk(q_mu);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int dev = it.buf.get_device();
@@ -271,6 +277,28 @@ void flush() {
 int64_t pending() {
   std::lock_guard<std::mutex> lk(q_mu);
   return (int64_t)q_items.size();
+}
+
+// A captured graph's deferred reductions: recorded at capture instead of queued (their partial
+// buffers live in the graph's memory and stay allocated with the record), queued again after each
+// replay — so they still join the one flush per backward instead of a flush per graph.
+void record_begin() {
+  TORCH_CHECK(t_record == nullptr, "grad_defer: nested record");
+  t_record = new std::vector<Item>();
+}
+
+std::shared_ptr<void> record_end() {
+  std::shared_ptr<std::vector<Item>> r(t_record);
+  t_record = nullptr;
+  return r;
+}
+
+void replay(const std::shared_ptr<void>& rec, void* stream) {
+  if (!rec) return;
+  for (const Item& it : *static_cast<const std::vector<Item>*>(rec.get())) {
+    Item c = it;
+    TORCH_CHECK(push(std::move(c), stream), "grad_defer: a recorded reduction cannot be queued");
+  }
 }
 
 bool push_splitk(const at::Tensor& ws, int splits, int64_t n8, int64_t m8, int64_t slab, uint16_t* out,

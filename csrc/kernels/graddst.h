@@ -16,6 +16,7 @@
 #pragma once
 #include <ATen/ATen.h>
 
+#include <memory>
 #include <vector>
 
 namespace nbd {
@@ -70,5 +71,10 @@ bool push_colred(const at::Tensor& part, int nparts, int ld, int W, int C, uint1
                  void* stream);
 void flush();
 int64_t pending();
+// Recording (this thread, around a graph capture): pushes are kept in the record, not queued;
+// replay() queues the recorded reductions on `stream` (after each replay of that graph).
+void record_begin();
+std::shared_ptr<void> record_end();
+void replay(const std::shared_ptr<void>& rec, void* stream);
 }  // namespace defer
 }  // namespace nbd
