@@ -29,7 +29,6 @@
 #include <torch/library.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <vector>
 
 #include "nbd_common.h"
@@ -53,8 +52,7 @@ struct CopyTable {
   uint64_t aligned_mask[kMaxT / 64];  // bit t: both src[t] and dst[t] are 16 B aligned
 };
 
-// U 16-B vectors per thread in flight, CH elements per block; NTS: source loads non-temporal
-template <typename S, typename D, bool ACC, int U = kUnroll, int64_t CH = kChunk, bool NTS = false>
+template <typename S, typename D, bool ACC>
 __global__ __launch_bounds__(kThreads) void multi_copy_kernel(CopyTable tab, int nt, float scale) {
   const int chunk = blockIdx.x;
   // chunk -> tensor: coarse hint, then a short forward scan (block-uniform, scalar loads).
@@ -62,37 +60,34 @@ __global__ __launch_bounds__(kThreads) void multi_copy_kernel(CopyTable tab, int
   // the kernel on the GPT-2 gradient set (4.5 vs 5.5 TB/s single tensor, ops_bench.py).
   int t = tab.hint[chunk / tab.group_chunks];
   while (t + 1 < nt && tab.chunk_prefix[t + 1] <= chunk) ++t;
-  const int64_t begin = (int64_t)(chunk - tab.chunk_prefix[t]) * CH;
-  const int64_t end = min(begin + CH, tab.numel[t]);
+  const int64_t begin = (int64_t)(chunk - tab.chunk_prefix[t]) * kChunk;
+  const int64_t end = min(begin + kChunk, tab.numel[t]);
   const S* __restrict__ src = static_cast<const S*>(tab.src[t]);
   D* __restrict__ dst = static_cast<D*>(tab.dst[t]);
 
   if ((tab.aligned_mask[t >> 6] >> (t & 63)) & 1ull) {
     const int64_t stride = (int64_t)kThreads * 8;
     int64_t i = begin + (int64_t)threadIdx.x * 8;
-    for (; i + (U - 1) * stride + 8 <= end; i += U * stride) {
-      float v[U][8];
+    for (; i + (kUnroll - 1) * stride + 8 <= end; i += kUnroll * stride) {
+      float v[kUnroll][8];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (NTS) load8_nt<S>(src + i + u * stride, v[u]);
-        else load8<S>(src + i + u * stride, v[u]);
-      }
+      for (int u = 0; u < kUnroll; ++u) load8<S>(src + i + u * stride, v[u]);
       if (ACC) {
-        float w[U][8];
+        float w[kUnroll][8];
 #pragma unroll
-        for (int u = 0; u < U; ++u) load8<D>(dst + i + u * stride, w[u]);
+        for (int u = 0; u < kUnroll; ++u) load8<D>(dst + i + u * stride, w[u]);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < kUnroll; ++u)
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[u][j] = fmaf(v[u][j], scale, w[u][j]);
       } else {
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < kUnroll; ++u)
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[u][j] *= scale;
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < kUnroll; ++u) {
         // non-temporal only for 16-bit destinations: +3-6 % there, but fp32 NT stores measured
         // 20 % slower (unflatten 3.4 vs 4.2 TB/s); accumulate is read-modify-write: keep cached
         if (!ACC && sizeof(D) == 2) store8_nt<D>(dst + i + u * stride, v[u]);
@@ -138,45 +133,8 @@ struct CopyItem {
   int64_t numel;
 };
 
-// The accumulating copy (DDP no_sync pre-reduce into the bucket) reads two streams and writes one:
-// NBD_K3ACC_VARIANT picks its per-block shape (A/B: benchmarks/ops_bench.py nosync_prereduce_64MiB).
-struct AccShape {
-  int unroll;
-  int64_t chunk;
-  bool nt_src;
-};
-static AccShape acc_shape() {
-  static const AccShape shapes[] = {{2, 8192, false}, {4, 16384, false}, {4, 8192, false}, {2, 16384, false},
-                                    {4, 16384, true}};
-  static const int v = [] {
-    const char* e = std::getenv("NBD_K3ACC_VARIANT");
-    const int x = e != nullptr ? std::atoi(e) : 0;
-    return x >= 0 && x < 5 ? x : 0;
-  }();
-  return shapes[v];
-}
-
-template <typename S, typename D, bool ACC>
-static void launch_variant(const AccShape& sh, int chunks, const CopyTable& tab, int nt, float scale,
-                           hipStream_t stream) {
-  if (!ACC || (sh.unroll == 2 && sh.chunk == 8192 && !sh.nt_src))
-    hipLaunchKernelGGL((multi_copy_kernel<S, D, ACC>), dim3(chunks), dim3(kThreads), 0, stream, tab, nt, scale);
-  else if (sh.unroll == 4 && sh.chunk == 16384 && !sh.nt_src)
-    hipLaunchKernelGGL((multi_copy_kernel<S, D, ACC, 4, 16384>), dim3(chunks), dim3(kThreads), 0, stream, tab, nt, scale);
-  else if (sh.unroll == 4 && sh.chunk == 8192)
-    hipLaunchKernelGGL((multi_copy_kernel<S, D, ACC, 4, 8192>), dim3(chunks), dim3(kThreads), 0, stream, tab, nt, scale);
-  else if (sh.unroll == 2 && sh.chunk == 16384)
-    hipLaunchKernelGGL((multi_copy_kernel<S, D, ACC, 2, 16384>), dim3(chunks), dim3(kThreads), 0, stream, tab, nt, scale);
-  else
-    hipLaunchKernelGGL((multi_copy_kernel<S, D, ACC, 4, 16384, true>), dim3(chunks), dim3(kThreads), 0, stream, tab, nt,
-                       scale);
-  C10_HIP_KERNEL_LAUNCH_CHECK();
-}
-
 template <typename S, typename D>
 static void launch_copy(const std::vector<CopyItem>& items, float scale, bool acc, hipStream_t stream) {
-  const AccShape sh = acc ? acc_shape() : AccShape{kUnroll, kChunk, false};
-  const int64_t chunk_elems = sh.chunk;
   size_t pos = 0;
   while (pos < items.size()) {
     CopyTable tab{};
@@ -191,7 +149,7 @@ static void launch_copy(const std::vector<CopyItem>& items, float scale, bool ac
       tab.chunk_prefix[nt] = chunks;
       if (((uintptr_t)it.src % 16 == 0) && ((uintptr_t)it.dst % 16 == 0))
         tab.aligned_mask[nt >> 6] |= (1ull << (nt & 63));
-      const int64_t c = (it.numel + chunk_elems - 1) / chunk_elems;
+      const int64_t c = (it.numel + kChunk - 1) / kChunk;
       TORCH_CHECK(chunks + c < (int64_t)INT32_MAX, "nbd bucket: too many chunks in one launch");
       chunks += (int32_t)c;
       ++nt;
@@ -205,8 +163,11 @@ static void launch_copy(const std::vector<CopyItem>& items, float scale, bool ac
       while (t + 1 < nt && tab.chunk_prefix[t + 1] <= first) ++t;
       tab.hint[g] = (uint8_t)t;
     }
-    if (acc) launch_variant<S, D, true>(sh, chunks, tab, nt, scale, stream);
-    else launch_variant<S, D, false>(sh, chunks, tab, nt, scale, stream);
+    if (acc)
+      hipLaunchKernelGGL((multi_copy_kernel<S, D, true>), dim3(chunks), dim3(kThreads), 0, stream, tab, nt, scale);
+    else
+      hipLaunchKernelGGL((multi_copy_kernel<S, D, false>), dim3(chunks), dim3(kThreads), 0, stream, tab, nt, scale);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
   }
 }
 

@@ -281,6 +281,10 @@ class LlamaModel(nn.Module):
             x, h = ops.add_rms_norm(x, a, layer.post_attention_layernorm.weight, c.rms_norm_eps)
             m = layer.mlp(h)
             x, h = ops.add_rms_norm(x, m, nxt.weight, c.rms_norm_eps)
+        if h.is_cuda and ops.native_available() and ops.block_graphs():
+            # per-block graphs: the last block's output is its graph's static memory — the model's
+            # output is the caller's to keep
+            h = h.clone()
         return h
 
     def _forward_cast(self, input_ids, cd, cos, sin):
@@ -315,6 +319,8 @@ class LlamaModel(nn.Module):
                 x, h = ops.add_rms_norm(x, ops.mlp_swiglu(h, w_gu, w_down), w_next, c.rms_norm_eps)
             else:
                 x, h = r
+        if ops.block_graphs():  # (see forward)
+            h = h.clone()
         return h
 
 
