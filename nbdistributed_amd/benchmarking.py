@@ -468,7 +468,9 @@ def _nbd_notebook_bench(steps, warm, bs=16, seq=128, mode="reference", small=Fal
         # eager: each bucket updated during backward (FlatAdamW(overlap=True): this step is
         # host-bound, the GPU has room for the update; without collectives only, and never
         # inside a graph — with collectives FlatAdamW falls back to the update in step())
-        opt = _FlatAdamW(model, lr=2e-5, capturable=graph, overlap=not graph)
+        # (block graphs: the update after backward — measured faster than the side-stream overlap
+        # with them, docs/FINDINGS.md §30)
+        opt = _FlatAdamW(model, lr=2e-5, capturable=graph, overlap=not graph and not blockg)
         sched = get_linear_schedule_with_warmup(opt, 100, 3 * (n // (bs * world_size)))
         sl = slice(rank * (n // world_size), (rank + 1) * (n // world_size))
         ids, mask, labels = ids[sl].to(device), mask[sl].to(device), labels[sl].to(device)
@@ -522,7 +524,7 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
                "nbd": "native Llama (HIP kernels, one autograd node per block), bf16 params + fp32 master "
                        "(FlatAdamW, buckets updated during backward at world 1), nbd DDP",
                "nbd_block_graphs": "as nbd (eager), each decoder block's forward replayed from its own HIP graph "
-                                   "(ops.block_graphs(1))",
+                                   "(ops.block_graphs(1)); FlatAdamW update after backward (no overlap)",
                "nbd_graph": "as nbd, whole step captured in one HIP graph (GraphedStep)"}
     modes = ["reference", "reference_native", "nbd", "nbd_block_graphs"]
     if _graph_arms(n):  # last of the main arms (bench_ddp's _graph_arms note)
