@@ -526,7 +526,9 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
                "nbd_block_graphs": "as nbd (eager), each decoder block's forward replayed from its own HIP graph "
                                    "(ops.block_graphs(1)); FlatAdamW update after backward (no overlap)",
                "nbd_graph": "as nbd, whole step captured in one HIP graph (GraphedStep)"}
-    modes = ["reference", "reference_native", "nbd", "nbd_block_graphs"]
+    modes = ["reference", "reference_native", "nbd"]
+    if n == 1:  # (the per-block graph arm: an eager-step variant, timed where the GPU is ours alone)
+        modes.append("nbd_block_graphs")
     if _graph_arms(n):  # last of the main arms (bench_ddp's _graph_arms note)
         modes.append("nbd_graph")
     for mode in modes:
