@@ -693,7 +693,9 @@ static std::tuple<Tensor, Tensor> llama_block_fwd(const Tensor& x, const Tensor&
 //    before backward, retain_graph) runs eagerly, as does any call whose weights, RoPE tables or
 //    aliased input moved, or that comes inside another capture (graphs.GraphedStep);
 //  * the returned tensors alias that memory: they hold this pass's values until the block's next
-//    replay (a caller keeping block outputs across steps must clone them).
+//    replay (a caller keeping block outputs across steps must clone them);
+//  * each (block, shape) keeps its activations allocated between steps: at most 4 shapes per block
+//    are graphed, further sequence lengths run eagerly.
 // The backward of a graph-forwarded block is captured too (its first graphed backward) when every
 // weight gradient goes to a DDP bucket slice (graddst.h): the claims made during the capture are
 // recorded, and a replay first checks that each parameter's destination (and whether it
@@ -881,6 +883,19 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
     } else if (++s.captures > 4) {
       s.off = true;
       return nullptr;
+    } else {
+      // each (block, shape) keeps its activations: a model fed many sequence lengths (dynamic
+      // padding) would grow without bound — at most kMaxShapes graphs per block, the rest eager
+      constexpr int kMaxShapes = 4;
+      int shapes = 0;
+      for (const auto& kv : g_slots)
+        shapes += std::get<0>(kv.first) == std::get<0>(key) && std::get<3>(kv.first) == std::get<3>(key) &&
+                  kv.second.g != nullptr;
+      if (shapes >= kMaxShapes) {
+        s.off = true;
+        ++g_stat[2];
+        return nullptr;
+      }
     }
   }
   if (gr) {

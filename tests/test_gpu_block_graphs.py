@@ -171,3 +171,31 @@ def test_block_graphs_inside_whole_step_capture(dev):
     l1, p1 = run(True)
     assert len(set(l0.tolist())) > 1  # the parameters move between replays
     assert torch.equal(l0, l1) and torch.equal(p0, p1)
+
+
+def test_block_graphs_shape_cap(dev):
+    """Each (block, shape) keeps its activations: past 4 sequence lengths a block runs eagerly."""
+    base = _model(dev, layers=1, seed=9)
+    g = torch.Generator(device=dev).manual_seed(2)
+    batches = [torch.randint(1, 49152, (2, T), device=dev, generator=g) for T in (128, 256, 384, 512, 640)]
+    lab = torch.tensor([0, 1], device=dev)
+
+    def run(mode):
+        ops.block_graphs(mode)
+        ops.block_graphs_reset()
+        m = copy.deepcopy(base)
+        out = []
+        for ids in batches:
+            for _ in range(3):
+                for p in m.parameters():
+                    p.grad = None
+                loss = m(ids, torch.ones_like(ids), lab)[0]
+                loss.backward()
+            out.append(torch.cat([loss.detach().view(1)] + [p.grad.float().flatten() for p in m.parameters()]))
+        torch.cuda.synchronize()
+        return out, ops.block_graphs_stats()["live"]
+
+    o0, _ = run(0)
+    o1, live = run(1)
+    assert live == 4, live
+    assert all(torch.equal(a, b) for a, b in zip(o0, o1))
