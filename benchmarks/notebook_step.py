@@ -10,6 +10,9 @@ nbd       : native Llama (models/llama.py, HIP kernels), bf16 flat DDP + FlatAda
 nbdgraph  : nbd captured once into a HIP graph (nbdistributed_amd.graphs) and replayed
 nbdbg     : nbd eager with one HIP graph per decoder block's forward (ops.block_graphs(1))
 nbdbg2    : nbdbg with each block's backward graphed too (ops.block_graphs(2))
+hfnative  : HF model + the one-line swap nbd.models.native(model) (fp32 master weights, bf16
+            compute), torch AdamW — the notebook's loop minus accelerate's wrappers
+hfnativebg: hfnative with per-block forward graphs (ops.block_graphs(1))
 """
 from __future__ import annotations
 
@@ -60,6 +63,12 @@ def main():
             model = model.to(dev)
             opt = torch.optim.AdamW(model.parameters(), lr=2e-5)
             fwd = model
+        elif mode.startswith("hfnative"):
+            from nbdistributed_amd.models import native as _native
+
+            model = _native(model.to(dev))
+            opt = torch.optim.AdamW(model.parameters(), lr=2e-5)
+            fwd = model
         else:
             fwd = NbdDDP(model.to(dev, torch.bfloat16), flat_params=True, grad_mode="bucket")
             opt = FlatAdamW(fwd, lr=2e-5, capturable=mode == "nbdgraph")  # overlap: NBD_ADAMW_OVERLAP
@@ -92,8 +101,8 @@ def main():
 
         from nbdistributed_amd import ops
 
-        if native:
-            ops.block_graphs({"nbdbg": 1, "nbdbg2": 2}.get(mode, 0))
+        if native or mode.startswith("hfnative"):
+            ops.block_graphs({"nbdbg": 1, "nbdbg2": 2, "hfnativebg": 1}.get(mode, 0))
         if mode == "nbdgraph":
             from nbdistributed_amd.graphs import GraphedStep
 
@@ -111,7 +120,7 @@ def main():
             loss = call(*batches[i % 8])
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t) / a.steps * 1e3
-        extra = f"  {ops.block_graphs_stats()}" if mode.startswith("nbdbg") else ""
+        extra = f"  {ops.block_graphs_stats()}" if mode.startswith("nbdbg") or mode == "hfnativebg" else ""
         if marks:  # host enqueue time vs GPU time per phase; GPU idle = the step's GPU span minus busy
             names = ("forward", "backward", "optimizer")
             host = [0.0] * 3

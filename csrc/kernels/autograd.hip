@@ -886,12 +886,16 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
     } else {
       // each (block, shape) keeps its activations: a model fed many sequence lengths (dynamic
       // padding) would grow without bound — at most kMaxShapes graphs per block, the rest eager
-      constexpr int kMaxShapes = 4;
-      int shapes = 0;
-      for (const auto& kv : g_slots)
+      // (and at most kMaxLive graphs in all: weights that move every step — per-forward casts
+      // landing at new addresses — must not capture without bound either)
+      constexpr int kMaxShapes = 4, kMaxLive = 512;
+      int shapes = 0, live = 0;
+      for (const auto& kv : g_slots) {
+        live += kv.second.g != nullptr;
         shapes += std::get<0>(kv.first) == std::get<0>(key) && std::get<3>(kv.first) == std::get<3>(key) &&
                   kv.second.g != nullptr;
-      if (shapes >= kMaxShapes) {
+      }
+      if (shapes >= kMaxShapes || live >= kMaxLive) {
         s.off = true;
         ++g_stat[2];
         return nullptr;
@@ -1235,7 +1239,8 @@ std::tuple<Tensor, Tensor> llama_block_ag(const Tensor& x, const Tensor& h, cons
                                           const Tensor& w_next, at::IntArrayRef plan_qkv, at::IntArrayRef plan_o,
                                           at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv, double scale, double eps,
                                           const optional<Tensor>& cos, const optional<Tensor>& sin) {
-  const bool graph = bg::enabled() && c10::GradMode::is_enabled() && x.is_cuda();
+  // (parameters only: per-forward weight casts — models.native() — land at new addresses)
+  const bool graph = bg::enabled() && c10::GradMode::is_enabled() && x.is_cuda() && w_qkv.is_leaf();
   auto r = LlamaBlockFn::apply(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp,
                                H, Hkv, scale, eps, cos, sin, graph);
   return {r[0], r[1]};
