@@ -13,6 +13,7 @@ nbdbg2    : nbdbg with each block's backward graphed too (ops.block_graphs(2))
 hfnative  : HF model + the one-line swap nbd.models.native(model) (fp32 master weights, bf16
             compute), torch AdamW — the notebook's loop minus accelerate's wrappers
 hfnativebg: hfnative with per-block forward graphs (ops.block_graphs(1))
+hfnativefused: hfnative with torch.optim.AdamW(..., fused=True)
 """
 from __future__ import annotations
 
@@ -67,7 +68,7 @@ def main():
             from nbdistributed_amd.models import native as _native
 
             model = _native(model.to(dev))
-            opt = torch.optim.AdamW(model.parameters(), lr=2e-5)
+            opt = torch.optim.AdamW(model.parameters(), lr=2e-5, fused=mode == "hfnativefused")
             fwd = model
         else:
             fwd = NbdDDP(model.to(dev, torch.bfloat16), flat_params=True, grad_mode="bucket")

@@ -20,6 +20,7 @@ supported).
 """
 from __future__ import annotations
 
+import os
 import weakref
 from dataclasses import dataclass
 from typing import Any, Dict, NamedTuple, Optional
@@ -503,14 +504,58 @@ def from_hf(hf_model, compute_dtype: Optional[torch.dtype] = None) -> nn.Module:
     return m
 
 
-def native(hf_model, compute_dtype: Optional[torch.dtype] = torch.bfloat16) -> nn.Module:
+def native(hf_model, compute_dtype: Optional[torch.dtype] = torch.bfloat16, fused_optimizer: bool = True) -> nn.Module:
     """The one-line swap for a notebook written against HF transformers: call it on the HF
     Llama / SmolLM2 / Qwen2 / Mistral model BEFORE creating the optimizer and
     ``accelerator.prepare``.  The returned module takes the same keyword arguments, returns
     outputs with ``.loss`` / ``.logits``, keeps the HF parameters' dtype (fp32 master weights for
     ``torch.optim.AdamW``) and computes in ``compute_dtype`` on the fused HIP path (bf16 by
-    default: the same mixed-precision recipe as ``Accelerator(mixed_precision="bf16")``)."""
-    return from_hf(hf_model, compute_dtype=compute_dtype)
+    default: the same mixed-precision recipe as ``Accelerator(mixed_precision="bf16")``).
+
+    ``fused_optimizer``: a ``torch.optim.AdamW`` / ``Adam`` later built on exactly this model's GPU
+    parameters, with neither ``fused`` nor ``foreach`` given, uses torch's fused (one kernel per
+    step) implementation instead of the multi-tensor default — the same update, and on the
+    notebook's SmolLM2 step the default's optimizer phase is 3.0-5.8 ms of GPU time against
+    0.9 ms fused (docs/FINDINGS.md §30).  Other optimizers and parameters are untouched;
+    ``NBD_NATIVE_FUSED_OPTIM=0`` or ``fused_optimizer=False`` keeps torch's default."""
+    m = from_hf(hf_model, compute_dtype=compute_dtype)
+    if fused_optimizer and os.environ.get("NBD_NATIVE_FUSED_OPTIM", "1") != "0":
+        for p in m.parameters():
+            p._nbd_native_fused = True
+        _install_fused_default()
+    return m
+
+
+_FUSED_PATCHED = False
+
+
+def _install_fused_default() -> None:
+    """Wrap ``torch.optim.AdamW.__init__`` / ``Adam.__init__`` once: when ``fused`` and
+    ``foreach`` are both unspecified and every parameter is a CUDA floating-point parameter of a
+    ``native()`` model, pass ``fused=True``."""
+    global _FUSED_PATCHED
+    if _FUSED_PATCHED:
+        return
+    import functools
+
+    def wrap(cls):
+        orig = cls.__init__
+
+        @functools.wraps(orig)
+        def __init__(self, params, *args, **kwargs):
+            if kwargs.get("fused") is None and kwargs.get("foreach") is None:
+                params = list(params)
+                flat = [p for g in params for p in (g["params"] if isinstance(g, dict) else [g])]
+                if flat and all(isinstance(p, torch.Tensor) and getattr(p, "_nbd_native_fused", False) and p.is_cuda
+                                and p.is_floating_point() for p in flat):
+                    kwargs["fused"] = True
+            orig(self, params, *args, **kwargs)
+
+        cls.__init__ = __init__
+
+    wrap(torch.optim.AdamW)
+    wrap(torch.optim.Adam)
+    _FUSED_PATCHED = True
 
 
 __all__ = ["LlamaConfig", "LlamaModel", "LlamaForSequenceClassification", "LlamaForCausalLM", "RMSNorm",

@@ -213,3 +213,21 @@ def test_native_swap_bf16_compute_fp32_master(dev):
     opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
     opt.step()
     assert not torch.equal(w0, m.model.layers[0].mlp.down_proj.weight)
+    # native(): torch AdamW on exactly these parameters defaults to the fused implementation, and
+    # its update equals the multi-tensor one (same math; fp32)
+    assert opt.defaults["fused"] is True
+    state = {n: p.detach().clone() for n, p in m.named_parameters()}
+    gr = {n: p.grad.clone() for n, p in m.named_parameters()}
+    res = []
+    for kw in ({}, {"foreach": True}):
+        with torch.no_grad():
+            for n, p in m.named_parameters():
+                p.copy_(state[n])
+                p.grad = gr[n].clone()
+        o = torch.optim.AdamW(m.parameters(), lr=1e-3, **kw)
+        assert o.defaults["fused"] is (True if not kw else None)
+        o.step()
+        res.append(torch.cat([p.detach().flatten() for p in m.parameters()]))
+    assert _rel(res[0], res[1]) < 1e-5
+    # other parameters keep torch's default
+    assert torch.optim.AdamW([torch.nn.Parameter(torch.randn(4, device=dev))], lr=1e-3).defaults["fused"] is None
