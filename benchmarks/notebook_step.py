@@ -14,6 +14,7 @@ hfnative  : HF model + the one-line swap nbd.models.native(model) (fp32 master w
             compute), torch AdamW — the notebook's loop minus accelerate's wrappers
 hfnativebg: hfnative with per-block forward graphs (ops.block_graphs(1))
 hfnativefused: hfnative with torch.optim.AdamW(..., fused=True)
+hfnativedefault: hfnative with the notebook's optimizer line unchanged (native() makes it fused)
 """
 from __future__ import annotations
 
@@ -68,7 +69,11 @@ def main():
             from nbdistributed_amd.models import native as _native
 
             model = _native(model.to(dev))
-            opt = torch.optim.AdamW(model.parameters(), lr=2e-5, fused=mode == "hfnativefused")
+            if mode == "hfnativedefault":  # the notebook's line as written (native() picks fused)
+                opt = torch.optim.AdamW(model.parameters(), lr=2e-5)
+            else:
+                opt = torch.optim.AdamW(model.parameters(), lr=2e-5, fused=mode == "hfnativefused")
+            print(f"{mode}: AdamW fused={opt.defaults.get('fused')}", flush=True)
             fwd = model
         else:
             fwd = NbdDDP(model.to(dev, torch.bfloat16), flat_params=True, grad_mode="bucket")
