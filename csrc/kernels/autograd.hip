@@ -1033,14 +1033,16 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
   const Tensor* ps[] = {&sv[1], &sv[2], &sv[6], &sv[7], &sv[9], &sv[12], &sv[13], &sv[17]};
   Tensor dst[8];
   bool acc[8] = {};
-  int mask = 0;
+  int mask = 0, wants = 0;
   for (int i = 0; i < 8; ++i) {
     if (!ps[i]->defined() || !ps[i]->requires_grad()) continue;
     dst[i] = graddst::peek(*ps[i], acc[i]);
     if (!dst[i].defined()) return false;
     mask |= (int)acc[i] << i;
+    wants |= 1 << i;
   }
-  const int key = mask | (int)need_x << 8 | (int)need_h << 9 | (int)has_dx << 10;
+  // one graph per (accumulate pattern, which parameters want gradients, which inputs do)
+  const int key = mask | (int)need_x << 8 | (int)need_h << 9 | (int)has_dx << 10 | wants << 11;
   auto param_index = [&](const c10::TensorImpl* impl) {
     for (int i = 0; i < 8; ++i)
       if (ps[i]->defined() && ps[i]->unsafeGetTensorImpl() == impl) return i;
@@ -1053,7 +1055,7 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
               (!B.dh_alias || dh_out.data_ptr() == B.dh_in.data_ptr());
     for (const auto& c : B.claims) {
       const int i = param_index(c.param);
-      ok = ok && i >= 0 && dst[i].data_ptr() == c.dst && acc[i] == c.acc;
+      ok = ok && i >= 0 && dst[i].defined() && dst[i].data_ptr() == c.dst && acc[i] == c.acc;
     }
     if (!ok) {
       G.bwd.erase(it);  // destinations moved: capture anew next time
