@@ -79,6 +79,8 @@ std::tuple<at::Tensor, at::Tensor> rms_bwd_into(const at::Tensor& x, const at::T
 namespace gemm {
 std::vector<at::Tensor> gemm_warm_take_refs();
 }  // namespace gemm
+void bucket_flatten_hip(at::TensorList tensors, const at::Tensor& bucket, at::IntArrayRef offsets, double scale,
+                        bool accumulate);
 namespace attn {
 std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                                 bool causal, double scale, const c10::optional<at::Tensor>& rope_cos,
@@ -1296,6 +1298,108 @@ std::vector<int64_t> llama_block_graphs_stats() {
           bg::g_stat[3].load(), bg::g_stat[4].load(), bg::g_stat[5].load()};
 }
 
+// ------------------------------------------------------- fp32 master weights, bf16 compute
+// One decoder layer's parameters cast into one flat compute-dtype buffer by one bucket_flatten
+// pass, and their gradients cast back into one flat fp32 buffer by another (models/llama.py
+// _CastGroup, the Python form of the same node): `models.native()` runs one per layer per
+// forward, and the Python autograd.Function around it was ≈20-30 µs of host time per call and
+// direction on a host-bound loop (docs/FINDINGS.md §30).
+static std::pair<std::vector<int64_t>, int64_t> flat_offsets(const std::vector<Tensor>& ts) {
+  std::vector<int64_t> offs;
+  offs.reserve(ts.size());
+  int64_t pos = 0;
+  for (const Tensor& t : ts) {
+    offs.push_back(pos);
+    pos += (t.numel() + 63) / 64 * 64;  // 64-element starts: every slice on the 16-B vector path
+  }
+  return {offs, pos};
+}
+
+static std::vector<Tensor> slices(const Tensor& buf, const std::vector<int64_t>& offs,
+                                  const std::vector<std::vector<int64_t>>& shapes) {
+  std::vector<Tensor> out;
+  out.reserve(offs.size());
+  for (size_t i = 0; i < offs.size(); ++i) {
+    int64_t n = 1;
+    for (int64_t d : shapes[i]) n *= d;
+    out.push_back(buf.narrow(0, offs[i], n).view(shapes[i]));
+  }
+  return out;
+}
+
+struct CastGroupFn : public torch::autograd::Function<CastGroupFn> {
+  static variable_list forward(AutogradContext* ctx, const variable_list& ps, int64_t dtype) {
+    at::AutoDispatchBelowADInplaceOrView guard;
+    TORCH_CHECK(!ps.empty(), "cast_group: no tensors");
+    auto [offs, total] = flat_offsets(ps);
+    std::vector<std::vector<int64_t>> shapes;
+    for (const Tensor& p : ps) {
+      TORCH_CHECK(p.is_cuda() && p.device() == ps[0].device() && p.scalar_type() == ps[0].scalar_type(),
+                  "cast_group: one device and dtype");
+      shapes.push_back(p.sizes().vec());
+    }
+    const Tensor buf = at::empty({total}, ps[0].options().dtype((at::ScalarType)dtype));
+    std::vector<Tensor> src;
+    src.reserve(ps.size());
+    for (const Tensor& p : ps) src.push_back(p.contiguous());
+    bucket_flatten_hip(src, buf, offs, 1.0, false);
+    std::vector<int64_t> flat_shapes;
+    for (const auto& sh : shapes) {
+      flat_shapes.push_back((int64_t)sh.size());
+      flat_shapes.insert(flat_shapes.end(), sh.begin(), sh.end());
+    }
+    ctx->saved_data["offs"] = offs;
+    ctx->saved_data["shapes"] = flat_shapes;
+    ctx->saved_data["meta"] = std::vector<int64_t>{total, (int64_t)ps[0].scalar_type()};
+    return slices(buf, offs, shapes);
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list gs) {
+    const auto offs = ctx->saved_data["offs"].toIntVector();
+    const auto flat = ctx->saved_data["shapes"].toIntVector();
+    const auto meta = ctx->saved_data["meta"].toIntVector();
+    std::vector<std::vector<int64_t>> shapes;
+    for (size_t i = 0; i < flat.size();) {
+      const int64_t r = flat[i];
+      shapes.emplace_back(flat.begin() + (int64_t)i + 1, flat.begin() + (int64_t)i + 1 + r);
+      i += (size_t)r + 1;
+    }
+    variable_list out(gs.size() + 1);  // (the dtype argument: none)
+    std::vector<Tensor> have;
+    std::vector<int64_t> have_offs;
+    for (size_t i = 0; i < gs.size(); ++i)
+      if (gs[i].defined()) {
+        have.push_back(gs[i].contiguous());
+        have_offs.push_back(offs[i]);
+      }
+    if (have.empty()) return out;
+    const Tensor buf = at::empty({meta[0]}, have[0].options().dtype((at::ScalarType)meta[1]));
+    bucket_flatten_hip(have, buf, have_offs, 1.0, false);
+    const auto views = slices(buf, offs, shapes);
+    for (size_t i = 0; i < gs.size(); ++i)
+      if (gs[i].defined()) out[i] = views[i];
+    return out;
+  }
+};
+
+std::vector<Tensor> cast_group_ag(at::TensorList ps, int64_t dtype) {
+  return CastGroupFn::apply(ps.vec(), dtype);
+}
+
+std::vector<Tensor> cast_group_noag(at::TensorList ps, int64_t dtype) {
+  const std::vector<Tensor> v = ps.vec();
+  auto [offs, total] = flat_offsets(v);
+  std::vector<std::vector<int64_t>> shapes;
+  std::vector<Tensor> src;
+  for (const Tensor& p : v) {
+    shapes.push_back(p.sizes().vec());
+    src.push_back(p.contiguous());
+  }
+  const Tensor buf = at::empty({total}, v[0].options().dtype((at::ScalarType)dtype));
+  bucket_flatten_hip(src, buf, offs, 1.0, false);
+  return slices(buf, offs, shapes);
+}
+
 }  // namespace ag
 }  // namespace nbd
 
@@ -1311,6 +1415,7 @@ TORCH_LIBRARY_IMPL(nbd, Autograd, m) {
   m.impl("add_layer_norm_ag", &nbd::ag::add_layer_norm_ag);
   m.impl("attn_qkv_ag", &nbd::ag::attn_qkv_ag);
   m.impl("llama_block_ag", &nbd::ag::llama_block_ag);
+  m.impl("cast_group_ag", &nbd::ag::cast_group_ag);
 }
 
 TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
@@ -1323,6 +1428,7 @@ TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
   m.impl("mlp_gelu_ag", &nbd::ag::mlp_gelu_noag);
   m.impl("mlp_swiglu_ag", &nbd::ag::mlp_swiglu_noag);
   m.impl("llama_block_ag", &nbd::ag::llama_block_noag);
+  m.impl("cast_group_ag", &nbd::ag::cast_group_noag);
 }
 
 // bookkeeping only (no device work): catch-all kernels

@@ -147,6 +147,20 @@ class _CastGroup(torch.autograd.Function):
         return (None, *out)
 
 
+_SCALAR_TYPE = {torch.float16: 5, torch.float32: 6, torch.bfloat16: 15}  # c10::ScalarType codes
+NATIVE_CAST = os.environ.get("NBD_NATIVE_CAST", "1") != "0"
+
+
+def cast_group(dtype, ps):
+    """``ps`` cast to ``dtype`` through one flat buffer, gradients cast back the same way: the C++
+    node (``torch.ops.nbd.cast_group_ag``, csrc/kernels/autograd.hip ``CastGroupFn``) on the GPU,
+    the Python ``_CastGroup`` otherwise (``NBD_NATIVE_CAST=0``: always)."""
+    ps = list(ps)
+    if NATIVE_CAST and ps[0].is_cuda and dtype in _SCALAR_TYPE and ops.native_available():
+        return tuple(torch.ops.nbd.cast_group_ag(ps, _SCALAR_TYPE[dtype]))
+    return _CastGroup.apply(dtype, *ps)
+
+
 class RMSNorm(nn.Module):
     def __init__(self, n: int, eps: float):
         super().__init__()
@@ -294,7 +308,7 @@ class LlamaModel(nn.Module):
         cast exactly once — go through one fused cast (``_CastGroup``)."""
         c = self.config
         x = ops.embedding(input_ids, self.embed_tokens.weight).to(cd)
-        (w_in,) = _CastGroup.apply(cd, self.layers[0].input_layernorm.weight)
+        (w_in,) = cast_group(cd, [self.layers[0].input_layernorm.weight])
         h = ops.rms_norm(x, w_in, c.rms_norm_eps)
         for i, layer in enumerate(self.layers):
             nxt = self.layers[i + 1].input_layernorm if i + 1 < len(self.layers) else self.norm
@@ -305,7 +319,7 @@ class LlamaModel(nn.Module):
                 ps.append(at.qkv_proj.bias)
             if at.o_proj.bias is not None:
                 ps.append(at.o_proj.bias)
-            ws = _CastGroup.apply(cd, *ps)
+            ws = cast_group(cd, ps)
             w_qkv, w_o, w_post, w_gu, w_down, w_next = ws[:6]
             extra = list(ws[6:])
             b_qkv = extra.pop(0) if at.qkv_proj.bias is not None else None

@@ -231,3 +231,26 @@ def test_native_swap_bf16_compute_fp32_master(dev):
     assert _rel(res[0], res[1]) < 1e-5
     # other parameters keep torch's default
     assert torch.optim.AdamW([torch.nn.Parameter(torch.randn(4, device=dev))], lr=1e-3).defaults["fused"] is None
+
+
+def test_cast_group_native_matches_python(dev):
+    """The C++ cast node (models.native's per-layer bf16 casts) against the Python _CastGroup:
+    identical values forward and identical fp32 gradients backward, odd sizes included."""
+    from nbdistributed_amd.models.llama import _CastGroup, cast_group
+
+    g = torch.Generator(device=dev).manual_seed(4)
+    shapes = [(576, 960), (576,), (7, 13), (1,), (3, 5, 9)]
+    ps = [torch.randn(s, device=dev, generator=g, requires_grad=True) for s in shapes]
+    gs = [torch.randn(s, device=dev, generator=g).to(torch.bfloat16) for s in shapes]
+    outs_c = cast_group(torch.bfloat16, ps)
+    outs_p = _CastGroup.apply(torch.bfloat16, *ps)
+    assert all(a.dtype == torch.bfloat16 and a.shape == b.shape and torch.equal(a, b) for a, b in zip(outs_c, outs_p))
+    gc = torch.autograd.grad(outs_c, ps, gs)
+    gp = torch.autograd.grad(outs_p, ps, gs)
+    assert all(a.dtype == torch.float32 and torch.equal(a, b) for a, b in zip(gc, gp))
+    # a gradient for only some outputs
+    gc2 = torch.autograd.grad(outs_c[0].float().sum() + outs_c[3].float().sum(), ps, allow_unused=True)
+    assert gc2[1] is None and gc2[0] is not None and torch.equal(gc2[3], torch.ones(1, device=dev))
+    with torch.inference_mode():
+        inf = cast_group(torch.bfloat16, [p.detach() for p in ps])
+    assert all(torch.equal(a, b) for a, b in zip(inf, outs_p))
