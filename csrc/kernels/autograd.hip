@@ -1237,14 +1237,19 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
   }
 };
 
+namespace castbuf {
+bool kept(const Tensor& t);  // (below, with the cast node)
+}  // namespace castbuf
+
 std::tuple<Tensor, Tensor> llama_block_ag(const Tensor& x, const Tensor& h, const Tensor& w_qkv,
                                           const optional<Tensor>& b_qkv, const Tensor& w_o, const optional<Tensor>& b_o,
                                           const Tensor& w_post, const Tensor& w_gu, const Tensor& w_down,
                                           const Tensor& w_next, at::IntArrayRef plan_qkv, at::IntArrayRef plan_o,
                                           at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv, double scale, double eps,
                                           const optional<Tensor>& cos, const optional<Tensor>& sin) {
-  // (parameters only: per-forward weight casts — models.native() — land at new addresses)
-  const bool graph = bg::enabled() && c10::GradMode::is_enabled() && x.is_cuda() && w_qkv.is_leaf();
+  // (parameters, or weights cast into a kept buffer — models.native(): stable addresses)
+  const bool graph = bg::enabled() && c10::GradMode::is_enabled() && x.is_cuda() &&
+                     (w_qkv.is_leaf() || castbuf::kept(w_qkv));
   auto r = LlamaBlockFn::apply(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp,
                                H, Hkv, scale, eps, cos, sin, graph);
   return {r[0], r[1]};
@@ -1327,18 +1332,68 @@ static std::vector<Tensor> slices(const Tensor& buf, const std::vector<int64_t>&
   return out;
 }
 
+// The cast buffer of a parameter group is kept and rewritten by the next forward when nothing
+// else holds it any more (the previous pass's autograd graph has released its saved weights):
+// the compute-dtype weights then stay at the same addresses from step to step, which is what lets
+// the per-block graphs (namespace bg) run on the fp32-master path too.  Still held (a second
+// forward before backward): a fresh buffer, as before.
+namespace castbuf {
+struct Entry {
+  c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl> first;  // the group's first parameter (validates the key)
+  Tensor buf;
+};
+std::mutex g_mu;
+std::unordered_map<const c10::TensorImpl*, Entry> g_bufs;
+std::unordered_map<const void*, int> g_addrs;  // data pointers of the kept buffers
+
+Tensor get(const Tensor& first, int64_t total, const at::TensorOptions& opt) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_bufs.size() > 4096) {  // forget the groups of dead parameters
+    for (auto it = g_bufs.begin(); it != g_bufs.end();) {
+      if (it->second.first.expired()) {
+        g_addrs.erase(it->second.buf.data_ptr());
+        it = g_bufs.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  auto it = g_bufs.find(first.unsafeGetTensorImpl());
+  if (it != g_bufs.end() && !it->second.first.expired() && it->second.buf.numel() == total &&
+      it->second.buf.scalar_type() == opt.dtype().toScalarType() && it->second.buf.device() == opt.device() &&
+      it->second.buf.storage().use_count() == 1)
+    return it->second.buf;
+  Tensor buf = at::empty({total}, opt);
+  if (it != g_bufs.end()) g_addrs.erase(it->second.buf.data_ptr());
+  g_bufs.insert_or_assign(first.unsafeGetTensorImpl(),
+                          Entry{c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>(
+                                    first.getIntrusivePtr()),
+                                buf});
+  g_addrs[buf.data_ptr()] = 1;
+  return buf;
+}
+
+// t lives in a kept cast buffer (its address is stable across steps)
+bool kept(const Tensor& t) {
+  if (!t.has_storage()) return false;
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_addrs.count(t.storage().data()) != 0;
+}
+}  // namespace castbuf
+
 struct CastGroupFn : public torch::autograd::Function<CastGroupFn> {
-  static variable_list forward(AutogradContext* ctx, const variable_list& ps, int64_t dtype) {
+  // (ps as a TensorList: only that form counts its elements as the node's inputs)
+  static variable_list forward(AutogradContext* ctx, at::TensorList ps, int64_t dtype) {
     at::AutoDispatchBelowADInplaceOrView guard;
     TORCH_CHECK(!ps.empty(), "cast_group: no tensors");
-    auto [offs, total] = flat_offsets(ps);
+    auto [offs, total] = flat_offsets(ps.vec());
     std::vector<std::vector<int64_t>> shapes;
     for (const Tensor& p : ps) {
       TORCH_CHECK(p.is_cuda() && p.device() == ps[0].device() && p.scalar_type() == ps[0].scalar_type(),
                   "cast_group: one device and dtype");
       shapes.push_back(p.sizes().vec());
     }
-    const Tensor buf = at::empty({total}, ps[0].options().dtype((at::ScalarType)dtype));
+    const Tensor buf = castbuf::get(ps[0], total, ps[0].options().dtype((at::ScalarType)dtype));
     std::vector<Tensor> src;
     src.reserve(ps.size());
     for (const Tensor& p : ps) src.push_back(p.contiguous());
@@ -1383,7 +1438,7 @@ struct CastGroupFn : public torch::autograd::Function<CastGroupFn> {
 };
 
 std::vector<Tensor> cast_group_ag(at::TensorList ps, int64_t dtype) {
-  return CastGroupFn::apply(ps.vec(), dtype);
+  return CastGroupFn::apply(ps, dtype);
 }
 
 std::vector<Tensor> cast_group_noag(at::TensorList ps, int64_t dtype) {

@@ -199,3 +199,43 @@ def test_block_graphs_shape_cap(dev):
     o1, live = run(1)
     assert live == 4, live
     assert all(torch.equal(a, b) for a, b in zip(o0, o1))
+
+
+def test_block_graphs_on_the_hf_swap_path(dev):
+    """models.native() (fp32 master weights cast per layer): the cast buffers are kept and
+    rewritten in place, so the blocks' bf16 weights keep their addresses and the forward graphs
+    replay; losses and updated fp32 weights equal graphs off."""
+    transformers = pytest.importorskip("transformers")
+    from nbdistributed_amd.models import SMOLLM2_135M, native
+
+    cfg = dict(SMOLLM2_135M)
+    cfg.update(num_hidden_layers=2, vocab_size=4096)
+    torch.manual_seed(0)
+    hf = transformers.LlamaForSequenceClassification(transformers.LlamaConfig(num_labels=2, pad_token_id=0, **cfg))
+    state = copy.deepcopy(hf.state_dict())
+    g = torch.Generator(device=dev).manual_seed(3)
+    ids = torch.randint(1, 4096, (4, 128), device=dev, generator=g)
+    lab = torch.tensor([0, 1, 1, 0], device=dev)
+
+    def run(mode):
+        ops.block_graphs(mode)
+        ops.block_graphs_reset()
+        hf.load_state_dict(state)
+        m = native(copy.deepcopy(hf).to(dev))
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+        s0 = ops.block_graphs_stats()
+        ls = []
+        for _ in range(6):
+            out = m(input_ids=ids, attention_mask=torch.ones_like(ids), labels=lab)
+            out.loss.backward()
+            opt.step()
+            opt.zero_grad()
+            ls.append(out.loss.detach())
+        torch.cuda.synchronize()
+        s1 = ops.block_graphs_stats()
+        return torch.stack(ls), torch.cat([p.detach().flatten() for p in m.parameters()]), s1["replays"] - s0["replays"]
+
+    l0, p0, _ = run(0)
+    l1, p1, replays = run(1)
+    assert replays >= 2 * 4, replays
+    assert torch.equal(l0, l1) and torch.equal(p0, p1)
