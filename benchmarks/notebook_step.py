@@ -12,7 +12,7 @@ nbdbg     : nbd eager with one HIP graph per decoder block's forward (ops.block_
 nbdbg2    : nbdbg with each block's backward graphed too (ops.block_graphs(2))
 hfnative  : HF model + the one-line swap nbd.models.native(model) (fp32 master weights, bf16
             compute), torch AdamW — the notebook's loop minus accelerate's wrappers
-hfnativebg: hfnative with per-block forward graphs (ops.block_graphs(1))
+hfnativebg: hfnativedefault with per-block forward graphs (ops.block_graphs(1))
 hfnativefused: hfnative with torch.optim.AdamW(..., fused=True)
 hfnativedefault: hfnative with the notebook's optimizer line unchanged (native() makes it fused)
 """
@@ -69,7 +69,7 @@ def main():
             from nbdistributed_amd.models import native as _native
 
             model = _native(model.to(dev))
-            if mode == "hfnativedefault":  # the notebook's line as written (native() picks fused)
+            if mode in ("hfnativedefault", "hfnativebg"):  # the notebook's line as written (native(): fused)
                 opt = torch.optim.AdamW(model.parameters(), lr=2e-5)
             else:
                 opt = torch.optim.AdamW(model.parameters(), lr=2e-5, fused=mode == "hfnativefused")

@@ -27,6 +27,7 @@
 #include <torch/csrc/autograd/custom_function.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <chrono>
@@ -756,6 +757,7 @@ std::unordered_map<const void*, std::weak_ptr<Graph>> g_outs;  // a graph's outp
 std::unordered_map<int64_t, std::weak_ptr<Graph>> g_by_id;      // for the backward
 int64_t g_next_id = 1;
 std::atomic<int> g_mode{-1};                                    // -1: not read from the env yet
+std::atomic<bool> g_suspended{false};                           // overrides per-model modes too
 // forward captures, replays, eager calls; backward captures, replays, eager calls
 std::atomic<int64_t> g_stat[6];
 
@@ -833,6 +835,13 @@ Tensor token(const std::shared_ptr<Graph>& gr) {
       at::TensorOptions().dtype(at::kLong));
 }
 }  // namespace bg
+
+namespace castbuf {  // (below, with the cast node)
+bool kept(const Tensor& t);
+// the warm-up references minus kept cast buffers: the cache keeps those alive, and a graph
+// holding them would make them look in use forever
+std::vector<Tensor> drop_kept(std::vector<Tensor> refs);
+}  // namespace castbuf
 
 // saved-list slots holding the call's weights / RoPE tables (the node's gradient targets)
 constexpr int kBlockWeightSlots[] = {1, 2, 6, 7, 9, 12, 13, 17, 19, 20};
@@ -931,7 +940,7 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
                                                    w_next, plan_qkv, plan_o, plan_mlp, H, Hkv, scale, eps, cos, sin,
                                                    &save);
   });
-  G->warm_refs = gemm::gemm_warm_take_refs();
+  G->warm_refs = castbuf::drop_kept(gemm::gemm_warm_take_refs());
   if (!err.empty()) {
     TORCH_WARN_ONCE("nbd: a decoder block's HIP graph capture failed (", err, "); the block runs eagerly");
     std::lock_guard<std::mutex> lk(g_mu);
@@ -1119,7 +1128,7 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
     err = capture(*B->g, [&] { block_bwd(sv, plans, H, Hkv, scale, shape, need_x, need_h, B->dx_in, B->dh_in, o); });
     B->deferred = rec.end();
   }
-  B->warm_refs = gemm::gemm_warm_take_refs();
+  B->warm_refs = castbuf::drop_kept(gemm::gemm_warm_take_refs());
   if (!err.empty()) G.bwd_off = true;
   TORCH_CHECK(err.empty(), "nbd: a decoder block's backward graph capture failed: ", err);
   // every weight gradient must be its claimed slice (else it would be static graph memory)
@@ -1169,14 +1178,14 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
                                const Tensor& w_post, const Tensor& w_gu, const Tensor& w_down, const Tensor& w_next,
                                at::IntArrayRef plan_qkv, at::IntArrayRef plan_o, at::IntArrayRef plan_mlp, int64_t H,
                                int64_t Hkv, double scale, double eps, const optional<Tensor>& cos,
-                               const optional<Tensor>& sin, bool graph) {
+                               const optional<Tensor>& sin, int64_t graph_mode) {
     const ht::Scope hs(ht::FWD);
     at::AutoDispatchBelowADInplaceOrView guard;
     ctx->set_materialize_grads(false);
     std::vector<Tensor> save;
     Tensor x_out, h_out;
     std::shared_ptr<bg::Graph> gr;
-    if (graph)
+    if (graph_mode >= 1)
       gr = block_graph(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp, H, Hkv,
                        scale, eps, cos, sin);
     if (gr) {
@@ -1188,7 +1197,7 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
       save.push_back(bg::token(gr));
       x_out = at::alias(gr->x_out);
       h_out = at::alias(gr->h_out);
-      if (bg::bwd_enabled()) ctx->saved_data["bg"] = gr->id;
+      if (graph_mode >= 2) ctx->saved_data["bg"] = gr->id;
     } else {
       std::tie(x_out, h_out) = llama_block_fwd(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv,
                                                plan_o, plan_mlp, H, Hkv, scale, eps, cos, sin, &save);
@@ -1237,21 +1246,20 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
   }
 };
 
-namespace castbuf {
-bool kept(const Tensor& t);  // (below, with the cast node)
-}  // namespace castbuf
 
 std::tuple<Tensor, Tensor> llama_block_ag(const Tensor& x, const Tensor& h, const Tensor& w_qkv,
                                           const optional<Tensor>& b_qkv, const Tensor& w_o, const optional<Tensor>& b_o,
                                           const Tensor& w_post, const Tensor& w_gu, const Tensor& w_down,
                                           const Tensor& w_next, at::IntArrayRef plan_qkv, at::IntArrayRef plan_o,
                                           at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv, double scale, double eps,
-                                          const optional<Tensor>& cos, const optional<Tensor>& sin) {
-  // (parameters, or weights cast into a kept buffer — models.native(): stable addresses)
-  const bool graph = bg::enabled() && c10::GradMode::is_enabled() && x.is_cuda() &&
-                     (w_qkv.is_leaf() || castbuf::kept(w_qkv));
+                                          const optional<Tensor>& cos, const optional<Tensor>& sin, int64_t graphs) {
+  // graphs: the caller's per-model mode (LlamaModel.block_graphs), -1 = the process setting;
+  // only parameters, or weights cast into a kept buffer (models.native(): stable addresses)
+  int64_t mode = graphs < 0 ? bg::mode() : std::min<int64_t>(graphs, 2);
+  if (bg::g_suspended.load(std::memory_order_relaxed)) mode = 0;  // (graphs.GraphedStep)
+  if (!(c10::GradMode::is_enabled() && x.is_cuda() && (w_qkv.is_leaf() || castbuf::kept(w_qkv)))) mode = 0;
   auto r = LlamaBlockFn::apply(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp,
-                               H, Hkv, scale, eps, cos, sin, graph);
+                               H, Hkv, scale, eps, cos, sin, mode);
   return {r[0], r[1]};
 }
 
@@ -1261,7 +1269,7 @@ std::tuple<Tensor, Tensor> llama_block_noag(const Tensor& x, const Tensor& h, co
                                             const Tensor& w_down, const Tensor& w_next, at::IntArrayRef plan_qkv,
                                             at::IntArrayRef plan_o, at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv,
                                             double scale, double eps, const optional<Tensor>& cos,
-                                            const optional<Tensor>& sin) {
+                                            const optional<Tensor>& sin, int64_t /*graphs*/) {
   return llama_block_fwd(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp, H, Hkv,
                          scale, eps, cos, sin, nullptr);
 }
@@ -1285,6 +1293,10 @@ int64_t llama_block_graphs(int64_t mode) {
   if (mode >= 0) bg::g_mode.store((int)std::min<int64_t>(mode, 2), std::memory_order_relaxed);
   return prev;
 }
+
+// Suspend every block graph, per-model modes included (graphs.GraphedStep's warm-up and
+// capture); returns the previous state.
+bool llama_block_graphs_suspend(bool on) { return bg::g_suspended.exchange(on); }
 
 // Drop every captured block graph (their static memory goes once no autograd node holds it).
 void llama_block_graphs_reset() {
@@ -1345,6 +1357,7 @@ struct Entry {
 std::mutex g_mu;
 std::unordered_map<const c10::TensorImpl*, Entry> g_bufs;
 std::unordered_map<const void*, int> g_addrs;  // data pointers of the kept buffers
+std::vector<Tensor> g_old;                      // replaced buffers (see get)
 
 Tensor get(const Tensor& first, int64_t total, const at::TensorOptions& opt) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -1360,11 +1373,16 @@ Tensor get(const Tensor& first, int64_t total, const at::TensorOptions& opt) {
   }
   auto it = g_bufs.find(first.unsafeGetTensorImpl());
   if (it != g_bufs.end() && !it->second.first.expired() && it->second.buf.numel() == total &&
-      it->second.buf.scalar_type() == opt.dtype().toScalarType() && it->second.buf.device() == opt.device() &&
-      it->second.buf.storage().use_count() == 1)
-    return it->second.buf;
+      it->second.buf.scalar_type() == opt.dtype().toScalarType() && it->second.buf.device() == opt.device()) {
+    if (it->second.buf.storage().use_count() == 1) return it->second.buf;
+    return at::empty({total}, opt);  // still held (a second forward before backward): a temporary
+  }
   Tensor buf = at::empty({total}, opt);
-  if (it != g_bufs.end()) g_addrs.erase(it->second.buf.data_ptr());
+  if (it != g_bufs.end()) {  // (the group changed shape: the old buffer may still be read by a
+    g_old.push_back(it->second.buf);  // captured warm-up — keep it, bounded)
+    if (g_old.size() > 64) g_old.erase(g_old.begin());
+    g_addrs.erase(it->second.buf.data_ptr());
+  }
   g_bufs.insert_or_assign(first.unsafeGetTensorImpl(),
                           Entry{c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>(
                                     first.getIntrusivePtr()),
@@ -1378,6 +1396,14 @@ bool kept(const Tensor& t) {
   if (!t.has_storage()) return false;
   std::lock_guard<std::mutex> lk(g_mu);
   return g_addrs.count(t.storage().data()) != 0;
+}
+
+std::vector<Tensor> drop_kept(std::vector<Tensor> refs) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  refs.erase(std::remove_if(refs.begin(), refs.end(),
+                            [](const Tensor& t) { return t.has_storage() && g_addrs.count(t.storage().data()) != 0; }),
+             refs.end());
+  return refs;
 }
 }  // namespace castbuf
 
@@ -1492,4 +1518,5 @@ TORCH_LIBRARY_FRAGMENT(nbd, m) {
   m.def("llama_block_graphs_reset() -> ()", &nbd::ag::llama_block_graphs_reset);
   m.def("llama_block_graphs_stats() -> int[]", &nbd::ag::llama_block_graphs_stats);
   m.def("host_timing(bool reset) -> str", &nbd::ag::host_timing);
+  m.def("llama_block_graphs_suspend(bool on) -> bool", &nbd::ag::llama_block_graphs_suspend);
 }

@@ -47,7 +47,7 @@ TORCH_LIBRARY(nbd, m) {
   m.def("attn_qkv_ag(Tensor qkv, int n_head, int n_kv, bool causal, float scale, Tensor? cos, Tensor? sin) -> Tensor");
   m.def("llama_block_ag(Tensor x, Tensor h, Tensor w_qkv, Tensor? b_qkv, Tensor w_o, Tensor? b_o, Tensor w_post, "
         "Tensor w_gu, Tensor w_down, Tensor w_next, int[] plan_qkv, int[] plan_o, int[] plan_mlp, int n_head, int n_kv, "
-        "float scale, float eps, Tensor? cos, Tensor? sin) -> (Tensor, Tensor)");
+        "float scale, float eps, Tensor? cos, Tensor? sin, int graphs=-1) -> (Tensor, Tensor)");
   m.def("cast_group_ag(Tensor[] ps, int dtype) -> Tensor[]");
   m.def("adamw_flat_multi(Tensor[] grads, Tensor(a!)[] params, Tensor(b!)[] masters, Tensor(c!)[] exp_avgs, "
         "Tensor(d!)[] exp_avg_sqs, float lr, float beta1, float beta2, float eps, float weight_decay, int step, "

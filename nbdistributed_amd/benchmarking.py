@@ -520,7 +520,8 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
                 "reference_samples_per_s": 32 / (REFERENCE_NOTEBOOK_MS_PER_STEP / 1e3)})
     recipes = {"reference": "HF model, fp32, accelerate DDP, torch AdamW (the notebook's recipe)",
                "reference_native": "the notebook's accelerate loop unchanged except model = nbd.models.native(model): "
-                                   "native Llama, fp32 master weights + torch AdamW, bf16 compute on the fused HIP path",
+                                   "native Llama, fp32 master weights + torch AdamW (fused: native()'s default), bf16 "
+                                   "compute on the fused HIP path, per-block forward graphs (native()'s default)",
                "nbd": "native Llama (HIP kernels, one autograd node per block), bf16 params + fp32 master "
                        "(FlatAdamW, buckets updated during backward at world 1), nbd DDP",
                "nbd_block_graphs": "as nbd (eager), each decoder block's forward replayed from its own HIP graph "

@@ -77,14 +77,14 @@ def _suspend_block_graphs():
         from .ops import _lib
 
         if _lib._loaded:
-            prev = int(torch.ops.nbd.llama_block_graphs(0))
+            prev = bool(torch.ops.nbd.llama_block_graphs_suspend(True))
     except (AttributeError, RuntimeError):
         prev = None
     try:
         yield
     finally:
         if prev is not None:
-            torch.ops.nbd.llama_block_graphs(prev)
+            torch.ops.nbd.llama_block_graphs_suspend(prev)
 
 
 class GraphedStep:

@@ -241,6 +241,8 @@ class LlamaModel(nn.Module):
         # fp32 parameters computed in this dtype on the fused GPU path (``native()``): the
         # parameters stay fp32 for the optimizer, each layer is cast once per forward
         self.compute_dtype: Optional[torch.dtype] = None
+        # per-block HIP graphs for this model (0 / 1 / 2, ops.block_graphs); None = process setting
+        self.block_graphs: Optional[int] = None
         # per-block HIP graphs (ops.block_graphs) hold static activations: drop them with the model
         weakref.finalize(self, _drop_block_graphs)
 
@@ -288,7 +290,8 @@ class LlamaModel(nn.Module):
                 # the whole block as one autograd node (GPU bf16; None -> the op-by-op path below)
                 r = ops.llama_block(x, h, at.qkv_proj.weight, at.qkv_proj.bias, at.o_proj.weight, at.o_proj.bias,
                                     layer.post_attention_layernorm.weight, layer.mlp.gate_up_proj.weight,
-                                    layer.mlp.down_proj.weight, nxt.weight, at.H, at.Hkv, c.rms_norm_eps, cos, sin)
+                                    layer.mlp.down_proj.weight, nxt.weight, at.H, at.Hkv, c.rms_norm_eps, cos, sin,
+                                    self._graph_mode())
                 if r is not None:
                     x, h = r
                     continue
@@ -296,11 +299,19 @@ class LlamaModel(nn.Module):
             x, h = ops.add_rms_norm(x, a, layer.post_attention_layernorm.weight, c.rms_norm_eps)
             m = layer.mlp(h)
             x, h = ops.add_rms_norm(x, m, nxt.weight, c.rms_norm_eps)
-        if h.is_cuda and ops.native_available() and ops.block_graphs():
+        if h.is_cuda and self._graphs_on():
             # per-block graphs: the last block's output is its graph's static memory — the model's
             # output is the caller's to keep
             h = h.clone()
         return h
+
+    def _graph_mode(self) -> int:
+        return -1 if self.block_graphs is None else int(self.block_graphs)
+
+    def _graphs_on(self) -> bool:
+        if self.block_graphs is not None:
+            return self.block_graphs > 0
+        return ops.native_available() and ops.block_graphs() > 0
 
     def _forward_cast(self, input_ids, cd, cos, sin):
         """fp32 parameters, ``cd`` compute: the embedding gathers fp32 rows (no table cast) and
@@ -325,7 +336,7 @@ class LlamaModel(nn.Module):
             b_qkv = extra.pop(0) if at.qkv_proj.bias is not None else None
             b_o = extra.pop(0) if at.o_proj.bias is not None else None
             r = ops.llama_block(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, at.H, at.Hkv,
-                                c.rms_norm_eps, cos, sin)
+                                c.rms_norm_eps, cos, sin, self._graph_mode())
             if r is None:  # (cast_dtype() checked the conditions: not expected)
                 qkv = ops.gemm_linear(h, w_qkv, b_qkv)
                 a = ops.gemm_linear(ops.attention_qkv(qkv, at.H, causal=True, n_kv_head=at.Hkv, rope=(cos, sin)),
@@ -334,7 +345,7 @@ class LlamaModel(nn.Module):
                 x, h = ops.add_rms_norm(x, ops.mlp_swiglu(h, w_gu, w_down), w_next, c.rms_norm_eps)
             else:
                 x, h = r
-        if ops.block_graphs():  # (see forward)
+        if self._graphs_on():  # (see forward)
             h = h.clone()
         return h
 
@@ -518,7 +529,8 @@ def from_hf(hf_model, compute_dtype: Optional[torch.dtype] = None) -> nn.Module:
     return m
 
 
-def native(hf_model, compute_dtype: Optional[torch.dtype] = torch.bfloat16, fused_optimizer: bool = True) -> nn.Module:
+def native(hf_model, compute_dtype: Optional[torch.dtype] = torch.bfloat16, fused_optimizer: bool = True,
+           block_graphs: int = 1) -> nn.Module:
     """The one-line swap for a notebook written against HF transformers: call it on the HF
     Llama / SmolLM2 / Qwen2 / Mistral model BEFORE creating the optimizer and
     ``accelerator.prepare``.  The returned module takes the same keyword arguments, returns
@@ -531,8 +543,18 @@ def native(hf_model, compute_dtype: Optional[torch.dtype] = torch.bfloat16, fuse
     step) implementation instead of the multi-tensor default — the same update, and on the
     notebook's SmolLM2 step the default's optimizer phase is 3.0-5.8 ms of GPU time against
     0.9 ms fused (docs/FINDINGS.md §30).  Other optimizers and parameters are untouched;
-    ``NBD_NATIVE_FUSED_OPTIM=0`` or ``fused_optimizer=False`` keeps torch's default."""
+    ``NBD_NATIVE_FUSED_OPTIM=0`` or ``fused_optimizer=False`` keeps torch's default.
+
+    ``block_graphs``: each decoder block's forward replayed from its own HIP graph (1, the
+    default; 2 adds the backward where gradients go to DDP bucket slices; 0 off — also with
+    ``NBD_BLOCK_GRAPHS=0``): the swapped loop's forward is host-bound (docs/FINDINGS.md §30).
+    The model's output is a fresh tensor as always; block-internal activations stay allocated
+    between steps (at most 4 sequence lengths per block are graphed)."""
     m = from_hf(hf_model, compute_dtype=compute_dtype)
+    if os.environ.get("NBD_BLOCK_GRAPHS") == "0":
+        block_graphs = 0
+    if hasattr(m, "model") and isinstance(m.model, LlamaModel):
+        m.model.block_graphs = int(block_graphs)
     if fused_optimizer and os.environ.get("NBD_NATIVE_FUSED_OPTIM", "1") != "0":
         for p in m.parameters():
             p._nbd_native_fused = True

@@ -619,12 +619,13 @@ _BLOCK_PLANS: dict = {}
 
 
 def llama_block(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, n_head: int, n_kv: int, eps: float,
-                cos, sin):
+                cos, sin, graphs: int = -1):
     """One pre-norm Llama decoder block as ONE autograd node: ``x1 = x + o_proj(attn(qkv(h)))``,
     ``h1 = rms(x1)·γ_post``, ``x2 = x1 + down(swiglu(gate_up(h1)))``, returns ``(x2, rms(x2)·γ_next)``
     — the per-op path's kernels in the same order, one Python call and one node instead of six and
     five (the eager SmolLM2 step is host-bound).  None when the block does not fit the fused path
-    (the caller then runs the ops one by one)."""
+    (the caller then runs the ops one by one).  ``graphs``: per-block HIP graph mode for this call
+    (0 / 1 / 2, see ``block_graphs``; -1 = the process setting)."""
     import torch
 
     if not (FUSED_BLOCK and FUSED_SWIGLU and NATIVE_AUTOGRAD and _fast(h, w_qkv, w_o, w_gu, w_down)
@@ -644,7 +645,8 @@ def llama_block(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, n_he
                  native_plan("mlp_swiglu", M, C, w_down.shape[1]))
         _BLOCK_PLANS[key] = plans
     return torch.ops.nbd.llama_block_ag(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plans[0],
-                                        plans[1], plans[2], int(n_head), int(n_kv), D ** -0.5, float(eps), cos, sin)
+                                        plans[1], plans[2], int(n_head), int(n_kv), D ** -0.5, float(eps), cos, sin,
+                                        int(graphs))
 
 
 def block_graphs(enable=None) -> int:

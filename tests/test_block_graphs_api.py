@@ -35,12 +35,13 @@ def test_graphed_step_suspends_block_graphs(native):
 
     ops.block_graphs(2)
     with _suspend_block_graphs():
-        assert ops.block_graphs() == 0
-    assert ops.block_graphs() == 2
+        assert torch.ops.nbd.llama_block_graphs_suspend(True) is True  # (suspended; stays so)
+        assert ops.block_graphs() == 2  # the process mode itself is untouched
+    assert torch.ops.nbd.llama_block_graphs_suspend(False) is False
     with pytest.raises(RuntimeError):
         with _suspend_block_graphs():
             raise RuntimeError("step failed")
-    assert ops.block_graphs() == 2  # restored on error too
+    assert torch.ops.nbd.llama_block_graphs_suspend(False) is False  # restored on error too
 
 
 def test_cpu_model_unaffected(native):

@@ -221,7 +221,9 @@ def test_block_graphs_on_the_hf_swap_path(dev):
         ops.block_graphs(mode)
         ops.block_graphs_reset()
         hf.load_state_dict(state)
-        m = native(copy.deepcopy(hf).to(dev))
+        m = native(copy.deepcopy(hf).to(dev))  # (native() turns block graphs on for its model)
+        assert m.model.block_graphs == 1
+        m.model.block_graphs = mode
         opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
         s0 = ops.block_graphs_stats()
         ls = []
