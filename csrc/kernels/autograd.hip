@@ -1059,9 +1059,14 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
       if (ps[i]->defined() && ps[i]->unsafeGetTensorImpl() == impl) return i;
     return -1;
   };
-  auto it = G.bwd.find(key);
-  if (it != G.bwd.end()) {
-    Bwd& B = *it->second;
+  std::shared_ptr<Bwd> found;  // (G.bwd under g_mu: is_graph_output reads it from the forward)
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = G.bwd.find(key);
+    if (it != G.bwd.end()) found = it->second;
+  }
+  if (found) {
+    Bwd& B = *found;
     bool ok = (!has_dx || !B.dx_alias || dx_out.data_ptr() == B.dx_in.data_ptr()) &&
               (!B.dh_alias || dh_out.data_ptr() == B.dh_in.data_ptr());
     for (const auto& c : B.claims) {
@@ -1069,7 +1074,8 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
       ok = ok && i >= 0 && dst[i].defined() && dst[i].data_ptr() == c.dst && acc[i] == c.acc;
     }
     if (!ok) {
-      G.bwd.erase(it);  // destinations moved: capture anew next time
+      std::lock_guard<std::mutex> lk(g_mu);
+      G.bwd.erase(key);  // destinations moved: capture anew next time
       return false;
     }
     if (has_dx && !B.dx_alias && dx_out.data_ptr() != B.dx_in.data_ptr()) B.dx_in.copy_(dx_out);
@@ -1164,8 +1170,8 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
   out = o;
   out[0] = B->g1.defined() ? at::alias(B->g1) : Tensor();
   out[1] = B->dh.defined() ? at::alias(B->dh) : Tensor();
-  G.bwd[key] = B;
   std::lock_guard<std::mutex> lk(g_mu);
+  G.bwd[key] = B;
   auto self = g_by_id.count(G.id) ? g_by_id[G.id] : std::weak_ptr<Graph>();
   if (B->g1.defined()) g_outs[B->g1.data_ptr()] = self;
   if (B->dh.defined()) g_outs[B->dh.data_ptr()] = self;
