@@ -710,6 +710,8 @@ static std::tuple<Tensor, Tensor> llama_block_fwd(const Tensor& x, const Tensor&
 // that AccumulateGrad keeps as .grad.
 // Same kernels, same order: bit-identical to the eager block (tests/test_gpu_block_graphs.py).
 namespace bg {
+using Key = std::tuple<const void*, int64_t, int64_t, int64_t>;  // (W_qkv, B, T, device)
+
 struct Bwd {
   std::unique_ptr<at::cuda::CUDAGraph> g;
   Tensor dx_in, dh_in;                    // static inputs (the incoming gradients)
@@ -731,6 +733,7 @@ struct Graph {
   std::vector<Tensor> warm_refs;       // storages the captured GEMM warm-ups read
   std::atomic<bool> armed{false};
   int64_t id = 0;
+  Key key{};
   std::map<int, std::shared_ptr<Bwd>> bwd;  // key: accumulate mask | need bits
   int bwd_captures = 0;
   bool bwd_off = false;
@@ -745,12 +748,49 @@ struct Graph {
     return nullptr;
   }
 };
+// A block call's arguments, kept (strong references) so that a stack capture can re-run it.
+struct Args {
+  Tensor w_qkv, w_o, w_post, w_gu, w_down, w_next;
+  optional<Tensor> b_qkv, b_o, cos, sin;
+  std::vector<int64_t> plan_qkv, plan_o, plan_mlp;
+  int64_t H = 0, Hkv = 0;
+  double scale = 0, eps = 0;
+};
+
+// Stack graphs (mode 1): every graph launch costs the GPU ≈8.5 µs of its own
+// (benchmarks/graph_chunks.py), so once a run of consecutive graphed blocks has replayed
+// steadily — each block's input the previous block's static output — the whole run is captured
+// as ONE graph, replayed at its first block's call; the following blocks' calls, arriving in the
+// recorded order with the recorded weights and the stack's outputs as inputs, are served from it
+// without a launch.  Any deviation drops the stack (back to per-block graphs).
+struct StackMember {
+  Key key;
+  std::vector<const void*> ptrs;
+  std::vector<int64_t> sig;
+  std::vector<Tensor> saved;  // weight slots empty
+  Tensor x_out, h_out;
+};
+struct Stack {
+  std::unique_ptr<at::cuda::CUDAGraph> g;
+  Tensor x_in, h_in;
+  std::vector<StackMember> m;
+  std::vector<Tensor> warm_refs;
+  size_t next = 0;             // members served in the current pass
+  std::atomic<int> held{0};    // served members whose autograd nodes still hold the memory
+  Key head{};
+};
+
 struct Slot {
   int eager = 0, captures = 0, misses = 0;
   bool off = false;
   std::shared_ptr<Graph> g;
+  std::shared_ptr<Args> args;  // (stack capture)
+  Key next_key{};              // the block that consumed this block's outputs last pass
+  bool has_next = false;
+  int steady = 0;              // consecutive per-block replays
+  std::shared_ptr<Stack> stack;  // a stack headed by this block
+  int stack_fail = 0;
 };
-using Key = std::tuple<const void*, int64_t, int64_t, int64_t>;  // (W_qkv, B, T, device)
 std::mutex g_mu;
 std::map<Key, Slot> g_slots;
 std::unordered_map<const void*, std::weak_ptr<Graph>> g_outs;  // a graph's output address -> graph
@@ -759,7 +799,8 @@ int64_t g_next_id = 1;
 std::atomic<int> g_mode{-1};                                    // -1: not read from the env yet
 std::atomic<bool> g_suspended{false};                           // overrides per-model modes too
 // forward captures, replays, eager calls; backward captures, replays, eager calls
-std::atomic<int64_t> g_stat[6];
+std::atomic<int64_t> g_stat[10];  // + stack captures, stack replays, stack-served blocks, stacks dropped
+std::weak_ptr<Stack> g_active;    // the stack serving the current pass
 
 // 0 off, 1 forward graphs, 2 forward and backward graphs (NBD_BLOCK_GRAPHS)
 int mode() {
@@ -772,6 +813,13 @@ int mode() {
   return m;
 }
 bool enabled() { return mode() >= 1; }
+bool stacks_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NBD_BLOCK_STACKS");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
 bool bwd_enabled() { return mode() >= 2; }
 
 bool stream_capturing() {
@@ -834,6 +882,43 @@ Tensor token(const std::shared_ptr<Graph>& gr) {
       },
       at::TensorOptions().dtype(at::kLong));
 }
+std::vector<std::shared_ptr<Stack>> g_dropped;  // dropped stacks: a replay may still be in flight
+
+// under g_mu: the block whose static output `x` is now feeds block `key`
+void link_pred(const Tensor& x, const Key& key) {
+  auto it = g_outs.find(x.data_ptr());
+  if (it == g_outs.end()) return;
+  auto pg = it->second.lock();
+  if (!pg) return;
+  auto ps = g_slots.find(pg->key);
+  if (ps == g_slots.end()) return;
+  ps->second.next_key = key;
+  ps->second.has_next = true;
+}
+
+// under g_mu: stop serving `st` (its head slot captures no new stack after two failures)
+void drop_stack(const std::shared_ptr<Stack>& st, const Key& head) {
+  auto it = g_slots.find(head);
+  if (it != g_slots.end() && it->second.stack == st) {
+    it->second.stack.reset();
+    ++it->second.stack_fail;
+  }
+  if (g_active.lock() == st) g_active.reset();
+  g_dropped.push_back(st);
+  if (g_dropped.size() > 8) g_dropped.erase(g_dropped.begin());
+  ++g_stat[9];
+}
+
+Tensor stack_token(const std::shared_ptr<Stack>& st) {
+  static int64_t dummy = 0;
+  std::weak_ptr<Stack> w = st;
+  return at::from_blob(
+      &dummy, {1},
+      [w](void*) {
+        if (auto s = w.lock()) s->held.fetch_sub(1, std::memory_order_acq_rel);
+      },
+      at::TensorOptions().dtype(at::kLong));
+}
 }  // namespace bg
 
 namespace castbuf {  // (below, with the cast node)
@@ -867,12 +952,20 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
   }
   for (at::IntArrayRef p : {plan_qkv, plan_o, plan_mlp}) sig.insert(sig.end(), p.begin(), p.end());
   const Key key{w_qkv.data_ptr(), h.size(0), h.size(1), h.get_device()};
+  auto make_args = [&] {
+    auto a = std::make_shared<Args>();
+    a->w_qkv = w_qkv, a->w_o = w_o, a->w_post = w_post, a->w_gu = w_gu, a->w_down = w_down, a->w_next = w_next;
+    a->b_qkv = b_qkv, a->b_o = b_o, a->cos = cos, a->sin = sin;
+    a->plan_qkv = plan_qkv.vec(), a->plan_o = plan_o.vec(), a->plan_mlp = plan_mlp.vec();
+    a->H = H, a->Hkv = Hkv, a->scale = scale, a->eps = eps;
+    return a;
+  };
   std::shared_ptr<Graph> gr;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     Slot& s = g_slots[key];
     if (s.off) return nullptr;
-    if (s.g && (s.g->ptrs != ptrs || s.g->sig != sig)) s.g.reset(), s.eager = 0;  // weights moved
+    if (s.g && (s.g->ptrs != ptrs || s.g->sig != sig)) s.g.reset(), s.eager = 0, s.args.reset(), s.steady = 0;
     if (s.g) {
       Graph& G = *s.g;
       const bool inputs_ok = (!G.x_alias || x.data_ptr() == G.x_in.data_ptr()) &&
@@ -887,6 +980,9 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
         return nullptr;
       }
       s.misses = 0;
+      ++s.steady;
+      if (!s.args) s.args = make_args();
+      if (G.x_alias) link_pred(x, key);
       gr = s.g;
     } else if (++s.eager < 3) {
       ++g_stat[2];
@@ -959,11 +1055,123 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
   g_outs[G->x_out.data_ptr()] = G;
   g_outs[G->h_out.data_ptr()] = G;
   G->id = g_next_id++;
+  G->key = key;
   g_by_id[G->id] = G;
   Slot& s = g_slots[key];
   s.g = G;
   s.misses = 0;
+  s.steady = 0;
+  s.args = make_args();
+  if (G->x_alias) link_pred(x, key);
   return G;
+}
+
+// A stack graph for this call (see bg::Stack): the head's call replays it, the following blocks'
+// calls are served from it.  {nullptr, 0} = not served (per-block path).
+static std::pair<std::shared_ptr<bg::Stack>, size_t> stack_serve(
+    const Tensor& x, const Tensor& h, const Tensor& w_qkv, const optional<Tensor>& b_qkv, const Tensor& w_o,
+    const optional<Tensor>& b_o, const Tensor& w_post, const Tensor& w_gu, const Tensor& w_down, const Tensor& w_next,
+    at::IntArrayRef plan_qkv, at::IntArrayRef plan_o, at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv, double scale,
+    double eps, const optional<Tensor>& cos, const optional<Tensor>& sin) {
+  using namespace bg;
+  if (stream_capturing()) return {nullptr, 0};
+  const Tensor* ts[] = {&w_qkv, b_qkv ? &*b_qkv : nullptr, &w_o, b_o ? &*b_o : nullptr, &w_post, &w_gu,
+                        &w_down, &w_next, cos ? &*cos : nullptr, sin ? &*sin : nullptr};
+  std::vector<const void*> ptrs;
+  std::vector<int64_t> sig{H, Hkv, (int64_t)(scale * 1e9), (int64_t)(eps * 1e12), (int64_t)x.scalar_type()};
+  for (const Tensor* t : ts) {
+    ptrs.push_back(t != nullptr ? t->data_ptr() : nullptr);
+    if (t != nullptr) sig.insert(sig.end(), t->sizes().begin(), t->sizes().end());
+    sig.push_back(-1);
+  }
+  for (at::IntArrayRef p : {plan_qkv, plan_o, plan_mlp}) sig.insert(sig.end(), p.begin(), p.end());
+  const Key key{w_qkv.data_ptr(), h.size(0), h.size(1), h.get_device()};
+  std::lock_guard<std::mutex> lk(g_mu);
+  // 1. the next member of the stack serving this pass
+  if (auto st = g_active.lock()) {
+    if (st->next > 0 && st->next < st->m.size()) {
+      StackMember& mb = st->m[st->next];
+      const StackMember& prev = st->m[st->next - 1];
+      if (mb.key == key && mb.ptrs == ptrs && mb.sig == sig && x.data_ptr() == prev.x_out.data_ptr() &&
+          h.data_ptr() == prev.h_out.data_ptr()) {
+        st->held.fetch_add(1, std::memory_order_acq_rel);
+        ++g_stat[8];
+        return {st, st->next++};
+      }
+      drop_stack(st, st->head);  // the pass left the recorded order
+    }
+  }
+  // 2. the head of a stack
+  auto it = g_slots.find(key);
+  if (it == g_slots.end()) return {nullptr, 0};
+  Slot& s = it->second;
+  if (!s.g || s.g->x_alias || s.g->ptrs != ptrs || s.g->sig != sig) return {nullptr, 0};
+  if (!s.stack) {
+    // 3. capture one: a steadily replaying chain of >= 2 graphed blocks starting here
+    if (s.stack_fail >= 2 || s.steady < 3 || !s.args) return {nullptr, 0};
+    std::vector<Key> chain{key};
+    for (Key k = key; chain.size() < 256;) {
+      const Slot& cs = g_slots[k];
+      if (!cs.has_next) break;
+      auto nit = g_slots.find(cs.next_key);
+      if (nit == g_slots.end() || !nit->second.g || !nit->second.args || nit->second.steady < 3 ||
+          !nit->second.g->x_alias || std::find(chain.begin(), chain.end(), cs.next_key) != chain.end())
+        break;
+      chain.push_back(cs.next_key);
+      k = cs.next_key;
+    }
+    if (chain.size() < 2) return {nullptr, 0};
+    auto st = std::make_shared<Stack>();
+    st->head = key;
+    st->x_in = at::empty_like(x, at::MemoryFormat::Contiguous);
+    st->h_in = at::empty_like(h, at::MemoryFormat::Contiguous);
+    st->m.resize(chain.size());
+    std::vector<std::shared_ptr<Args>> args;
+    for (size_t i = 0; i < chain.size(); ++i) {
+      const Slot& cs = g_slots[chain[i]];
+      st->m[i].key = chain[i];
+      st->m[i].ptrs = cs.g->ptrs;
+      st->m[i].sig = cs.g->sig;
+      args.push_back(cs.args);
+    }
+    st->g = std::make_unique<at::cuda::CUDAGraph>();
+    const std::string err = capture(*st->g, [&] {
+      Tensor cx = st->x_in, ch = st->h_in;
+      for (size_t i = 0; i < args.size(); ++i) {
+        const Args& a = *args[i];
+        std::vector<Tensor> save;
+        std::tie(st->m[i].x_out, st->m[i].h_out) =
+            llama_block_fwd(cx, ch, a.w_qkv, a.b_qkv, a.w_o, a.b_o, a.w_post, a.w_gu, a.w_down, a.w_next, a.plan_qkv,
+                            a.plan_o, a.plan_mlp, a.H, a.Hkv, a.scale, a.eps, a.cos, a.sin, &save);
+        for (int j : kBlockWeightSlots) save[j] = Tensor();
+        st->m[i].saved = std::move(save);
+        cx = st->m[i].x_out;
+        ch = st->m[i].h_out;
+      }
+    });
+    st->warm_refs = castbuf::drop_kept(gemm::gemm_warm_take_refs());
+    if (!err.empty()) {
+      ++s.stack_fail;
+      TORCH_WARN_ONCE("nbd: a stack of decoder-block graphs failed to capture (", err, "); per-block graphs stay");
+      return {nullptr, 0};
+    }
+    ++g_stat[6];
+    s.stack = st;
+  }
+  Stack& st = *s.stack;
+  if (st.m[0].ptrs != ptrs || st.m[0].sig != sig) {
+    drop_stack(s.stack, key);
+    return {nullptr, 0};
+  }
+  if (st.held.load(std::memory_order_acquire) != 0) return {nullptr, 0};  // the last pass still holds it
+  if (st.x_in.data_ptr() != x.data_ptr()) st.x_in.copy_(x);
+  if (st.h_in.data_ptr() != h.data_ptr()) st.h_in.copy_(h);
+  st.g->replay();
+  st.next = 1;
+  st.held.store(1, std::memory_order_release);
+  g_active = s.stack;
+  ++g_stat[7];
+  return {s.stack, 0};
 }
 
 // The block's backward into `out` (the node's 20 outputs).
@@ -1191,10 +1399,24 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
     std::vector<Tensor> save;
     Tensor x_out, h_out;
     std::shared_ptr<bg::Graph> gr;
-    if (graph_mode >= 1)
+    std::pair<std::shared_ptr<bg::Stack>, size_t> sh{nullptr, 0};
+    if (graph_mode == 1 && bg::stacks_enabled())
+      sh = stack_serve(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp, H, Hkv,
+                       scale, eps, cos, sin);
+    if (!sh.first && graph_mode >= 1)
       gr = block_graph(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp, H, Hkv,
                        scale, eps, cos, sin);
-    if (gr) {
+    if (sh.first) {
+      const bg::StackMember& mb = sh.first->m[sh.second];
+      save = mb.saved;
+      const Tensor none;
+      const Tensor* ts[] = {&w_qkv, b_qkv ? &*b_qkv : &none, &w_o, b_o ? &*b_o : &none, &w_post, &w_gu,
+                            &w_down, &w_next, cos ? &*cos : &none, sin ? &*sin : &none};
+      for (size_t i = 0; i < std::size(kBlockWeightSlots); ++i) save[kBlockWeightSlots[i]] = *ts[i];
+      save.push_back(bg::stack_token(sh.first));
+      x_out = at::alias(mb.x_out);
+      h_out = at::alias(mb.h_out);
+    } else if (gr) {
       save = gr->saved;
       const Tensor none;
       const Tensor* ts[] = {&w_qkv, b_qkv ? &*b_qkv : &none, &w_o, b_o ? &*b_o : &none, &w_post, &w_gu,
@@ -1307,8 +1529,11 @@ bool llama_block_graphs_suspend(bool on) { return bg::g_suspended.exchange(on); 
 // Drop every captured block graph (their static memory goes once no autograd node holds it).
 void llama_block_graphs_reset() {
   std::map<bg::Key, bg::Slot> slots;
+  std::vector<std::shared_ptr<bg::Stack>> dropped;
   std::lock_guard<std::mutex> lk(bg::g_mu);
   slots.swap(bg::g_slots);
+  dropped.swap(bg::g_dropped);
+  bg::g_active.reset();
   bg::g_outs.clear();
 }
 
@@ -1318,7 +1543,8 @@ std::vector<int64_t> llama_block_graphs_stats() {
   int64_t live = 0;
   for (const auto& kv : bg::g_slots) live += kv.second.g != nullptr;
   return {bg::g_stat[0].load(), bg::g_stat[1].load(), bg::g_stat[2].load(), live,
-          bg::g_stat[3].load(), bg::g_stat[4].load(), bg::g_stat[5].load()};
+          bg::g_stat[3].load(), bg::g_stat[4].load(), bg::g_stat[5].load(),
+          bg::g_stat[6].load(), bg::g_stat[7].load(), bg::g_stat[8].load(), bg::g_stat[9].load()};
 }
 
 // ------------------------------------------------------- fp32 master weights, bf16 compute
@@ -1359,13 +1585,19 @@ namespace castbuf {
 struct Entry {
   c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl> first;  // the group's first parameter (validates the key)
   Tensor buf;
+  std::shared_ptr<std::atomic<bool>> busy;  // a cast node of an earlier pass still owns it
 };
 std::mutex g_mu;
 std::unordered_map<const c10::TensorImpl*, Entry> g_bufs;
 std::unordered_map<const void*, int> g_addrs;  // data pointers of the kept buffers
 std::vector<Tensor> g_old;                      // replaced buffers (see get)
 
-Tensor get(const Tensor& first, int64_t total, const at::TensorOptions& opt) {
+// The buffer for this group's cast and, when it is the kept one, the flag its node releases
+// (a token among the node's saved tensors: freed by that node's backward — which runs after every
+// node that saved the cast weights — or with the node).  Storage use counts cannot tell: the
+// block graphs keep references to the weights they were captured with.
+std::pair<Tensor, std::shared_ptr<std::atomic<bool>>> get(const Tensor& first, int64_t total,
+                                                          const at::TensorOptions& opt) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_bufs.size() > 4096) {  // forget the groups of dead parameters
     for (auto it = g_bufs.begin(); it != g_bufs.end();) {
@@ -1380,10 +1612,11 @@ Tensor get(const Tensor& first, int64_t total, const at::TensorOptions& opt) {
   auto it = g_bufs.find(first.unsafeGetTensorImpl());
   if (it != g_bufs.end() && !it->second.first.expired() && it->second.buf.numel() == total &&
       it->second.buf.scalar_type() == opt.dtype().toScalarType() && it->second.buf.device() == opt.device()) {
-    if (it->second.buf.storage().use_count() == 1) return it->second.buf;
-    return at::empty({total}, opt);  // still held (a second forward before backward): a temporary
+    if (!it->second.busy->exchange(true)) return {it->second.buf, it->second.busy};
+    return {at::empty({total}, opt), nullptr};  // still owned (a second forward before backward): a temporary
   }
   Tensor buf = at::empty({total}, opt);
+  auto busy = std::make_shared<std::atomic<bool>>(true);
   if (it != g_bufs.end()) {  // (the group changed shape: the old buffer may still be read by a
     g_old.push_back(it->second.buf);  // captured warm-up — keep it, bounded)
     if (g_old.size() > 64) g_old.erase(g_old.begin());
@@ -1392,9 +1625,16 @@ Tensor get(const Tensor& first, int64_t total, const at::TensorOptions& opt) {
   g_bufs.insert_or_assign(first.unsafeGetTensorImpl(),
                           Entry{c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>(
                                     first.getIntrusivePtr()),
-                                buf});
+                                buf, busy});
   g_addrs[buf.data_ptr()] = 1;
-  return buf;
+  return {buf, busy};
+}
+
+Tensor release_token(std::shared_ptr<std::atomic<bool>> busy) {
+  static int64_t dummy = 0;
+  return at::from_blob(
+      &dummy, {1}, [busy](void*) { busy->store(false, std::memory_order_release); },
+      at::TensorOptions().dtype(at::kLong));
 }
 
 // t lives in a kept cast buffer (its address is stable across steps)
@@ -1425,7 +1665,8 @@ struct CastGroupFn : public torch::autograd::Function<CastGroupFn> {
                   "cast_group: one device and dtype");
       shapes.push_back(p.sizes().vec());
     }
-    const Tensor buf = castbuf::get(ps[0], total, ps[0].options().dtype((at::ScalarType)dtype));
+    auto [buf, busy] = castbuf::get(ps[0], total, ps[0].options().dtype((at::ScalarType)dtype));
+    if (busy) ctx->save_for_backward({castbuf::release_token(busy)});
     std::vector<Tensor> src;
     src.reserve(ps.size());
     for (const Tensor& p : ps) src.push_back(p.contiguous());

@@ -680,6 +680,6 @@ def block_graphs_stats() -> dict:
     import torch
 
     _require()
-    c, r, e, n, bc, br, be = torch.ops.nbd.llama_block_graphs_stats()
+    c, r, e, n, bc, br, be, sc, sr, ss, sd = torch.ops.nbd.llama_block_graphs_stats()
     return {"captures": c, "replays": r, "eager": e, "live": n, "bwd_captures": bc, "bwd_replays": br,
-            "bwd_eager": be}
+            "bwd_eager": be, "stack_captures": sc, "stack_replays": sr, "stack_served": ss, "stacks_dropped": sd}

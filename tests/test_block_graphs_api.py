@@ -25,7 +25,8 @@ def test_modes_and_stats(native):
     assert ops.block_graphs(7) == 1     # clamped to 2
     assert ops.block_graphs() == 2
     st = ops.block_graphs_stats()
-    assert set(st) == {"captures", "replays", "eager", "live", "bwd_captures", "bwd_replays", "bwd_eager"}
+    assert set(st) == {"captures", "replays", "eager", "live", "bwd_captures", "bwd_replays", "bwd_eager",
+                       "stack_captures", "stack_replays", "stack_served", "stacks_dropped"}
     ops.block_graphs_reset()
     assert ops.block_graphs_stats()["live"] == 0
 

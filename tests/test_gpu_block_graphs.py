@@ -241,3 +241,49 @@ def test_block_graphs_on_the_hf_swap_path(dev):
     l1, p1, replays = run(1)
     assert replays >= 2 * 4, replays
     assert torch.equal(l0, l1) and torch.equal(p0, p1)
+
+
+def test_block_stack_graph_bit_identical_and_deviation(dev):
+    """After the per-block graphs replay steadily, a run of consecutive blocks becomes ONE stack
+    graph (one launch per forward); its results equal eager.  A pass that calls the blocks in
+    another order drops the stack and still computes the right thing."""
+    base = _model(dev, layers=4, seed=11)
+    batches = _batches(dev, n=2)
+
+    def run(mode, reorder_at=None):
+        ops.block_graphs(mode)
+        ops.block_graphs_reset()
+        m = copy.deepcopy(base)
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-3, foreach=False)
+        ls = []
+        for i in range(12):
+            layers = m.model.layers
+            if reorder_at is not None and i == reorder_at:
+                # (block 0 unchanged: the stack's head replays; block 1 arrives with another
+                # next-norm weight and is not the recorded member -> the stack is dropped)
+                m.model.layers = torch.nn.ModuleList([layers[0], layers[1], layers[3], layers[2]])
+            ids, lab = batches[i % 2]
+            loss = m(ids, torch.ones_like(ids), lab)[0]
+            loss.backward()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            m.model.layers = layers
+            ls.append(loss.detach())
+        torch.cuda.synchronize()
+        return torch.stack(ls), torch.cat([p.detach().float().flatten() for p in m.parameters()])
+
+    l0, p0 = run(0)
+    s0 = ops.block_graphs_stats()
+    l1, p1 = run(1)
+    s1 = ops.block_graphs_stats()
+    assert torch.equal(l0, l1) and torch.equal(p0, p1)
+    assert s1["stack_captures"] - s0["stack_captures"] == 1, s1
+    assert s1["stack_replays"] - s0["stack_replays"] >= 4, s1
+    assert s1["stack_served"] - s0["stack_served"] >= 3 * 4, s1
+    # a pass in another block order (at step 9, after the stack formed): dropped, still exact
+    l2, p2 = run(0, reorder_at=9)
+    s2 = ops.block_graphs_stats()
+    l3, p3 = run(1, reorder_at=9)
+    s3 = ops.block_graphs_stats()
+    assert torch.equal(l2, l3) and torch.equal(p2, p3)
+    assert s3["stacks_dropped"] - s2["stacks_dropped"] >= 1, s3
