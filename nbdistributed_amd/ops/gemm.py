@@ -656,8 +656,9 @@ def block_graphs(enable=None) -> int:
     then on — one graph launch for its seven kernels.  The block's outputs then live in static
     memory: they keep this pass's values until that block's next forward, so a caller keeping
     block outputs across steps must clone them.  ``enable=2`` (``NBD_BLOCK_GRAPHS=2``) graphs the
-    backward too where every weight gradient goes to a DDP bucket slice.  Bit-identical to the
-    eager block.  ``enable=None`` queries; True = 1; returns the previous mode (0, 1, 2)."""
+    backward too where every weight gradient goes to a DDP bucket slice.  In mode 1 a run of
+    blocks that replays steadily is chained into one stack graph (one launch per forward;
+    ``NBD_BLOCK_STACKS=0``: per-block graphs only).  Bit-identical to the eager block.  ``enable=None`` queries; True = 1; returns the previous mode (0, 1, 2)."""
     import torch
 
     _require()
