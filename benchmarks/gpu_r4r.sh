@@ -3,5 +3,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 for i in 1 2 3; do
-  timeout -k 10 420 python -u bench.py > gpurun_out/bench_r4r$i.json 2> gpurun_out/bench_r4r$i.log || exit $?
+  timeout -k 10 420 python -u bench.py > gpurun_out/bench_r4ac$i.json 2> gpurun_out/bench_r4ac$i.log || exit $?
 done
