@@ -1105,9 +1105,9 @@ static std::pair<std::shared_ptr<bg::Stack>, size_t> stack_serve(
   auto it = g_slots.find(key);
   if (it == g_slots.end()) return {nullptr, 0};
   Slot& s = it->second;
-  if (!s.g || s.g->x_alias || s.g->ptrs != ptrs || s.g->sig != sig) return {nullptr, 0};
   if (!s.stack) {
     // 3. capture one: a steadily replaying chain of >= 2 graphed blocks starting here
+    if (!s.g || s.g->x_alias || s.g->ptrs != ptrs || s.g->sig != sig) return {nullptr, 0};
     if (s.stack_fail >= 2 || s.steady < 3 || !s.args) return {nullptr, 0};
     std::vector<Key> chain{key};
     for (Key k = key; chain.size() < 256;) {
@@ -1157,6 +1157,14 @@ static std::pair<std::shared_ptr<bg::Stack>, size_t> stack_serve(
     }
     ++g_stat[6];
     s.stack = st;
+    // the members' own graphs are not replayed while the stack serves: free their static memory
+    // (a block the stack stops serving captures its own graph again after two eager calls)
+    for (const Key& k : chain) {
+      Slot& ms = g_slots[k];
+      ms.g.reset();
+      ms.eager = 0;
+      ms.steady = 0;
+    }
   }
   Stack& st = *s.stack;
   if (st.m[0].ptrs != ptrs || st.m[0].sig != sig) {
