@@ -99,10 +99,11 @@ def test_block_graphs_second_forward_before_backward(dev):
     assert eager == 2  # the second forward's two blocks
 
 
-@pytest.mark.parametrize("mode", [1, 2])
-def test_block_graphs_ddp_buckets_and_no_sync(dev, mode):
+@pytest.mark.parametrize("mode,force", [(1, False), (2, False), (2, True)])
+def test_block_graphs_ddp_buckets_and_no_sync(dev, mode, force):
     """DDP bucket gradients (graddst slices), alternating plain and no_sync-accumulated steps: in
-    mode 2 the backward graphs replay with both accumulate patterns."""
+    mode 2 the backward graphs replay with both accumulate patterns; force: the N-GPU code path
+    (a real RCCL all-reduce per bucket at world size 1) with the recorded deferred reductions."""
     from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP
     from nbdistributed_amd.parallel.backend import init_data_plane
     import torch.distributed as dist
@@ -118,7 +119,7 @@ def test_block_graphs_ddp_buckets_and_no_sync(dev, mode):
 
     def run(graphs):
         ops.block_graphs(graphs)
-        m = NbdDDP(copy.deepcopy(base), flat_params=True, grad_mode="bucket")
+        m = NbdDDP(copy.deepcopy(base), flat_params=True, grad_mode="bucket", force_collectives=force)
         outs = []
         for k in (1, 2, 1, 2):
             for p in m.parameters():
