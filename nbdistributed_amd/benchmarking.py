@@ -566,6 +566,12 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
                                        "'nbd*' = native bf16 Llama + FlatAdamW (bf16 params, fp32 master in the optimizer)")
     if "ms_per_step" in out.get("reference", {}) and "ms_per_step" in out.get("reference_native", {}):
         out["reference_native_speedup_same_loop"] = out["reference"]["ms_per_step"] / out["reference_native"]["ms_per_step"]
+    # the eager loop against the whole-step graph (same recipe): plain, and with block/stack graphs
+    g = out.get("nbd_graph", {}).get("ms_per_step")
+    if g:
+        for k in ("nbd", "nbd_block_graphs"):
+            if "ms_per_step" in out.get(k, {}):
+                out[f"{k}_vs_graph"] = out[k]["ms_per_step"] / g
     return out
 
 
