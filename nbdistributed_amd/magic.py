@@ -299,6 +299,11 @@ class MagicCore:
                 self.p(f"  ├─ Memory: {alloc:.1f}GB / {tot:.1f}GB ({pct:.1f}% used)")
                 self.p(f"  ├─ Reserved: {info.get('gpu_memory_reserved', 0.0):.1f}GB   HBM in use (all procs): {used:.1f}GB")
                 self.p(f"  ├─ Backend: {info.get('backend')} (RCCL {info.get('rccl_version')})  HIP {info.get('hip_version')}")
+                bgs = info.get("block_graphs")
+                if bgs and (bgs.get("mode") or bgs.get("live") or bgs.get("stack_replays")):
+                    self.p(f"  ├─ Block graphs: mode {bgs.get('mode')}, {bgs.get('live')} live, "
+                           f"{bgs.get('replays')} replays, {bgs.get('stack_replays')} stack replays "
+                           f"({bgs.get('stack_served')} blocks served), {bgs.get('eager')} eager calls")
             else:
                 self.p(f"  ├─ Device: {info.get('gpu_name', 'CPU')}  backend {info.get('backend')}")
             if info.get("running") and "dead_reason" not in info:

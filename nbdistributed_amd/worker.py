@@ -244,6 +244,14 @@ class DistributedWorker:
             from .parallel.backend import rccl_version
 
             st["rccl_version"] = rccl_version()
+            ops_lib = sys.modules.get("nbdistributed_amd.ops._lib")
+            if ops_lib is not None and getattr(ops_lib, "_loaded", False):  # (never loads it for a status)
+                try:
+                    from .ops import block_graphs, block_graphs_stats
+
+                    st["block_graphs"] = dict(block_graphs_stats(), mode=block_graphs())
+                except Exception:  # noqa: BLE001 - status must not fail
+                    pass
         if torch is not None:
             st["torch_version"] = torch.__version__
             st["hip_version"] = getattr(torch.version, "hip", None)

@@ -188,3 +188,27 @@ def test_graphed_training_step_matches_eager(gpu_session):
     r = gpu_session.execute(GRAPH, render=False, raise_on_error=False)
     assert r.ok, r.errors
     assert r.results[0]["echo"] == "(True, True, 5, 7)", r.results[0]
+
+
+def test_status_reports_block_graph_activity(gpu_session):
+    """%dist_status's per-rank block-graph line: the worker reports the per-block / stack graph
+    counters once the native ops are loaded."""
+    code = """
+from nbdistributed_amd import ops
+from nbdistributed_amd.models.llama import LlamaConfig, LlamaForSequenceClassification
+torch.manual_seed(0)
+_m = LlamaForSequenceClassification(LlamaConfig.smollm2_135m(num_hidden_layers=2)).to(device, torch.bfloat16)
+_m.model.block_graphs = 1
+_ids = torch.randint(1, 49152, (2, 128), device=device)
+for _ in range(8):
+    _m(_ids, torch.ones_like(_ids), torch.tensor([0, 1], device=device))[0].backward()
+torch.cuda.synchronize()
+ops.block_graphs_stats()["stack_replays"]
+"""
+    r = gpu_session.execute(code, render=False)
+    assert r.ok, r.errors
+    assert int(r.results[0]["echo"]) >= 1, r.results[0]
+    st = gpu_session.status()
+    bg = st[0].get("block_graphs")
+    assert bg is not None and bg["stack_replays"] >= 1 and bg["captures"] >= 2, bg
+    gpu_session.execute("del _m\nimport gc; gc.collect()", render=False)
