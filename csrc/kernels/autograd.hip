@@ -953,9 +953,13 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
   for (at::IntArrayRef p : {plan_qkv, plan_o, plan_mlp}) sig.insert(sig.end(), p.begin(), p.end());
   const Key key{w_qkv.data_ptr(), h.size(0), h.size(1), h.get_device()};
   auto make_args = [&] {
+    // variable_data(): the data only — a registry holding a cast weight's autograd history would
+    // keep that pass's AccumulateGrad nodes alive (the stream hazard of x_in below)
+    auto vd = [](const optional<Tensor>& t) { return t ? optional<Tensor>(t->variable_data()) : c10::nullopt; };
     auto a = std::make_shared<Args>();
-    a->w_qkv = w_qkv, a->w_o = w_o, a->w_post = w_post, a->w_gu = w_gu, a->w_down = w_down, a->w_next = w_next;
-    a->b_qkv = b_qkv, a->b_o = b_o, a->cos = cos, a->sin = sin;
+    a->w_qkv = w_qkv.variable_data(), a->w_o = w_o.variable_data(), a->w_post = w_post.variable_data();
+    a->w_gu = w_gu.variable_data(), a->w_down = w_down.variable_data(), a->w_next = w_next.variable_data();
+    a->b_qkv = vd(b_qkv), a->b_o = vd(b_o), a->cos = vd(cos), a->sin = vd(sin);
     a->plan_qkv = plan_qkv.vec(), a->plan_o = plan_o.vec(), a->plan_mlp = plan_mlp.vec();
     a->H = H, a->Hkv = Hkv, a->scale = scale, a->eps = eps;
     return a;

@@ -288,3 +288,38 @@ def test_block_stack_graph_bit_identical_and_deviation(dev):
     s3 = ops.block_graphs_stats()
     assert torch.equal(l2, l3) and torch.equal(p2, p3)
     assert s3["stacks_dropped"] - s2["stacks_dropped"] >= 1, s3
+
+
+def test_stack_then_whole_step_graph(dev):
+    """Eager steps long enough for a stack graph, then the same model captured whole by
+    GraphedStep (block graphs suspended inside): losses and parameters equal the run without
+    block graphs — the graph registries hold no autograd history that could leak into the
+    capture (the stream hazard of FINDINGS §30)."""
+    from nbdistributed_amd.graphs import GraphedStep
+
+    base = _model(dev, layers=2, seed=13)
+    batches = _batches(dev, n=1)
+
+    def run(mode):
+        ops.block_graphs(mode)
+        ops.block_graphs_reset()
+        m = copy.deepcopy(base)
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-3, capturable=True, foreach=False)
+
+        def step(x, y):
+            loss = m(x, torch.ones_like(x), y)[0]
+            loss.backward()
+            opt.step()
+            opt.zero_grad(set_to_none=False)
+            return loss.detach()
+
+        ls = [step(*batches[0]).clone() for _ in range(9)]  # eager: per-block graphs, then a stack
+        call = GraphedStep(step, batches[0], warmup=2, optimizers=[opt])
+        ls += [call(*batches[0]).clone() for _ in range(4)]
+        torch.cuda.synchronize()
+        return torch.stack(ls), torch.cat([p.detach().float().flatten() for p in m.parameters()])
+
+    l0, p0 = run(0)
+    l1, p1 = run(1)
+    assert ops.block_graphs_stats()["stack_replays"] >= 1
+    assert torch.equal(l0, l1) and torch.equal(p0, p1)
