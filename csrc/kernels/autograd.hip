@@ -841,9 +841,23 @@ bool is_graph_output(const Tensor& x) {
 
 // Capture `body` into `g` on a side stream ordered after the caller's stream, which then waits
 // for it.  Returns the error ("" = captured).
+// A stream of our own per device for the captures: a pool stream could be the one a process
+// group's collectives run on (ProcessGroupNCCL takes its streams from the same pool).
+c10::hip::HIPStreamMasqueradingAsCUDA capture_stream(c10::DeviceIndex dev) {
+  static std::mutex mu;
+  static std::unordered_map<int, hipStream_t> streams;
+  std::lock_guard<std::mutex> lk(mu);
+  hipStream_t& st = streams[dev];
+  if (st == nullptr) {
+    const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, dev));
+    C10_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  }
+  return c10::hip::getStreamFromExternalMasqueradingAsCUDA(st, dev);
+}
+
 std::string capture(at::cuda::CUDAGraph& g, const std::function<void()>& body) {
   auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA();
-  auto side = c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, cur.device_index());
+  auto side = capture_stream(cur.device_index());
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   C10_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
   C10_HIP_CHECK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
