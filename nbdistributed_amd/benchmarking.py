@@ -72,15 +72,29 @@ from nbdistributed_amd.parallel import DistributedDataParallel as _NbdDDP
 from nbdistributed_amd.optim import FlatAdamW as _FlatAdamW
 from torch.nn.parallel import DistributedDataParallel as _TorchDDP
 
-def _nbd_time_steps(step, steps, warm):
+def _nbd_time_steps(step, steps, warm, per_step=False):
+    # per_step: a HIP event after every timed step (graph replays), so a slow arm shows whether
+    # its first replays or its steady state are slow
     for _ in range(warm):
         step()
     _nbd_barrier()
+    evs = None
+    if per_step and device.type == "cuda":
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        evs[0].record()
     t = _t.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
         out = step()
+        if evs is not None:
+            evs[i + 1].record()
     _nbd_sync()
-    return (_t.perf_counter() - t) / steps * 1e3, float(out)
+    ms = (_t.perf_counter() - t) / steps * 1e3
+    if evs is None:
+        return ms, float(out)
+    d = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+    rest = sorted(d[3:]) or sorted(d)
+    return ms, float(out), {"replay_ms_first3": [round(x, 4) for x in d[:3]],
+                            "replay_ms_median": round(rest[len(rest) // 2], 4), "replay_ms_max": round(max(d), 4)}
 
 def _nbd_wrap(m, impl, **kw):
     if impl == "nbd":
@@ -115,11 +129,11 @@ def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small", force=False):
         from nbdistributed_amd.graphs import GraphedStep
         g = GraphedStep(step, (x,), warmup=3, optimizers=[opt])
         run = lambda: g(x)
-    ms, loss = _nbd_time_steps(run, steps, warm)
+    res = _nbd_time_steps(run, steps, warm, per_step=impl == "flatgraph")
     del model, opt, m, x, run
     if device.type == "cuda":
         torch.cuda.empty_cache()
-    return ms, loss
+    return res
 
 def _nbd_linear_bench(steps, warm, rows, impl, dim=4096):
     torch.manual_seed(0)
@@ -141,13 +155,63 @@ def _nbd_linear_bench(steps, warm, rows, impl, dim=4096):
 """
 
 
+def _echo(d) -> str:
+    return d.get("echo") or d["output"].strip().splitlines()[-1]  # echo = the last expression only
+
+
 def _max_over_ranks(res) -> float:
-    vals = []
+    return max(float(_echo(res.results[r]).strip("()").split(",")[0]) for r in res.ranks)
+
+
+def _replay_detail(res) -> Optional[Dict[str, Any]]:
+    """The per-replay HIP-event record (``_nbd_time_steps(per_step=True)``) of the slowest rank,
+    or None (eager arms, CPU)."""
+    import ast
+
+    best = None
     for r in res.ranks:
-        d = res.results[r]
-        out = d.get("echo") or d["output"].strip().splitlines()[-1]  # echo = the last expression only
-        vals.append(float(out.strip("()").split(",")[0]))
-    return max(vals)
+        try:
+            t = ast.literal_eval(_echo(res.results[r]))
+        except (ValueError, SyntaxError):
+            continue
+        if isinstance(t, tuple) and len(t) >= 3 and isinstance(t[2], dict) and (best is None or t[0] > best[0]):
+            best = (t[0], dict(t[2], rank=r))
+    return None if best is None else best[1]
+
+
+def _err(e: BaseException) -> str:
+    if hasattr(e, "result") and e.args:  # DistributedExecutionError: its str() holds every traceback
+        return f"{type(e).__name__}: {e.args[0]}"[:800]
+    return f"{type(e).__name__}: {e}"[:800]
+
+
+def _rank_tracebacks(e: BaseException) -> Optional[Dict[str, str]]:
+    """Per-rank tail of the first exception of a failed cell (ranks that died: why), so an arm
+    that can only fail at N > 1 is diagnosable from the result line alone."""
+    res = getattr(e, "result", None)
+    if res is None:
+        return None
+    out = {}
+    for r, info in sorted(getattr(res, "errors", {}).items()):
+        tb = (info.get("traceback") or "").rstrip() or str(info.get("error"))
+        out[str(r)] = tb[-700:]
+    for r, why in sorted(getattr(res, "dead", {}).items()):
+        out[str(r)] = f"died: {why}"
+    return out or None
+
+
+def _record_error(dst: Dict[str, Any], key: str, e: BaseException) -> None:
+    dst[key] = _err(e)
+    tbs = _rank_tracebacks(e)
+    if tbs:
+        dst[key + "_rank_tracebacks"] = tbs
+
+
+_ARM_T0 = [time.monotonic()]  # run_all's start: arm start offsets are relative to it
+
+
+def _arm_start(out: Dict[str, Any], arm: str) -> None:
+    out.setdefault("arm_start_s", {})[arm] = round(time.monotonic() - _ARM_T0[0], 2)
 
 
 def _graph_arms(n: int) -> bool:
@@ -177,6 +241,7 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
     # primary: bf16 params re-homed into the DDP buckets + FlatAdamW (fp32 master/moments, one
     # fused HIP kernel per bucket reading the all-reduced bucket); secondary: fp32 params +
     # autocast + torch fused AdamW through nbd DDP (bf16 wire)
+    _arm_start(out, "flat")
     r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flat', {config!r})", render=False)
     ms = _max_over_ranks(r)
     toks = n * B * T / (ms / 1e3)
@@ -186,12 +251,13 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
         out["mfu"] = 6 * 124_439_808 * toks / (2.5e15 * n)
     tick()
     try:  # ZeRO-2: reduce-scattered gradients, optimizer on this rank's slice, parameter all-gather
+        _arm_start(out, "zero2")
         r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'zero', {config!r})", render=False)
         zms = _max_over_ranks(r)
         out.update(zero2_ms_per_step=zms, zero2_tokens_per_s=n * B * T / (zms / 1e3),
                    zero2_recipe="as the primary recipe with DistributedDataParallel(shard=True) (ZeRO-2)")
     except Exception as e:  # noqa: BLE001 - recorded, the other recipes still run
-        out["zero2_error"] = f"{type(e).__name__}: {e}"[:400]
+        _record_error(out, "zero2_error", e)
         if isinstance(e, TimeoutError):
             raise
     tick()
@@ -216,12 +282,16 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
     tick()
     if _graph_arms(n):
         try:
+            _arm_start(out, "graph")
             r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flatgraph', {config!r})", render=False)
             gms = _max_over_ranks(r)
             out.update(graph_ms_per_step=gms, graph_tokens_per_s=n * B * T / (gms / 1e3),
                        graph_recipe="as the primary recipe, whole step captured in one HIP graph (GraphedStep)")
+            rd = _replay_detail(r)
+            if rd:
+                out["graph_replays"] = rd
         except Exception as e:  # noqa: BLE001
-            out["graph_error"] = f"{type(e).__name__}: {e}"[:400]
+            _record_error(out, "graph_error", e)
             if isinstance(e, TimeoutError):
                 raise
         tick()
@@ -234,11 +304,15 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
         out["collective_path"] = cp
         for key, impl in (("ms_per_step", "flat"), ("graph_ms_per_step", "flatgraph"), ("zero2_ms_per_step", "zero")):
             try:
+                _arm_start(cp, key)
                 r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, {impl!r}, {config!r}, force=True)",
                                     render=False)
                 cp[key] = _max_over_ranks(r)
+                rd = _replay_detail(r)
+                if rd:
+                    cp[key.replace("ms_per_step", "replays")] = rd
             except Exception as e:  # noqa: BLE001 - recorded, the other arms still run
-                cp[key.replace("ms_per_step", "error")] = f"{type(e).__name__}: {e}"[:400]
+                _record_error(cp, key.replace("ms_per_step", "error"), e)
                 if isinstance(e, TimeoutError):
                     raise
             tick()
@@ -490,7 +564,7 @@ def _nbd_notebook_bench(steps, warm, bs=16, seq=128, mode="reference", small=Fal
             sched.step()
             return out
     try:
-        ms, loss = _nbd_time_steps(step, steps, warm)
+        res = _nbd_time_steps(step, steps, warm, per_step=mode in ("nbd_graph", "nbd_block_graphs"))
     finally:
         if mode == "nbd_block_graphs" and device.type == "cuda":
             _ops.block_graphs(_prev_bg)
@@ -498,7 +572,7 @@ def _nbd_notebook_bench(steps, warm, bs=16, seq=128, mode="reference", small=Fal
     gc.collect()
     if device.type == "cuda":
         torch.cuda.empty_cache()
-    return ms, loss
+    return res
 """
 
 REFERENCE_NOTEBOOK_MS_PER_STEP = 126.6  # BASELINE.md: 1 epoch = 14.56 s / 115 steps, 2 GPUs
@@ -534,27 +608,37 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
         modes.append("nbd_graph")
     for mode in modes:
         try:
+            _arm_start(out, mode)
             r = session.execute(f"_nbd_notebook_bench({steps}, {warmup}, mode={mode!r}, small={small})", render=False)
         except Exception as e:  # noqa: BLE001 - recorded, the other arms still run
-            out[mode] = {"error": f"{type(e).__name__}: {e}"[:400]}
+            out[mode] = {}
+            _record_error(out[mode], "error", e)
             if isinstance(e, TimeoutError):
                 raise
             continue
         ms = _max_over_ranks(r)
         out[mode] = {"ms_per_step": ms, "samples_per_s": n * 16 / (ms / 1e3), "recipe": recipes[mode]}
+        rd = _replay_detail(r)
+        if rd:
+            out[mode]["replays"] = rd
         tick()
     if n == 1 and force_collectives:  # the N-GPU code path on one GPU (see bench_ddp)
         for mode, base in (("nbd_collective_path", "nbd"), ("nbd_graph_collective_path", "nbd_graph")):
             if "ms_per_step" not in out.get(base, {}):
                 continue
             try:
+                _arm_start(out, mode)
                 r = session.execute(f"_nbd_notebook_bench({steps}, {warmup}, mode={base!r}, small={small}, force=True)",
                                     render=False)
                 ms = _max_over_ranks(r)
                 out[mode] = {"ms_per_step": ms, "vs_no_collectives": ms / out[base]["ms_per_step"],
                              "recipe": recipes[base] + "; real RCCL collectives per bucket (forced at world size 1)"}
+                rd = _replay_detail(r)
+                if rd:
+                    out[mode]["replays"] = rd
             except Exception as e:  # noqa: BLE001
-                out[mode] = {"error": f"{type(e).__name__}: {e}"[:400]}
+                out[mode] = {}
+                _record_error(out[mode], "error", e)
                 if isinstance(e, TimeoutError):
                     raise
             tick()
@@ -653,10 +737,9 @@ def _phase(session, out: Dict[str, Any], name: str, fn, timeout_s: float, deadli
         out[name] = fn()
     except Exception as e:  # noqa: BLE001 - recorded in the result line
         part = out.get(name)
-        if isinstance(part, dict) and part:  # arms measured before the failure stay
-            part["error"] = f"{type(e).__name__}: {e}"[:800]
-        else:
-            out[name] = {"error": f"{type(e).__name__}: {e}"[:800]}
+        if not (isinstance(part, dict) and part):  # arms measured before the failure stay
+            part = out[name] = {}
+        _record_error(part, "error", e)
         _log(f"phase {name} failed: {type(e).__name__}: {str(e)[:300]}")
         if isinstance(e, TimeoutError):
             out["aborted"] = name
@@ -675,6 +758,8 @@ def _phase(session, out: Dict[str, Any], name: str, fn, timeout_s: float, deadli
 # The driver allows bench.py 600 s in all (torchrun start, imports and RCCL init included): the
 # phases share a global budget well inside it, and the result is checkpointed after each phase
 DEFAULT_DEADLINE_S = float(os.environ.get("NBD_BENCH_DEADLINE_S", "420"))
+# all-reduce size cap when the workers have no GPU (gloo on the CPU: plumbing, not bandwidth)
+CPU_AR_BYTES = int(os.environ.get("NBD_BENCH_CPU_AR_BYTES", str(1 << 20)))
 
 
 def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: bool = False,
@@ -686,6 +771,7 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
     caller can persist what has been measured (bench.py writes it where rank 0 reads it, even if
     a later phase hangs)."""
     n = session.world_size
+    _ARM_T0[0] = time.monotonic()
     deadline = time.monotonic() + (DEFAULT_DEADLINE_S if deadline_s is None else deadline_s)
     prev_deadline = getattr(session, "deadline", None)
     session.deadline = deadline
@@ -726,16 +812,21 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
                    phase_timeout_s, deadline)
             ckpt(out)
         gpu = bool(session.ready.get(0, {}).get("cuda_available"))
-        if allreduce and gpu:
-            _log(f"phase 2: {ar_bytes / 2**30:.2f} GiB bf16 all_reduce")
-            _phase(session, out, "allreduce", lambda: bench_allreduce(session, ar_bytes), phase_timeout_s, deadline, 10.0)
+        if not gpu:  # CPU/gloo (tests, a GPU-less host): the same cells on small buffers
+            ar_bytes = min(ar_bytes, CPU_AR_BYTES)
+        if allreduce:
+            _log(f"phase 2: {ar_bytes / 2**20:.2f} MiB bf16 all_reduce")
+            _phase(session, out, "allreduce", lambda: bench_allreduce(session, ar_bytes, iters=20 if gpu else 3,
+                                                                      warm=5 if gpu else 1),
+                   phase_timeout_s, deadline, 10.0)
             ar = out["allreduce"]
             if "time_ms" in ar:
                 _log(f"all_reduce {ar['time_ms']:.3f} ms busbw {ar['busbw_GBps']}")
             ckpt(out)
-        if sweep and gpu:
+        if sweep:
             _log("phase 3: all_reduce sweep")
-            _phase(session, out, "sweep", lambda: bench_sweep(session), phase_timeout_s, deadline, 20.0)
+            _phase(session, out, "sweep", lambda: bench_sweep(session, max_bytes=1 << 30 if gpu else CPU_AR_BYTES),
+                   phase_timeout_s, deadline, 20.0)
             ckpt(out)
         if bcast and gpu:
             _log("phase 3b: %%rank[0] Linear(4096) build + broadcast (config 3)")
@@ -766,6 +857,17 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
         return out
     finally:
         session.deadline = prev_deadline
+
+
+def error_line(error: str, n: int, steps: int, warmup: int) -> Dict[str, Any]:
+    """The result line when nothing could be measured (e.g. the ranks never all joined): the
+    contract keys with a null value and the reason."""
+    return {"metric": METRIC, "value": None, "unit": "ms", "n_gpus": n, "steps": steps, "warmup": warmup,
+            "ms_per_step": None, "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic",
+            "config": {"model": "%%distributed trivial cell (1 + 1) + 1 GiB bf16 all_reduce cell via RCCL/xGMI",
+                       "global_batch": None, "seq_len": None, "parallelism": f"dp{n}"},
+            "error": error}
 
 
 def result_line(res: Dict[str, Any], n: int, steps: int, warmup: int) -> Dict[str, Any]:

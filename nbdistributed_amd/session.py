@@ -169,6 +169,8 @@ class Session:
         self.init_s: Optional[float] = None
         self._native_lock = threading.Lock()
         self.last_cell: Optional[CellResult] = None
+        # why the last start()/attach() failed: ranks connected to the control plane / READY
+        self.start_failure: Optional[Dict[str, Any]] = None
 
     # ------------------------------------------------------------------ lifecycle
     @property
@@ -209,7 +211,8 @@ class Session:
             self.ready = comm.wait_ready(list(range(num_processes)),
                                          startup_timeout if startup_timeout is not None else self.cfg.startup_timeout_s,
                                          alive=pm.dead_ranks)
-        except BaseException:
+        except BaseException as e:
+            self._record_start_failure(comm, e)
             self.shutdown(graceful=False)
             raise
         self.started_at = time.time()
@@ -234,12 +237,18 @@ class Session:
             on_endpoint(comm.endpoint, comm.token)
         try:
             self.ready = comm.wait_ready(list(range(world_size)), startup_timeout or self.cfg.startup_timeout_s)
-        except BaseException:
+        except BaseException as e:
+            self._record_start_failure(comm, e)
             self.shutdown(graceful=False)
             raise
         self.gpu_ids = [self.ready[r].get("gpu_id") for r in range(world_size)]
         self.started_at = time.time()
         return self.ready
+
+    def _record_start_failure(self, comm: CommunicationManager, e: BaseException) -> None:
+        ready = [r for r, d in comm.ready.items() if isinstance(d, dict) and "error" not in d]
+        self.start_failure = {"connected": len(set(comm.connected) | set(ready)), "ready": len(ready),
+                              "world": self.world_size, "error": f"{type(e).__name__}: {e}"}
 
     def shutdown(self, graceful: bool = True, timeout: float = 5.0) -> None:
         comm, pm = self.comm, self.pm

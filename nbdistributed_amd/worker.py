@@ -676,6 +676,12 @@ def main(argv=None) -> int:
                               gpu_id=args.gpu_id, device_index=args.device_index, backend=args.backend,
                               token=token, capture=not args.no_capture)
     code = 0
+    stall = os.environ.get("NBD_FAULT_STALL_RANK")
+    if stall is not None and int(stall) == w.rank:
+        # fault injection (tests): this rank never joins — the coordinator's bounded rendezvous
+        # must report it instead of waiting forever
+        time.sleep(float(os.environ.get("NBD_FAULT_STALL_S", "3600")))
+        return 4
     try:
         w.connect()
         try:

@@ -108,6 +108,58 @@ def test_bench_py_contract_cpu(n):
     assert d["cell_magic_p50_ms"] > 0 and "ide_sync=True" in d["cell_magic_note"]
     # every worker reports the process group it sees
     assert d["rccl_world_size"] == {str(r): n for r in range(n)}
+    assert d["launch"].startswith("self" if n == 1 else "attach")
+
+
+def _selflaunch(n, env_extra=None, timeout=300, args=()):
+    """``python bench.py --gpus N`` with no torchrun variables: bench.py starts its own N workers."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "TORCHELASTIC_RUN_ID")}
+    env.update({"NBD_BENCH_IPYTHON": "0"}, **(env_extra or {}))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "10", "--warmup", "2",
+           "--no-ddp", "--no-notebook", "--no-bcast", *args]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd="/tmp", env=env)
+    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
+    return res, lines
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_py_self_launch(n):
+    """Without torchrun, ``--gpus N`` starts N workers itself (as ``%dist_init -n N``): every rank
+    sees a world of N and the all-reduce cells report a bus bandwidth."""
+    res, lines = _selflaunch(n)
+    assert res.returncode == 0 and len(lines) == 1, res.stdout[-2000:] + res.stderr[-3000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["value"] > 0 and d["config"]["parallelism"] == f"dp{n}"
+    assert d["rccl_world_size"] == {str(r): n for r in range(n)}
+    assert d["allreduce_busbw_GBps"] is not None and d["allreduce_busbw_GBps"] > 0 and d["allreduce_correct"]
+    assert d["allreduce_peak_busbw_GBps"] > 0 and d["launch"].startswith("self")
+
+
+def test_bench_py_rank_that_never_joins_is_reported():
+    """One rank never starts: the line (value null, "rendezvous: 1/2 ranks joined") is printed
+    before the rendezvous limit runs out, with a non-zero exit status — never a silent hang."""
+    res, lines = _selflaunch(2, {"NBD_FAULT_STALL_RANK": "1", "NBD_BENCH_RENDEZVOUS_S": "20"}, timeout=120)
+    assert len(lines) == 1, res.stdout[-2000:] + res.stderr[-3000:]
+    d = json.loads(lines[0])
+    assert d["value"] is None and d["error"] == "rendezvous: 1/2 ranks joined", d
+    assert d["rendezvous"]["ready"] == 0 and res.returncode == 3
+
+
+def test_bench_py_torchrun_rank_that_never_joins_is_reported():
+    """The same under torchrun: rank 1 never connects, rank 0 is stuck in the RCCL/gloo rendezvous;
+    rank 0 still prints the error line once its coordinator gives up."""
+    env = dict(os.environ, NBD_FAULT_STALL_RANK="1", NBD_BENCH_RENDEZVOUS_S="15", NBD_BENCH_GRACE_S="3",
+               NBD_BENCH_IPYTHON="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29657", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "5", "--warmup", "1"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=150, cwd="/tmp", env=env)
+    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, res.stdout[-2000:] + res.stderr[-3000:]
+    d = json.loads(lines[0])
+    assert d["value"] is None and d["error"].startswith("rendezvous: ") and d["error"].endswith("/2 ranks joined")
+    assert res.returncode != 0
 
 
 def test_world1_reports_no_bandwidth():
@@ -137,7 +189,7 @@ def test_magic_path_cells(sess):
 
 
 def _run_bench(env_extra, timeout=240):
-    env = dict(os.environ, **env_extra)
+    env = dict(os.environ, NBD_BENCH_IPYTHON="0", **env_extra)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "1"]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd="/tmp", env=env)
     lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
@@ -158,6 +210,7 @@ def test_bench_line_survives_the_hard_deadline():
     the checkpointed result itself."""
     res, lines = _run_bench({"NBD_BENCH_FAULT_HANG": "600", "NBD_BENCH_DEADLINE_S": "400",
                              "NBD_BENCH_HARD_S": "30", "NBD_BENCH_GRACE_S": "3"})
-    assert res.returncode == 0 and len(lines) == 1, res.stdout[-2000:] + res.stderr[-3000:]
+    # a partial line is printed, and the exit status says the run did not complete
+    assert res.returncode == 3 and len(lines) == 1, res.stdout[-2000:] + res.stderr[-3000:]
     d = json.loads(lines[0])
-    assert d["value"] > 0 and d["partial"] is True
+    assert d["value"] > 0 and d["partial"] is True and d["partial_reason"] == "hard deadline"
