@@ -20,12 +20,12 @@ def load_library(build: bool = True) -> bool:
             return _loaded
         import torch
 
-        from .._native import OPS_HIP_SOURCES, OPS_LIB, build_ops
+        from .._native import OPS_HIP_SOURCES, build_ops, ops_lib_path
 
         try:
             path = os.environ.get("NBD_OPS_LIB")
             if not path:
-                path = str(build_ops()) if build and OPS_HIP_SOURCES else str(OPS_LIB)
+                path = str(build_ops()) if build and OPS_HIP_SOURCES else str(ops_lib_path())
             torch.ops.load_library(path)
             _loaded = True
         except Exception as e:  # pragma: no cover - reported by native_available()/_require
