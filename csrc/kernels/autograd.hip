@@ -40,6 +40,7 @@
 #include <mutex>
 #include <tuple>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "gemm_common.h"
 #include "graddst.h"
@@ -778,9 +779,11 @@ struct Stack {
   size_t next = 0;             // members served in the current pass
   std::atomic<int> held{0};    // served members whose autograd nodes still hold the memory
   Key head{};
+  int64_t owner = 0;           // the head slot's owner (per-model reset)
 };
 
 struct Slot {
+  int64_t owner = 0;  // the model that made the calls (LlamaModel's id; per-model reset)
   int eager = 0, captures = 0, misses = 0;
   bool off = false;
   std::shared_ptr<Graph> g;
@@ -801,6 +804,7 @@ std::atomic<bool> g_suspended{false};                           // overrides per
 // forward captures, replays, eager calls; backward captures, replays, eager calls
 std::atomic<int64_t> g_stat[10];  // + stack captures, stack replays, stack-served blocks, stacks dropped
 std::weak_ptr<Stack> g_active;    // the stack serving the current pass
+std::atomic<int> g_fail_bwd{0};   // fault injection (tests): fail this many backward captures
 
 // 0 off, 1 forward graphs, 2 forward and backward graphs (NBD_BLOCK_GRAPHS)
 int mode() {
@@ -952,7 +956,7 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
                                               const Tensor& w_down, const Tensor& w_next, at::IntArrayRef plan_qkv,
                                               at::IntArrayRef plan_o, at::IntArrayRef plan_mlp, int64_t H,
                                               int64_t Hkv, double scale, double eps, const optional<Tensor>& cos,
-                                              const optional<Tensor>& sin) {
+                                              const optional<Tensor>& sin, int64_t owner) {
   using namespace bg;
   if (stream_capturing()) return nullptr;  // inside a whole-step capture: the outer graph takes it
   const Tensor* ts[] = {&w_qkv, b_qkv ? &*b_qkv : nullptr, &w_o, b_o ? &*b_o : nullptr, &w_post, &w_gu,
@@ -982,6 +986,7 @@ static std::shared_ptr<bg::Graph> block_graph(const Tensor& x, const Tensor& h, 
   {
     std::lock_guard<std::mutex> lk(g_mu);
     Slot& s = g_slots[key];
+    s.owner = owner;
     if (s.off) return nullptr;
     if (s.g && (s.g->ptrs != ptrs || s.g->sig != sig)) s.g.reset(), s.eager = 0, s.args.reset(), s.steady = 0;
     if (s.g) {
@@ -1141,6 +1146,7 @@ static std::pair<std::shared_ptr<bg::Stack>, size_t> stack_serve(
     if (chain.size() < 2) return {nullptr, 0};
     auto st = std::make_shared<Stack>();
     st->head = key;
+    st->owner = s.owner;
     st->x_in = at::empty_like(x, at::MemoryFormat::Contiguous);
     st->h_in = at::empty_like(h, at::MemoryFormat::Contiguous);
     st->m.resize(chain.size());
@@ -1365,12 +1371,25 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
       }
       bool ended = false;
     } rec(&B->claims);
-    err = capture(*B->g, [&] { block_bwd(sv, plans, H, Hkv, scale, shape, need_x, need_h, B->dx_in, B->dh_in, o); });
+    err = capture(*B->g, [&] {
+      block_bwd(sv, plans, H, Hkv, scale, shape, need_x, need_h, B->dx_in, B->dh_in, o);
+      int f = g_fail_bwd.load();
+      while (f > 0 && !g_fail_bwd.compare_exchange_weak(f, f - 1)) {
+      }
+      if (f > 0) throw std::runtime_error("injected backward capture failure");
+    });
     B->deferred = rec.end();
   }
   B->warm_refs = castbuf::drop_kept(gemm::gemm_warm_take_refs());
-  if (!err.empty()) G.bwd_off = true;
-  TORCH_CHECK(err.empty(), "nbd: a decoder block's backward graph capture failed: ", err);
+  if (!err.empty()) {
+    // nothing captured ran: undo the pass bookkeeping of the claims made while capturing, so the
+    // eager backward the caller runs next claims the same bucket slices (a training step must not
+    // be lost to a performance feature)
+    G.bwd_off = true;
+    graddst::release(B->claims);
+    TORCH_WARN_ONCE("nbd: a decoder block's backward graph capture failed (", err, "); the block's backward runs eagerly");
+    return false;
+  }
   // every weight gradient must be its claimed slice (else it would be static graph memory)
   B->slot.assign(B->claims.size(), -1);
   bool valid = true;
@@ -1422,6 +1441,8 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
     const ht::Scope hs(ht::FWD);
     at::AutoDispatchBelowADInplaceOrView guard;
     ctx->set_materialize_grads(false);
+    const int64_t owner = graph_mode >> 8;  // (llama_block_ag packs the model id above the mode)
+    graph_mode &= 0xff;
     std::vector<Tensor> save;
     Tensor x_out, h_out;
     std::shared_ptr<bg::Graph> gr;
@@ -1431,7 +1452,7 @@ struct LlamaBlockFn : public torch::autograd::Function<LlamaBlockFn> {
                        scale, eps, cos, sin);
     if (!sh.first && graph_mode >= 1)
       gr = block_graph(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp, H, Hkv,
-                       scale, eps, cos, sin);
+                       scale, eps, cos, sin, owner);
     if (sh.first) {
       const bg::StackMember& mb = sh.first->m[sh.second];
       save = mb.saved;
@@ -1506,14 +1527,16 @@ std::tuple<Tensor, Tensor> llama_block_ag(const Tensor& x, const Tensor& h, cons
                                           const Tensor& w_post, const Tensor& w_gu, const Tensor& w_down,
                                           const Tensor& w_next, at::IntArrayRef plan_qkv, at::IntArrayRef plan_o,
                                           at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv, double scale, double eps,
-                                          const optional<Tensor>& cos, const optional<Tensor>& sin, int64_t graphs) {
+                                          const optional<Tensor>& cos, const optional<Tensor>& sin, int64_t graphs,
+                                          int64_t owner) {
   // graphs: the caller's per-model mode (LlamaModel.block_graphs), -1 = the process setting;
   // only parameters, or weights cast into a kept buffer (models.native(): stable addresses)
   int64_t mode = graphs < 0 ? bg::mode() : std::min<int64_t>(graphs, 2);
   if (bg::g_suspended.load(std::memory_order_relaxed)) mode = 0;  // (graphs.GraphedStep)
   if (!(c10::GradMode::is_enabled() && x.is_cuda() && (w_qkv.is_leaf() || castbuf::kept(w_qkv)))) mode = 0;
+  // owner: the model's id (LlamaModel), recorded with its block graphs for a per-model reset
   auto r = LlamaBlockFn::apply(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp,
-                               H, Hkv, scale, eps, cos, sin, mode);
+                               H, Hkv, scale, eps, cos, sin, mode | (std::max<int64_t>(owner, 0) << 8));
   return {r[0], r[1]};
 }
 
@@ -1523,7 +1546,7 @@ std::tuple<Tensor, Tensor> llama_block_noag(const Tensor& x, const Tensor& h, co
                                             const Tensor& w_down, const Tensor& w_next, at::IntArrayRef plan_qkv,
                                             at::IntArrayRef plan_o, at::IntArrayRef plan_mlp, int64_t H, int64_t Hkv,
                                             double scale, double eps, const optional<Tensor>& cos,
-                                            const optional<Tensor>& sin, int64_t /*graphs*/) {
+                                            const optional<Tensor>& sin, int64_t /*graphs*/, int64_t /*owner*/) {
   return llama_block_fwd(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plan_qkv, plan_o, plan_mlp, H, Hkv,
                          scale, eps, cos, sin, nullptr);
 }
@@ -1562,6 +1585,63 @@ void llama_block_graphs_reset() {
   bg::g_active.reset();
   bg::g_outs.clear();
 }
+
+// Drop the block graphs made by one model (LlamaModel's finalizer): the other models' graphs stay.
+void llama_block_graphs_reset_owner(int64_t owner) {
+  std::vector<bg::Slot> drop;  // (destroyed after the lock is released)
+  std::vector<std::shared_ptr<bg::Stack>> stacks;  // dropped stacks of this model go too
+  std::lock_guard<std::mutex> lk(bg::g_mu);
+  auto active = bg::g_active.lock();
+  for (auto it = bg::g_slots.begin(); it != bg::g_slots.end();) {
+    if (it->second.owner != owner) {
+      ++it;
+      continue;
+    }
+    if (active && it->second.stack == active) bg::g_active.reset();
+    drop.push_back(std::move(it->second));
+    it = bg::g_slots.erase(it);
+  }
+  for (auto it = bg::g_dropped.begin(); it != bg::g_dropped.end();) {
+    if ((*it)->owner == owner) {
+      stacks.push_back(*it);
+      it = bg::g_dropped.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  std::unordered_set<const bg::Graph*> gone;
+  for (const auto& s : drop)
+    if (s.g) gone.insert(s.g.get());
+  for (auto it = bg::g_outs.begin(); it != bg::g_outs.end();) {
+    auto g = it->second.lock();
+    it = (!g || gone.count(g.get())) ? bg::g_outs.erase(it) : std::next(it);
+  }
+}
+
+// The private memory pools of every live block / stack graph, as [id0, id1, ...] pairs: the
+// caching allocator's segments in those pools are the memory block graphs hold (%dist_status).
+std::vector<int64_t> llama_block_graphs_pools() {
+  std::vector<int64_t> out;
+  auto add = [&](const std::unique_ptr<at::cuda::CUDAGraph>& g) {
+    if (!g) return;
+    const auto id = g->pool();
+    out.push_back((int64_t)id.first);
+    out.push_back((int64_t)id.second);
+  };
+  std::lock_guard<std::mutex> lk(bg::g_mu);
+  for (const auto& kv : bg::g_slots) {
+    if (kv.second.g) {
+      add(kv.second.g->g);
+      for (const auto& b : kv.second.g->bwd) add(b.second->g);
+    }
+    if (kv.second.stack) add(kv.second.stack->g);
+  }
+  for (const auto& st : bg::g_dropped) add(st->g);
+  return out;
+}
+
+// Tests: make the next `n` backward block-graph captures fail (the eager fallback must run).
+void llama_block_graphs_fault(int64_t n) { bg::g_fail_bwd.store((int)n); }
 
 // [captures, replays, eager calls, live graphs, backward captures, replays, eager calls]
 std::vector<int64_t> llama_block_graphs_stats() {
@@ -1789,6 +1869,9 @@ TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
 TORCH_LIBRARY_FRAGMENT(nbd, m) {
   m.def("llama_block_graphs(int mode) -> int", &nbd::ag::llama_block_graphs);
   m.def("llama_block_graphs_reset() -> ()", &nbd::ag::llama_block_graphs_reset);
+  m.def("llama_block_graphs_reset_owner(int owner) -> ()", &nbd::ag::llama_block_graphs_reset_owner);
+  m.def("llama_block_graphs_pools() -> int[]", &nbd::ag::llama_block_graphs_pools);
+  m.def("llama_block_graphs_fault(int n) -> ()", &nbd::ag::llama_block_graphs_fault);
   m.def("llama_block_graphs_stats() -> int[]", &nbd::ag::llama_block_graphs_stats);
   m.def("host_timing(bool reset) -> str", &nbd::ag::host_timing);
   m.def("llama_block_graphs_suspend(bool on) -> bool", &nbd::ag::llama_block_graphs_suspend);

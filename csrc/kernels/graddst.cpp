@@ -63,6 +63,15 @@ at::Tensor claim(const at::Tensor& param, bool& acc) {
 
 at::Tensor peek(const at::Tensor& param, bool& acc) { return lookup(param, acc, false); }
 
+void release(const std::vector<ClaimRecord>& claims) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (const ClaimRecord& c : claims) {
+    if (c.dst == nullptr) continue;  // that claim handed nothing out
+    auto it = g_map.find(c.param);
+    if (it != g_map.end() && it->second.gen == g_gen && it->second.dst.data_ptr() == c.dst) it->second.gen = 0;
+  }
+}
+
 at::Tensor hand_back(const at::Tensor& param, const at::Tensor& dst, bool acc) {
   // AccumulateGrad steals a gradient only while .grad is unset; the slice already holds the sum
   if (acc) param.mutable_grad().reset();

@@ -41,6 +41,10 @@ struct ClaimRecord {
 };
 void record_claims(std::vector<ClaimRecord>* log);
 
+// Undo the pass bookkeeping of recorded claims (a graph capture that failed: nothing it captured
+// ran, so the slices were never written and may be claimed again in this pass).
+void release(const std::vector<ClaimRecord>& claims);
+
 }  // namespace graddst
 
 // Deferred weight-gradient reductions (defer.hip).  A split-K weight-gradient GEMM writes fp32

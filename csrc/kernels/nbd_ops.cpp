@@ -27,6 +27,7 @@ TORCH_LIBRARY(nbd, m) {
   m.def("embedding_bwd(Tensor dy, Tensor idx, int V, Tensor(a!)? grad_out=None, bool accumulate=False) -> Tensor");
   m.def("embedding_tokpos(Tensor idx, Tensor wte, Tensor pos, Tensor wpe, int vocab=-1, Tensor(a!)? err=None) -> Tensor");
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, int n_rot, int head_dim, bool inverse) -> ()");
+  m.def("seqcls_prep(Tensor ids, Tensor? mask, int pad_id, bool has_pad, Tensor(a!) bad) -> (Tensor, Tensor)");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");
   m.def("xent_fwd(Tensor logits, Tensor target, int ignore_index) -> (Tensor, Tensor)");
@@ -47,7 +48,7 @@ TORCH_LIBRARY(nbd, m) {
   m.def("attn_qkv_ag(Tensor qkv, int n_head, int n_kv, bool causal, float scale, Tensor? cos, Tensor? sin) -> Tensor");
   m.def("llama_block_ag(Tensor x, Tensor h, Tensor w_qkv, Tensor? b_qkv, Tensor w_o, Tensor? b_o, Tensor w_post, "
         "Tensor w_gu, Tensor w_down, Tensor w_next, int[] plan_qkv, int[] plan_o, int[] plan_mlp, int n_head, int n_kv, "
-        "float scale, float eps, Tensor? cos, Tensor? sin, int graphs=-1) -> (Tensor, Tensor)");
+        "float scale, float eps, Tensor? cos, Tensor? sin, int graphs=-1, int owner=0) -> (Tensor, Tensor)");
   m.def("cast_group_ag(Tensor[] ps, int dtype) -> Tensor[]");
   m.def("adamw_flat_multi(Tensor[] grads, Tensor(a!)[] params, Tensor(b!)[] masters, Tensor(c!)[] exp_avgs, "
         "Tensor(d!)[] exp_avg_sqs, float lr, float beta1, float beta2, float eps, float weight_decay, int step, "

@@ -300,10 +300,12 @@ class MagicCore:
                 self.p(f"  ├─ Reserved: {info.get('gpu_memory_reserved', 0.0):.1f}GB   HBM in use (all procs): {used:.1f}GB")
                 self.p(f"  ├─ Backend: {info.get('backend')} (RCCL {info.get('rccl_version')})  HIP {info.get('hip_version')}")
                 bgs = info.get("block_graphs")
-                if bgs and (bgs.get("mode") or bgs.get("live") or bgs.get("stack_replays")):
+                if bgs and (bgs.get("mode") or bgs.get("live") or bgs.get("stack_replays") or bgs.get("pools")):
                     self.p(f"  ├─ Block graphs: mode {bgs.get('mode')}, {bgs.get('live')} live, "
                            f"{bgs.get('replays')} replays, {bgs.get('stack_replays')} stack replays "
                            f"({bgs.get('stack_served')} blocks served), {bgs.get('eager')} eager calls")
+                    self.p(f"  ├─ Block-graph memory (framework-held): {bgs.get('reserved_gib', 0.0):.2f}GB reserved "
+                           f"in {bgs.get('pools', 0)} graph pools ({bgs.get('allocated_gib', 0.0):.2f}GB allocated)")
             else:
                 self.p(f"  ├─ Device: {info.get('gpu_name', 'CPU')}  backend {info.get('backend')}")
             if info.get("running") and "dead_reason" not in info:

@@ -14,12 +14,24 @@ i.e. ~12 kernels per block instead of ~70, nothing that synchronises with the ho
 caching-allocator memory — so the whole training step captures into a HIP graph
 (``nbdistributed_amd.graphs.GraphedStep``).  The GPU path needs bf16/f16, head_dim 64 and a
 sequence length that is a multiple of 128; anything else (CPU, fp32) runs the same math in
-plain PyTorch.  Attention is causal with right padding, like the notebook's tokenizer output:
-a non-pad query only ever sees non-pad keys, so no padding mask is needed (left padding is not
-supported).
+plain PyTorch.
+
+HF semantics kept by the one-line swap (``native()``):
+
+* ``attention_mask``: the fused path runs causal attention without a key mask, exact for right
+  padding.  The sequence classifier rotates left-padded rows into right-padded ones in one kernel
+  (``ops.seqcls_prep``; RoPE scores depend on position differences only) and re-indexes the
+  pooled token; a mask with holes is reported (ValueError at the next call: the check is read
+  without a host sync).  The causal LM needs right padding (reported the same way).
+* forward (pre-)hooks and backward hooks on the decoder layers or any of their submodules (or
+  global module hooks): the model then runs module by module, HF's structure — each layer is
+  called as ``layer(hidden_states, ...)`` and returns the residual stream, attention honours the
+  full ``attention_mask`` — so every hook fires and sees HF's activations.
 """
 from __future__ import annotations
 
+import itertools
+import logging
 import os
 import weakref
 from dataclasses import dataclass
@@ -171,6 +183,25 @@ class RMSNorm(nn.Module):
         return ops.rms_norm(x, self.weight, self.eps)
 
 
+def _masked_attention(qkv, H: int, Hkv: int, cos, sin, key_mask):
+    """Causal GQA attention where key ``j`` of row ``b`` is visible only if ``key_mask[b, j]``
+    (HF's 4-D mask from ``attention_mask``).  A query with no visible key (a left pad) attends to
+    itself — its output feeds nothing a real token reads.  PyTorch SDPA: the module path only."""
+    from ..ops.llama import rope_
+
+    B, T, W = qkv.shape
+    D = W // (H + 2 * Hkv)
+    qkv = rope_(qkv.contiguous().clone(), cos, sin, H + Hkv, D)
+    q = qkv[:, :, : H * D].view(B, T, H, D).transpose(1, 2)
+    k = qkv[:, :, H * D:(H + Hkv) * D].view(B, T, Hkv, D).transpose(1, 2)
+    v = qkv[:, :, (H + Hkv) * D:].view(B, T, Hkv, D).transpose(1, 2)
+    causal = torch.ones(T, T, dtype=torch.bool, device=qkv.device).tril()
+    allow = causal[None] & key_mask.bool()[:, None, :]
+    allow = allow | torch.eye(T, dtype=torch.bool, device=qkv.device)[None]
+    y = F.scaled_dot_product_attention(q, k, v, attn_mask=allow[:, None], scale=D ** -0.5, enable_gqa=Hkv != H)
+    return y.transpose(1, 2).reshape(B, T, H * D)
+
+
 class LlamaAttention(nn.Module):
     def __init__(self, c: LlamaConfig):
         super().__init__()
@@ -179,14 +210,17 @@ class LlamaAttention(nn.Module):
         self.o_proj = nn.Linear(self.H * self.D, c.hidden_size, bias=c.o_bias)
         self.window = c.sliding_window
 
-    def forward(self, x, cos, sin, kv=None):
+    def forward(self, x, cos, sin, kv=None, key_mask=None):
         if self.window is not None and x.shape[1] > self.window:
             raise NotImplementedError(f"sliding-window attention: {x.shape[1]} positions > window {self.window}")
         # RoPE is applied inside the attention kernels on the HIP path (rope_ + SDPA otherwise)
         qkv = ops.gemm_linear(x, self.qkv_proj.weight, self.qkv_proj.bias)  # HIP MFMA GEMM on GPU bf16
         if kv is not None:  # (KVCache, layer): generation prefill, before anything rotates qkv in place
             kv[0].store(kv[1], qkv, rope=(cos, sin))
-        a = ops.attention_qkv(qkv, self.H, causal=True, n_kv_head=self.Hkv, rope=(cos, sin))
+        if key_mask is not None:
+            a = _masked_attention(qkv, self.H, self.Hkv, cos, sin, key_mask)
+        else:
+            a = ops.attention_qkv(qkv, self.H, causal=True, n_kv_head=self.Hkv, rope=(cos, sin))
         return ops.gemm_linear(a, self.o_proj.weight, self.o_proj.bias)
 
     def decode(self, x, norm_w, eps, cache, layer: int, pos, rope):
@@ -220,12 +254,69 @@ class LlamaDecoderLayer(nn.Module):
         self.post_attention_layernorm = RMSNorm(c.hidden_size, c.rms_norm_eps)
         self.mlp = LlamaMLP(c)
 
+    def forward(self, hidden_states, cos, sin, key_mask=None):
+        """HF ``LlamaDecoderLayer.forward``'s structure (the module path, taken when hooks are
+        registered): residual stream in, residual stream out, every submodule called as a module."""
+        kw = {} if key_mask is None else {"key_mask": key_mask}
+        x = hidden_states + self.self_attn(self.input_layernorm(hidden_states), cos, sin, **kw)
+        return x + self.mlp(self.post_attention_layernorm(x))
 
-def _drop_block_graphs() -> None:
+
+def _drop_block_graphs(owner: int) -> None:
     try:
-        ops.block_graphs_reset()
+        ops.block_graphs_reset(owner)
     except Exception:  # interpreter shutdown
         pass
+
+
+_OWNER_IDS = itertools.count(1)
+
+
+def _global_hooks() -> bool:
+    from torch.nn.modules import module as _m
+
+    return bool(_m._global_forward_hooks or _m._global_forward_pre_hooks or _m._global_backward_hooks
+                or getattr(_m, "_global_backward_pre_hooks", None))
+
+
+class _MaskCheck:
+    """A device-side flag about the attention masks seen (``ops.seqcls_prep``), read one call
+    late without a host sync: a pinned copy and an event per call; the next call raises if the
+    flag had a failing bit by then.  Not armed inside a graph capture."""
+
+    def __init__(self):
+        self.dev = None
+        self.host = None
+        self.ev = None
+
+    def flag(self, device):
+        if self.dev is None or self.dev.device != device:
+            self.dev = torch.zeros(1, dtype=torch.int32, device=device)
+            self.host = torch.zeros(1, dtype=torch.int32, pin_memory=device.type == "cuda")
+            self.ev = None
+        return self.dev
+
+    def poll(self, fail_bits: int, what: str) -> None:
+        if self.ev is not None and not torch.cuda.is_current_stream_capturing() and self.ev.query():
+            v = int(self.host[0])
+            self.ev = None
+            if v & fail_bits:
+                self.dev.zero_()
+                raise ValueError(f"nbd Llama: an attention_mask {what} (a batch of an earlier call; the fused path "
+                                 "checks masks without synchronising) — register no hooks to keep the fused path, "
+                                 "or see models/llama.py's module docstring")
+
+    def arm(self, fail_bits: int, what: str) -> None:
+        if self.dev.device.type != "cuda":
+            if int(self.dev[0]) & fail_bits:
+                self.dev.zero_()
+                raise ValueError(f"nbd Llama: attention_mask {what}")
+            return
+        if torch.cuda.is_current_stream_capturing():
+            return
+        self.host.copy_(self.dev, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
 
 
 class LlamaModel(nn.Module):
@@ -243,8 +334,11 @@ class LlamaModel(nn.Module):
         self.compute_dtype: Optional[torch.dtype] = None
         # per-block HIP graphs for this model (0 / 1 / 2, ops.block_graphs); None = process setting
         self.block_graphs: Optional[int] = None
-        # per-block HIP graphs (ops.block_graphs) hold static activations: drop them with the model
-        weakref.finalize(self, _drop_block_graphs)
+        # per-block HIP graphs (ops.block_graphs) hold static activations: drop this model's
+        # graphs (only) with it
+        self._bg_owner = next(_OWNER_IDS)
+        weakref.finalize(self, _drop_block_graphs, self._bg_owner)
+        self._hook_probe = None
 
     def cast_dtype(self, input_ids) -> Optional[torch.dtype]:
         """The dtype the fp32 parameters are cast to for this forward, or None (run as stored).
@@ -270,8 +364,36 @@ class LlamaModel(nn.Module):
                                               scaling=self.config.rope_scaling)
         return self._rope[key]
 
-    def forward(self, input_ids, cache=None):
-        """``cache`` (a ``generation.KVCache``) receives every layer's rotated k and v."""
+    def hooked(self) -> bool:
+        """Any forward / backward hook on the embedding, a decoder layer, one of their submodules,
+        the final norm — or a global module hook: then ``forward`` runs module by module."""
+        key = (len(self.layers), id(self.layers[0]) if len(self.layers) else 0,
+               id(self.layers[-1].self_attn) if len(self.layers) else 0, id(self.layers[-1].mlp) if len(self.layers) else 0)
+        if self._hook_probe is None or self._hook_probe[0] != key:
+            mods = [self.embed_tokens, self.norm] + [m for layer in self.layers for m in layer.modules()]
+            dicts = []
+            for m in mods:
+                dicts += [m._forward_hooks, m._forward_pre_hooks, m._backward_hooks,
+                          getattr(m, "_backward_pre_hooks", {})]
+            self._hook_probe = (key, dicts)
+        return any(self._hook_probe[1]) or _global_hooks()
+
+    def forward_modules(self, input_ids, attention_mask=None):
+        """Module-by-module forward in HF's structure (hooks fire; ``attention_mask`` masks keys
+        exactly as HF does).  Parameters compute in their own dtype."""
+        T = input_ids.shape[1]
+        cos, sin = self.rope(T, input_ids.device)
+        key_mask = None if attention_mask is None else attention_mask != 0
+        x = self.embed_tokens(input_ids)
+        for layer in self.layers:
+            x = layer(x, cos, sin, key_mask) if key_mask is not None else layer(x, cos, sin)
+        return self.norm(x)
+
+    def forward(self, input_ids, cache=None, attention_mask=None):
+        """``cache`` (a ``generation.KVCache``) receives every layer's rotated k and v.
+        ``attention_mask`` given, or hooks registered: the module path (``forward_modules``)."""
+        if cache is None and (attention_mask is not None or self.hooked()):
+            return self.forward_modules(input_ids, attention_mask)
         c = self.config
         T = input_ids.shape[1]
         cos, sin = self.rope(T, input_ids.device)
@@ -291,7 +413,7 @@ class LlamaModel(nn.Module):
                 r = ops.llama_block(x, h, at.qkv_proj.weight, at.qkv_proj.bias, at.o_proj.weight, at.o_proj.bias,
                                     layer.post_attention_layernorm.weight, layer.mlp.gate_up_proj.weight,
                                     layer.mlp.down_proj.weight, nxt.weight, at.H, at.Hkv, c.rms_norm_eps, cos, sin,
-                                    self._graph_mode())
+                                    self._graph_mode(), self._bg_owner)
                 if r is not None:
                     x, h = r
                     continue
@@ -336,7 +458,7 @@ class LlamaModel(nn.Module):
             b_qkv = extra.pop(0) if at.qkv_proj.bias is not None else None
             b_o = extra.pop(0) if at.o_proj.bias is not None else None
             r = ops.llama_block(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, at.H, at.Hkv,
-                                c.rms_norm_eps, cos, sin, self._graph_mode())
+                                c.rms_norm_eps, cos, sin, self._graph_mode(), self._bg_owner)
             if r is None:  # (cast_dtype() checked the conditions: not expected)
                 qkv = ops.gemm_linear(h, w_qkv, b_qkv)
                 a = ops.gemm_linear(ops.attention_qkv(qkv, at.H, causal=True, n_kv_head=at.Hkv, rope=(cos, sin)),
@@ -376,13 +498,19 @@ class LlamaForSequenceClassification(_LlamaPreTrained):
 
     def forward(self, input_ids, attention_mask=None, labels=None, **hf_kwargs):
         _check_hf_kwargs(hf_kwargs)
-        h = self.model(input_ids)
+        if self.model.hooked():  # HF's structure, exact key masking: every hook fires
+            h = self.model.forward_modules(input_ids, attention_mask)
+            last = ops.mask._ref_seqcls_prep(input_ids, None, self.config.pad_token_id)[1]
+        else:
+            # fused path: left-padded rows rotated to right padding, pooled index in the rotated
+            # rows — one kernel, no host sync (ops.seqcls_prep); holes are reported next call
+            chk = self.__dict__.setdefault("_mask_check", _MaskCheck())
+            chk.poll(1, "with holes (not one contiguous run per row) is not supported by the fused path")
+            ids, last = ops.seqcls_prep(input_ids, attention_mask, self.config.pad_token_id,
+                                        chk.flag(input_ids.device))
+            chk.arm(1, "with holes (not one contiguous run per row) is not supported by the fused path")
+            h = self.model(ids)
         B, T, C = h.shape
-        if self.config.pad_token_id is None:
-            last = torch.full((B,), T - 1, dtype=torch.int64, device=h.device)
-        else:  # rightmost non-pad token (device-side, no host sync)
-            nonpad = (input_ids != self.config.pad_token_id).to(torch.int32)
-            last = (torch.arange(T, device=h.device, dtype=torch.int32) * nonpad).argmax(-1)
         # gather (backward = scatter-add: no sort, graph-safe) instead of advanced indexing
         pooled = torch.gather(h, 1, last.view(B, 1, 1).expand(B, 1, C)).squeeze(1)
         w = self.score.weight
@@ -406,12 +534,24 @@ class LlamaForCausalLM(_LlamaPreTrained):
         if c.tie_word_embeddings:
             self.lm_head.weight = self.model.embed_tokens.weight
 
-    def forward(self, input_ids, labels=None, return_logits: bool = True):
+    def forward(self, input_ids, labels=None, return_logits: bool = True, attention_mask=None):
         """Next-token loss of ``labels`` (shifted here: ``logits[:, t]`` predicts ``labels[:, t+1]``).
         Under context parallelism (``parallel.context.parallelize_llama_context``) the shard's
         ``labels`` must come already shifted on the full sequence (``context.shift_labels``) and
-        the loss is this rank's ``context_loss`` share of the group-wide token mean."""
-        h = self.model(input_ids)
+        the loss is this rank's ``context_loss`` share of the group-wide token mean.
+        ``attention_mask``: right padding on the fused path (real tokens' logits and the loss
+        over them equal HF's; anything else is reported at the next call); with hooks registered
+        any mask, exactly (the module path)."""
+        if self.model.hooked():
+            h = self.model.forward_modules(input_ids, attention_mask)
+        else:
+            if attention_mask is not None:
+                chk = self.__dict__.setdefault("_mask_check", _MaskCheck())
+                what = "that is not right-padded is not supported by the fused causal-LM path"
+                chk.poll(3, what)
+                ops.seqcls_prep(input_ids, attention_mask, None, chk.flag(input_ids.device))
+                chk.arm(3, what)
+            h = self.model(input_ids)
         logits = self.lm_head(h)
         loss = None
         if labels is not None:
@@ -559,40 +699,75 @@ def native(hf_model, compute_dtype: Optional[torch.dtype] = torch.bfloat16, fuse
         for p in m.parameters():
             p._nbd_native_fused = True
         _install_fused_default()
+        global _NATIVE_LIVE
+        _NATIVE_LIVE += 1
+        weakref.finalize(m, _native_released)
     return m
 
 
-_FUSED_PATCHED = False
+# torch.optim.AdamW / Adam __init__ wrapped while native() models are alive: originals + wrappers
+_FUSED_ORIG: Dict[type, Any] = {}
+_FUSED_WRAP: Dict[type, Any] = {}
+_NATIVE_LIVE = 0
+_LOG = logging.getLogger("nbdistributed_amd")
+_LOGGED = [False]
+
+
+def _native_released() -> None:
+    global _NATIVE_LIVE
+    _NATIVE_LIVE -= 1
+    if _NATIVE_LIVE <= 0:
+        _NATIVE_LIVE = 0
+        restore_optimizer_defaults()
+
+
+def restore_optimizer_defaults() -> None:
+    """Undo ``native()``'s fused-AdamW default now (it is undone by itself when the last
+    ``native()`` model is garbage-collected).  A wrapper someone installed over ours stays."""
+    for cls, orig in list(_FUSED_ORIG.items()):
+        if cls.__init__ is _FUSED_WRAP.get(cls):
+            cls.__init__ = orig
+        _FUSED_ORIG.pop(cls, None)
+        _FUSED_WRAP.pop(cls, None)
 
 
 def _install_fused_default() -> None:
-    """Wrap ``torch.optim.AdamW.__init__`` / ``Adam.__init__`` once: when ``fused`` and
-    ``foreach`` are both unspecified and every parameter is a CUDA floating-point parameter of a
-    ``native()`` model, pass ``fused=True``."""
-    global _FUSED_PATCHED
-    if _FUSED_PATCHED:
-        return
+    """Wrap ``torch.optim.AdamW.__init__`` / ``Adam.__init__`` while ``native()`` models live:
+    when ``fused`` and ``foreach`` are both unspecified and every parameter is a CUDA
+    floating-point parameter of a ``native()`` model, pass ``fused=True``.  Said once in the log;
+    undone when the last such model is collected (or ``restore_optimizer_defaults()``)."""
     import functools
 
-    def wrap(cls):
+    for cls in (torch.optim.AdamW, torch.optim.Adam):
+        if cls in _FUSED_ORIG:
+            continue
         orig = cls.__init__
 
-        @functools.wraps(orig)
-        def __init__(self, params, *args, **kwargs):
-            if kwargs.get("fused") is None and kwargs.get("foreach") is None:
-                params = list(params)
-                flat = [p for g in params for p in (g["params"] if isinstance(g, dict) else [g])]
-                if flat and all(isinstance(p, torch.Tensor) and getattr(p, "_nbd_native_fused", False) and p.is_cuda
-                                and p.is_floating_point() for p in flat):
-                    kwargs["fused"] = True
-            orig(self, params, *args, **kwargs)
+        def make(orig):
+            @functools.wraps(orig)
+            def __init__(self, params, *args, **kwargs):
+                if kwargs.get("fused") is None and kwargs.get("foreach") is None:
+                    params = list(params)
+                    flat = [p for g in params for p in (g["params"] if isinstance(g, dict) else [g])]
+                    if flat and all(isinstance(p, torch.Tensor) and getattr(p, "_nbd_native_fused", False) and p.is_cuda
+                                    and p.is_floating_point() for p in flat):
+                        kwargs["fused"] = True
+                orig(self, params, *args, **kwargs)
 
-        cls.__init__ = __init__
+            return __init__
 
-    wrap(torch.optim.AdamW)
-    wrap(torch.optim.Adam)
-    _FUSED_PATCHED = True
+        w = make(orig)
+        _FUSED_ORIG[cls] = orig
+        _FUSED_WRAP[cls] = w
+        cls.__init__ = w
+    if not _LOGGED[0]:
+        _LOGGED[0] = True
+        _LOG.warning("nbdistributed_amd: native(): torch.optim.AdamW/Adam built on a native() model's GPU parameters "
+                     "without fused=/foreach= use fused=True (the same update, one kernel); restored when the last "
+                     "native() model is collected. Keep torch's default with native(..., fused_optimizer=False) or "
+                     "NBD_NATIVE_FUSED_OPTIM=0.")
 
 
 __all__ = ["LlamaConfig", "LlamaModel", "LlamaForSequenceClassification", "LlamaForCausalLM", "RMSNorm",
-           "from_hf", "native", "hf_to_nbd_state_dict", "SequenceClassifierOutput", "CausalLMOutput"]
+           "from_hf", "native", "hf_to_nbd_state_dict", "SequenceClassifierOutput", "CausalLMOutput",
+           "restore_optimizer_defaults"]

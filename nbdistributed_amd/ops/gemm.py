@@ -619,13 +619,14 @@ _BLOCK_PLANS: dict = {}
 
 
 def llama_block(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, n_head: int, n_kv: int, eps: float,
-                cos, sin, graphs: int = -1):
+                cos, sin, graphs: int = -1, owner: int = 0):
     """One pre-norm Llama decoder block as ONE autograd node: ``x1 = x + o_proj(attn(qkv(h)))``,
     ``h1 = rms(x1)·γ_post``, ``x2 = x1 + down(swiglu(gate_up(h1)))``, returns ``(x2, rms(x2)·γ_next)``
     — the per-op path's kernels in the same order, one Python call and one node instead of six and
     five (the eager SmolLM2 step is host-bound).  None when the block does not fit the fused path
     (the caller then runs the ops one by one).  ``graphs``: per-block HIP graph mode for this call
-    (0 / 1 / 2, see ``block_graphs``; -1 = the process setting)."""
+    (0 / 1 / 2, see ``block_graphs``; -1 = the process setting); ``owner``: the calling model's id,
+    kept with its block graphs so that ``block_graphs_reset(owner)`` drops that model's only."""
     import torch
 
     if not (FUSED_BLOCK and FUSED_SWIGLU and NATIVE_AUTOGRAD and _fast(h, w_qkv, w_o, w_gu, w_down)
@@ -646,7 +647,7 @@ def llama_block(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, n_he
         _BLOCK_PLANS[key] = plans
     return torch.ops.nbd.llama_block_ag(x, h, w_qkv, b_qkv, w_o, b_o, w_post, w_gu, w_down, w_next, plans[0],
                                         plans[1], plans[2], int(n_head), int(n_kv), D ** -0.5, float(eps), cos, sin,
-                                        int(graphs))
+                                        int(graphs), int(owner))
 
 
 def block_graphs(enable=None) -> int:
@@ -665,14 +666,44 @@ def block_graphs(enable=None) -> int:
     return int(torch.ops.nbd.llama_block_graphs(-1 if enable is None else int(enable)))
 
 
-def block_graphs_reset() -> None:
-    """Drop every captured block graph (a LlamaModel being garbage-collected does this)."""
+def block_graphs_reset(owner=None) -> None:
+    """Drop captured block graphs: every one, or (``owner``) those made by one model — what a
+    LlamaModel being garbage-collected does, so a throwaway model never costs a live one its
+    graphs."""
     from . import _lib
 
     if _lib._loaded:
         import torch
 
-        torch.ops.nbd.llama_block_graphs_reset()
+        if owner is None:
+            torch.ops.nbd.llama_block_graphs_reset()
+        else:
+            torch.ops.nbd.llama_block_graphs_reset_owner(int(owner))
+
+
+def block_graphs_memory(device=None) -> dict:
+    """Device memory the block graphs hold: the caching allocator's segments in their private
+    pools (static activations, inputs and outputs kept between steps).  {"graphs": n,
+    "reserved_bytes": ..., "allocated_bytes": ...}; zeros when none are live."""
+    from . import _lib
+
+    out = {"graphs": 0, "reserved_bytes": 0, "allocated_bytes": 0}
+    if not _lib._loaded:
+        return out
+    import torch
+
+    ids = list(torch.ops.nbd.llama_block_graphs_pools())
+    pools = {(ids[i], ids[i + 1]) for i in range(0, len(ids), 2)}
+    out["graphs"] = len(ids) // 2
+    if not pools:
+        return out
+    dev = torch.cuda.current_device() if device is None else torch.device(device).index
+    for seg in torch.cuda.memory_snapshot():
+        if seg.get("device") != dev or tuple(seg.get("segment_pool_id", (0, 0))) not in pools:
+            continue
+        out["reserved_bytes"] += int(seg.get("total_size", 0))
+        out["allocated_bytes"] += int(seg.get("allocated_size", 0))
+    return out
 
 
 def block_graphs_stats() -> dict:

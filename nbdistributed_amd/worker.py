@@ -247,9 +247,15 @@ class DistributedWorker:
             ops_lib = sys.modules.get("nbdistributed_amd.ops._lib")
             if ops_lib is not None and getattr(ops_lib, "_loaded", False):  # (never loads it for a status)
                 try:
-                    from .ops import block_graphs, block_graphs_stats
+                    from .ops import block_graphs, block_graphs_memory, block_graphs_stats
 
-                    st["block_graphs"] = dict(block_graphs_stats(), mode=block_graphs())
+                    bg = dict(block_graphs_stats(), mode=block_graphs())
+                    mem = block_graphs_memory(d)
+                    # the static activations/inputs/outputs the graphs keep between steps: memory
+                    # the framework holds, not the user's tensors
+                    bg.update(pools=mem["graphs"], reserved_gib=mem["reserved_bytes"] / gib,
+                              allocated_gib=mem["allocated_bytes"] / gib)
+                    st["block_graphs"] = bg
                 except Exception:  # noqa: BLE001 - status must not fail
                     pass
         if torch is not None:

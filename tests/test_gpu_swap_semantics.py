@@ -1,0 +1,212 @@
+"""GPU: the one-line swap keeps HF semantics and the block graphs stay a pure
+performance feature.
+
+* ``ops.seqcls_prep`` (csrc/kernels/mask.hip) against its PyTorch reference;
+* a left-padded batch through ``native()`` (bf16 fused path) matches the fp32 HF model's logits
+  and loss, as the right-padded batch does;
+* a forward hook on ``layers[3]`` fires on the GPU model and sees HF's activations;
+* a backward block-graph capture that fails falls back to the eager backward with eager-equal
+  gradients (the claims made while capturing are rolled back);
+* dropping one model's block graphs leaves another model's graphs alone;
+* the memory the block graphs hold is reported (``ops.block_graphs_memory``)."""
+import copy
+import gc
+import os
+
+import pytest
+import torch
+
+from nbdistributed_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def dev(require_gpu):
+    assert ops.native_available(), ops._load_error
+    prev = ops.block_graphs()
+    ops.block_graphs_reset()
+    yield torch.device("cuda", 0)
+    ops.block_graphs(prev)
+    ops.block_graphs_reset()
+
+
+def _rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+@pytest.mark.parametrize("dtype", [torch.int64, torch.int32, torch.bool])
+def test_seqcls_prep_matches_reference(dev, dtype):
+    from nbdistributed_amd.ops.mask import _ref_seqcls_prep
+
+    g = torch.Generator().manual_seed(0)
+    B, T = 37, 300
+    ids = torch.randint(1, 1000, (B, T), generator=g)
+    lens = torch.randint(0, T + 1, (B,), generator=g)
+    left = torch.rand(B, generator=g) < 0.5
+    ar = torch.arange(T)
+    mask = torch.where(left[:, None], ar[None] >= T - lens[:, None], ar[None] < lens[:, None])
+    ids = ids * mask
+    mask_d = mask.to(dtype)
+    for pad in (0, None):
+        bad_r = torch.zeros(1, dtype=torch.int32)
+        r_ids, r_pool = _ref_seqcls_prep(ids, mask_d, pad, bad_r)
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        k_ids, k_pool = ops.seqcls_prep(ids.to(dev), mask_d.to(dev), pad, bad)
+        assert torch.equal(k_ids.cpu(), r_ids) and torch.equal(k_pool.cpu(), r_pool)
+        assert int(bad.cpu()) == int(bad_r) == 2  # left-padded rows present, no holes
+    holes = mask.clone()
+    holes[3, :] = True
+    holes[3, 7] = False
+    bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    ops.seqcls_prep(ids.to(dev), holes.to(dev), 0, bad)
+    assert int(bad.cpu()) & 1
+
+
+def _hf_and_native(dev, layers=2):
+    transformers = pytest.importorskip("transformers")
+    import nbdistributed_amd as nbd
+    from nbdistributed_amd.models import SMOLLM2_135M
+
+    cfg = dict(SMOLLM2_135M)
+    cfg.update(num_hidden_layers=layers, vocab_size=4096)
+    torch.manual_seed(0)
+    hf = transformers.LlamaForSequenceClassification(
+        transformers.LlamaConfig(num_labels=2, pad_token_id=0, **cfg)).to(dev)
+    return hf, nbd.models.native(hf)
+
+
+def _batch(dev, left: bool, B=4, T=128):
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(1, 4096, (B, T), generator=g)
+    lens = torch.tensor([T, 100, 57, 9])[:B]
+    ar = torch.arange(T)
+    mask = (ar[None] >= T - lens[:, None]) if left else (ar[None] < lens[:, None])
+    return (ids * mask).to(dev), mask.long().to(dev), torch.tensor([0, 1, 1, 0])[:B].to(dev)
+
+
+@pytest.mark.parametrize("left", [False, True])
+def test_native_padded_batch_matches_hf(dev, left):
+    hf, m = _hf_and_native(dev)
+    ids, mask, labels = _batch(dev, left)
+    assert not m.model.hooked()
+    for _ in range(3):  # (block graphs capture after two eager calls: replays too)
+        out = m(input_ids=ids, attention_mask=mask, labels=labels)
+    ref = hf(input_ids=ids, attention_mask=mask, labels=labels)
+    assert _rel(out.logits.float(), ref.logits) < 5e-2, (out.logits, ref.logits)
+    assert abs(float(out.loss) - float(ref.loss)) < 3e-2
+    if left:  # ... and equal to the same rows right-padded through the fused path
+        rids, rmask, _ = _batch(dev, False)
+        r = m(input_ids=rids, attention_mask=rmask, labels=labels)
+        assert _rel(out.logits.float(), r.logits.float()) < 2e-2
+
+
+def test_native_mask_with_holes_raises_next_call(dev):
+    hf, m = _hf_and_native(dev)
+    ids, mask, labels = _batch(dev, False)
+    mask[1, 5] = 0
+    m(input_ids=ids, attention_mask=mask, labels=labels)
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError, match="holes"):
+        m(input_ids=ids, attention_mask=torch.ones_like(mask), labels=labels)
+
+
+def test_native_layer_hook_fires_with_hf_activations(dev):
+    hf, m = _hf_and_native(dev, layers=4)
+    ids, mask, labels = _batch(dev, True)
+    seen = {}
+
+    def grab(tag):
+        def hook(mod, args, out):
+            seen[tag] = (args[0].detach().float(), out.detach().float())
+        return hook
+
+    hs = [hf.model.layers[3].register_forward_hook(grab("hf")), m.model.layers[3].register_forward_hook(grab("nbd"))]
+    try:
+        ref = hf(input_ids=ids, attention_mask=mask, labels=labels)
+        out = m(input_ids=ids, attention_mask=mask, labels=labels)
+    finally:
+        for h in hs:
+            h.remove()
+    valid = mask.bool()
+    for i in (0, 1):
+        assert _rel(seen["nbd"][i][valid], seen["hf"][i][valid]) < 1e-3  # (module path: fp32 compute)
+    assert _rel(out.logits.float(), ref.logits) < 1e-3
+    assert not m.model.hooked()
+
+
+def _ddp_step_grads(base, batches, graphs, fail=0):
+    from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP
+
+    ops.block_graphs(graphs)
+    m = NbdDDP(copy.deepcopy(base), flat_params=True, grad_mode="bucket")
+    outs = []
+    for step in range(4):
+        if step == 2 and fail:
+            torch.ops.nbd.llama_block_graphs_fault(fail)
+        for p in m.parameters():
+            p.grad = None
+        ids, lab = batches[step % len(batches)]
+        m(ids, torch.ones_like(ids), lab)[0].backward()
+        torch.cuda.synchronize()
+        outs.append(torch.cat([b.buffer.float() for b in m.buckets]))
+    m.unpatch()
+    return outs
+
+
+def test_backward_capture_failure_falls_back_to_eager(dev):
+    """Mode 2 (backward graphs into DDP bucket slices): the first backward capture is forced to
+    fail; that step's gradients still equal the eager step's (claims rolled back, eager backward)."""
+    import torch.distributed as dist
+
+    from nbdistributed_amd.models.llama import LlamaConfig, LlamaForSequenceClassification
+    from nbdistributed_amd.parallel.backend import init_data_plane
+
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29571")
+        init_data_plane("rccl", 0, 1, dev)
+    torch.manual_seed(5)
+    base = LlamaForSequenceClassification(LlamaConfig.smollm2_135m(num_hidden_layers=2)).to(dev, torch.bfloat16)
+    g = torch.Generator(device=dev).manual_seed(1)
+    batches = [(torch.randint(1, 49152, (8, 128), device=dev, generator=g), torch.randint(0, 2, (8,), device=dev, generator=g))
+               for _ in range(2)]
+    ref = _ddp_step_grads(base, batches, 0)
+    ops.block_graphs_reset()
+    with pytest.warns(UserWarning, match="backward graph capture failed"):
+        got = _ddp_step_grads(base, batches, 2, fail=100)
+    torch.ops.nbd.llama_block_graphs_fault(0)
+    assert all(torch.equal(a, b) for a, b in zip(ref, got))
+
+
+def test_per_model_graph_reset_and_memory(dev):
+    from nbdistributed_amd.models.llama import LlamaConfig, LlamaForSequenceClassification
+
+    def model(seed):
+        torch.manual_seed(seed)
+        return LlamaForSequenceClassification(LlamaConfig.smollm2_135m(num_hidden_layers=2)).to(dev, torch.bfloat16)
+
+    ids = torch.randint(1, 49152, (4, 128), device=dev)
+    lab = torch.randint(0, 2, (4,), device=dev)
+    ops.block_graphs(1)
+    keep, throw = model(1), model(2)
+    for m in (keep, throw):
+        for _ in range(4):
+            m(ids, torch.ones_like(ids), lab)[0].backward()
+    torch.cuda.synchronize()
+    live = ops.block_graphs_stats()["live"] + ops.block_graphs_stats()["stack_captures"]
+    mem = ops.block_graphs_memory()
+    assert mem["graphs"] >= 2 and mem["reserved_bytes"] > 0 and mem["reserved_bytes"] >= mem["allocated_bytes"]
+    pools_before = mem["graphs"]
+    del throw
+    gc.collect()
+    mem2 = ops.block_graphs_memory()
+    assert 0 < mem2["graphs"] < pools_before, (mem, mem2)  # the live model kept its graphs
+    r0 = ops.block_graphs_stats()["replays"] + ops.block_graphs_stats()["stack_replays"]
+    keep(ids, torch.ones_like(ids), lab)[0].backward()
+    r1 = ops.block_graphs_stats()["replays"] + ops.block_graphs_stats()["stack_replays"]
+    assert r1 > r0 and live > 0  # replayed, not recaptured from scratch
+    del keep
+    gc.collect()
+    assert ops.block_graphs_memory()["graphs"] == 0
