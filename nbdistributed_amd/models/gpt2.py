@@ -1,11 +1,15 @@
 """GPT-2 (124M "small" by default) for the BASELINE config-5 DDP loop.
 
 BASELINE.json config 5: "00_accelerate.ipynb-style GPT-2-small DDP loop, bf16, synthetic tokens"
-(124,439,808 parameters with the tied LM head).  Plain PyTorch modules; on
-MI355X the GEMMs go to hipBLASLt and attention to PyTorch's fused SDPA (AOTriton/CK flash
-kernels) — or, for bf16 with head dim 64, the HIP flash-attention kernels (``ops.attention_qkv``);
-the LM-head loss is the fused HIP cross-entropy (``ops.cross_entropy``, no fp32 copy
-of the 8192 x 50257 logits).
+(124,439,808 parameters with the tied LM head).  On MI355X in bf16 the hot path
+is the framework's own gfx950 kernels: every transformer Linear runs on the hand-written MFMA
+GEMMs (``ops.gemm_linear`` / ``ops.mlp_gelu``: csrc/kernels/gemm.hip, fused bias / GELU
+epilogues, grouped dgrad + wgrad backward writing into the DDP buckets), attention on the HIP
+flash kernels (``ops.attention_qkv``, csrc/kernels/attn.hip), add + LayerNorm on norm.hip and the
+loss on the fused HIP cross-entropy (``ops.linear_cross_entropy``, no fp32 copy of the
+8192 x 50257 logits).  The tied LM-head products (8192 x 50304 x 768, three per step) are the
+one place a library GEMM (hipBLASLt) runs: it measured faster than the hand-written 256x256
+kernel on them (docs/FINDINGS.md §10, §29).  CPU / fp32: the same model in plain PyTorch.
 Random init (no checkpoints: no network), GPT-2 initialisation scheme.
 """
 from __future__ import annotations
