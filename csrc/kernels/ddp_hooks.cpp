@@ -176,7 +176,9 @@ void ddp_hooks_reattach(int64_t handle, const std::vector<at::Tensor>& params, c
   for (size_t i = 0; i < params.size(); ++i) attach(s, params[i], (int)bucket_of[i]);
 }
 
-// Remove this handle's hooks (restoring any hook they wrapped) and forget the handle.
+// Remove this handle's hooks (restoring any hook they wrapped) and forget the handle.  Our hook may
+// sit anywhere in a parameter's chain: a DDP built over the same module before this one was
+// collected (a re-run notebook cell) wraps this handle's hook as its `prev` — splice it out there.
 void ddp_hooks_remove(int64_t handle, const std::vector<at::Tensor>& params) {
   std::shared_ptr<State> s;
   {
@@ -190,10 +192,32 @@ void ddp_hooks_remove(int64_t handle, const std::vector<at::Tensor>& params) {
     if (!p.defined()) continue;
     auto& slot = torch::autograd::impl::post_acc_grad_hooks(p);
     auto* h = dynamic_cast<BucketHook*>(slot.get());
-    if (h == nullptr || h->st != s) continue;
-    std::unique_ptr<torch::autograd::PostAccumulateGradHook> prev = std::move(h->prev);
-    torch::autograd::impl::set_post_acc_grad_hooks(p, std::move(prev));
+    if (h == nullptr) continue;
+    if (h->st == s) {  // outermost
+      std::unique_ptr<torch::autograd::PostAccumulateGradHook> prev = std::move(h->prev);
+      torch::autograd::impl::set_post_acc_grad_hooks(p, std::move(prev));
+      continue;
+    }
+    for (BucketHook* outer = h; outer != nullptr;) {  // inner: unlink from the hook wrapping it
+      auto* inner = dynamic_cast<BucketHook*>(outer->prev.get());
+      if (inner == nullptr) break;
+      if (inner->st == s) {
+        std::unique_ptr<torch::autograd::PostAccumulateGradHook> rest = std::move(inner->prev);
+        outer->prev = std::move(rest);  // destroys `inner`
+        break;
+      }
+      outer = inner;
+    }
   }
+}
+
+// BucketHook layers on a parameter (tests: a removed DDP leaves none behind).
+int64_t ddp_hooks_depth(const at::Tensor& p) {
+  int64_t n = 0;
+  for (auto* h = dynamic_cast<BucketHook*>(torch::autograd::impl::post_acc_grad_hooks(p).get()); h != nullptr;
+       h = dynamic_cast<BucketHook*>(h->prev.get()))
+    ++n;
+  return n;
 }
 
 }  // namespace ddp_hooks
@@ -207,4 +231,5 @@ TORCH_LIBRARY_FRAGMENT(nbd, m) {
   m.def("ddp_hooks_intact(int handle, Tensor[] params) -> int", &nbd::ddp_hooks::ddp_hooks_intact);
   m.def("ddp_hooks_reattach(int handle, Tensor[] params, int[] bucket_of) -> ()", &nbd::ddp_hooks::ddp_hooks_reattach);
   m.def("ddp_hooks_remove(int handle, Tensor[] params) -> ()", &nbd::ddp_hooks::ddp_hooks_remove);
+  m.def("ddp_hooks_depth(Tensor param) -> int", &nbd::ddp_hooks::ddp_hooks_depth);
 }

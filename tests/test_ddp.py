@@ -205,6 +205,34 @@ gone = int(torch.ops.nbd.ddp_hooks_intact(handle, params)) == 0
         assert r.results[rank]["output"] == "(True, True, True, True)", r.results[rank]
 
 
+def test_rerun_cell_ddp_leaves_no_dead_hook_layers(sess):
+    """A notebook cell that builds DDP over the same module again: the new DDP's hooks wrap the
+    old ones (the old DDP is still alive then); once the old one is collected its hook layer is
+    spliced out of the chain — one BucketHook per parameter, gradients still torch DDP's."""
+    code = """
+import gc
+m = copy.deepcopy(base)
+d1 = NbdDDP(m, bucket_cap_mb=0.01, first_bucket_mb=0.005, cpp_hooks=True)
+d2 = NbdDDP(m, bucket_cap_mb=0.01, first_bucket_mb=0.005, cpp_hooks=True)   # the re-run cell
+p0 = m.a.weight
+both = int(torch.ops.nbd.ddp_hooks_depth(p0))
+del d1
+gc.collect()
+after = int(torch.ops.nbd.ddp_hooks_depth(p0))
+gr, go = run(ref, 1), run(d2, 1)
+same = all(torch.allclose(a, b, atol=1e-6, rtol=1e-5) for a, b in zip(gr, go) if a is not None)
+h2 = d2._hook_handle
+del d2
+gc.collect()
+(both, after, same, int(torch.ops.nbd.ddp_hooks_depth(p0)))
+"""
+    sess.execute(SETUP, render=False)
+    sess.execute(STEP, render=False)
+    r = sess.execute(code, render=False)
+    for rank in (0, 1):
+        assert r.results[rank]["output"] == "(2, 1, True, 0)", r.results[rank]
+
+
 def test_cpp_bucket_hook_callback_error_reaches_backward():
     """A failure inside the bucket callback (called from the C++ hook on the autograd engine's
     thread) surfaces as an exception from backward(), and the DDP is usable afterwards."""
