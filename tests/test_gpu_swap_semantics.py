@@ -78,12 +78,17 @@ def _hf_and_native(dev, layers=2):
 
 
 def _batch(dev, left: bool, B=4, T=128):
+    """The same token rows right-padded, or shifted to the right end (left-padded)."""
     g = torch.Generator().manual_seed(3)
     ids = torch.randint(1, 4096, (B, T), generator=g)
     lens = torch.tensor([T, 100, 57, 9])[:B]
     ar = torch.arange(T)
-    mask = (ar[None] >= T - lens[:, None]) if left else (ar[None] < lens[:, None])
-    return (ids * mask).to(dev), mask.long().to(dev), torch.tensor([0, 1, 1, 0])[:B].to(dev)
+    mask = ar[None] < lens[:, None]
+    ids = ids * mask
+    if left:
+        ids = torch.stack([torch.roll(ids[b], int(T - lens[b])) for b in range(B)])
+        mask = torch.stack([torch.roll(mask[b], int(T - lens[b])) for b in range(B)])
+    return ids.to(dev), mask.long().to(dev), torch.tensor([0, 1, 1, 0])[:B].to(dev)
 
 
 @pytest.mark.parametrize("left", [False, True])
@@ -194,6 +199,7 @@ def test_per_model_graph_reset_and_memory(dev):
     for m in (keep, throw):
         for _ in range(4):
             m(ids, torch.ones_like(ids), lab)[0].backward()
+    del m  # (the loop variable would keep `throw` alive)
     torch.cuda.synchronize()
     live = ops.block_graphs_stats()["live"] + ops.block_graphs_stats()["stack_captures"]
     mem = ops.block_graphs_memory()
