@@ -6,8 +6,8 @@
 // sees a later pad key).  A left-padded row is made right-padded by rotating it left by its pad
 // count: RoPE attention scores depend only on position differences, so every real token's
 // attention (and everything after it) is unchanged, and the pooled token is re-indexed into the
-// rotated row.  One workgroup per row does all of it in one launch (the notebook step is
-// host-bound: five torch ops would cost five launches):
+// rotated row.  One launch does all of it (the notebook step is
+// host-bound: five torch ops would cost five launches; one wave per row):
 //
 //   off  = first position with mask != 0 (0 for an all-zero row)
 //   ids_out[b, j] = ids[b, (j + off) mod T]
@@ -26,20 +26,37 @@
 namespace nbd {
 namespace mask {
 
-constexpr int kThreads = 256;  // 4 waves per row
+constexpr int kThreads = 256;  // 4 waves = 4 rows per workgroup; one wave per row
 
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// One wave per row: the row's statistics are wave reductions (cross-lane shuffles, no LDS, no
+// barrier), so a batch of short rows costs one launch's latency and nothing more.
 template <typename M>
 __global__ __launch_bounds__(kThreads) void seqcls_prep_kernel(const int64_t* __restrict__ ids,
-                                                               const M* __restrict__ mask, int64_t T, int64_t pad_id,
-                                                               int has_pad, int64_t* __restrict__ ids_out,
+                                                               const M* __restrict__ mask, int64_t B, int64_t T,
+                                                               int64_t pad_id, int has_pad, int64_t* __restrict__ ids_out,
                                                                int64_t* __restrict__ pool, int32_t* __restrict__ bad) {
-  __shared__ int s_first, s_last, s_cnt, s_lastnp;
-  const int64_t b = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (b >= B) return;  // (wave-uniform)
   const int64_t* row = ids + b * T;
-  if (threadIdx.x == 0) s_first = (int)T, s_last = -1, s_cnt = 0, s_lastnp = -1;
-  __syncthreads();
   int first = (int)T, last = -1, cnt = 0, lastnp = -1;
-  for (int64_t j = threadIdx.x; j < T; j += kThreads) {
+  for (int64_t j = lane; j < T; j += 64) {
     const bool on = mask == nullptr || mask[b * T + j] != M(0);
     if (on) {
       first = min(first, (int)j);
@@ -48,24 +65,23 @@ __global__ __launch_bounds__(kThreads) void seqcls_prep_kernel(const int64_t* __
     }
     if (!has_pad || row[j] != pad_id) lastnp = max(lastnp, (int)j);
   }
-  atomicMin(&s_first, first);
-  atomicMax(&s_last, last);
-  atomicAdd(&s_cnt, cnt);
-  atomicMax(&s_lastnp, lastnp);
-  __syncthreads();
-  const int64_t off = s_cnt == 0 ? 0 : s_first;
-  for (int64_t j = threadIdx.x; j < T; j += kThreads) {
+  first = wave_min(first);
+  last = wave_max(last);
+  cnt = wave_sum(cnt);
+  lastnp = wave_max(lastnp);
+  const int64_t off = cnt == 0 ? 0 : first;
+  for (int64_t j = lane; j < T; j += 64) {
     int64_t src = j + off;
     if (src >= T) src -= T;
     ids_out[b * T + j] = row[src];
   }
-  if (threadIdx.x == 0) {
+  if (lane == 0) {
     // HF: argmax(arange · non-pad) — the last non-pad position, 0 when the row is all pad
-    const int64_t np = s_lastnp < 0 ? 0 : s_lastnp;
+    const int64_t np = lastnp < 0 ? 0 : lastnp;
     pool[b] = (np - off + T) % T;
     int flag = 0;
-    if (s_cnt != 0 && s_last - s_first + 1 != s_cnt) flag |= 1;  // holes
-    if (s_cnt != 0 && s_first != 0) flag |= 2;                     // not right-padded
+    if (cnt != 0 && last - first + 1 != cnt) flag |= 1;  // holes
+    if (cnt != 0 && first != 0) flag |= 2;               // not right-padded
     if (flag) atomicOr(bad, flag);
   }
 }
@@ -81,11 +97,11 @@ std::tuple<at::Tensor, at::Tensor> seqcls_prep_hip(const at::Tensor& ids, const 
   auto pool = at::empty({B}, ids.options());
   if (B == 0 || T == 0) return {ids_out, pool};
   const hipStream_t st = at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-  const dim3 grid((unsigned)B), block(kThreads);
+  const dim3 grid((unsigned)((B + kThreads / 64 - 1) / (kThreads / 64))), block(kThreads);
   auto launch = [&](auto tag, const at::Tensor* m) {
     using M = decltype(tag);
     hipLaunchKernelGGL((seqcls_prep_kernel<M>), grid, block, 0, st, ids.data_ptr<int64_t>(),
-                       m ? static_cast<const M*>(m->data_ptr()) : nullptr, T, pad_id, has_pad ? 1 : 0,
+                       m ? static_cast<const M*>(m->data_ptr()) : nullptr, B, T, pad_id, has_pad ? 1 : 0,
                        ids_out.data_ptr<int64_t>(), pool.data_ptr<int64_t>(), bad.data_ptr<int32_t>());
   };
   if (!mask || !mask->defined()) {

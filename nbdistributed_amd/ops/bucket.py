@@ -54,7 +54,7 @@ def bucket_flatten(tensors: Sequence, bucket=None, offsets: Optional[Sequence[in
     tensors = list(tensors)
     if offsets is None:
         offsets, total = plan_offsets([t.numel() for t in tensors], align)
-    else:
+    elif bucket is None:  # (the no_sync pre-reduce passes both: no per-tensor Python loop on its path)
         total = max((o + t.numel() for o, t in zip(offsets, tensors)), default=0)
     if bucket is None:
         dev = tensors[0].device if tensors else "cpu"
