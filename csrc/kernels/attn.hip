@@ -621,40 +621,20 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
 
 // One launch for both backward passes: blocks [0, nkv) compute dK/dV, the rest dQ — the two
 // are independent, and for short sequences (SmolLM2: T = 128) neither fills the chip alone.
-// PAIR (causal, an even number of 128-row blocks): each workgroup runs two blocks of one (batch,
-// head) whose causal weights are complementary — key blocks kb and nblk-1-kb (dK/dV), query blocks
-// qb and nblk-1-qb (dQ) — so every workgroup of a kind carries the same work (nblk+1 tiles of the
-// one-block average) and its prologue / epilogue are amortised over twice the tiles.
-template <bool CAUSAL, bool FD, bool PAIR>
+// (Pairing complementary causal blocks in one workgroup — key blocks kb and nblk-1-kb, query
+// blocks qb and nblk-1-qb — was measured 14 % slower at B8 H12 T1024: docs/FINDINGS.md §31.)
+template <bool CAUSAL, bool FD>
 __global__ __launch_bounds__(NT, 2) void bwd_kernel(View q, View k, View v, View dout, View out,
                                                      const float* __restrict__ lse,
                                                      const float* __restrict__ delta, MView dq, MView dk, MView dv,
                                                      int Hq, int Hkv, int T, int nblk, float sc2, float scale,
-                                                     int group, Rope rp, int nkv, int gsplit, int64_t split_stride,
-                                                     int nq) {
-  if constexpr (PAIR) {
-    const int hkv = nkv / 2;  // workgroups of dK/dV pairs; then nq / 2 of dQ pairs
-    if ((int)blockIdx.x < hkv) {
-      const int per = nkv / nblk, p = blockIdx.x, bhs = p % per, kbp = p / per;
-      dkdv_body<CAUSAL, FD>(kbp * per + bhs, nkv, q, k, v, dout, out, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale,
-                            group, rp, gsplit, split_stride);
-      __syncthreads();  // (the second block reuses the LDS tiles)
-      dkdv_body<CAUSAL, FD>((nblk - 1 - kbp) * per + bhs, nkv, q, k, v, dout, out, lse, delta, dk, dv, Hkv, T, nblk,
-                            sc2, scale, group, rp, gsplit, split_stride);
-    } else {
-      const int per = nq / nblk, p = blockIdx.x - hkv, bh = p % per, qbp = p / per;
-      dq_body<CAUSAL, FD>(qbp * per + bh, nq, q, k, v, dout, out, lse, delta, dq, Hq, T, nblk, sc2, scale, group, rp);
-      __syncthreads();
-      dq_body<CAUSAL, FD>((nblk - 1 - qbp) * per + bh, nq, q, k, v, dout, out, lse, delta, dq, Hq, T, nblk, sc2, scale,
-                          group, rp);
-    }
-  } else {
-    if ((int)blockIdx.x < nkv)
-      dkdv_body<CAUSAL, FD>(blockIdx.x, nkv, q, k, v, dout, out, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale, group, rp,
-                            gsplit, split_stride);
-    else
-      dq_body<CAUSAL, FD>(blockIdx.x - nkv, nq, q, k, v, dout, out, lse, delta, dq, Hq, T, nblk, sc2, scale, group, rp);
-  }
+                                                     int group, Rope rp, int nkv, int gsplit, int64_t split_stride) {
+  if ((int)blockIdx.x < nkv)
+    dkdv_body<CAUSAL, FD>(blockIdx.x, nkv, q, k, v, dout, out, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale, group, rp,
+                          gsplit, split_stride);
+  else
+    dq_body<CAUSAL, FD>(blockIdx.x - nkv, gridDim.x - nkv, q, k, v, dout, out, lse, delta, dq, Hq, T, nblk, sc2, scale,
+                        group, rp);
 }
 
 // dk/dv[b, h, t, :] = Σ_s part[s][b][h][t][:] (fp32 sum of the gsplit partials); 8 elements per thread
@@ -808,27 +788,16 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     dkw = MView{static_cast<uint16_t*>(pk.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
     dvw = MView{static_cast<uint16_t*>(pv.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
   }
-  // causal pairs of complementary blocks per workgroup (NBD_ATTN_PAIR=0/1 forces off/on for A/B)
-  static const int pair_env = [] {
-    const char* e = std::getenv("NBD_ATTN_PAIR");
-    return e == nullptr ? -1 : std::atoi(e);
-  }();
-  const bool pair = causal && nblk % 2 == 0 && (pair_env >= 0 ? pair_env == 1 : false);
-#define NBD_BWD(C_, F_, P_)                                                                                       \
-  hipLaunchKernelGGL((bwd_kernel<C_, F_, P_>), dim3((unsigned)(P_ ? (nkv + nq) / 2 : nkv + nq)), dim3(NT), bwd_pad(), \
-                     st, qv, kv, vv, dov, ov, lse.data_ptr<float>(), dptr, dqv, dkw, dvw, H, Hkv, T, nblk, sc2,      \
-                     (float)scale, group, rp, nkv, gsplit, split_stride, nq)
+#define NBD_BWD(C_, F_)                                                                                      \
+  hipLaunchKernelGGL((bwd_kernel<C_, F_>), dim3((unsigned)(nkv + nq)), dim3(NT), bwd_pad(), st, qv, kv, vv, dov, ov,   \
+                     lse.data_ptr<float>(), dptr, dqv, dkw, dvw, H, Hkv, T, nblk, sc2, (float)scale, group, rp, nkv, \
+                     gsplit, split_stride)
   if (causal) {
-    if (pair) {
-      if (fd) NBD_BWD(true, true, true);
-      else NBD_BWD(true, false, true);
-    } else {
-      if (fd) NBD_BWD(true, true, false);
-      else NBD_BWD(true, false, false);
-    }
+    if (fd) NBD_BWD(true, true);
+    else NBD_BWD(true, false);
   } else {
-    if (fd) NBD_BWD(false, true, false);
-    else NBD_BWD(false, false, false);
+    if (fd) NBD_BWD(false, true);
+    else NBD_BWD(false, false);
   }
 #undef NBD_BWD
   C10_HIP_KERNEL_LAUNCH_CHECK();

@@ -25,6 +25,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <type_traits>
 
 #include "nbd_common.h"
 
@@ -48,7 +50,9 @@ __device__ __forceinline__ void device_hyper(AdamArgs& a, const float* dstep, co
   }
 }
 
-template <typename G, typename P>
+// U = 8-element groups per thread per iteration (all their loads issued before any math: 112·U
+// bytes in flight per lane); NTL = non-temporal loads (every byte is read once per step).
+template <typename G, typename P, int U, bool NTL>
 __global__ __launch_bounds__(256) void adamw_flat_kernel(const G* __restrict__ grad, P* __restrict__ param,
                                                          float* __restrict__ master, float* __restrict__ m,
                                                          float* __restrict__ v, const float* __restrict__ gscale,
@@ -59,13 +63,47 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(const G* __restrict__ g
   const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t nth = (int64_t)gridDim.x * 256;
   const int64_t nv = n / 8;
-  for (int64_t k = tid; k < nv; k += nth) {
+  auto ld = [](auto* p, float (&x)[8]) {
+    using T = std::remove_cv_t<std::remove_pointer_t<decltype(p)>>;
+    if constexpr (NTL) load8_nt<T>(p, x);
+    else load8<T>(p, x);
+  };
+  int64_t k = tid;
+  for (; k + (U - 1) * nth < nv; k += U * nth) {
+    float g[U][8], w[U][8], mm[U][8], vv[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = (k + u * nth) * 8;
+      ld(grad + i, g[u]);
+      ld(master + i, w[u]);
+      ld(m + i, mm[u]);
+      ld(v + i, vv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = (k + u * nth) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gj = g[u][j] * a.grad_scale;
+        mm[u][j] = fmaf(a.beta1, mm[u][j], (1.f - a.beta1) * gj);
+        vv[u][j] = fmaf(a.beta2, vv[u][j], (1.f - a.beta2) * gj * gj);
+        const float denom = sqrtf(vv[u][j]) * a.inv_sqrt_bc2 + a.eps;
+        w[u][j] = w[u][j] * a.wd_factor - a.step_size * (mm[u][j] / denom);
+      }
+      store8<float>(master + i, w[u]);
+      store8<float>(m + i, mm[u]);
+      store8<float>(v + i, vv[u]);
+      if (sizeof(P) == 2) store8_nt<P>(param + i, w[u]);
+      else store8<P>(param + i, w[u]);
+    }
+  }
+  for (; k < nv; k += nth) {  // (U > 1: the groups left over)
     const int64_t i = k * 8;
     float g[8], w[8], mm[8], vv[8];
-    load8<G>(grad + i, g);
-    load8<float>(master + i, w);
-    load8<float>(m + i, mm);
-    load8<float>(v + i, vv);
+    ld(grad + i, g);
+    ld(master + i, w);
+    ld(m + i, mm);
+    ld(v + i, vv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float gj = g[j] * a.grad_scale;
@@ -93,15 +131,33 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(const G* __restrict__ g
   }
 }
 
+// NBD_ADAMW_BLOCKS (A/B): grid cap in workgroups (default 2048 = 8 per CU, grid-stride);
+// NBD_ADAMW_VARIANT: 1 = two 8-element groups per thread per iteration, 2 = that with
+// non-temporal loads, 3 = one group with non-temporal loads (all measured slower: FINDINGS §31)
+static int adamw_env(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e == nullptr ? dflt : std::atoi(e);
+}
+
 template <typename G, typename P>
 static void launch_adamw(const at::Tensor& grad, const at::Tensor& param, const at::Tensor& master,
                          const at::Tensor& m, const at::Tensor& v, const float* gs, const float* dstep,
                          const float* dlr, int64_t n, const AdamArgs& a, hipStream_t st) {
+  static const int cap = std::max(1, adamw_env("NBD_ADAMW_BLOCKS", 256 * 8));
+  static const int variant = adamw_env("NBD_ADAMW_VARIANT", 0);
   const int64_t work = (n + 7) / 8;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 256 * 8));
-  hipLaunchKernelGGL((adamw_flat_kernel<G, P>), dim3((unsigned)blocks), dim3(256), 0, st,
-                     static_cast<const G*>(grad.data_ptr()), static_cast<P*>(param.data_ptr()),
-                     master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), gs, dstep, dlr, n, a);
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, cap));
+#define NBD_ADAMW(U_, NT_)                                                                                        \
+  hipLaunchKernelGGL((adamw_flat_kernel<G, P, U_, NT_>), dim3((unsigned)blocks), dim3(256), 0, st,                 \
+                     static_cast<const G*>(grad.data_ptr()), static_cast<P*>(param.data_ptr()), master.data_ptr<float>(), \
+                     m.data_ptr<float>(), v.data_ptr<float>(), gs, dstep, dlr, n, a)
+  switch (variant) {
+    case 1: NBD_ADAMW(2, false); break;
+    case 2: NBD_ADAMW(2, true); break;
+    case 3: NBD_ADAMW(1, true); break;
+    default: NBD_ADAMW(1, false); break;
+  }
+#undef NBD_ADAMW
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 

@@ -133,7 +133,7 @@ def test_tensor_summary_2d_noncontiguous(dev):
 
 @pytest.mark.parametrize("gdt", ["f32", "bf16"])
 @pytest.mark.parametrize("pdt", ["f32", "bf16", "f16"])
-@pytest.mark.parametrize("n", [1, 7, 8, 1000, 16389, 1 << 20])
+@pytest.mark.parametrize("n", [1, 7, 8, 1000, 16389, 1 << 20, (1 << 23) + 37])  # (the last: every thread runs its unrolled groups)
 @pytest.mark.parametrize("clip", [False, True])
 def test_adamw_flat_matches_reference(dev, gdt, pdt, n, clip):
     g = torch.Generator(device="cpu").manual_seed(n)
