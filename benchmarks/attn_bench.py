@@ -41,11 +41,32 @@ def _median_ms(fn, iters: int) -> float:
     return t[len(t) // 2]
 
 
+def _pipelined_ms(fn, iters: int, reps: int = 20) -> float:
+    for _ in range(5):
+        fn()
+    ts = []
+    for _ in range(max(3, iters // 10)):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / reps)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", default="", help="comma-separated shape names")
+    ap.add_argument("--shape", action="append", default=[],
+                    help="extra shape name,B,H,Hkv,T,causal(0/1) (repeatable)")
     a = ap.parse_args()
+    for sh in a.shape:
+        nm, B_, H_, K_, T_, c_ = sh.split(",")
+        SHAPES.append((nm, int(B_), int(H_), int(K_), int(T_), c_ == "1"))
     assert _lib.load_library(), _lib._load_error
     dev = torch.device("cuda")
     out = {"lib": os.environ.get("NBD_OPS_LIB", "in-tree")}
@@ -62,8 +83,13 @@ def main() -> None:
         t_f = _median_ms(lambda: torch.ops.nbd.attn_fwd(q, k, v, causal, scale, None, None), a.iters)
         t_b = _median_ms(lambda: torch.ops.nbd.attn_bwd(do, q, k, v, o, lse, causal, scale, dq, dk, dv, None, None),
                          a.iters)
+        # back-to-back launches (the host's launch work under the previous kernel): GPU time per call
+        t_fp = _pipelined_ms(lambda: torch.ops.nbd.attn_fwd(q, k, v, causal, scale, None, None), a.iters)
+        t_bp = _pipelined_ms(lambda: torch.ops.nbd.attn_bwd(do, q, k, v, o, lse, causal, scale, dq, dk, dv, None, None),
+                             a.iters)
         fl = 4.0 * B * H * T * T * 64 * (0.5 if causal else 1.0)
         out[name] = {"fwd_us": round(t_f * 1e3, 2), "bwd_us": round(t_b * 1e3, 2),
+                     "fwd_us_pipelined": round(t_fp * 1e3, 2), "bwd_us_pipelined": round(t_bp * 1e3, 2),
                      "fwd_TFs": round(fl / t_f / 1e9, 1), "bwd_TFs": round(2.5 * fl / t_b / 1e9, 1)}
         print(name, out[name], flush=True)
     print(json.dumps(out))

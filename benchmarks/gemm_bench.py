@@ -39,6 +39,25 @@ def timeit(fn, iters=20, warm=5):
     return statistics.median(ts)
 
 
+def timeit_pipelined(fn, reps=20, rounds=7, warm=5):
+    """GPU time per call with `reps` launches back to back between two events (each launch's host
+    work overlaps the previous kernel: no launch gap inside the window), median over rounds."""
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(rounds):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e) / reps)
+    return statistics.median(ts)
+
+
 def linears():
     out = []
     T = 8 * 1024
@@ -56,7 +75,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
     ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="time back-to-back launches (GPU time, no host launch gaps) for both columns")
+    ap.add_argument("--tunableop", action="store_true",
+                    help="torch column with PyTorch TunableOp: hipBLASLt/rocBLAS solutions searched per shape")
     a = ap.parse_args()
+    global timeit
+    if a.pipelined:
+        timeit = timeit_pipelined  # noqa: F811
+    if a.tunableop:
+        tun = torch.cuda.tunable
+        tun.enable(True)
+        tun.tuning_enable(True)
+        tun.set_filename("/tmp/nbd_gemm_bench_tunableop.csv")
     from nbdistributed_amd import ops
 
     ops.load_library()
@@ -75,6 +106,9 @@ def main():
         }
         for prod, (tfn, (M, NN, KK), a_km, b_kn, A, B) in cases.items():
             flop = 2.0 * M * NN * KK
+            if a.tunableop:  # the search runs at the first call of a shape; time the chosen solution
+                tfn()
+                torch.cuda.synchronize()
             t_torch = timeit(tfn)
             t_nbd = timeit(lambda: G.matmul(A, B, a_km=a_km, b_kn=b_kn))
             ref = tfn().float()

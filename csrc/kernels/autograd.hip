@@ -719,6 +719,8 @@ struct Bwd {
   bool dx_alias = false, dh_alias = false;  // ...that are another block graph's outputs
   Tensor g1, dh;                          // static outputs: the gradients of x and h
   std::vector<graddst::ClaimRecord> claims;  // in capture order
+  std::vector<int> pidx;                  // the saved parameter each claim was made for (by position:
+                                          // native()'s cast weights are new tensors every step)
   std::vector<int> slot;                  // the node output each claim's slice is returned as
   std::vector<Tensor> warm_refs;
   std::shared_ptr<void> deferred;          // its deferred reductions (defer::record_begin)
@@ -1309,8 +1311,9 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
     Bwd& B = *found;
     bool ok = (!has_dx || !B.dx_alias || dx_out.data_ptr() == B.dx_in.data_ptr()) &&
               (!B.dh_alias || dh_out.data_ptr() == B.dh_in.data_ptr());
-    for (const auto& c : B.claims) {
-      const int i = param_index(c.param);
+    for (size_t k = 0; k < B.claims.size(); ++k) {
+      const auto& c = B.claims[k];
+      const int i = B.pidx[k];
       ok = ok && i >= 0 && dst[i].defined() && dst[i].data_ptr() == c.dst && acc[i] == c.acc;
     }
     if (!ok) {
@@ -1320,8 +1323,9 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
     }
     if (has_dx && !B.dx_alias && dx_out.data_ptr() != B.dx_in.data_ptr()) B.dx_in.copy_(dx_out);
     if (!B.dh_alias && dh_out.data_ptr() != B.dh_in.data_ptr()) B.dh_in.copy_(dh_out);
-    for (const auto& c : B.claims) {  // the pass bookkeeping of the captured claims
-      const int i = param_index(c.param);
+    for (size_t k = 0; k < B.claims.size(); ++k) {  // the pass bookkeeping of the captured claims
+      const auto& c = B.claims[k];
+      const int i = B.pidx[k];
       bool a = false;
       const Tensor d = graddst::claim(*ps[i], a);
       TORCH_CHECK(d.defined() && d.data_ptr() == c.dst && a == c.acc, "nbd: block graph claim changed");
@@ -1331,7 +1335,7 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
     out[0] = need_x ? at::alias(B.g1) : Tensor();
     out[1] = need_h ? at::alias(B.dh) : Tensor();
     for (size_t k = 0; k < B.claims.size(); ++k) {
-      const int i = param_index(B.claims[k].param);
+      const int i = B.pidx[k];
       if (B.slot[k] >= 0) out[B.slot[k]] = graddst::hand_back(*ps[i], dst[i], B.claims[k].acc);
     }
     return true;
@@ -1391,6 +1395,8 @@ static bool block_bwd_graph(bg::Graph& G, const std::vector<Tensor>& sv,
     return false;
   }
   // every weight gradient must be its claimed slice (else it would be static graph memory)
+  B->pidx.resize(B->claims.size());
+  for (size_t k = 0; k < B->claims.size(); ++k) B->pidx[k] = param_index(B->claims[k].param);
   B->slot.assign(B->claims.size(), -1);
   bool valid = true;
   for (int i = 0; i < 8; ++i) {
@@ -1692,6 +1698,8 @@ struct Entry {
   c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl> first;  // the group's first parameter (validates the key)
   Tensor buf;
   std::shared_ptr<std::atomic<bool>> busy;  // a cast node of an earlier pass still owns it
+  Tensor gbuf;  // the kept cast's gradient buffer (same layout): its slices are the cast weights'
+                // registered gradient destinations (graddst::set), allocated on first use
 };
 std::mutex g_mu;
 std::unordered_map<const c10::TensorImpl*, Entry> g_bufs;
@@ -1736,6 +1744,15 @@ std::pair<Tensor, std::shared_ptr<std::atomic<bool>>> get(const Tensor& first, i
   return {buf, busy};
 }
 
+// The gradient buffer of the group whose kept cast buffer is `buf` (allocated on first use).
+Tensor grad_buf(const Tensor& first, const Tensor& buf) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_bufs.find(first.unsafeGetTensorImpl());
+  if (it == g_bufs.end() || !it->second.buf.is_same(buf)) return Tensor();
+  if (!it->second.gbuf.defined()) it->second.gbuf = at::empty_like(buf);
+  return it->second.gbuf;
+}
+
 Tensor release_token(std::shared_ptr<std::atomic<bool>> busy) {
   static int64_t dummy = 0;
   return at::from_blob(
@@ -1759,6 +1776,20 @@ std::vector<Tensor> drop_kept(std::vector<Tensor> refs) {
 }
 }  // namespace castbuf
 
+// Gradient destinations for the cast weights (NBD_CAST_GRAD_DEST=0: off).  A kept cast (stable
+// addresses) gets a kept gradient buffer of the same layout; cast_group_ag registers each returned
+// weight's slice of it (graddst::set), so the decoder block's backward writes the weight gradients
+// there — static addresses, which is what lets the block's backward run as a HIP graph (bg, mode 2)
+// on the fp32-master path — and the cast node's backward reads them from one place.
+static bool cast_grad_dest_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("NBD_CAST_GRAD_DEST");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+thread_local Tensor t_cast_gbuf;  // forward -> cast_group_ag: the gradient buffer to register
+
 struct CastGroupFn : public torch::autograd::Function<CastGroupFn> {
   // (ps as a TensorList: only that form counts its elements as the node's inputs)
   static variable_list forward(AutogradContext* ctx, at::TensorList ps, int64_t dtype) {
@@ -1773,6 +1804,7 @@ struct CastGroupFn : public torch::autograd::Function<CastGroupFn> {
     }
     auto [buf, busy] = castbuf::get(ps[0], total, ps[0].options().dtype((at::ScalarType)dtype));
     if (busy) ctx->save_for_backward({castbuf::release_token(busy)});
+    t_cast_gbuf = busy && cast_grad_dest_on() ? castbuf::grad_buf(ps[0], buf) : Tensor();
     std::vector<Tensor> src;
     src.reserve(ps.size());
     for (const Tensor& p : ps) src.push_back(p.contiguous());
@@ -1799,6 +1831,9 @@ struct CastGroupFn : public torch::autograd::Function<CastGroupFn> {
       i += (size_t)r + 1;
     }
     variable_list out(gs.size() + 1);  // (the dtype argument: none)
+    // weight gradients written into the registered slices may still have reductions queued
+    // (defer.hip: nothing else flushes them on this path)
+    if (defer::pending() > 0) defer::flush();
     std::vector<Tensor> have;
     std::vector<int64_t> have_offs;
     for (size_t i = 0; i < gs.size(); ++i)
@@ -1817,7 +1852,16 @@ struct CastGroupFn : public torch::autograd::Function<CastGroupFn> {
 };
 
 std::vector<Tensor> cast_group_ag(at::TensorList ps, int64_t dtype) {
-  return CastGroupFn::apply(ps, dtype);
+  t_cast_gbuf = Tensor();
+  std::vector<Tensor> out = CastGroupFn::apply(ps, dtype);
+  const Tensor gbuf = std::move(t_cast_gbuf);
+  t_cast_gbuf = Tensor();
+  if (gbuf.defined() && c10::GradMode::is_enabled()) {
+    auto [offs, total] = flat_offsets(ps.vec());
+    for (size_t i = 0; i < out.size(); ++i)
+      if (out[i].requires_grad()) graddst::set(out[i], gbuf.narrow(0, offs[i], out[i].numel()).view(out[i].sizes()));
+  }
+  return out;
 }
 
 std::vector<Tensor> cast_group_noag(at::TensorList ps, int64_t dtype) {

@@ -4,6 +4,7 @@
 #include <c10/util/intrusive_ptr.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <mutex>
 #include <unordered_map>
 
@@ -30,7 +31,7 @@ void record_claims(std::vector<ClaimRecord>* log) { t_log = log; }
 // claim() with `take` = hand it out (pass bookkeeping, flush on a second use); peek() without
 static at::Tensor lookup(const at::Tensor& param, bool& acc, bool take) {
   acc = false;
-  if (!param.defined() || !param.requires_grad() || !param.is_leaf()) return at::Tensor();
+  if (!param.defined() || !param.requires_grad()) return at::Tensor();
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_map.empty()) return at::Tensor();
   auto it = g_map.find(param.unsafeGetTensorImpl());
@@ -43,7 +44,7 @@ static at::Tensor lookup(const at::Tensor& param, bool& acc, bool take) {
     if (take) defer::flush();
     return at::Tensor();
   }
-  const at::Tensor& g = param.grad();
+  const at::Tensor g = param.is_leaf() ? param.grad() : at::Tensor();  // (a registered cast: no .grad)
   if (g.defined()) {
     // accumulate only onto our own slice; any other .grad (set by the user) keeps the normal path
     if (g.data_ptr() != e.dst.data_ptr() || !g.sizes().equals(e.dst.sizes()) || g.scalar_type() != e.dst.scalar_type())
@@ -90,19 +91,28 @@ void purge_expired_locked() {
 }
 }  // namespace
 
-void set_grad_dest(const at::Tensor& param, const c10::optional<at::Tensor>& dst) {
+void set(const at::Tensor& param, const at::Tensor& dst) {
   std::lock_guard<std::mutex> lk(g_mu);
-  purge_expired_locked();
+  // (amortised: the cast weights of models.native() register afresh at every forward)
+  static size_t purge_at = 64;
+  if (g_map.size() >= purge_at) {
+    purge_expired_locked();
+    purge_at = std::max<size_t>(64, 2 * g_map.size());
+  }
   const c10::TensorImpl* key = param.unsafeGetTensorImpl();
-  if (!dst || !dst->defined()) {
+  if (!dst.defined()) {
     g_map.erase(key);
     return;
   }
-  TORCH_CHECK(dst->sizes().equals(param.sizes()) && dst->scalar_type() == param.scalar_type() &&
-                  dst->device() == param.device() && dst->is_contiguous(),
+  TORCH_CHECK(dst.sizes().equals(param.sizes()) && dst.scalar_type() == param.scalar_type() &&
+                  dst.device() == param.device() && dst.is_contiguous(),
               "set_grad_dest: the destination must be a contiguous tensor of the parameter's shape, dtype and device");
   g_map.erase(key);
-  g_map.emplace(key, Entry(param.getIntrusivePtr(), *dst));
+  g_map.emplace(key, Entry(param.getIntrusivePtr(), dst));
+}
+
+void set_grad_dest(const at::Tensor& param, const c10::optional<at::Tensor>& dst) {
+  graddst::set(param, dst ? *dst : at::Tensor());
 }
 
 void grad_dest_new_pass() {

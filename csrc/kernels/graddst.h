@@ -22,6 +22,11 @@
 namespace nbd {
 namespace graddst {
 
+// Register `dst` as `param`'s gradient destination (undefined dst: remove).  `param` is normally a
+// leaf (DDP's parameters); a non-leaf registered here — a kept compute-dtype cast of an fp32
+// master weight (autograd.hip CastGroupFn) — has no .grad, so its writes never accumulate.
+void set(const at::Tensor& param, const at::Tensor& dst);
+
 // The registered destination of `param`'s gradient if this write may go there (else undefined).
 // `acc` = the destination already holds `param`'s accumulated gradient: add to it.
 at::Tensor claim(const at::Tensor& param, bool& acc);

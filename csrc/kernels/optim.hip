@@ -17,7 +17,8 @@
 // 28 bytes per parameter for bf16 params (read 2 + 12, write 12 + 2) instead of the eager chain
 // (bf16->fp32 grad cast, unflatten, multi-tensor AdamW over fp32 params, fp32->bf16 weight cast in
 // every autocast forward).  Pure HBM streaming: 16 B per lane per access, 8 elements per thread
-// per iteration, grid-stride over <= 2048 blocks, non-temporal stores for the 16-bit param copy.
+// per thread, one thread per 8-element group (no grid-stride loop: measured 8 % faster than a
+// 2048-block grid-stride, FINDINGS §31), non-temporal stores for the 16-bit param copy.
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -131,7 +132,9 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(const G* __restrict__ g
   }
 }
 
-// NBD_ADAMW_BLOCKS (A/B): grid cap in workgroups (default 2048 = 8 per CU, grid-stride);
+// NBD_ADAMW_BLOCKS (A/B): grid cap in workgroups (default none: one thread per 8-element group —
+// 0.648 ms against 0.700 for the former 2048-block grid-stride default, 124 M parameters,
+// profiles/adamw_grid_r5.txt);
 // NBD_ADAMW_VARIANT: 1 = two 8-element groups per thread per iteration, 2 = that with
 // non-temporal loads, 3 = one group with non-temporal loads (all measured slower: FINDINGS §31)
 static int adamw_env(const char* name, int dflt) {
@@ -143,7 +146,7 @@ template <typename G, typename P>
 static void launch_adamw(const at::Tensor& grad, const at::Tensor& param, const at::Tensor& master,
                          const at::Tensor& m, const at::Tensor& v, const float* gs, const float* dstep,
                          const float* dlr, int64_t n, const AdamArgs& a, hipStream_t st) {
-  static const int cap = std::max(1, adamw_env("NBD_ADAMW_BLOCKS", 256 * 8));
+  static const int cap = std::max(1, adamw_env("NBD_ADAMW_BLOCKS", 1 << 30));
   static const int variant = adamw_env("NBD_ADAMW_VARIANT", 0);
   const int64_t work = (n + 7) / 8;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, cap));

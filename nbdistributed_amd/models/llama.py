@@ -670,7 +670,7 @@ def from_hf(hf_model, compute_dtype: Optional[torch.dtype] = None) -> nn.Module:
 
 
 def native(hf_model, compute_dtype: Optional[torch.dtype] = torch.bfloat16, fused_optimizer: bool = True,
-           block_graphs: int = 1) -> nn.Module:
+           block_graphs: Optional[int] = None) -> nn.Module:
     """The one-line swap for a notebook written against HF transformers: call it on the HF
     Llama / SmolLM2 / Qwen2 / Mistral model BEFORE creating the optimizer and
     ``accelerator.prepare``.  The returned module takes the same keyword arguments, returns
@@ -691,6 +691,8 @@ def native(hf_model, compute_dtype: Optional[torch.dtype] = torch.bfloat16, fuse
     The model's output is a fresh tensor as always; block-internal activations stay allocated
     between steps (at most 4 sequence lengths per block are graphed)."""
     m = from_hf(hf_model, compute_dtype=compute_dtype)
+    if block_graphs is None:
+        block_graphs = int(os.environ.get("NBD_NATIVE_BLOCK_GRAPHS", "1"))
     if os.environ.get("NBD_BLOCK_GRAPHS") == "0":
         block_graphs = 0
     if hasattr(m, "model") and isinstance(m.model, LlamaModel):

@@ -216,3 +216,36 @@ def test_per_model_graph_reset_and_memory(dev):
     del keep
     gc.collect()
     assert ops.block_graphs_memory()["graphs"] == 0
+
+
+def test_native_backward_graphs_match_eager_backward(dev):
+    """native(..., block_graphs=2): the cast weights' gradients go to kept buffers (graddst), so
+    each decoder block's backward is captured and replayed as a HIP graph on the fp32-master path;
+    the fp32 gradients equal the eager backward's (block_graphs=1), step after step, and a second
+    backward without zero_grad accumulates."""
+    transformers = pytest.importorskip("transformers")
+    import nbdistributed_amd as nbd
+    from nbdistributed_amd.models import SMOLLM2_135M
+
+    cfg = dict(SMOLLM2_135M)
+    cfg.update(num_hidden_layers=3, vocab_size=4096)
+    torch.manual_seed(0)
+    hf = transformers.LlamaForSequenceClassification(
+        transformers.LlamaConfig(num_labels=2, pad_token_id=0, **cfg)).to(dev)
+    m1 = nbd.models.native(copy.deepcopy(hf), block_graphs=1)
+    m2 = nbd.models.native(copy.deepcopy(hf), block_graphs=2)
+    ids, mask, labels = _batch(dev, False)
+    s0 = ops.block_graphs_stats()
+    for step in range(5):
+        grads = []
+        for m in (m1, m2):
+            m.zero_grad(set_to_none=True)
+            m(input_ids=ids, attention_mask=mask, labels=labels).loss.backward()
+            if step == 4:  # accumulate a second micro-batch
+                m(input_ids=ids, attention_mask=mask, labels=labels).loss.backward()
+            torch.cuda.synchronize()
+            grads.append([p.grad.clone() for p in m.parameters()])
+        for a, b in zip(*grads):
+            assert torch.equal(a, b), (step, float((a - b).abs().max()))
+    s1 = ops.block_graphs_stats()
+    assert s1["bwd_captures"] > s0["bwd_captures"] and s1["bwd_replays"] - s0["bwd_replays"] >= 3 * 3, (s0, s1)
