@@ -4,7 +4,7 @@ set -e
 R=$GRAFT_REPO_ROOT
 cd $R
 export PYTHONUNBUFFERED=1
-timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_attn.py tests/test_gpu_llama.py tests/test_gpu_swap_semantics.py tests/test_gpu_block_graphs.py > gpurun_out/r5g_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_swap_semantics.py tests/test_gpu_block_graphs.py tests/test_gpu_graddst.py tests/test_gpu_llama.py tests/test_gpu_attn.py > gpurun_out/r5g_tests.log 2>&1
 SH="--only smollm2_causal,gpt2_causal,b1,b4,b64,t256 --shape b1,1,9,3,128,1 --shape b4,4,9,3,128,1 --shape b64,64,9,3,128,1 --shape t256,16,9,3,256,1"
 for i in 1 2; do
   echo "== auto round $i"; timeout -k 10 120 python -u benchmarks/attn_bench.py $SH

@@ -10,12 +10,30 @@ import csv
 import glob
 import os
 import re
+import sqlite3
 
 
 def short(name: str, n: int = 110) -> str:
     name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name) if name.startswith("void ") or "(" in name else name
     return name if len(name) <= n else name[: n - 3] + "..."
+
+
+def db_rows(path):
+    """rocprofv3's SQLite output (ROCm 7 default): the same per-kernel statistics as the CSV
+    ``kernel_stats`` file, and the first dispatch's resources per kernel."""
+    c = sqlite3.connect(path)
+    q = ("select name, count(*), sum(duration), avg(duration), min(duration), max(duration) "
+         "from kernels group by name")
+    agg = list(c.execute(q))
+    total = sum(r[2] for r in agg) or 1.0
+    rows = [{"Name": n, "Calls": str(k), "TotalDurationNs": str(t), "AverageNs": str(av), "MinNs": str(mn),
+             "MaxNs": str(mx), "Percentage": str(100.0 * t / total)} for n, k, t, av, mn, mx in agg]
+    res = {}
+    for n, v, a, sg, lds, wx, gx in c.execute(
+            "select name, vgpr_count, accum_vgpr_count, sgpr_count, lds_size, workgroup_x, grid_x from kernels"):
+        res.setdefault(n, (v, a, sg, lds, wx, gx))
+    return rows, res
 
 
 def main():
@@ -35,8 +53,13 @@ def main():
             if nm not in res:
                 res[nm] = (r.get("VGPR_Count"), r.get("Accum_VGPR_Count"), r.get("SGPR_Count"), r.get("LDS_Block_Size"),
                            r.get("Workgroup_Size_X"), r.get("Grid_Size_X"))
-    for path in stats:
-        rows = list(csv.DictReader(open(path)))
+    tables = [list(csv.DictReader(open(path))) for path in stats]
+    if not stats:
+        for path in glob.glob(os.path.join(a.prof_dir, "**", "*.db"), recursive=True):
+            rows, r2 = db_rows(path)
+            tables.append(rows)
+            res.update(r2)
+    for rows in tables:
         total = sum(float(r["TotalDurationNs"]) for r in rows)
         ours = [r for r in rows if "nbd::" in r["Name"]]
         if ours:

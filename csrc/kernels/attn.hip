@@ -54,7 +54,7 @@ typedef __attribute__((address_space(3))) s4v lds_s4v;
 
 constexpr int D = 64;
 constexpr int NT = 256;     // threads per workgroup (4 waves)
-constexpr int BLK = 128;    // rows owned by a four-wave workgroup (queries in fwd/dq, keys in dkdv)
+constexpr int BLK = 128;    // rows owned by a workgroup (queries in fwd/dq, keys in dkdv)
 constexpr int TILE = 64;    // rows per swept tile
 constexpr int RS = 72;      // LDS row stride (elements) of row-read images: 144 B
 constexpr int RSV = 96;     // LDS row stride of transpose-only images: 192 B (tr reads conflict-free)
@@ -168,87 +168,66 @@ __device__ __forceinline__ void store_dT_rope(uint16_t* rowp, const f16x& a0, co
   }
 }
 
-// tile staging with the two halves of a row in one thread (row = c/4, chunks c%4 and c%4 + 4 for
-// slot c = tid + i·NTH), so the rotation can be applied between the global load and the LDS store
-template <int NTH>
+// tile staging with the two halves of a row in one thread (row = tid/4, chunks q and q+4), so
+// the rotation can be applied between the global load and the LDS store
 struct StagePair {
-  static constexpr int P = 256 / NTH;  // 64 rows x 4 chunk pairs over the workgroup
-  s8v a[P], b[P];
+  s8v a, b;
   __device__ __forceinline__ void load(const uint16_t* base, int64_t st, int tid) {
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const int c = tid + i * NTH;
-      const uint16_t* p = base + (c >> 2) * st + (c & 3) * 8;
-      a[i] = ld16(p);
-      b[i] = ld16(p + 32);
-    }
+    const uint16_t* p = base + (tid >> 2) * st + (tid & 3) * 8;
+    a = ld16(p);
+    b = ld16(p + 32);
   }
   __device__ __forceinline__ void rope(const Rope& rp, int t0, int tid) {
-    if (rp.cos == nullptr) return;
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const int c = tid + i * NTH;
-      rope8(a[i], b[i], rp, t0 + (c >> 2), (c & 3) * 8);
-    }
+    if (rp.cos != nullptr) rope8(a, b, rp, t0 + (tid >> 2), (tid & 3) * 8);
   }
   __device__ __forceinline__ void store(uint16_t* lds, int stride, int tid) const {
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const int c = tid + i * NTH;
-      uint16_t* p = lds + (c >> 2) * stride + (c & 3) * 8;
-      st16(p, a[i]);
-      st16(p + 32, b[i]);
-    }
+    uint16_t* p = lds + (tid >> 2) * stride + (tid & 3) * 8;
+    st16(p, a);
+    st16(p + 32, b);
   }
 };
 
-// cooperative tile staging: 64 rows x 64 d, 512 16-B chunks (chunk c = row c/8, dims 8(c%8)..)
-template <int NTH>
+// cooperative tile staging: 64 rows x 64 d, 512 16-B chunks, 2 per thread
 struct Stage2 {
-  static constexpr int P = 512 / NTH;
-  s8v a[P];
+  s8v a[2];
   __device__ __forceinline__ void load(const uint16_t* base, int64_t st, int tid) {
 #pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const int c = tid + i * NTH;
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * NT;
       a[i] = ld16(base + (c >> 3) * st + (c & 7) * 8);
     }
   }
   __device__ __forceinline__ void store(uint16_t* lds, int stride, int tid) const {
 #pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const int c = tid + i * NTH;
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * NT;
       st16(lds + (c >> 3) * stride + (c & 7) * 8, a[i]);
     }
   }
 };
 
 // ============================================================================ forward
-// NW waves per workgroup: NW = 4 (128 queries) by default; NW = 1 (32 queries, four times the
-// workgroups) where B·H·T/128 workgroups cannot fill the chip (short sequences: the notebook's
-// T = 128 gives 144 four-wave workgroups for 256 CUs)
-template <bool CAUSAL, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void fwd_kernel(View q, View k, View v, MView o, float* __restrict__ lse,
-                                                          int H, int T, int nblk, float sc2, int group, Rope rp) {
-  constexpr int NTH = 64 * NW, BQ = 32 * NW;
+template <bool CAUSAL>
+__global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MView o, float* __restrict__ lse,
+                                                     int H, int T, int nblk, float sc2, int group, Rope rp) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[TILE * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[TILE * RSV];
   const int bh = blockIdx.x % (gridDim.x / nblk);
   const int qb = CAUSAL ? nblk - 1 - blockIdx.x / (gridDim.x / nblk) : blockIdx.x / (gridDim.x / nblk);
   const int b = bh / H, hh = bh % H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int q0 = qb * BQ + w * 32;  // this wave's first query
-  const int qi = q0 + r;            // this lane's query
-  const int kh = hh / group;        // GQA: the key/value head of this query head
+  const int q0 = qb * BLK + w * 32;  // this wave's first query
+  const int qi = q0 + r;             // this lane's query
+  const int kh = hh / group;         // GQA: the key/value head of this query head
   s8v qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qf[s] = ld16(q.row(b, hh, qi) + 16 * s + 8 * h);
   if (rp.cos != nullptr) rope_frag(qf, rp, qi, h);
   f16x acc_o[2] = {zero16(), zero16()};
   float m = -INFINITY, l = 0.f;
-  const int ntiles = CAUSAL ? (qb * BQ + BQ + TILE - 1) / TILE : T / TILE;
-  StagePair<NTH> sk;
-  Stage2<NTH> sv;
+  const int ntiles = CAUSAL ? (qb * BLK + BLK) / TILE : T / TILE;
+  StagePair sk;
+  Stage2 sv;
   sk.load(k.row(b, kh, 0), k.st, tid);
   sv.load(v.row(b, kh, 0), v.st, tid);
   sk.rope(rp, 0, tid);
@@ -377,10 +356,9 @@ __global__ __launch_bounds__(NT) void bwd_pre_kernel(View dout, View out, float*
 // workgroups for SmolLM2 (9 query / 3 kv heads) instead of one workgroup sweeping all 3 heads.
 // δ of a 64-row tile from register-staged dO and O chunks (Stage2 mapping: chunk c = tid + i·NT
 // is row c/8, dims 8(c%8)..+8): 8-element partial dot, summed over the row's 8 consecutive lanes
-template <int NTH>
-__device__ __forceinline__ void tile_delta(const Stage2<NTH>& dO, const Stage2<NTH>& O, float* Ds, int tid) {
+__device__ __forceinline__ void tile_delta(const Stage2& dO, const Stage2& O, float* Ds, int tid) {
 #pragma unroll
-  for (int i = 0; i < Stage2<NTH>::P; ++i) {
+  for (int i = 0; i < 2; ++i) {
     float acc = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e)
@@ -388,14 +366,14 @@ __device__ __forceinline__ void tile_delta(const Stage2<NTH>& dO, const Stage2<N
     acc += __shfl_xor(acc, 1, 64);
     acc += __shfl_xor(acc, 2, 64);
     acc += __shfl_xor(acc, 4, 64);
-    if ((tid & 7) == 0) Ds[(tid + i * NTH) >> 3] = -acc;  // stored negated: the dP accumulator's start
+    if ((tid & 7) == 0) Ds[(tid + i * NT) >> 3] = -acc;  // stored negated: the dP accumulator's start
   }
 }
 
 // FD (fused δ, short sequences): δ = Σ_d dO·O is computed from the staged dO tile and an O tile
 // loaded beside it, instead of by bwd_pre_kernel — one launch less where each (query head, tile)
 // is swept by one key block anyway (T ≤ 256).
-template <bool CAUSAL, bool FD, int NW>
+template <bool CAUSAL, bool FD>
 __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, View v, View dout, View out,
                                           const float* __restrict__ lse, const float* __restrict__ delta, MView dk,
                                           MView dv, int H, int T, int nblk, float sc2, float scale, int group,
@@ -413,8 +391,7 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
   const int gpw = group / gsplit;
   const int Hq = H * group;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
-  constexpr int NTH = 64 * NW, BKEY = 32 * NW;
-  const int key0 = kb0 * BKEY + w * 32;
+  const int key0 = kb0 * BLK + w * 32;
   const int ki = key0 + r;  // this lane's key
   s8v kf[4], vf[4];
 #pragma unroll
@@ -424,14 +401,14 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
   }
   if (rp.cos != nullptr) rope_frag(kf, rp, ki, h);
   f16x dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
-  const int t0 = CAUSAL ? (kb0 * BKEY) / TILE : 0;
+  const int t0 = CAUSAL ? (kb0 * BLK) / TILE : 0;
   const int nt = T / TILE;
   for (int g = split * gpw; g < (split + 1) * gpw; ++g) {
     const int hq = kvh * group + g;
     const float* lse_bh = lse + ((int64_t)b * Hq + hq) * T;
     const float* del_bh = FD ? nullptr : delta + ((int64_t)b * Hq + hq) * T;
-    StagePair<NTH> sq;
-    Stage2<NTH> so, sov;  // dO tile; O tile (FD only)
+    StagePair sq;
+    Stage2 so, sov;  // dO tile; O tile (FD only)
     float lv = 0.f, dlv = 0.f;
     sq.load(q.row(b, hq, t0 * TILE), q.st, tid);
     so.load(dout.row(b, hq, t0 * TILE), dout.st, tid);
@@ -535,7 +512,7 @@ __device__ __forceinline__ void dkdv_body(int blk, int nblocks, View q, View k, 
 }
 
 // ============================================================================ backward: dQ
-template <bool CAUSAL, bool FD, int NW>
+template <bool CAUSAL, bool FD>
 __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, View v, View dout, View out,
                                         const float* __restrict__ lse, const float* __restrict__ delta, MView dq,
                                         int H, int T, int nblk, float sc2, float scale, int group, Rope rp) {
@@ -546,8 +523,7 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
   const int qb = CAUSAL ? nblk - 1 - blk / per : blk / per;
   const int b = bh / H, hh = bh % H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
-  constexpr int NTH = 64 * NW, BQ = 32 * NW;
-  const int q0 = qb * BQ + w * 32;
+  const int q0 = qb * BLK + w * 32;
   const int qi = q0 + r;
   const int kh = hh / group;
   s8v qf[4], of[4];
@@ -575,9 +551,9 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
   f16x ndl;  // −δ of this lane's query in every register: the dP^T accumulator's start (dS = P·dP)
 #pragma unroll
   for (int i = 0; i < 16; ++i) ndl[i] = -dl;
-  const int ntiles = CAUSAL ? (qb * BQ + BQ + TILE - 1) / TILE : T / TILE;
-  StagePair<NTH> sk;
-  Stage2<NTH> sv;
+  const int ntiles = CAUSAL ? (qb * BLK + BLK) / TILE : T / TILE;
+  StagePair sk;
+  Stage2 sv;
   sk.load(k.row(b, kh, 0), k.st, tid);
   sv.load(v.row(b, kh, 0), v.st, tid);
   sk.rope(rp, 0, tid);
@@ -647,17 +623,17 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
 // are independent, and for short sequences (SmolLM2: T = 128) neither fills the chip alone.
 // (Pairing complementary causal blocks in one workgroup — key blocks kb and nblk-1-kb, query
 // blocks qb and nblk-1-qb — was measured 14 % slower at B8 H12 T1024: docs/FINDINGS.md §31.)
-template <bool CAUSAL, bool FD, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void bwd_kernel(View q, View k, View v, View dout, View out,
+template <bool CAUSAL, bool FD>
+__global__ __launch_bounds__(NT, 2) void bwd_kernel(View q, View k, View v, View dout, View out,
                                                      const float* __restrict__ lse,
                                                      const float* __restrict__ delta, MView dq, MView dk, MView dv,
                                                      int Hq, int Hkv, int T, int nblk, float sc2, float scale,
                                                      int group, Rope rp, int nkv, int gsplit, int64_t split_stride) {
   if ((int)blockIdx.x < nkv)
-    dkdv_body<CAUSAL, FD, NW>(blockIdx.x, nkv, q, k, v, dout, out, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale, group, rp,
+    dkdv_body<CAUSAL, FD>(blockIdx.x, nkv, q, k, v, dout, out, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale, group, rp,
                           gsplit, split_stride);
   else
-    dq_body<CAUSAL, FD, NW>(blockIdx.x - nkv, gridDim.x - nkv, q, k, v, dout, out, lse, delta, dq, Hq, T, nblk, sc2, scale,
+    dq_body<CAUSAL, FD>(blockIdx.x - nkv, gridDim.x - nkv, q, k, v, dout, out, lse, delta, dq, Hq, T, nblk, sc2, scale,
                         group, rp);
 }
 
@@ -701,16 +677,6 @@ static int bwd_pad() {
   return v;
 }
 
-// Waves per workgroup: one where B·H·T/128 four-wave workgroups cannot fill the chip's 256 CUs
-// (four times the workgroups, no barrier across waves), four otherwise; NBD_ATTN_NW=1|4 forces.
-// (read per call, so tests can pin either layout)
-static int waves_per_wg(int64_t wgs4) {
-  const char* e = std::getenv("NBD_ATTN_NW");
-  const int forced = e == nullptr ? 0 : std::atoi(e);
-  if (forced == 1 || forced == 4) return forced;
-  return wgs4 < 256 ? 1 : 4;
-}
-
 static View view_of(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.size(3) == D && t.stride(3) == 1, "attn: ", name,
               " must be a [B, H, T, 64] GPU view with a contiguous last dim");
@@ -729,7 +695,7 @@ static void check_shapes(const at::Tensor& q, const at::Tensor& k, const at::Ten
               "attn: k and v must match, and share batch and length with q");
   TORCH_CHECK(k.size(1) > 0 && q.size(1) % k.size(1) == 0, "attn: query heads must be a multiple of key/value heads");
   TORCH_CHECK(q.size(2) % BLK == 0 && q.size(2) >= BLK, "attn: sequence length must be a positive multiple of 128");
-  TORCH_CHECK(q.size(0) * q.size(1) * (q.size(2) / 32) < (1LL << 31), "attn: grid too large");
+  TORCH_CHECK(q.size(0) * q.size(1) * (q.size(2) / BLK) < (1LL << 31), "attn: grid too large");
 }
 
 static Rope rope_of(const c10::optional<at::Tensor>& c, const c10::optional<at::Tensor>& s, int64_t T) {
@@ -756,22 +722,16 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::T
   MView ov = mview_of(o, "out");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-  const int nw = waves_per_wg((int64_t)B * H * (T / BLK));
-  const int nblk = T / (32 * nw);
+  const int nblk = T / BLK;
   const dim3 grid((unsigned)(B * H * nblk));
   const float sc2 = (float)scale * kLog2e;
   const int group = H / (int)k.size(1);
-#define NBD_FWD(C_, W_)                                                                                       \
-  hipLaunchKernelGGL((fwd_kernel<C_, W_>), grid, dim3(64 * W_), fwd_pad(), st, qv, kv, vv, ov, lse.data_ptr<float>(), \
-                     H, T, nblk, sc2, group, rp)
-  if (nw == 1) {
-    if (causal) NBD_FWD(true, 1);
-    else NBD_FWD(false, 1);
-  } else {
-    if (causal) NBD_FWD(true, 4);
-    else NBD_FWD(false, 4);
-  }
-#undef NBD_FWD
+  if (causal)
+    hipLaunchKernelGGL((fwd_kernel<true>), grid, dim3(NT), fwd_pad(), st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
+                       sc2, group, rp);
+  else
+    hipLaunchKernelGGL((fwd_kernel<false>), grid, dim3(NT), fwd_pad(), st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
+                       sc2, group, rp);
   C10_HIP_KERNEL_LAUNCH_CHECK();
   return {o, lse};
 }
@@ -793,14 +753,13 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
   MView dqv = mview_of(dq, "dq"), dkv = mview_of(dk, "dk"), dvv = mview_of(dv, "dv");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-  const int nw = waves_per_wg((int64_t)B * H * (T / BLK));
-  const int nblk = T / (32 * nw);
+  const int nblk = T / BLK;
   // short sequences: δ inside the main kernel (each (query head, tile) is swept by <= 2 key blocks)
   static const int fd_env = [] {  // NBD_ATTN_FD=1 / 0: force the fused-δ path on / off (A/B)
     const char* e = std::getenv("NBD_ATTN_FD");
     return e == nullptr ? -1 : std::atoi(e);
   }();
-  const bool fd = fd_env >= 0 ? fd_env == 1 : T <= 2 * BLK;
+  const bool fd = fd_env >= 0 ? fd_env == 1 : nblk <= 2;
   at::Tensor delta;
   if (!fd) {
     delta = at::empty({B, H, T}, lse.options());
@@ -813,11 +772,13 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
   const int Hkv = (int)k.size(1), group = H / Hkv;
   const float sc2 = (float)scale * kLog2e;
   // GQA with few key/value workgroups: split each kv head's query-head group over workgroups
+  // (below 128 of them: SmolLM2 B16 T128 has 48 and runs its backward in 16.8 µs split against
+  // 23.4 unsplit; at B64, 192, unsplit is faster, 24.9 against 39.0 — profiles/attn_nw_gsplit_r5.txt)
   static const int gsplit_env = [] {  // NBD_ATTN_GSPLIT=1: never split (A/B)
     const char* e = std::getenv("NBD_ATTN_GSPLIT");
     return e == nullptr ? 0 : std::atoi(e);
   }();
-  const int gsplit = gsplit_env == 1 ? 1 : (group > 1 && B * Hkv * nblk < 256) ? group : 1;
+  const int gsplit = gsplit_env == 1 ? 1 : (group > 1 && B * Hkv * nblk < 128) ? group : 1;
   const int nkv = B * Hkv * nblk * gsplit, nq = B * H * nblk;
   MView dkw = dkv, dvw = dvv;
   at::Tensor pk, pv;
@@ -829,26 +790,16 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     dkw = MView{static_cast<uint16_t*>(pk.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
     dvw = MView{static_cast<uint16_t*>(pv.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
   }
-#define NBD_BWD(C_, F_, W_)                                                                                     \
-  hipLaunchKernelGGL((bwd_kernel<C_, F_, W_>), dim3((unsigned)(nkv + nq)), dim3(64 * W_), bwd_pad(), st, qv, kv, vv, \
-                     dov, ov, lse.data_ptr<float>(), dptr, dqv, dkw, dvw, H, Hkv, T, nblk, sc2, (float)scale, group, rp, \
-                     nkv, gsplit, split_stride)
-  if (nw == 1) {
-    if (causal) {
-      if (fd) NBD_BWD(true, true, 1);
-      else NBD_BWD(true, false, 1);
-    } else {
-      if (fd) NBD_BWD(false, true, 1);
-      else NBD_BWD(false, false, 1);
-    }
+#define NBD_BWD(C_, F_)                                                                                      \
+  hipLaunchKernelGGL((bwd_kernel<C_, F_>), dim3((unsigned)(nkv + nq)), dim3(NT), bwd_pad(), st, qv, kv, vv, dov, ov,   \
+                     lse.data_ptr<float>(), dptr, dqv, dkw, dvw, H, Hkv, T, nblk, sc2, (float)scale, group, rp, nkv, \
+                     gsplit, split_stride)
+  if (causal) {
+    if (fd) NBD_BWD(true, true);
+    else NBD_BWD(true, false);
   } else {
-    if (causal) {
-      if (fd) NBD_BWD(true, true, 4);
-      else NBD_BWD(true, false, 4);
-    } else {
-      if (fd) NBD_BWD(false, true, 4);
-      else NBD_BWD(false, false, 4);
-    }
+    if (fd) NBD_BWD(false, true);
+    else NBD_BWD(false, false);
   }
 #undef NBD_BWD
   C10_HIP_KERNEL_LAUNCH_CHECK();

@@ -51,15 +51,16 @@ def synthetic_mrpc(n: int = 3668, seq_len: int = 128, vocab: int = 49152, seed: 
     return ids, mask, labels
 
 
-def native(hf_model, compute_dtype=None):
+def native(hf_model, compute_dtype=None, **kw):
     """Swap an HF Llama-family model for the framework's native one (``llama.native``): same
     call signature and ``.loss`` / ``.logits`` outputs, fp32 master parameters, bf16 compute on
-    the fused HIP path.  ``model = nbd.models.native(model)`` before creating the optimizer."""
+    the fused HIP path.  ``model = nbd.models.native(model)`` before creating the optimizer.
+    Keywords (``fused_optimizer``, ``block_graphs``) go to ``llama.native``."""
     import torch
 
     from .llama import native as _native
 
-    return _native(hf_model, compute_dtype=compute_dtype or torch.bfloat16)
+    return _native(hf_model, compute_dtype=compute_dtype or torch.bfloat16, **kw)
 
 
 __all__ = ["GPT2", "GPT2Config", "linear_4096", "smollm2_135m_classifier", "synthetic_mrpc", "SMOLLM2_135M", "native"]

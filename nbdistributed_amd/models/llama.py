@@ -438,11 +438,15 @@ class LlamaModel(nn.Module):
     def _forward_cast(self, input_ids, cd, cos, sin):
         """fp32 parameters, ``cd`` compute: the embedding gathers fp32 rows (no table cast) and
         casts them; each block's weights — with the NEXT norm's weight, so every parameter is
-        cast exactly once — go through one fused cast (``_CastGroup``)."""
+        cast exactly once — go through one fused cast (``_CastGroup``).  Every layer is cast
+        before the first block runs: a stack graph (ops.block_graphs) replays all the blocks at the
+        first block's call, so a cast issued between two block calls would land after the stack
+        had read that layer's weights — the previous step's."""
         c = self.config
         x = ops.embedding(input_ids, self.embed_tokens.weight).to(cd)
         (w_in,) = cast_group(cd, [self.layers[0].input_layernorm.weight])
         h = ops.rms_norm(x, w_in, c.rms_norm_eps)
+        per_layer = []
         for i, layer in enumerate(self.layers):
             nxt = self.layers[i + 1].input_layernorm if i + 1 < len(self.layers) else self.norm
             at, mlp = layer.self_attn, layer.mlp
@@ -452,7 +456,22 @@ class LlamaModel(nn.Module):
                 ps.append(at.qkv_proj.bias)
             if at.o_proj.bias is not None:
                 ps.append(at.o_proj.bias)
-            ws = cast_group(cd, ps)
+            per_layer.append(ps)
+        # layers per cast node: all of them at world size 1 (one cast launch forward; backward, one
+        # flush of the queued reductions and one cast back — instead of one of each per layer);
+        # one per layer when gradients are all-reduced (DDP's buckets then fill as the backward
+        # goes, overlapping the collectives with it).  NBD_NATIVE_CAST_LAYERS overrides.
+        k = _cast_layers(len(per_layer))
+        casts = []
+        for g in range(0, len(per_layer), k):
+            grp = per_layer[g:g + k]
+            out = cast_group(cd, [p for ps in grp for p in ps])
+            pos = 0
+            for ps in grp:
+                casts.append(out[pos:pos + len(ps)])
+                pos += len(ps)
+        for layer, ws in zip(self.layers, casts):
+            at = layer.self_attn
             w_qkv, w_o, w_post, w_gu, w_down, w_next = ws[:6]
             extra = list(ws[6:])
             b_qkv = extra.pop(0) if at.qkv_proj.bias is not None else None
@@ -470,6 +489,15 @@ class LlamaModel(nn.Module):
         if self._graphs_on():  # (see forward)
             h = h.clone()
         return h
+
+
+def _cast_layers(n: int) -> int:
+    env = os.environ.get("NBD_NATIVE_CAST_LAYERS")
+    if env:
+        return max(1, min(n, int(env)))
+    import torch.distributed as dist
+
+    return 1 if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1 else max(1, n)
 
 
 class _LlamaPreTrained(nn.Module):
@@ -697,6 +725,11 @@ def native(hf_model, compute_dtype: Optional[torch.dtype] = torch.bfloat16, fuse
         block_graphs = 0
     if hasattr(m, "model") and isinstance(m.model, LlamaModel):
         m.model.block_graphs = int(block_graphs)
+    # the decoder blocks write the cast weights' gradients into kept buffers (autograd.hip
+    # CastGroupFn): their split-K and norm-column reductions can be queued and issued together
+    # (graddst.h defer; the cast node's backward flushes them) — 4 launches per layer become 2
+    if os.environ.get("NBD_GRAD_DEFER", "1") != "0" and ops.native_available():
+        ops.graddst.defer_enable(True)
     if fused_optimizer and os.environ.get("NBD_NATIVE_FUSED_OPTIM", "1") != "0":
         for p in m.parameters():
             p._nbd_native_fused = True

@@ -14,14 +14,6 @@ def dev(require_gpu):
     return torch.device("cuda", 0)
 
 
-@pytest.fixture(params=["1", "4"])
-def nw(request, monkeypatch):
-    """Both workgroup layouts (one wave = 32 rows / four waves = 128 rows per workgroup): the
-    automatic choice depends on B·H·T, so small test shapes would only see the one-wave form."""
-    monkeypatch.setenv("NBD_ATTN_NW", request.param)
-    return int(request.param)
-
-
 def ref_attn(q, k, v, causal, scale):
     q, k, v = q.float(), k.float(), v.float()
     s = (q @ k.transpose(-1, -2)) * scale
@@ -38,7 +30,7 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("B,H,T", [(1, 1, 128), (2, 3, 256), (1, 2, 384)])
-def test_flash_forward_backward(dev, nw, causal, B, H, T):
+def test_flash_forward_backward(dev, causal, B, H, T):
     g = torch.Generator(device="cpu").manual_seed(T + H)
     q, k, v, do = (torch.randn(B, H, T, 64, generator=g).to(dev, torch.bfloat16) for _ in range(4))
     scale = 0.125
@@ -55,7 +47,7 @@ def test_flash_forward_backward(dev, nw, causal, B, H, T):
         assert _rel(a, b) < 3e-2, (name, _rel(a, b))
 
 
-_GQA_CASES = [(2, 9, 3, 128), (4, 8, 2, 256), (1, 6, 1, 384), (16, 9, 3, 128)]
+_GQA_CASES = [(2, 9, 3, 128), (4, 8, 2, 256), (1, 6, 1, 384), (16, 9, 3, 128), (64, 9, 3, 128)]
 
 
 def _gqa_case(dev, B, H, Hkv, T, causal):
@@ -71,9 +63,10 @@ def _gqa_case(dev, B, H, Hkv, T, causal):
 
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("B,H,Hkv,T", _GQA_CASES)
-def test_flash_gqa_backward(dev, nw, causal, B, H, Hkv, T):
+def test_flash_gqa_backward(dev, causal, B, H, Hkv, T):
     """Grouped-query backward, incl. the query-head groups split over workgroups and summed by
-    gqa_reduce_kernel (B·Hkv·T/128 < 256), against fp32 attention on repeated K/V."""
+    gqa_reduce_kernel (B·Hkv·T/128 < 128), and one workgroup per key/value head sweeping its group
+    (B64: 192), against fp32 attention on repeated K/V."""
     (q, k, v, do), (out, dq, dk, dv) = _gqa_case(dev, B, H, Hkv, T, causal)
     rep = H // Hkv
     qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
@@ -85,7 +78,7 @@ def test_flash_gqa_backward(dev, nw, causal, B, H, Hkv, T):
 
 
 @pytest.mark.parametrize("causal", [True, False])
-def test_flash_deferred_rescale_branch(dev, nw, causal):
+def test_flash_deferred_rescale_branch(dev, causal):
     """Scores that grow along the keys, by a different rate per query: some waves rescale O at
     every 64-key tile (growth > 2^4 per tile), others keep a stale running max for several tiles
     (the forward's deferred-rescale branch is data-dependent: random data rarely takes it)."""

@@ -160,12 +160,9 @@ def test_llama_training_step_graph_capture(dev):
     assert max(abs(a - b) for a, b in zip(eager[3:], graphed)) < 2e-2, (eager, graphed)
 
 
-@pytest.mark.parametrize("nw", ["1", "4"])
 @pytest.mark.parametrize("Hkv", [3, 9])
-def test_attention_with_fused_rope_matches_separate_rope(dev, Hkv, nw, monkeypatch):
-    """RoPE inside the attention kernels == rope_ kernel + attention (fwd and packed dqkv), in
-    both workgroup layouts (NBD_ATTN_NW: one wave or four per workgroup)."""
-    monkeypatch.setenv("NBD_ATTN_NW", nw)
+def test_attention_with_fused_rope_matches_separate_rope(dev, Hkv):
+    """RoPE inside the attention kernels == rope_ kernel + attention (fwd and packed dqkv)."""
     B, T, H, D = 2, 256, 9, 64
     qkv = torch.randn(B, T, (H + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
     dy = torch.randn(B, T, H * D, device=dev, dtype=torch.bfloat16)

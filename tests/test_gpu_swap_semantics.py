@@ -218,6 +218,45 @@ def test_per_model_graph_reset_and_memory(dev):
     assert ops.block_graphs_memory()["graphs"] == 0
 
 
+@pytest.mark.parametrize("cast_layers", [None, "1", "3"])
+def test_native_graphs_follow_optimizer_updates(dev, cast_layers, monkeypatch):
+    """native() with torch AdamW over enough steps for the stack graph (one graph replaying every
+    block at the first block's call) to form: block_graphs 0 (eager), 1 and 2 give the same losses
+    and gradients at every step.  (The fp32-master path casts each layer's weights; a cast issued
+    between two block calls used to land after the stack had read them — one step stale.)  Cast
+    nodes of all layers (world size 1), one per layer, and groups of 3 of the 4 layers."""
+    transformers = pytest.importorskip("transformers")
+    import nbdistributed_amd as nbd
+    from nbdistributed_amd.models import SMOLLM2_135M
+
+    if cast_layers:
+        monkeypatch.setenv("NBD_NATIVE_CAST_LAYERS", cast_layers)
+    cfg = dict(SMOLLM2_135M)
+    cfg.update(num_hidden_layers=4, vocab_size=4096)
+    torch.manual_seed(0)
+    hf = transformers.LlamaForSequenceClassification(
+        transformers.LlamaConfig(num_labels=2, pad_token_id=0, **cfg)).to(dev)
+    ms = [nbd.models.native(copy.deepcopy(hf), block_graphs=g) for g in (0, 1, 2)]
+    opts = [torch.optim.AdamW(m.parameters(), lr=1e-3) for m in ms]
+    ids, mask, labels = _batch(dev, False)
+    s0 = ops.block_graphs_stats()
+    for step in range(12):
+        losses, grads = [], []
+        for m, o in zip(ms, opts):
+            out = m(input_ids=ids, attention_mask=mask, labels=labels)
+            out.loss.backward()
+            losses.append(float(out.loss.detach()))
+            grads.append([p.grad.clone() for p in m.parameters()])
+            o.step()
+            o.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        assert losses[0] == losses[1] == losses[2], (step, losses)
+        for k in (1, 2):
+            assert all(torch.equal(a, b) for a, b in zip(grads[0], grads[k])), (step, k)
+    s1 = ops.block_graphs_stats()
+    assert s1["stack_replays"] > s0["stack_replays"], (s0, s1)  # the stack graph did serve forwards
+
+
 def test_native_backward_graphs_match_eager_backward(dev):
     """native(..., block_graphs=2): the cast weights' gradients go to kept buffers (graddst), so
     each decoder block's backward is captured and replayed as a HIP graph on the fp32-master path;
