@@ -773,9 +773,15 @@ struct StackMember {
   std::vector<Tensor> saved;  // weight slots empty
   Tensor x_out, h_out;
 };
+// Casts of fp32 master weights into kept compute-dtype buffers (CastGroupFn) since process start.
+// A stack replays every member at the head's call, so a cast between two member calls would be
+// read one step late: serving checks that none ran since the head's replay.
+std::atomic<uint64_t> g_cast_epoch{0};
+
 struct Stack {
   std::unique_ptr<at::cuda::CUDAGraph> g;
   Tensor x_in, h_in;
+  uint64_t cast_epoch = 0;     // g_cast_epoch at the head's replay
   std::vector<StackMember> m;
   std::vector<Tensor> warm_refs;
   size_t next = 0;             // members served in the current pass
@@ -1119,6 +1125,11 @@ static std::pair<std::shared_ptr<bg::Stack>, size_t> stack_serve(
       const StackMember& prev = st->m[st->next - 1];
       if (mb.key == key && mb.ptrs == ptrs && mb.sig == sig && x.data_ptr() == prev.x_out.data_ptr() &&
           h.data_ptr() == prev.h_out.data_ptr()) {
+        // the replay already ran this member on the weights as they were at the head's call
+        TORCH_CHECK(g_cast_epoch.load(std::memory_order_acquire) == st->cast_epoch,
+                    "nbd: a decoder block's weights were cast after its stack graph had replayed (the block would "
+                    "read the previous values): cast every layer before the first block (models/llama.py "
+                    "_forward_cast), or turn block graphs off (NBD_BLOCK_GRAPHS=0)");
         st->held.fetch_add(1, std::memory_order_acq_rel);
         ++g_stat[8];
         return {st, st->next++};
@@ -1202,6 +1213,7 @@ static std::pair<std::shared_ptr<bg::Stack>, size_t> stack_serve(
   if (st.h_in.data_ptr() != h.data_ptr()) st.h_in.copy_(h);
   st.g->replay();
   st.next = 1;
+  st.cast_epoch = g_cast_epoch.load(std::memory_order_acquire);
   st.held.store(1, std::memory_order_release);
   g_active = s.stack;
   ++g_stat[7];
@@ -1803,6 +1815,7 @@ struct CastGroupFn : public torch::autograd::Function<CastGroupFn> {
       shapes.push_back(p.sizes().vec());
     }
     auto [buf, busy] = castbuf::get(ps[0], total, ps[0].options().dtype((at::ScalarType)dtype));
+    bg::g_cast_epoch.fetch_add(1, std::memory_order_acq_rel);
     if (busy) ctx->save_for_backward({castbuf::release_token(busy)});
     t_cast_gbuf = busy && cast_grad_dest_on() ? castbuf::grad_buf(ps[0], buf) : Tensor();
     std::vector<Tensor> src;
