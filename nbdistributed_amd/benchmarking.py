@@ -212,6 +212,7 @@ _ARM_T0 = [time.monotonic()]  # run_all's start: arm start offsets are relative 
 
 def _arm_start(out: Dict[str, Any], arm: str) -> None:
     out.setdefault("arm_start_s", {})[arm] = round(time.monotonic() - _ARM_T0[0], 2)
+    _log(f"  arm {arm} starts")  # (a progress line per arm: long multi-rank arms are not silent)
 
 
 def _graph_arms(n: int) -> bool:
@@ -224,9 +225,11 @@ def _graph_arms(n: int) -> bool:
 
 def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 1024, compare_torch: bool = True,
               linear_rows: int = 8192, config: str = "small", linear_dim: int = 4096,
-              force_collectives: bool = True, out: Optional[Dict[str, Any]] = None, tick=None) -> Dict[str, Any]:
+              force_collectives: bool = True, out: Optional[Dict[str, Any]] = None, tick=None,
+              graph: Optional[bool] = None) -> Dict[str, Any]:
     """BASELINE configs 4 and 5 as notebook cells: DDP steps timed inside each worker (max over
-    ranks).  GPT-2 small, synthetic tokens.  Primary number: bf16 parameters living in the DDP
+    ranks).  ``graph`` (default: ``_graph_arms``) runs the whole-step graph arm here; run_all
+    defers it at N > 1 (``bench_ddp_graph``) until every eager arm is measured.  GPT-2 small, synthetic tokens.  Primary number: bf16 parameters living in the DDP
     buckets, fp32 master weights and moments in ``FlatAdamW`` (fused HIP AdamW per bucket).  Also
     reported: fp32 params + bf16 autocast + torch fused AdamW through nbd DDP (``amp_*``) and
     through torch DDP (``torch_ddp_*``).  ``out`` is filled arm by arm (``tick()`` after each), so
@@ -280,20 +283,8 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
         r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'torch', {linear_dim})", render=False)
         lin["torch_ddp_ms_per_step"] = _max_over_ranks(r)
     tick()
-    if _graph_arms(n):
-        try:
-            _arm_start(out, "graph")
-            r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flatgraph', {config!r})", render=False)
-            gms = _max_over_ranks(r)
-            out.update(graph_ms_per_step=gms, graph_tokens_per_s=n * B * T / (gms / 1e3),
-                       graph_recipe="as the primary recipe, whole step captured in one HIP graph (GraphedStep)")
-            rd = _replay_detail(r)
-            if rd:
-                out["graph_replays"] = rd
-        except Exception as e:  # noqa: BLE001
-            _record_error(out, "graph_error", e)
-            if isinstance(e, TimeoutError):
-                raise
+    if _graph_arms(n) if graph is None else graph:
+        bench_ddp_graph(session, out, steps, warmup, B, T, config)
         tick()
     if n == 1 and force_collectives:
         # the world > 1 code path on this one GPU: every bucket's all-reduce (reduce-scatter +
@@ -319,6 +310,25 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
         if "ms_per_step" in cp:
             cp["vs_no_collectives"] = cp["ms_per_step"] / ms
     return out
+
+
+def bench_ddp_graph(session, out: Dict[str, Any], steps: int = 20, warmup: int = 5, B: int = 8, T: int = 1024,
+                    config: str = "small") -> None:
+    """The GPT-2 DDP step as one HIP graph (GraphedStep) into ``out`` (bench_ddp's dict)."""
+    n = session.world_size
+    try:
+        _arm_start(out, "graph")
+        r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flatgraph', {config!r})", render=False)
+        gms = _max_over_ranks(r)
+        out.update(graph_ms_per_step=gms, graph_tokens_per_s=n * B * T / (gms / 1e3),
+                   graph_recipe="as the primary recipe, whole step captured in one HIP graph (GraphedStep)")
+        rd = _replay_detail(r)
+        if rd:
+            out["graph_replays"] = rd
+    except Exception as e:  # noqa: BLE001
+        _record_error(out, "graph_error", e)
+        if isinstance(e, TimeoutError):
+            raise
 
 
 def _log(msg: str) -> None:
@@ -578,8 +588,20 @@ def _nbd_notebook_bench(steps, warm, bs=16, seq=128, mode="reference", small=Fal
 REFERENCE_NOTEBOOK_MS_PER_STEP = 126.6  # 1 epoch = 14.56 s / 115 steps, 2 GPUs
 
 
+NOTEBOOK_RECIPES = {"reference": "HF model, fp32, accelerate DDP, torch AdamW (the notebook's recipe)",
+                    "reference_native": "the notebook's accelerate loop unchanged except model = nbd.models.native(model): "
+                                        "native Llama, fp32 master weights + torch AdamW (fused: native()'s default), bf16 "
+                                        "compute on the fused HIP path, per-block forward graphs (native()'s default)",
+                    "nbd": "native Llama (HIP kernels, one autograd node per block), bf16 params + fp32 master "
+                            "(FlatAdamW, buckets updated during backward at world 1), nbd DDP",
+                    "nbd_block_graphs": "as nbd (eager), each decoder block's forward replayed from its own HIP graph "
+                                        "(ops.block_graphs(1)); FlatAdamW update after backward (no overlap)",
+                    "nbd_graph": "as nbd, whole step captured in one HIP graph (GraphedStep)"}
+
+
 def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = False,
-                   force_collectives: bool = True, out: Optional[Dict[str, Any]] = None, tick=None) -> Dict[str, Any]:
+                   force_collectives: bool = True, out: Optional[Dict[str, Any]] = None, tick=None,
+                   graph: Optional[bool] = None) -> Dict[str, Any]:
     """The reference's own measured workload (SmolLM2-135M-cls fine-tune, 126.6
     ms/step, ≈252 samples/s on 2 GPUs) as notebook cells, max over ranks."""
     n = session.world_size
@@ -592,20 +614,39 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
                 "seq_len": 128, "data": "synthetic MRPC-shaped",
                 "reference_ms_per_step": REFERENCE_NOTEBOOK_MS_PER_STEP,
                 "reference_samples_per_s": 32 / (REFERENCE_NOTEBOOK_MS_PER_STEP / 1e3)})
-    recipes = {"reference": "HF model, fp32, accelerate DDP, torch AdamW (the notebook's recipe)",
-               "reference_native": "the notebook's accelerate loop unchanged except model = nbd.models.native(model): "
-                                   "native Llama, fp32 master weights + torch AdamW (fused: native()'s default), bf16 "
-                                   "compute on the fused HIP path, per-block forward graphs (native()'s default)",
-               "nbd": "native Llama (HIP kernels, one autograd node per block), bf16 params + fp32 master "
-                       "(FlatAdamW, buckets updated during backward at world 1), nbd DDP",
-               "nbd_block_graphs": "as nbd (eager), each decoder block's forward replayed from its own HIP graph "
-                                   "(ops.block_graphs(1)); FlatAdamW update after backward (no overlap)",
-               "nbd_graph": "as nbd, whole step captured in one HIP graph (GraphedStep)"}
     modes = ["reference", "reference_native", "nbd"]
     if n == 1:  # (the per-block graph arm: an eager-step variant, timed where the GPU is ours alone)
         modes.append("nbd_block_graphs")
-    if _graph_arms(n):  # last of the main arms (bench_ddp's _graph_arms note)
+    if _graph_arms(n) if graph is None else graph:  # last of the main arms (bench_ddp's _graph_arms note)
         modes.append("nbd_graph")
+    _notebook_arms(session, out, modes, steps, warmup, small, tick)
+    if n == 1 and force_collectives:  # the N-GPU code path on one GPU (see bench_ddp)
+        for mode, base in (("nbd_collective_path", "nbd"), ("nbd_graph_collective_path", "nbd_graph")):
+            if "ms_per_step" not in out.get(base, {}):
+                continue
+            try:
+                _arm_start(out, mode)
+                r = session.execute(f"_nbd_notebook_bench({steps}, {warmup}, mode={base!r}, small={small}, force=True)",
+                                    render=False)
+                ms = _max_over_ranks(r)
+                out[mode] = {"ms_per_step": ms, "vs_no_collectives": ms / out[base]["ms_per_step"],
+                             "recipe": NOTEBOOK_RECIPES[base] + "; real RCCL collectives per bucket (forced at world size 1)"}
+                rd = _replay_detail(r)
+                if rd:
+                    out[mode]["replays"] = rd
+            except Exception as e:  # noqa: BLE001
+                out[mode] = {}
+                _record_error(out[mode], "error", e)
+                if isinstance(e, TimeoutError):
+                    raise
+            tick()
+    _notebook_summary(out)
+    return out
+
+
+def _notebook_arms(session, out: Dict[str, Any], modes: List[str], steps: int, warmup: int, small: bool,
+                   tick) -> None:
+    n = session.world_size
     for mode in modes:
         try:
             _arm_start(out, mode)
@@ -617,31 +658,24 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
                 raise
             continue
         ms = _max_over_ranks(r)
-        out[mode] = {"ms_per_step": ms, "samples_per_s": n * 16 / (ms / 1e3), "recipe": recipes[mode]}
+        _log(f"  notebook {mode}: {ms:.2f} ms/step")
+        out[mode] = {"ms_per_step": ms, "samples_per_s": n * 16 / (ms / 1e3), "recipe": NOTEBOOK_RECIPES[mode]}
         rd = _replay_detail(r)
         if rd:
             out[mode]["replays"] = rd
         tick()
-    if n == 1 and force_collectives:  # the N-GPU code path on one GPU (see bench_ddp)
-        for mode, base in (("nbd_collective_path", "nbd"), ("nbd_graph_collective_path", "nbd_graph")):
-            if "ms_per_step" not in out.get(base, {}):
-                continue
-            try:
-                _arm_start(out, mode)
-                r = session.execute(f"_nbd_notebook_bench({steps}, {warmup}, mode={base!r}, small={small}, force=True)",
-                                    render=False)
-                ms = _max_over_ranks(r)
-                out[mode] = {"ms_per_step": ms, "vs_no_collectives": ms / out[base]["ms_per_step"],
-                             "recipe": recipes[base] + "; real RCCL collectives per bucket (forced at world size 1)"}
-                rd = _replay_detail(r)
-                if rd:
-                    out[mode]["replays"] = rd
-            except Exception as e:  # noqa: BLE001
-                out[mode] = {}
-                _record_error(out[mode], "error", e)
-                if isinstance(e, TimeoutError):
-                    raise
-            tick()
+
+
+def bench_notebook_graph(session, out: Dict[str, Any], steps: int = 20, warmup: int = 5, small: bool = False,
+                         tick=None) -> Dict[str, Any]:
+    """The notebook step as one HIP graph into ``out`` (bench_notebook's dict): run_all's last
+    phase at N > 1, after every eager arm."""
+    _notebook_arms(session, out, ["nbd_graph"], steps, warmup, small, tick or (lambda: None))
+    _notebook_summary(out)
+    return out
+
+
+def _notebook_summary(out: Dict[str, Any]) -> None:
     # same-recipe comparisons only: the fp32 HF arm and the bf16 native arms differ in precision
     # and model implementation, so no cross-recipe "speedup" is printed (VERDICT r3 weak 9)
     out["reference_vs_native_note"] = ("'reference' = HF fp32 model through accelerate (the notebook as written); "
@@ -656,7 +690,6 @@ def bench_notebook(session, steps: int = 20, warmup: int = 5, small: bool = Fals
         for k in ("nbd", "nbd_block_graphs"):
             if "ms_per_step" in out.get(k, {}):
                 out[f"{k}_vs_graph"] = out[k]["ms_per_step"] / g
-    return out
 
 
 BCAST_BUILD = """
@@ -835,10 +868,15 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
             if "per_param_ms" in rb:
                 _log(f"broadcast per-param {rb['per_param_ms']:.3f} ms, coalesced {rb['coalesced_ms']:.3f} ms")
             ckpt(out)
+        # at N > 1 the whole-step graph arms run last, after every eager arm of both workloads: a
+        # capture that fails there (a collective's unjoined side-stream work, say) must not cost
+        # the measured eager numbers of the later phases
+        defer_graphs = n > 1 and _graph_arms(n)
         if ddp and gpu:
             _log("phase 4: DDP steps (GPT-2 small bf16 config 5, Linear 4096 config 4)")
             out["ddp"] = {}
-            _phase(session, out, "ddp", lambda: bench_ddp(session, steps=ddp_steps, out=out["ddp"], tick=lambda: ckpt(out)),
+            _phase(session, out, "ddp", lambda: bench_ddp(session, steps=ddp_steps, out=out["ddp"], tick=lambda: ckpt(out),
+                                                          graph=False if defer_graphs else None),
                    phase_timeout_s, deadline, 60.0)
             d = out["ddp"]
             if "ms_per_step" in d:
@@ -848,12 +886,24 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
             _log("phase 5: reference notebook workload (SmolLM2-135M-cls, bs16, seq128)")
             out["notebook"] = {}
             _phase(session, out, "notebook",
-                   lambda: bench_notebook(session, steps=ddp_steps, out=out["notebook"], tick=lambda: ckpt(out)),
+                   lambda: bench_notebook(session, steps=ddp_steps, out=out["notebook"], tick=lambda: ckpt(out),
+                                          graph=False if defer_graphs else None),
                    phase_timeout_s, deadline, 60.0)
             nb = out["notebook"]
             if "ms_per_step" in nb.get("reference", {}) and "ms_per_step" in nb.get("nbd", {}):
                 _log(f"notebook fp32 {nb['reference']['ms_per_step']:.2f} ms/step, nbd {nb['nbd']['ms_per_step']:.2f}")
             ckpt(out)
+        if defer_graphs and gpu and (ddp or notebook):
+            _log("phase 6: whole-step HIP graph arms (GraphedStep)")
+            if ddp and isinstance(out.get("ddp"), dict) and "ms_per_step" in out["ddp"]:
+                _phase(session, out, "ddp_graph", lambda: bench_ddp_graph(session, out["ddp"], steps=ddp_steps),
+                       phase_timeout_s, deadline, 60.0)
+                ckpt(out)
+            if notebook and isinstance(out.get("notebook"), dict):
+                _phase(session, out, "notebook_graph",
+                       lambda: bench_notebook_graph(session, out["notebook"], steps=ddp_steps, tick=lambda: ckpt(out))
+                       and None, phase_timeout_s, deadline, 60.0)
+                ckpt(out)
         return out
     finally:
         session.deadline = prev_deadline
@@ -939,5 +989,8 @@ def result_line(res: Dict[str, Any], n: int, steps: int, warmup: int) -> Dict[st
         line["aborted_phase"] = res["aborted"]
     for k in ("ddp", "rank_broadcast", "notebook"):
         if k in res:
+            line[k] = res[k]
+    for k in ("ddp_graph", "notebook_graph"):  # run_all's deferred graph phase (N > 1): only a failure
+        if isinstance(res.get(k), dict) and res[k]:
             line[k] = res[k]
     return line

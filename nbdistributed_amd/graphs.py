@@ -87,6 +87,39 @@ def _suspend_block_graphs():
             torch.ops.nbd.llama_block_graphs_suspend(prev)
 
 
+def _capture(graph, body, pool=None) -> None:
+    """``body()`` captured into ``graph`` on a fresh stream; whatever happens, the caller's stream
+    and the device's default RNG come back usable.  (``torch.cuda.graph`` leaves its capture
+    stream current when ``capture_end`` raises — e.g. ``hipErrorStreamCaptureUnjoined`` from a
+    collective whose side-stream work was not joined — and skips the RNG's capture epilogue, so
+    ``torch.manual_seed`` and every later random op on the thread failed.  A failed capture here
+    costs only this graph.)"""
+    import gc
+
+    torch.cuda.synchronize()
+    gc.collect()
+    gen = torch.cuda.default_generators[torch.cuda.current_device()]
+    rng = gen.clone_state()  # (not capturing: put back if the capture fails half way)
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        graph.capture_begin(pool=pool, capture_error_mode="thread_local")
+        try:
+            try:
+                body()
+            except BaseException:
+                try:
+                    graph.capture_end()
+                except Exception:  # noqa: BLE001 - the body's error is the one to report
+                    pass
+                raise
+            graph.capture_end()
+        except BaseException:
+            gen.graphsafe_set_state(rng)
+            raise
+    torch.cuda.current_stream().wait_stream(stream)
+
+
 class GraphedStep:
     """``step = GraphedStep(fn, example_args, optimizers=[opt])``; ``out = step(*args)``.
 
@@ -124,8 +157,7 @@ class GraphedStep:
         # watchdog thread keeps querying its events meanwhile, which "global" mode turns into a
         # hipErrorStreamCaptureUnsupported abort (seen intermittently on this stack)
         _take_warm_refs()  # (drop references left by an earlier capture that nobody took)
-        with torch.cuda.graph(self.graph, pool=pool, capture_error_mode="thread_local"):
-            self.static_out = fn(*self.static_args)
+        _capture(self.graph, lambda: setattr(self, "static_out", fn(*self.static_args)), pool)
         # the captured GEMMs' next-weight warm-up reads (csrc/kernels/gemm.hip, namespace warm)
         # are frozen pointers into those weights' storages: hold them as long as the graph
         self._warm_refs = _take_warm_refs()
