@@ -140,8 +140,9 @@ class _DecodeLoop:
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: tensor-parallel decode steps hold RCCL all-reduces, and ProcessGroupNCCL's
         # watchdog thread keeps querying its events during capture
-        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-            self.step()
+        from .graphs import _capture
+
+        _capture(self.graph, self.step)  # (a failed capture leaves the stream and RNG usable)
         # capture does not execute: the state is still the pre-capture one
 
     def __call__(self):

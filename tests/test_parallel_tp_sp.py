@@ -29,6 +29,9 @@ def _entry(rank, fn, n, port):
     dist.init_process_group("gloo", rank=rank, world_size=n)
     try:
         fn(rank, n)
+        # every rank done before any tears its gloo pairs down: a peer closing its sockets while
+        # another still exchanges made gloo's I/O thread call std::terminate (SIGABRT, ~1 run in 6)
+        dist.barrier()
     finally:
         dist.destroy_process_group()
 
