@@ -1725,14 +1725,14 @@ std::vector<Tensor> g_old;                      // replaced buffers (see get)
 std::pair<Tensor, std::shared_ptr<std::atomic<bool>>> get(const Tensor& first, int64_t total,
                                                           const at::TensorOptions& opt) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_bufs.size() > 4096) {  // forget the groups of dead parameters
-    for (auto it = g_bufs.begin(); it != g_bufs.end();) {
-      if (it->second.first.expired()) {
-        g_addrs.erase(it->second.buf.data_ptr());
-        it = g_bufs.erase(it);
-      } else {
-        ++it;
-      }
+  // forget the groups of dead parameters (a re-run `model = native(...)` cell must not keep the
+  // old model's cast and gradient buffers); the map holds a few groups per live model
+  for (auto it = g_bufs.begin(); it != g_bufs.end();) {
+    if (it->second.first.expired()) {
+      g_addrs.erase(it->second.buf.data_ptr());
+      it = g_bufs.erase(it);
+    } else {
+      ++it;
     }
   }
   auto it = g_bufs.find(first.unsafeGetTensorImpl());
@@ -1763,6 +1763,19 @@ Tensor grad_buf(const Tensor& first, const Tensor& buf) {
   if (it == g_bufs.end() || !it->second.buf.is_same(buf)) return Tensor();
   if (!it->second.gbuf.defined()) it->second.gbuf = at::empty_like(buf);
   return it->second.gbuf;
+}
+
+// [live groups, cast-buffer bytes, gradient-buffer bytes] held for models.native()'s kept casts
+// (bytes of every held group: a dead model's stay until the next cast purges them; %dist_status)
+std::vector<int64_t> memory() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int64_t n = 0, cb = 0, gb = 0;
+  for (const auto& kv : g_bufs) {
+    n += !kv.second.first.expired();
+    cb += kv.second.buf.nbytes();
+    if (kv.second.gbuf.defined()) gb += kv.second.gbuf.nbytes();
+  }
+  return {n, cb, gb};
 }
 
 Tensor release_token(std::shared_ptr<std::atomic<bool>> busy) {
@@ -1932,4 +1945,5 @@ TORCH_LIBRARY_FRAGMENT(nbd, m) {
   m.def("llama_block_graphs_stats() -> int[]", &nbd::ag::llama_block_graphs_stats);
   m.def("host_timing(bool reset) -> str", &nbd::ag::host_timing);
   m.def("llama_block_graphs_suspend(bool on) -> bool", &nbd::ag::llama_block_graphs_suspend);
+  m.def("cast_buffers_memory() -> int[]", &nbd::ag::castbuf::memory);
 }

@@ -306,6 +306,9 @@ class MagicCore:
                            f"({bgs.get('stack_served')} blocks served), {bgs.get('eager')} eager calls")
                     self.p(f"  ├─ Block-graph memory (framework-held): {bgs.get('reserved_gib', 0.0):.2f}GB reserved "
                            f"in {bgs.get('pools', 0)} graph pools ({bgs.get('allocated_gib', 0.0):.2f}GB allocated)")
+                    if bgs.get("cast_groups"):
+                        self.p(f"  ├─ native() weight casts (framework-held): {bgs.get('cast_gib', 0.0):.2f}GB in "
+                               f"{bgs.get('cast_groups')} kept cast + gradient buffers")
             else:
                 self.p(f"  ├─ Device: {info.get('gpu_name', 'CPU')}  backend {info.get('backend')}")
             if info.get("running") and "dead_reason" not in info:

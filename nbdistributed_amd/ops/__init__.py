@@ -45,7 +45,8 @@ from .bucket import (_ref_flatten, _ref_prereduce, _ref_unflatten, bucket_flatte
                      plan_offsets, prereduce_into_bucket)
 from .decode import decode_attention, decode_attention_reference, linear_small, linear_small_reference
 from .embedding import embedding, embedding_tok_pos
-from .gemm import block_graphs, block_graphs_memory, block_graphs_reset, block_graphs_stats, gemm_linear, llama_block, mlp_gelu, mlp_swiglu
+from .gemm import (block_graphs, block_graphs_memory, block_graphs_reset, block_graphs_stats, cast_buffers_memory,
+                   gemm_linear, llama_block, mlp_gelu, mlp_swiglu)
 from .llama import rope_, rope_tables, swiglu
 from .loss import cross_entropy, linear_cross_entropy
 from .mask import seqcls_prep
@@ -62,6 +63,6 @@ def __getattr__(name):
 
 __all__ = ["bucket_flatten", "bucket_unflatten", "local_prereduce", "prereduce_into_bucket", "graddst", "adamw_flat", "cross_entropy", "linear_cross_entropy",
            "flash_attention", "attention_qkv", "decode_attention", "decode_attention_reference", "linear_small", "linear_small_reference", "flash_supported", "layer_norm", "add_layer_norm", "linear",
-           "colsum", "embedding", "embedding_tok_pos", "gemm_linear", "llama_block", "block_graphs", "block_graphs_memory", "block_graphs_reset", "block_graphs_stats", "mlp_gelu", "mlp_swiglu", "rms_norm", "add_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary",
+           "colsum", "embedding", "embedding_tok_pos", "gemm_linear", "llama_block", "block_graphs", "block_graphs_memory", "block_graphs_reset", "block_graphs_stats", "cast_buffers_memory", "mlp_gelu", "mlp_swiglu", "rms_norm", "add_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary",
            "tensor_summary_text", "tensor_summary_raw", "plan_offsets", "native_available", "load_library",
            "SUMMARY_FIELDS", "seqcls_prep"]

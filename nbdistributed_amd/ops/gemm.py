@@ -706,6 +706,16 @@ def block_graphs_memory(device=None) -> dict:
     return out
 
 
+def cast_buffers_memory() -> dict:
+    """The kept compute-dtype casts of ``models.native()``'s fp32 master weights and their gradient
+    buffers (autograd.hip ``castbuf``): memory the framework holds between steps."""
+    import torch
+
+    _require()
+    n, cb, gb = torch.ops.nbd.cast_buffers_memory()
+    return {"groups": n, "cast_bytes": cb, "grad_bytes": gb}
+
+
 def block_graphs_stats() -> dict:
     """Counters of the per-block graphs: forward captures, replays, eager calls in graph mode, live
     graphs; backward captures, replays (captures included) and eager backwards of graphed forwards."""

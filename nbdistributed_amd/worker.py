@@ -247,7 +247,7 @@ class DistributedWorker:
             ops_lib = sys.modules.get("nbdistributed_amd.ops._lib")
             if ops_lib is not None and getattr(ops_lib, "_loaded", False):  # (never loads it for a status)
                 try:
-                    from .ops import block_graphs, block_graphs_memory, block_graphs_stats
+                    from .ops import block_graphs, block_graphs_memory, block_graphs_stats, cast_buffers_memory
 
                     bg = dict(block_graphs_stats(), mode=block_graphs())
                     mem = block_graphs_memory(d)
@@ -255,6 +255,8 @@ class DistributedWorker:
                     # the framework holds, not the user's tensors
                     bg.update(pools=mem["graphs"], reserved_gib=mem["reserved_bytes"] / gib,
                               allocated_gib=mem["allocated_bytes"] / gib)
+                    cm = cast_buffers_memory()  # native()'s kept weight casts + gradient buffers
+                    bg.update(cast_groups=cm["groups"], cast_gib=(cm["cast_bytes"] + cm["grad_bytes"]) / gib)
                     st["block_graphs"] = bg
                 except Exception:  # noqa: BLE001 - status must not fail
                     pass

@@ -288,3 +288,24 @@ def test_native_backward_graphs_match_eager_backward(dev):
             assert torch.equal(a, b), (step, float((a - b).abs().max()))
     s1 = ops.block_graphs_stats()
     assert s1["bwd_captures"] > s0["bwd_captures"] and s1["bwd_replays"] - s0["bwd_replays"] >= 3 * 3, (s0, s1)
+
+
+def test_native_cast_buffers_reported_and_released(dev):
+    """native()'s kept weight casts and their gradient buffers are reported
+    (ops.cast_buffers_memory, shown by %dist_status) and released with the model: a re-run
+    `model = native(...)` cell does not keep the previous model's buffers."""
+    hf, m = _hf_and_native(dev, layers=2)
+    ids, mask, labels = _batch(dev, False)
+    m(input_ids=ids, attention_mask=mask, labels=labels).loss.backward()
+    torch.cuda.synchronize()
+    mem = ops.cast_buffers_memory()
+    n_bf16 = sum(p.numel() for n, p in m.named_parameters() if ".layers." in n)
+    assert mem["groups"] >= 1 and mem["cast_bytes"] >= 2 * n_bf16 and mem["grad_bytes"] >= 2 * n_bf16, mem
+    del m, hf
+    gc.collect()
+    hf2, m2 = _hf_and_native(dev, layers=2)  # the next cast purges the dead model's groups
+    m2(input_ids=ids, attention_mask=mask, labels=labels).loss.backward()
+    torch.cuda.synchronize()
+    mem2 = ops.cast_buffers_memory()  # (bytes of every held group: one model's, not two)
+    assert mem2["groups"] == mem["groups"] and mem2["cast_bytes"] == mem["cast_bytes"], (mem, mem2)
+    assert mem2["grad_bytes"] == mem["grad_bytes"], (mem, mem2)
