@@ -15,6 +15,7 @@ Random init (no checkpoints: no network), GPT-2 initialisation scheme.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -40,8 +41,9 @@ class GPT2Config:
     # the token table (and the tied LM head) is stored with its rows padded to a multiple of this
     # from 4096 classes up: zero rows that never receive a gradient, so the LM-head GEMMs run on an
     # aligned vocabulary (hipBLASLt on 50257 vs 50304 columns: 2.18 vs 1.75 ms per GPT-2 step,
-    # docs/FINDINGS.md §16) with no per-step padded copy of the weight.  1 = no padding.
-    vocab_pad: int = 128
+    # docs/FINDINGS.md §16) with no per-step padded copy of the weight.  1 = no padding.  256 with
+    # the hand-written LM head (NBD_LMHEAD_HIP=1), whose 256x256 forward tiles the vocabulary.
+    vocab_pad: int = 256 if os.environ.get("NBD_LMHEAD_HIP", "0") == "1" else 128
 
     @property
     def padded_vocab(self) -> int:

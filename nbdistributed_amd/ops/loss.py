@@ -78,8 +78,11 @@ def _xent_fn():
             N = h2.shape[0]
             chunk = LM_HEAD_CHUNK if 0 < LM_HEAD_CHUNK < N else N
             dh = None
+            hip = _hip_ok(h2, wp)
+            if hip:
+                chunk = N  # (row chunks are a hipBLASLt experiment)
             if chunk == N:
-                logits_p = torch.mm(h2, wp.t())
+                logits_p = _hip_logits(h2, wp) if hip else torch.mm(h2, wp.t())
                 loss_rows, _ = torch.ops.nbd.xent_fused(logits_p[:, :V] if Vp != V else logits_p, target,
                                                         ignore_index, scale)
             else:
@@ -101,6 +104,7 @@ def _xent_fn():
                         torch.mm(lc, wp, out=dh[r0:r1])
             # logits now hold d(loss)/d(logits) for grad_out = 1 (and dh = dlogits·W, if fused)
             ctx.save_for_backward(h2, wp, logits_p, w, dh)
+            ctx.hip = hip
             ctx.rows = w.shape[0]
             ctx.copied = wp is not w
             return loss_rows.sum() * scale[0]
@@ -113,19 +117,24 @@ def _xent_fn():
             g = grad.to(h2.dtype)
             dh = None
             if ctx.needs_input_grad[0]:
-                dh = dh_fused.mul_(g) if dh_fused is not None else torch.mm(dlogits, wp).mul_(g)
+                if dh_fused is not None:
+                    dh = dh_fused.mul_(g)
+                else:
+                    dh = (_hip_dgrad(dlogits, wp) if ctx.hip else torch.mm(dlogits, wp)).mul_(g)
             dw = None
             if ctx.needs_input_grad[1]:
                 hg = h2 * g
                 dst, acc = graddst.claim(w) if not ctx.copied else (None, False)
                 if dst is not None:  # straight into the DDP bucket slice (graddst.py)
-                    if acc:
+                    if ctx.hip:
+                        _hip_wgrad(dlogits, hg, out=dst, accum=acc)
+                    elif acc:
                         dst.addmm_(dlogits.t(), hg)
                     else:
                         torch.mm(dlogits.t(), hg, out=dst)
                     dw = graddst.hand_back(w, dst, acc)
                 else:
-                    dw = torch.mm(dlogits.t(), hg)[:ctx.rows]
+                    dw = (_hip_wgrad(dlogits, hg) if ctx.hip else torch.mm(dlogits.t(), hg))[:ctx.rows]
             return dh, dw, None, None, None, None, None
 
     _XentFn = (_FusedCrossEntropy, _LinearCrossEntropy)
@@ -164,6 +173,53 @@ LM_HEAD_WARM_BYTES = int(float(os.environ.get("NBD_LM_HEAD_WARM_MB", "0")) * (1 
 # rows per LM-head chunk (0 = one [N, Vp] GEMM): GEMM -> in-place loss gradient -> input-gradient
 # GEMM per chunk, so a chunk's logits are re-read from the 256 MB MALL rather than from HBM
 LM_HEAD_CHUNK = int(os.environ.get("NBD_LMHEAD_CHUNK", "0"))
+# NBD_LMHEAD_HIP=1: the head's three products on the hand-written MFMA kernels instead of
+# hipBLASLt — forward on the 256x256 phase-interleaved kernel (gemm256.hip) when tokens and padded
+# vocabulary are multiples of 256, else the 128x128 8-wave kernel; input gradient on the 128x128
+# kernel split 2-4 ways along the vocabulary; weight gradient on the 128x128 kernel, accumulated
+# straight into a DDP bucket slice when one is claimed.  Opt-in: on GPT-2 small (8192 x 50304 x
+# 768) it measured slower than the library (docs/FINDINGS.md §33).
+LM_HEAD_HIP = os.environ.get("NBD_LMHEAD_HIP", "0") == "1"
+
+
+def _hip_ok(h2, wp) -> bool:
+    import torch
+
+    N, C = h2.shape
+    return (LM_HEAD_HIP and h2.is_cuda and h2.dtype == torch.bfloat16 and wp.dtype == torch.bfloat16
+            and N % 128 == 0 and wp.shape[0] % 128 == 0 and C % 128 == 0)
+
+
+def _hip_logits(h2, wp):
+    """logits [N, Vp] = h2·wpᵀ on the hand-written kernels."""
+    import torch
+
+    N, Vp = h2.shape[0], wp.shape[0]
+    out = torch.empty(N, Vp, dtype=h2.dtype, device=h2.device)
+    tile = 86256256 if N % 256 == 0 and Vp % 256 == 0 else 82128128
+    torch.ops.nbd.gemm(h2, wp, out, False, False, None, 0, None, None, 1, tile)
+    return out
+
+
+def _hip_dgrad(dlogits, wp):
+    """dh [N, C] = dlogits·wp (wp read as [K = Vp][C]), split along the vocabulary."""
+    import torch
+
+    steps = wp.shape[0] // 64
+    S = next(s for s in (4, 3, 2, 1) if steps % s == 0)
+    dh = torch.empty(dlogits.shape[0], wp.shape[1], dtype=dlogits.dtype, device=dlogits.device)
+    torch.ops.nbd.gemm(dlogits, wp, dh, False, True, None, 0, None, None, S, 82128128)
+    return dh
+
+
+def _hip_wgrad(dlogits, hg, out=None, accum=False):
+    """dW [Vp, C] = dlogitsᵀ·hg (both read as [K = tokens][...]) into ``out`` (+= with accum)."""
+    import torch
+
+    if out is None:
+        out = torch.empty(dlogits.shape[1], hg.shape[1], dtype=hg.dtype, device=hg.device)
+    torch.ops.nbd.gemm(dlogits, hg, out, True, True, None, 0, None, None, 1, 82128128, 1 if accum else 0)
+    return out
 
 
 def linear_cross_entropy(h, weight, target, ignore_index: int = -100, reduction: str = "mean", vocab: int = -1):

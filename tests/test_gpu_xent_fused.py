@@ -87,3 +87,50 @@ def test_gpt2_fused_head_matches_logits_path(dev):
     l2.backward()
     assert abs(float(l1) - float(l2)) < 1e-2
     assert _rel(g1, m.wte.weight.grad) < 3e-2
+
+
+@pytest.mark.parametrize("reduction", ["mean", "sum"])
+@pytest.mark.parametrize("V,C,N", [(50257, 768, 512), (5000, 256, 512), (4200, 256, 384)])
+def test_linear_cross_entropy_hand_written_products(dev, reduction, V, C, N, monkeypatch):
+    """NBD_LMHEAD_HIP: the head's forward, input- and weight-gradient products on the hand-written
+    kernels (256x256 forward when tokens and padded vocabulary are multiples of 256 — 5000 -> 5120
+    — else 128x128; split-K input gradient; 128x128 weight gradient) against fp32 torch
+    F.linear + F.cross_entropy: loss, dh and dW."""
+    from nbdistributed_amd.ops import loss as L
+
+    monkeypatch.setattr(L, "LM_HEAD_HIP", True)
+    torch.manual_seed(3)
+    h = (torch.randn(N, C, device=dev) * 0.5).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(V, C, device=dev) * 0.05).to(torch.bfloat16).requires_grad_()
+    tgt = torch.randint(0, V, (N,), device=dev)
+    tgt[3] = -100
+    loss = ops.linear_cross_entropy(h, w, tgt, reduction=reduction)
+    (loss * 2.0).backward()
+    hr, wr = h.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    lr = F.cross_entropy(F.linear(hr, wr), tgt, ignore_index=-100, reduction=reduction)
+    (lr * 2.0).backward()
+    assert abs(float(loss) - float(lr)) < 2e-2 * max(1.0, abs(float(lr)))
+    assert _rel(h.grad, hr.grad) < 3e-2
+    assert _rel(w.grad, wr.grad) < 3e-2
+
+
+def test_hand_written_head_runs_no_library_gemm(dev, monkeypatch):
+    """With NBD_LMHEAD_HIP the head issues only nbd kernels: torch.mm is never called."""
+    from nbdistributed_amd.ops import loss as L
+
+    monkeypatch.setattr(L, "LM_HEAD_HIP", True)
+    calls = []
+    real_mm = torch.mm
+
+    def spy(*a, **k):
+        calls.append(a[0].shape)
+        return real_mm(*a, **k)
+
+    monkeypatch.setattr(torch, "mm", spy)
+    h = torch.randn(256, 256, device=dev).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(4096, 256, device=dev) * 0.05).to(torch.bfloat16).requires_grad_()
+    tgt = torch.randint(0, 4096, (256,), device=dev)
+    ops.linear_cross_entropy(h, w, tgt).backward()
+    torch.cuda.synchronize()
+    assert calls == []
+    assert h.grad is not None and w.grad is not None
