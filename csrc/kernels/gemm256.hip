@@ -45,26 +45,41 @@ __device__ __forceinline__ int hmap(int lr, int X) {
 }
 
 // DMA one half image (16 KiB = 16 wave-pieces of 1 KiB; 2 per wave).  Row image [128][64] or
-// tr image [64][128], the same swizzles as gemm_common.h's Pieces<128, TR, 8>.
+// tr image [64][128], the same swizzles as gemm_common.h's Pieces<128, TR, 8>.  The per-lane part
+// of each piece's source address is a 32-bit byte offset computed once per kernel (HalfPieces);
+// each stage only moves the wave-uniform base (SGPRs) — the saddr form of the DMA (glds16s).
+// With 64-bit per-lane pointers the transposed layouts ran out of VGPRs: hipcc spilled three
+// of them inside the K-loop and each reload's vmcnt(0) drained the DMA pipeline (docs/FINDINGS.md
+// §33).
 template <bool TR, int GRP>
-__device__ __forceinline__ void stage_half(const uint16_t* __restrict__ g, int64_t ld, int r0, int k0, uint8_t* img,
-                                           int X, int wave, int lane) {
+struct HalfPieces {
+  uint32_t off[2][2];  // [half X][piece]
+  __device__ __forceinline__ HalfPieces(int64_t ld, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int wbase = (i * 8 + wave) * 1024;
-    const int byte = wbase + lane * 16;
-    const uint16_t* src;
-    if constexpr (!TR) {
-      const int r = byte >> 7, pc = (byte >> 4) & 7;
-      src = g + (int64_t)(r0 + hmap<GRP>(r, X)) * ld + k0 + 8 * (pc ^ row_swz(r));
-    } else {
-      const int k = byte >> 8, pc = (byte & 255) >> 4;
-      const int lc = 8 * (pc ^ (tr_swz<128>(k) >> 1));
-      src = g + (int64_t)(k0 + k) * ld + r0 + hmap<GRP>(lc, X);
-    }
-    glds16(src, img + wbase);
+    for (int X = 0; X < 2; ++X)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int byte = (i * 8 + wave) * 1024 + lane * 16;
+        int64_t e;
+        if constexpr (!TR) {
+          const int r = byte >> 7, pc = (byte >> 4) & 7;
+          e = (int64_t)hmap<GRP>(r, X) * ld + 8 * (pc ^ row_swz(r));
+        } else {
+          const int k = byte >> 8, pc = (byte & 255) >> 4;
+          const int lc = 8 * (pc ^ (tr_swz<128>(k) >> 1));
+          e = (int64_t)k * ld + hmap<GRP>(lc, X);
+        }
+        off[X][i] = (uint32_t)(2 * e);
+      }
   }
-}
+  // K-tile at k0 of the operand rows (columns, TR) r0.. into img
+  __device__ __forceinline__ void stage(const uint16_t* g, int64_t ld, int r0, int k0, uint8_t* img, int X,
+                                        int wave) const {
+    const uint16_t* base = TR ? g + (int64_t)k0 * ld + r0 : g + (int64_t)r0 * ld + k0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16s(base, off[X][i], img + (i * 8 + wave) * 1024);
+  }
+};
 
 // Phase boundaries.  The LDS reads of a phase must be complete before its closing barrier (the
 // WAR guard for the next DMA into the half they read): V = 0 waits lgkmcnt(0) right after the
@@ -124,12 +139,10 @@ __global__ __launch_bounds__(NTH, 2) void kernel(Args p) {
         for (int j = 0; j < 4; ++j) acc[a][b][i][j] = f4{0.f, 0.f, 0.f, 0.f};
   s8v af[2][4], bf[2][2], bq[2][2];  // [kk][fragment]: A, B (and, V = 3, the B0 fragments kept)
 
-  auto stage_a = [&](int t, uint8_t* buf, int X) {
-    stage_half<A_KM, 64>(A, p.lda, m0, t * BK, buf + X * HALF, X, wave, lane);
-  };
-  auto stage_b = [&](int t, uint8_t* buf, int X) {
-    stage_half<B_KN, 32>(B, p.ldb, n0, t * BK, buf + (2 + X) * HALF, X, wave, lane);
-  };
+  const HalfPieces<A_KM, 64> pa(p.lda, wave, lane);
+  const HalfPieces<B_KN, 32> pb(p.ldb, wave, lane);
+  auto stage_a = [&](int t, uint8_t* buf, int X) { pa.stage(A, p.lda, m0, t * BK, buf + X * HALF, X, wave); };
+  auto stage_b = [&](int t, uint8_t* buf, int X) { pb.stage(B, p.ldb, n0, t * BK, buf + (2 + X) * HALF, X, wave); };
   auto read_a = [&](const uint8_t* buf, int X) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)

@@ -41,9 +41,10 @@ class GPT2Config:
     # the token table (and the tied LM head) is stored with its rows padded to a multiple of this
     # from 4096 classes up: zero rows that never receive a gradient, so the LM-head GEMMs run on an
     # aligned vocabulary (hipBLASLt on 50257 vs 50304 columns: 2.18 vs 1.75 ms per GPT-2 step,
-    # docs/FINDINGS.md §16) with no per-step padded copy of the weight.  1 = no padding.  256 with
-    # the hand-written LM head (NBD_LMHEAD_HIP=1), whose 256x256 forward tiles the vocabulary.
-    vocab_pad: int = 256 if os.environ.get("NBD_LMHEAD_HIP", "0") == "1" else 128
+    # docs/FINDINGS.md §16) with no per-step padded copy of the weight.  1 = no padding.  512 with
+    # the hand-written LM head (NBD_LMHEAD_HIP=1): 256x256 tiles over the vocabulary and an input
+    # gradient split 8 ways into whole K-tiles (ops/loss.py _hip_dgrad).
+    vocab_pad: int = 512 if os.environ.get("NBD_LMHEAD_HIP", "0") == "1" else 128
 
     @property
     def padded_vocab(self) -> int:

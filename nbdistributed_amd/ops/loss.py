@@ -174,12 +174,13 @@ LM_HEAD_WARM_BYTES = int(float(os.environ.get("NBD_LM_HEAD_WARM_MB", "0")) * (1 
 # GEMM per chunk, so a chunk's logits are re-read from the 256 MB MALL rather than from HBM
 LM_HEAD_CHUNK = int(os.environ.get("NBD_LMHEAD_CHUNK", "0"))
 # NBD_LMHEAD_HIP=1: the head's three products on the hand-written MFMA kernels instead of
-# hipBLASLt — forward on the 256x256 phase-interleaved kernel (gemm256.hip) when tokens and padded
-# vocabulary are multiples of 256, else the 128x128 8-wave kernel; input gradient on the 128x128
-# kernel split 2-4 ways along the vocabulary; weight gradient on the 128x128 kernel, accumulated
-# straight into a DDP bucket slice when one is claimed.  Opt-in: on GPT-2 small (8192 x 50304 x
-# 768) it measured slower than the library (docs/FINDINGS.md §33).
+# hipBLASLt — the 256x256 phase-interleaved kernel (gemm256.hip) wherever tokens, padded vocabulary
+# and width are multiples of 256 (GPT2 then pads its table to a multiple of 512, so the input
+# gradient splits 8 ways along the vocabulary: 3 whole rounds of 256 workgroups), else the 128x128
+# 8-wave kernel; the weight gradient is accumulated straight into a DDP bucket slice when one is
+# claimed.  Opt-in: on GPT-2 small it measured slower than the library (docs/FINDINGS.md §33).
 LM_HEAD_HIP = os.environ.get("NBD_LMHEAD_HIP", "0") == "1"
+_T256, _T128 = 86256256, 82128128
 
 
 def _hip_ok(h2, wp) -> bool:
@@ -190,35 +191,43 @@ def _hip_ok(h2, wp) -> bool:
             and N % 128 == 0 and wp.shape[0] % 128 == 0 and C % 128 == 0)
 
 
+def _big(*dims) -> bool:
+    return all(d % 256 == 0 for d in dims)
+
+
 def _hip_logits(h2, wp):
     """logits [N, Vp] = h2·wpᵀ on the hand-written kernels."""
     import torch
 
     N, Vp = h2.shape[0], wp.shape[0]
     out = torch.empty(N, Vp, dtype=h2.dtype, device=h2.device)
-    tile = 86256256 if N % 256 == 0 and Vp % 256 == 0 else 82128128
-    torch.ops.nbd.gemm(h2, wp, out, False, False, None, 0, None, None, 1, tile)
+    torch.ops.nbd.gemm(h2, wp, out, False, False, None, 0, None, None, 1, _T256 if _big(N, Vp) else _T128)
     return out
 
 
 def _hip_dgrad(dlogits, wp):
-    """dh [N, C] = dlogits·wp (wp read as [K = Vp][C]), split along the vocabulary."""
+    """dh [N, C] = dlogits·wp (wp read as [K = Vp][C]), split along the vocabulary: the most splits
+    up to 8 that divide it into whole K-tiles (N·C/256² tiles x splits workgroups)."""
     import torch
 
-    steps = wp.shape[0] // 64
-    S = next(s for s in (4, 3, 2, 1) if steps % s == 0)
-    dh = torch.empty(dlogits.shape[0], wp.shape[1], dtype=dlogits.dtype, device=dlogits.device)
-    torch.ops.nbd.gemm(dlogits, wp, dh, False, True, None, 0, None, None, S, 82128128)
+    N, (Vp, C) = dlogits.shape[0], wp.shape
+    steps = Vp // 64
+    S = next(s for s in (8, 6, 4, 3, 2, 1) if steps % s == 0)
+    dh = torch.empty(N, C, dtype=dlogits.dtype, device=dlogits.device)
+    torch.ops.nbd.gemm(dlogits, wp, dh, False, True, None, 0, None, None, S, _T256 if _big(N, C) else _T128)
     return dh
 
 
 def _hip_wgrad(dlogits, hg, out=None, accum=False):
-    """dW [Vp, C] = dlogitsᵀ·hg (both read as [K = tokens][...]) into ``out`` (+= with accum)."""
+    """dW [Vp, C] = dlogitsᵀ·hg (both read as [K = tokens][...]) into ``out`` (+= with accum: the
+    128x128 kernel, the one with an accumulating epilogue)."""
     import torch
 
+    Vp, C = dlogits.shape[1], hg.shape[1]
     if out is None:
-        out = torch.empty(dlogits.shape[1], hg.shape[1], dtype=hg.dtype, device=hg.device)
-    torch.ops.nbd.gemm(dlogits, hg, out, True, True, None, 0, None, None, 1, 82128128, 1 if accum else 0)
+        out = torch.empty(Vp, C, dtype=hg.dtype, device=hg.device)
+    tile = _T256 if _big(Vp, C) and not accum else _T128
+    torch.ops.nbd.gemm(dlogits, hg, out, True, True, None, 0, None, None, 1, tile, 1 if accum else 0)
     return out
 
 
