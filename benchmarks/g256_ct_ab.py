@@ -8,7 +8,9 @@ checked against an fp32 torch product of the same bf16 operands.
 Round 5 ran it with two temporary variants 6 / 7 (= 4 / 0 with each operand half a contiguous
 128-row / 128-column block instead of bands of 64 rows / 32 columns, so a transposed image's DMA
 reads whole 256-B runs per k-row): no gain on any layout, removed (docs/FINDINGS.md §33,
-profiles/g256_contig_halves_ab_r5.txt).
+profiles/g256_contig_halves_ab_r5.txt); and with a temporary persistent variant 6 (one workgroup
+per CU walking the tiles, C stored straight from the accumulators): slower on the LM-head forward,
+removed (profiles/g256_persistent_ab_r5.txt).
 """
 from __future__ import annotations
 

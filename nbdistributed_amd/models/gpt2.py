@@ -8,8 +8,9 @@ epilogues, grouped dgrad + wgrad backward writing into the DDP buckets), attenti
 flash kernels (``ops.attention_qkv``, csrc/kernels/attn.hip), add + LayerNorm on norm.hip and the
 loss on the fused HIP cross-entropy (``ops.linear_cross_entropy``, no fp32 copy of the
 8192 x 50257 logits).  The tied LM-head products (8192 x 50304 x 768, three per step) are the
-one place a library GEMM (hipBLASLt) runs: it measured faster than the hand-written 256x256
-kernel on them (docs/FINDINGS.md §10, §29).  CPU / fp32: the same model in plain PyTorch.
+one place a library GEMM (hipBLASLt) runs by default: it measured faster than the hand-written
+256x256 kernel on them (docs/FINDINGS.md §10, §29, §33; ``NBD_LMHEAD_HIP=1`` runs them on it,
+1.4 % slower per step).  CPU / fp32: the same model in plain PyTorch.
 Random init (no checkpoints: no network), GPT-2 initialisation scheme.
 """
 from __future__ import annotations
