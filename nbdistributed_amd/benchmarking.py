@@ -550,8 +550,8 @@ def _nbd_notebook_bench(steps, warm, bs=16, seq=128, mode="reference", small=Fal
             from nbdistributed_amd import ops as _ops
             _prev_bg = _ops.block_graphs(1)
         # eager: each bucket updated during backward (FlatAdamW(overlap=True): this step is
-        # host-bound, the GPU has room for the update; without collectives only, and never
-        # inside a graph — with collectives FlatAdamW falls back to the update in step())
+        # host-bound, the GPU has room for the update; with collectives as soon as the bucket's
+        # all-reduce has landed; never inside a graph)
         # (block graphs: the update after backward — measured faster than the side-stream overlap
         # with them, docs/FINDINGS.md §30)
         opt = _FlatAdamW(model, lr=2e-5, capturable=graph, overlap=not graph and not blockg)

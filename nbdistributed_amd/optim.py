@@ -44,15 +44,15 @@ class FlatAdamW(torch.optim.Optimizer):
         (:class:`nbdistributed_amd.graphs.GraphedStep` calls :meth:`sync_hyper` before each
         replay to push the current ``param_groups[0]['lr']``).
 
-        ``overlap=True`` (one rank, unsharded, eager): each bucket is updated on a side stream as
-        soon as DDP finalises its gradient during backward, so the memory-bound update runs under
-        the rest of the backward; ``step()`` then only completes the bookkeeping.  It pays where
-        the eager step is host-bound (small models: the GPU idles between launches), not where
-        the GPU is busy (GPT-2 small: 1.7 % slower) and not inside a HIP graph (skipped there).
-        Call ``step()`` once after every synchronising backward (the update happens in that
-        backward).  At world
-        size > 1 it falls back to the update in ``step()`` (the bucket is final only after its
-        collective).  ``None``: ``NBD_ADAMW_OVERLAP=1`` turns it on."""
+        ``overlap=True`` (unsharded, eager): each bucket is updated on a side stream as soon as
+        its gradient is final during backward — at world size 1 when DDP finalises it, at world
+        size > 1 when its all-reduce has landed (the update stream waits for the bucket's event
+        on DDP's communication stream) — so the memory-bound update runs under the rest of the
+        backward and the remaining collectives; ``step()`` then only completes the bookkeeping.
+        It pays where the eager step is host-bound (small models: the GPU idles between
+        launches), not where the GPU is busy (GPT-2 small: 1.7 % slower) and not inside a HIP
+        graph (skipped there).  Call ``step()`` once after every synchronising backward (the
+        update happens in that backward).  ``None``: ``NBD_ADAMW_OVERLAP=1`` turns it on."""
         if not getattr(ddp, "flat_params", False) or ddp.grad_mode != "bucket":
             raise ValueError("FlatAdamW needs DistributedDataParallel(..., flat_params=True, grad_mode='bucket')")
         super().__init__(list(ddp.params), dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
@@ -68,8 +68,7 @@ class FlatAdamW(torch.optim.Optimizer):
         self._multi = None  # (grads, params, masters, exp_avgs, exp_avg_sqs) of the one-call update
         if overlap is None:
             overlap = _OVERLAP
-        self.overlap = (bool(overlap) and not self.sharded and not getattr(ddp, "_collectives", False)
-                        and dev.type == "cuda")
+        self.overlap = bool(overlap) and not self.sharded and dev.type == "cuda"
         self._updated: List[int] = []  # buckets updated during the current backward (overlap)
         if self.overlap:
             self._opt_stream = torch.cuda.Stream(device=dev)
@@ -113,7 +112,9 @@ class FlatAdamW(torch.optim.Optimizer):
             torch.autograd.Variable._execution_engine.queue_callback(self._join)
         done = getattr(b, "done", None)
         if getattr(self.ddp, "_side", False) and getattr(self.ddp, "_per_bucket_wait", False) and done is not None:
-            self._opt_stream.wait_event(done)  # the bucket was finished on DDP's comm stream
+            # the bucket was finished on DDP's comm stream: its all-reduce (world > 1) and any
+            # post-division have landed once this event has
+            self._opt_stream.wait_event(done)
         self._opt_stream.wait_stream(cur)
         g = self.param_groups[0]
         st = self.flat_state[b.index]

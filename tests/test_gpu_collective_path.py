@@ -8,7 +8,8 @@
   subgroups through the ``rccl`` creator;
 * DistributedDataParallel with ``force_collectives=True``: the world > 1 path (per-bucket
   collectives on the side stream, per-bucket events, in-place ZeRO-2 reduce-scatter / all-gather,
-  RCCL inside a captured HIP graph) against the world-1 path, which issues no collective;
+  RCCL inside a captured HIP graph, FlatAdamW updating each bucket once its all-reduce landed)
+  against the world-1 path, which issues no collective;
 * no_sync gradient accumulation with a weight used twice per pass (ADVICE r3, high);
 * the GEMM next-weight warm-up under graph capture: a graph whose warm-up
   reads another model's weight keeps that storage alive, and replays bit-identically to a graph
@@ -99,10 +100,11 @@ cfg = GPT2Config(vocab_size=4096, n_positions=256, n_embd=256, n_layer=2, n_head
 torch.manual_seed(0)
 base = GPT2(cfg).to(device, torch.bfloat16)
 ids = torch.randint(0, 4096, (4, 256), generator=torch.Generator().manual_seed(1)).to(device)
-def run(force, shard=False, graph=False, steps=4):
+def run(force, shard=False, graph=False, steps=4, overlap=False):
     m = NbdDDP(copy.deepcopy(base), flat_params=True, grad_mode="bucket", shard=shard, bucket_cap_mb=1.0,
                first_bucket_mb=0.25, force_collectives=force)
-    opt = FlatAdamW(m, lr=1e-3, capturable=graph)
+    opt = FlatAdamW(m, lr=1e-3, capturable=graph, overlap=overlap)
+    assert opt.overlap == overlap
     def step(x):
         _, loss = m(x, x, return_logits=False)
         loss.backward()
@@ -117,11 +119,13 @@ l1, p1, c1, _ = run(True)
 l2, p2, _, _ = run(True, shard=True)
 l3, p3, _, _ = run(True, graph=True)
 l4, p4, _, _ = run(False, graph=True)
+l5, p5, _, _ = run(True, overlap=True)   # each bucket updated on the update stream once its all-reduce landed
 def close(a, b):
     return (a - b).abs().max().item() <= 1e-6 + 1e-3 * b.abs().max().item()
 def lclose(a, b):
     return max(abs(x - y) for x, y in zip(a, b)) <= 1e-3
-(c0, c1, nb > 2, l0[0] == l1[0], lclose(l1, l0), lclose(l2, l0), lclose(l3, l4), close(p1, p0), close(p2, p0), close(p3, p4))
+(c0, c1, nb > 2, l0[0] == l1[0], lclose(l1, l0), lclose(l2, l0), lclose(l3, l4), close(p1, p0), close(p2, p0), close(p3, p4),
+ l5 == l1, torch.equal(p5, p1))
 """
 
 
@@ -130,7 +134,7 @@ def test_forced_collective_path_matches_world1_path(sess):
     reduce-scatter/all-gather, and the same inside a captured HIP graph, all match the
     collective-free world-1 path."""
     out = _echo(sess.execute(CODE_FORCED, render=False))
-    assert out == "(False, True, True, True, True, True, True, True, True, True)", out
+    assert out == "(False, True, True, True, True, True, True, True, True, True, True, True)", out
 
 
 CODE_NOSYNC_TWICE = """
