@@ -10,7 +10,7 @@ Round 5 ran it with two temporary variants 6 / 7 (= 4 / 0 with each operand half
 reads whole 256-B runs per k-row): no gain on any layout, removed (docs/FINDINGS.md §33,
 profiles/g256_contig_halves_ab_r5.txt); and with a temporary persistent variant 6 (one workgroup
 per CU walking the tiles, C stored straight from the accumulators): slower on the LM-head forward,
-removed (profiles/g256_persistent_ab_r5.txt).
+removed (profiles/g256_persistent_ab_r5.txt).  Variant 6 now = 4 with non-temporal C stores.
 """
 from __future__ import annotations
 

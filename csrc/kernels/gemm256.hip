@@ -116,7 +116,11 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
 }
 
-template <bool A_KM, bool B_KN, int EPI, int V>
+// NTS: the C tile leaves with non-temporal stores (an output far larger than the L2s and the
+// MALL — the LM head's logits — gains nothing from being cached on its way out: LM-head forward
+// 659 -> 611 us, docs/FINDINGS.md §33).  Split-K slabs keep plain stores: the reduce kernel reads
+// them right back.
+template <bool A_KM, bool B_KN, int EPI, int V, bool NTS = false>
 __global__ __launch_bounds__(NTH, 2) void kernel(Args p) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[BYTES];  // one LDS object (guide §5 item 4a)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -302,7 +306,8 @@ __global__ __launch_bounds__(NTH, 2) void kernel(Args p) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= dgelu_tanh(h[e]);
     }
-    store8<bf16_t>(reinterpret_cast<bf16_t*>(p.c) + off, v);
+    if constexpr (NTS) store8_nt<bf16_t>(reinterpret_cast<bf16_t*>(p.c) + off, v);
+    else store8<bf16_t>(reinterpret_cast<bf16_t*>(p.c) + off, v);
   }
 }
 
@@ -329,6 +334,11 @@ static void launch_layout(const Args& p, int epi, dim3 grid, hipStream_t st) {
   TORCH_CHECK(false, "nbd::gemm: the 256x256 kernel has no epilogue ", epi, " for this layout");
 }
 
+template <bool A_KM, bool B_KN>
+static void launch_nts(const Args& p, dim3 grid, hipStream_t st) {
+  hipLaunchKernelGGL((kernel<A_KM, B_KN, EPI_NONE, 4, true>), grid, dim3(NTH), 0, st, p);
+}
+
 template <int V>
 static void launch_v(const Args& p, bool a_km, bool b_kn, int epi, dim3 grid, hipStream_t st) {
   if (!a_km && !b_kn)
@@ -341,10 +351,21 @@ static void launch_v(const Args& p, bool a_km, bool b_kn, int epi, dim3 grid, hi
 
 }  // namespace g256
 
-// variant (tile code "stages" digit - 2): schedule experiments, see phase_open / tile
+// variant (tile code "stages" digit - 2): schedule experiments, see phase_open / tile; 6 = 4 with
+// non-temporal C stores
 void launch_gemm256(const Args& p, bool a_km, bool b_kn, int epi, dim3 grid, hipStream_t st, int variant) {
   TORCH_CHECK(p.M % 256 == 0 && p.N % 256 == 0 && p.K % BK == 0, "nbd::gemm: 256x256 tiles need M, N % 256 == 0");
   TORCH_CHECK(grid.y == 1 || epi == EPI_NONE, "nbd::gemm: 256x256 split-K only without an epilogue");
+  if (variant == 6) {  // 4 with non-temporal C stores (plain products; split-K slabs stay cached)
+    TORCH_CHECK(epi == EPI_NONE, "nbd::gemm: variant 6 stores plain products");
+    if (!a_km && !b_kn)
+      g256::launch_nts<false, false>(p, grid, st);
+    else if (!a_km && b_kn)
+      g256::launch_nts<false, true>(p, grid, st);
+    else
+      g256::launch_nts<true, true>(p, grid, st);
+    return;
+  }
   switch (variant) {
     case 1: g256::launch_v<1>(p, a_km, b_kn, epi, grid, st); break;
     case 2: g256::launch_v<2>(p, a_km, b_kn, epi, grid, st); break;

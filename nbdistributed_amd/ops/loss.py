@@ -180,7 +180,10 @@ LM_HEAD_CHUNK = int(os.environ.get("NBD_LMHEAD_CHUNK", "0"))
 # 8-wave kernel; the weight gradient is accumulated straight into a DDP bucket slice when one is
 # claimed.  Opt-in: on GPT-2 small it measured slower than the library (docs/FINDINGS.md §33).
 LM_HEAD_HIP = os.environ.get("NBD_LMHEAD_HIP", "0") == "1"
-_T256, _T128 = 86256256, 82128128
+# the 256x256 kernel (for the forward with non-temporal C stores, variant 6: the 823 MB of GPT-2
+# logits outgrow every cache on their way out — 660 -> 611 us isolated; the weight gradient, a
+# 77 MB output, measured 643 vs 651 us with them: plain stores), the 128x128 8-wave kernel
+_T256_NT, _T256, _T128 = 88256256, 86256256, 82128128
 
 
 def _hip_ok(h2, wp) -> bool:
@@ -201,7 +204,7 @@ def _hip_logits(h2, wp):
 
     N, Vp = h2.shape[0], wp.shape[0]
     out = torch.empty(N, Vp, dtype=h2.dtype, device=h2.device)
-    torch.ops.nbd.gemm(h2, wp, out, False, False, None, 0, None, None, 1, _T256 if _big(N, Vp) else _T128)
+    torch.ops.nbd.gemm(h2, wp, out, False, False, None, 0, None, None, 1, _T256_NT if _big(N, Vp) else _T128)
     return out
 
 

@@ -34,7 +34,7 @@ def _err(x, ref):
     return float((x.float() - ref).abs().max() / ref.abs().max().clamp_min(1e-6))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("layout", LAYOUTS, ids=["fwd", "dgrad", "wgrad"])
 @pytest.mark.parametrize("shape", [(256, 256, 64), (256, 256, 128), (256, 512, 192), (512, 256, 320),
                                    (768, 1024, 768), (256, 256, 1088)])
@@ -59,11 +59,12 @@ def test_gemm256_identity_with_asymmetric_b():
 
 @pytest.mark.parametrize("layout", LAYOUTS, ids=["fwd", "dgrad", "wgrad"])
 @pytest.mark.parametrize("splits", [2, 4])
-def test_gemm256_split_k(layout, splits):
+@pytest.mark.parametrize("variant", [0, 6])  # 6: non-temporal C stores (slabs keep plain stores)
+def test_gemm256_split_k(layout, splits, variant):
     M, N, K = 256, 512, 2048
     a_km, b_kn = layout
     a, b = _operands(M, N, K, a_km, b_kn, seed=1)
-    c = G.matmul(a, b, a_km=a_km, b_kn=b_kn, tile=T256, splits=splits)
+    c = G.matmul(a, b, a_km=a_km, b_kn=b_kn, tile=T256 + (variant + 2) * 1000000, splits=splits)
     assert _err(c, _ref(a, b, a_km, b_kn)) < 1e-2
 
 
