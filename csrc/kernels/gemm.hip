@@ -866,7 +866,10 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "nbd::gemm: 2-D operands");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kBFloat16,
               "nbd::gemm: bf16 operands");
-  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && c.is_contiguous(), "nbd::gemm: contiguous operands");
+  // A may be a row-strided view (unit inner stride, row stride >= its width: a column block of a
+  // wider matrix, e.g. the LM head's weight gradient split by vocabulary rows); B and C contiguous
+  TORCH_CHECK(a.stride(1) == 1 && a.stride(0) >= a.size(1) && b.is_contiguous() && c.is_contiguous(),
+              "nbd::gemm: contiguous operands (A: unit inner stride)");
   const int M = a_km ? a.size(1) : a.size(0);
   const int K = a_km ? a.size(0) : a.size(1);
   const int N = b_kn ? b.size(1) : b.size(0);
@@ -912,7 +915,7 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   // per-lane DMA offsets are 32-bit byte offsets within one tile's rows (gemm_common.h Pieces)
   {
     const int64_t ra = a_km ? BK : t.bm, rb = b_kn ? BK : (epi == EPI_SWIGLU ? N / 2 + t.bn : t.bn);
-    TORCH_CHECK(ra * a.size(1) * 2 < (1LL << 32) && rb * b.size(1) * 2 < (1LL << 32),
+    TORCH_CHECK(ra * a.stride(0) * 2 < (1LL << 32) && rb * b.size(1) * 2 < (1LL << 32),
                 "nbd::gemm: row stride too large for 32-bit DMA offsets");
   }
   const int tiles = (M / t.bm) * (N / t.bn);
@@ -932,7 +935,7 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   p.M = M;
   p.N = N;
   p.K = K / S;
-  p.lda = a.size(1);
+  p.lda = a.stride(0);
   p.ldb = b.size(1);
   p.ldc = cN;
   p.tiles_m = M / t.bm;

@@ -221,16 +221,44 @@ def _hip_dgrad(dlogits, wp):
     return dh
 
 
+_CUS = []
+
+
+def _cus(dev) -> int:
+    if not _CUS:
+        import torch
+
+        _CUS.append(int(torch.cuda.get_device_properties(dev).multi_processor_count))
+    return _CUS[0]
+
+
 def _hip_wgrad(dlogits, hg, out=None, accum=False):
     """dW [Vp, C] = dlogitsᵀ·hg (both read as [K = tokens][...]) into ``out`` (+= with accum: the
-    128x128 kernel, the one with an accumulating epilogue)."""
+    128x128 kernel, the one with an accumulating epilogue).  On the 256x256 kernel the vocabulary
+    rows are cut in two launches so that no round of one-workgroup-per-CU tiles runs part-empty:
+    whole rounds unsplit, the remaining tile rows split along the tokens to fill one more round
+    (GPT-2: 594 tiles = 2.3 rounds of 256 CUs -> 510 tiles + 84 tiles x 2 splits; a single
+    launch pays a third, 30 %-full round)."""
     import torch
 
     Vp, C = dlogits.shape[1], hg.shape[1]
     if out is None:
         out = torch.empty(Vp, C, dtype=hg.dtype, device=hg.device)
-    tile = _T256 if _big(Vp, C) and not accum else _T128
-    torch.ops.nbd.gemm(dlogits, hg, out, True, True, None, 0, None, None, 1, tile, 1 if accum else 0)
+    if accum or not _big(Vp, C):
+        torch.ops.nbd.gemm(dlogits, hg, out, True, True, None, 0, None, None, 1, _T128, 1 if accum else 0)
+        return out
+    cus, tn, rows = _cus(hg.device), C // 256, Vp // 256
+    r1 = min(rows, (rows * tn // cus) * cus // tn)  # tile rows in whole rounds
+    r2 = rows - r1
+    S = 1
+    while r2 and r2 * tn * S * 2 <= cus and (dlogits.shape[0] // 64) % (S * 2) == 0:
+        S *= 2
+    if r1 == 0 or r2 == 0 or S == 1:
+        torch.ops.nbd.gemm(dlogits, hg, out, True, True, None, 0, None, None, 1, _T256, 0)
+        return out
+    c1 = r1 * 256
+    torch.ops.nbd.gemm(dlogits[:, :c1], hg, out[:c1], True, True, None, 0, None, None, 1, _T256, 0)
+    torch.ops.nbd.gemm(dlogits[:, c1:], hg, out[c1:], True, True, None, 0, None, None, S, _T256, 0)
     return out
 
 

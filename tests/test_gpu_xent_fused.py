@@ -90,7 +90,9 @@ def test_gpt2_fused_head_matches_logits_path(dev):
 
 
 @pytest.mark.parametrize("reduction", ["mean", "sum"])
-@pytest.mark.parametrize("V,C,N", [(50257, 768, 512), (5000, 256, 512), (4200, 256, 384)])
+# (38400, 512, 512): 300 weight-gradient tiles on 256 CUs — one whole round unsplit plus 44 tiles
+# split 4 ways along the tokens, the second launch reading a column block of the logits
+@pytest.mark.parametrize("V,C,N", [(50257, 768, 512), (5000, 256, 512), (4200, 256, 384), (38400, 512, 512)])
 def test_linear_cross_entropy_hand_written_products(dev, reduction, V, C, N, monkeypatch):
     """NBD_LMHEAD_HIP: the head's forward, input- and weight-gradient products on the hand-written
     kernels (256x256 forward when tokens and padded vocabulary are multiples of 256 — 5000 -> 5120
