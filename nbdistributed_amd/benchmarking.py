@@ -101,12 +101,26 @@ def _nbd_wrap(m, impl, **kw):
         return _NbdDDP(m, **kw)
     return _TorchDDP(m, device_ids=[device.index] if device.type == "cuda" else None, bucket_cap_mb=25)
 
-def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small", force=False):
+def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small", force=False, lmhead_hip=False):
     # force: the multi-rank DDP code path even at world size 1 (real collectives per bucket)
+    # lmhead_hip: the LM head's three GEMMs on the hand-written 256x256 kernel (NBD_LMHEAD_HIP),
+    # the table padded to a multiple of 512 for it
     if impl == "flatgraph" and device.type != "cuda":
         impl = "flat"   # HIP graphs need a GPU
+    import nbdistributed_amd.ops.loss as _lm
+    prev_hip = _lm.LM_HEAD_HIP
+    _lm.LM_HEAD_HIP = bool(lmhead_hip) or prev_hip
+    try:
+        return _nbd_gpt2_bench_body(steps, warm, B, T, impl, config, force, 512 if lmhead_hip else 0)
+    finally:
+        _lm.LM_HEAD_HIP = prev_hip
+
+def _nbd_gpt2_bench_body(steps, warm, B, T, impl, config, force, vocab_pad):
     torch.manual_seed(0)
-    m = GPT2(getattr(GPT2Config, config)()).to(device)
+    cfg = getattr(GPT2Config, config)()
+    if vocab_pad:
+        cfg.vocab_pad = vocab_pad
+    m = GPT2(cfg).to(device)
     amp = impl not in ("flat", "flatgraph", "zero")
     if not amp:   # bf16 params in the DDP buckets + fp32 master/moments in FlatAdamW
         m = m.to(torch.bfloat16)
@@ -329,6 +343,24 @@ def bench_ddp_graph(session, out: Dict[str, Any], steps: int = 20, warmup: int =
         _record_error(out, "graph_error", e)
         if isinstance(e, TimeoutError):
             raise
+    if bool(session.ready.get(0, {}).get("cuda_available")):
+        # the same graphed step with no library GEMM: the LM head on the hand-written kernels
+        try:
+            _arm_start(out, "graph_lmhead_hip")
+            r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flatgraph', {config!r}, "
+                                f"lmhead_hip=True)", render=False)
+            hms = _max_over_ranks(r)
+            out.update(graph_lmhead_hip_ms_per_step=hms,
+                       graph_lmhead_hip_recipe="as graph, the LM head's forward / input- / weight-gradient GEMMs on "
+                                               "the hand-written 256x256 HIP kernel instead of hipBLASLt "
+                                               "(NBD_LMHEAD_HIP=1; no library GEMM in the step)")
+            rd = _replay_detail(r)
+            if rd:
+                out["graph_lmhead_hip_replays"] = rd
+        except Exception as e:  # noqa: BLE001
+            _record_error(out, "graph_lmhead_hip_error", e)
+            if isinstance(e, TimeoutError):
+                raise
 
 
 def _log(msg: str) -> None:
