@@ -53,6 +53,9 @@ TORCH_LIBRARY(nbd, m) {
   m.def("adamw_flat_multi(Tensor[] grads, Tensor(a!)[] params, Tensor(b!)[] masters, Tensor(c!)[] exp_avgs, "
         "Tensor(d!)[] exp_avg_sqs, float lr, float beta1, float beta2, float eps, float weight_decay, int step, "
         "float grad_scale, Tensor? grad_scale_t=None, Tensor? step_t=None, Tensor? lr_t=None) -> ()");
+
+  m.def("adamw_tensors(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avgs, Tensor(c!)[] exp_avg_sqs, "
+        "Tensor[] steps, float lr, float beta1, float beta2, float eps, float weight_decay) -> ()");
   m.def("adamw_flat(Tensor grad, Tensor(a!) param, Tensor(b!) master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "
         "float lr, float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, Tensor? grad_scale_t=None, Tensor? step_t=None, Tensor? lr_t=None) -> ()");
 }

@@ -233,6 +233,135 @@ void adamw_flat_hip(const at::Tensor& grad, const at::Tensor& param, const at::T
   }
 }
 
+// ---- per-parameter AdamW over a tensor list (torch.optim.AdamW's state layout) ----------------
+// The one-line HF swap (models.native) keeps HF's fp32 parameters and the notebook's own
+// torch.optim.AdamW: its fused implementation runs the update as several chunked launches
+// (0.92 ms per SmolLM2 step, profiles/hfnative_prof_r5final.md).  Here: one launch per <= 128
+// tensors — the table (pointers, sizes, chunk prefix; ≈7.7 KiB) travels in the kernel arguments
+// as bucket.hip's multi_copy does — 8 Ki-element chunks, 16 B per lane per access, each
+// tensor's own device-side step count (torch keeps one per parameter) read once per workgroup.
+// Math in torch's fused AdamW order: decoupled decay, moments, bias corrections from the step,
+// denom = sqrt(v) / sqrt(bc2) + eps.
+constexpr int kAT = 128;
+constexpr int64_t kAChunk = 8192;
+constexpr int kAHint = 1024;
+
+struct AdamTable {
+  float* p[kAT];
+  const float* g[kAT];
+  float* m[kAT];
+  float* v[kAT];
+  const float* step[kAT];
+  int64_t numel[kAT];
+  int32_t chunk_prefix[kAT + 1];
+  int32_t group_chunks;
+  uint8_t hint[kAHint];
+  uint64_t aligned_mask[kAT / 64];
+};
+
+__device__ __forceinline__ void adamw_elem(float& w, float& mm, float& vv, float g, float lr_wd, float b1, float b2,
+                                           float step_size, float sqrt_bc2, float eps) {
+  w -= lr_wd * w;
+  mm = b1 * mm + (1.f - b1) * g;
+  vv = b2 * vv + (1.f - b2) * g * g;
+  const float denom = sqrtf(vv) / sqrt_bc2 + eps;
+  w -= step_size * mm / denom;
+}
+
+__global__ __launch_bounds__(256) void adamw_tensors_kernel(AdamTable tab, int nt, float lr, float b1, float b2,
+                                                            float eps, float wd) {
+  const int chunk = blockIdx.x;
+  int t = tab.hint[chunk / tab.group_chunks];
+  while (t + 1 < nt && tab.chunk_prefix[t + 1] <= chunk) ++t;
+  const int64_t begin = (int64_t)(chunk - tab.chunk_prefix[t]) * kAChunk;
+  const int64_t end = min(begin + kAChunk, tab.numel[t]);
+  const float stepv = *tab.step[t];
+  const float step_size = lr / (1.f - powf(b1, stepv));
+  const float sqrt_bc2 = sqrtf(1.f - powf(b2, stepv));
+  const float lr_wd = lr * wd;
+  float* __restrict__ P = tab.p[t];
+  const float* __restrict__ G = tab.g[t];
+  float* __restrict__ M = tab.m[t];
+  float* __restrict__ V = tab.v[t];
+  if ((tab.aligned_mask[t >> 6] >> (t & 63)) & 1ull) {
+    int64_t i = begin + (int64_t)threadIdx.x * 8;
+    for (; i + 8 <= end; i += 256 * 8) {
+      float g[8], w[8], mm[8], vv[8];
+      load8<float>(G + i, g);
+      load8<float>(P + i, w);
+      load8<float>(M + i, mm);
+      load8<float>(V + i, vv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) adamw_elem(w[j], mm[j], vv[j], g[j], lr_wd, b1, b2, step_size, sqrt_bc2, eps);
+      store8<float>(P + i, w);
+      store8<float>(M + i, mm);
+      store8<float>(V + i, vv);
+    }
+    for (int64_t k = i; k < end && k < i + 8; ++k)  // < 8 trailing elements (the tensor's last chunk)
+      adamw_elem(P[k], M[k], V[k], G[k], lr_wd, b1, b2, step_size, sqrt_bc2, eps);
+  } else {
+    for (int64_t k = begin + threadIdx.x; k < end; k += 256)
+      adamw_elem(P[k], M[k], V[k], G[k], lr_wd, b1, b2, step_size, sqrt_bc2, eps);
+  }
+}
+
+void adamw_tensors_hip(at::TensorList params, at::TensorList grads, at::TensorList exp_avgs,
+                       at::TensorList exp_avg_sqs, at::TensorList steps, double lr, double beta1, double beta2,
+                       double eps, double weight_decay) {
+  const size_t n = params.size();
+  TORCH_CHECK(grads.size() == n && exp_avgs.size() == n && exp_avg_sqs.size() == n && steps.size() == n,
+              "adamw_tensors: one grad, exp_avg, exp_avg_sq and step per parameter");
+  if (n == 0) return;
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t k = params[i].numel();
+    for (const at::Tensor* x : {&params[i], &grads[i], &exp_avgs[i], &exp_avg_sqs[i]})
+      TORCH_CHECK(x->is_cuda() && x->scalar_type() == at::kFloat && x->is_contiguous() && x->numel() == k &&
+                      x->device() == params[0].device(),
+                  "adamw_tensors: contiguous float32 GPU parameter / grad / moments of equal size");
+    TORCH_CHECK(steps[i].is_cuda() && steps[i].scalar_type() == at::kFloat && steps[i].numel() == 1,
+                "adamw_tensors: each step count is a 1-element float32 GPU tensor");
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(params[0].device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  size_t pos = 0;
+  while (pos < n) {
+    AdamTable tab{};
+    int nt = 0;
+    int64_t chunks = 0;
+    for (; pos < n && nt < kAT; ++pos) {
+      const int64_t k = params[pos].numel();
+      if (k == 0) continue;
+      const int64_t c = (k + kAChunk - 1) / kAChunk;
+      if (chunks + c > (int64_t)INT32_MAX / 2 && nt > 0) break;
+      tab.p[nt] = params[pos].data_ptr<float>();
+      tab.g[nt] = grads[pos].data_ptr<float>();
+      tab.m[nt] = exp_avgs[pos].data_ptr<float>();
+      tab.v[nt] = exp_avg_sqs[pos].data_ptr<float>();
+      tab.step[nt] = steps[pos].data_ptr<float>();
+      tab.numel[nt] = k;
+      tab.chunk_prefix[nt] = (int32_t)chunks;
+      bool al = true;
+      for (const void* ptr : {(const void*)tab.p[nt], (const void*)tab.g[nt], (const void*)tab.m[nt],
+                              (const void*)tab.v[nt]})
+        al = al && ((uintptr_t)ptr % 16 == 0);
+      if (al) tab.aligned_mask[nt >> 6] |= 1ull << (nt & 63);
+      chunks += c;
+      ++nt;
+    }
+    if (nt == 0) continue;
+    tab.chunk_prefix[nt] = (int32_t)chunks;
+    tab.group_chunks = (int32_t)std::max<int64_t>(1, (chunks + kAHint - 1) / kAHint);
+    for (int h = 0, t = 0; h < kAHint; ++h) {
+      const int64_t first = (int64_t)h * tab.group_chunks;
+      while (t + 1 < nt && tab.chunk_prefix[t + 1] <= first) ++t;
+      tab.hint[h] = (uint8_t)t;
+    }
+    hipLaunchKernelGGL(adamw_tensors_kernel, dim3((unsigned)chunks), dim3(256), 0, st, tab, nt, (float)lr,
+                       (float)beta1, (float)beta2, (float)eps, (float)weight_decay);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+}
+
 // Every bucket's update from one call (FlatAdamW.step's fast path): the same per-bucket kernels
 // in bucket order, without a Python round trip and an op dispatch per bucket (an eager small-model
 // step is host-bound: docs/FINDINGS.md §27).
@@ -254,4 +383,5 @@ void adamw_flat_multi_hip(at::TensorList grads, at::TensorList params, at::Tenso
 TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
   m.impl("adamw_flat", &nbd::adamw_flat_hip);
   m.impl("adamw_flat_multi", &nbd::adamw_flat_multi_hip);
+  m.impl("adamw_tensors", &nbd::adamw_tensors_hip);
 }

@@ -710,8 +710,10 @@ def native(hf_model, compute_dtype: Optional[torch.dtype] = torch.bfloat16, fuse
     parameters, with neither ``fused`` nor ``foreach`` given, uses torch's fused (one kernel per
     step) implementation instead of the multi-tensor default — the same update, and on the
     notebook's SmolLM2 step the default's optimizer phase is 3.0-5.8 ms of GPU time against
-    0.9 ms fused (docs/FINDINGS.md §30).  Other optimizers and parameters are untouched;
-    ``NBD_NATIVE_FUSED_OPTIM=0`` or ``fused_optimizer=False`` keeps torch's default.
+    0.9 ms fused (docs/FINDINGS.md §30); an ``AdamW`` then steps through ``nbd::adamw_tensors``
+    (one HIP launch per 128 parameters, torch's state; ``NBD_NATIVE_NBD_ADAMW=0`` keeps torch's
+    fused kernel).  Other optimizers and parameters are untouched; ``NBD_NATIVE_FUSED_OPTIM=0``
+    or ``fused_optimizer=False`` keeps torch's default.
 
     ``block_graphs``: each decoder block's forward replayed from its own HIP graph (1, the
     default; 2 adds the backward where gradients go to DDP bucket slices; 0 off — also with
@@ -781,13 +783,21 @@ def _install_fused_default() -> None:
         def make(orig):
             @functools.wraps(orig)
             def __init__(self, params, *args, **kwargs):
+                ours = False
                 if kwargs.get("fused") is None and kwargs.get("foreach") is None:
                     params = list(params)
                     flat = [p for g in params for p in (g["params"] if isinstance(g, dict) else [g])]
                     if flat and all(isinstance(p, torch.Tensor) and getattr(p, "_nbd_native_fused", False) and p.is_cuda
                                     and p.is_floating_point() for p in flat):
                         kwargs["fused"] = True
+                        ours = True
                 orig(self, params, *args, **kwargs)
+                if ours and os.environ.get("NBD_NATIVE_NBD_ADAMW", "1") != "0":
+                    # AdamW: the same update as one HIP launch per <= 128 parameters, torch's state
+                    # layout (optim.install_fast_adamw; torch's fused step whenever they could differ)
+                    from ..optim import install_fast_adamw
+
+                    install_fast_adamw(self)
 
             return __init__
 

@@ -238,3 +238,91 @@ class FlatAdamW(torch.optim.Optimizer):
             self._param_slice(b).copy_(st["master"].to(b.param_flat.dtype))
             if self.sharded and self.ddp._collectives:
                 dist.all_gather_into_tensor(b.param_flat, self._param_slice(b), group=self.ddp.pg)
+
+
+# ---------------------------------------------------------------------------------------------
+# torch.optim.AdamW with torch's own per-parameter state, one HIP launch per <= 128 parameters
+# (``nbd::adamw_tensors``, csrc/kernels/optim.hip) — what ``models.native()`` installs on the
+# notebook's own AdamW (NBD_NATIVE_NBD_ADAMW=0 keeps torch's fused step).
+
+_FALLBACK_KEYS = ("amsgrad", "maximize", "capturable", "differentiable")
+
+
+def _fast_adamw_ok(opt) -> bool:
+    """Every condition under which the HIP step is torch's update exactly (else torch's step
+    runs): plain hyper-parameters, no step hooks, no graph capture, contiguous fp32 GPU
+    parameters / gradients, fused-style (device, fp32) step counts in any existing state."""
+    from torch.optim import optimizer as _topt
+
+    if (getattr(opt, "_optimizer_step_pre_hooks", None) or getattr(opt, "_optimizer_step_post_hooks", None)
+            or getattr(_topt, "_global_optimizer_pre_hooks", None) or getattr(_topt, "_global_optimizer_post_hooks", None)):
+        return False
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        return False
+    for group in opt.param_groups:
+        if any(group.get(k) for k in _FALLBACK_KEYS) or torch.is_tensor(group["lr"]):
+            return False
+        if any(torch.is_tensor(b) for b in group["betas"]):
+            return False
+        for p in group["params"]:
+            g = p.grad
+            if g is None:
+                continue
+            if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and g.dtype == torch.float32
+                    and not g.is_sparse and g.is_contiguous() and g.device == p.device):
+                return False
+            st = opt.state.get(p)
+            if st:
+                s_ = st.get("step")
+                if not (torch.is_tensor(s_) and s_.is_cuda and s_.dtype == torch.float32 and s_.numel() == 1
+                        and st["exp_avg"].is_contiguous() and st["exp_avg_sq"].is_contiguous()):
+                    return False
+    return True
+
+
+def _fast_adamw_step(self, closure=None, **kwargs):
+    """``torch.optim.AdamW.step`` (decoupled weight decay, bias-corrected moments, torch's state
+    layout) as ``nbd::adamw_tensors`` launches; torch's own step whenever ``_fast_adamw_ok``
+    says the two might differ (or extra arguments such as a GradScaler's are passed)."""
+    if kwargs or not _fast_adamw_ok(self):
+        return type(self).step(self, closure, **kwargs)
+    loss = None
+    if closure is not None:
+        with torch.enable_grad():
+            loss = closure()
+    with torch.no_grad():
+        for group in self.param_groups:
+            ps, gs, ms, vs, ss = [], [], [], [], []
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                if len(st) == 0:  # as torch's fused AdamW initialises it
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                ps.append(p)
+                gs.append(p.grad)
+                ms.append(st["exp_avg"])
+                vs.append(st["exp_avg_sq"])
+                ss.append(st["step"])
+            if not ps:
+                continue
+            torch._foreach_add_(ss, 1.0)
+            b1, b2 = group["betas"]
+            torch.ops.nbd.adamw_tensors(ps, gs, ms, vs, ss, float(group["lr"]), float(b1), float(b2),
+                                        float(group["eps"]), float(group["weight_decay"]))
+    return loss
+
+
+def install_fast_adamw(opt) -> bool:
+    """Give this ``torch.optim.AdamW`` instance the HIP step (a bound method on the instance, so
+    LR schedulers and ``accelerate`` wrap it as they wrap torch's).  Returns False (nothing
+    changed) for other classes or without the native library."""
+    if type(opt) is not torch.optim.AdamW or not ops.native_available():
+        return False
+    import types
+
+    opt.step = types.MethodType(_fast_adamw_step, opt)
+    opt._nbd_fast_step = True
+    return True

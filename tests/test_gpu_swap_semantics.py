@@ -309,3 +309,69 @@ def test_native_cast_buffers_reported_and_released(dev):
     mem2 = ops.cast_buffers_memory()  # (bytes of every held group: one model's, not two)
     assert mem2["groups"] == mem["groups"] and mem2["cast_bytes"] == mem["cast_bytes"], (mem, mem2)
     assert mem2["grad_bytes"] == mem["grad_bytes"], (mem, mem2)
+
+
+def test_fast_adamw_matches_torch_fused_adamw(dev):
+    """nbd::adamw_tensors (optim.install_fast_adamw, what native() gives the notebook's AdamW)
+    against torch's fused AdamW: 300 parameters (three table launches), odd sizes, two parameter
+    groups with their own lr / weight decay, a parameter without a gradient, an LR scheduler;
+    parameters and the per-parameter state after 6 steps."""
+    from nbdistributed_amd.optim import install_fast_adamw
+
+    torch.manual_seed(5)
+    shapes = [(7,), (1000, 3), (33, 65), (4096,), (5, 5, 5)] * 60
+    ref = [torch.randn(s, device=dev).requires_grad_() for s in shapes]
+    mine = [p.detach().clone().requires_grad_() for p in ref]
+
+    def groups(ps):
+        return [{"params": ps[:150], "lr": 3e-3, "weight_decay": 0.1},
+                {"params": ps[150:], "lr": 1e-3, "weight_decay": 0.0}]
+
+    oa = torch.optim.AdamW(groups(ref), betas=(0.9, 0.95), eps=1e-6, fused=True)
+    ob = torch.optim.AdamW(groups(mine), betas=(0.9, 0.95), eps=1e-6, fused=True)
+    assert install_fast_adamw(ob)
+    sa = torch.optim.lr_scheduler.LinearLR(oa, 1.0, 0.5, total_iters=6)
+    sb = torch.optim.lr_scheduler.LinearLR(ob, 1.0, 0.5, total_iters=6)
+    for step in range(6):
+        for ps, o, s in ((ref, oa, sa), (mine, ob, sb)):
+            for i, p in enumerate(ps):
+                p.grad = None if i == 3 else torch.randn(p.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(100 * step + i))
+            o.step()
+            s.step()
+    torch.cuda.synchronize()
+    for p, q in zip(ref, mine):
+        assert _rel(q, p) < 1e-6
+    for p, q in zip(ref, mine):
+        if p.grad is None:
+            assert len(ob.state[q]) == 0
+            continue
+        sa_, sb_ = oa.state[p], ob.state[q]
+        assert float(sb_["step"]) == float(sa_["step"]) == 6.0
+        assert _rel(sb_["exp_avg"], sa_["exp_avg"]) < 1e-6
+        assert _rel(sb_["exp_avg_sq"], sa_["exp_avg_sq"]) < 1e-6
+
+
+def test_native_gives_the_notebook_adamw_the_hip_step(dev, monkeypatch):
+    """models.native(): an AdamW built afterwards on the swapped model steps through
+    nbd::adamw_tensors (the op runs), and NBD_NATIVE_NBD_ADAMW=0 keeps torch's fused step."""
+    from transformers import LlamaConfig as HFConfig, LlamaForSequenceClassification as HFSeqCls
+
+    from nbdistributed_amd.models import native
+
+    cfg = HFConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                   num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128, num_labels=2,
+                   pad_token_id=0)
+    torch.manual_seed(0)
+    m = native(HFSeqCls(cfg).to(dev))
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+    assert getattr(opt, "_nbd_fast_step", False)
+    ids = torch.randint(1, 512, (2, 64), device=dev)
+    out = m(input_ids=ids, labels=torch.tensor([0, 1], device=dev))
+    out.loss.backward()
+    opt.step()
+    assert all(float(opt.state[p]["step"]) == 1.0 for p in m.parameters() if p.grad is not None)
+    monkeypatch.setenv("NBD_NATIVE_NBD_ADAMW", "0")
+    opt2 = torch.optim.AdamW(m.parameters(), lr=1e-3)
+    assert not getattr(opt2, "_nbd_fast_step", False)
+    del m, opt, opt2
+    gc.collect()

@@ -135,3 +135,30 @@ def test_flat_adamw_drives_lr_scheduler(sess):
 def test_flat_adamw_requires_bucket_mode(sess):
     r = sess.execute("FlatAdamW(NbdDDP(copy.deepcopy(base)))", render=False, raise_on_error=False)
     assert not r.ok and "flat_params=True" in str(r.errors)
+
+
+def test_fast_adamw_falls_back_to_torch_off_gpu_and_survives_an_lr_scheduler():
+    """optim.install_fast_adamw binds the HIP step to the instance: an LR scheduler wraps it as it
+    wraps torch's (it reads ``step.__func__``), and off the GPU the update is torch's own."""
+    from nbdistributed_amd.optim import install_fast_adamw
+
+    torch.manual_seed(0)
+    a = torch.nn.Linear(16, 8)
+    b = torch.nn.Linear(16, 8)
+    b.load_state_dict(a.state_dict())
+    oa = torch.optim.AdamW(a.parameters(), lr=1e-2, weight_decay=0.1)
+    ob = torch.optim.AdamW(b.parameters(), lr=1e-2, weight_decay=0.1)
+    installed = install_fast_adamw(ob)
+    assert installed == ops.native_available()
+    sa = torch.optim.lr_scheduler.StepLR(oa, 2, 0.5)
+    sb = torch.optim.lr_scheduler.StepLR(ob, 2, 0.5)
+    x = torch.randn(4, 16)
+    for _ in range(4):
+        for m, o, s in ((a, oa, sa), (b, ob, sb)):
+            o.zero_grad()
+            m(x).square().mean().backward()
+            o.step()
+            s.step()
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.equal(p, q)
+    assert ob.state_dict()["state"].keys() == oa.state_dict()["state"].keys()
