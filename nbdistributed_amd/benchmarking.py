@@ -101,21 +101,23 @@ def _nbd_wrap(m, impl, **kw):
         return _NbdDDP(m, **kw)
     return _TorchDDP(m, device_ids=[device.index] if device.type == "cuda" else None, bucket_cap_mb=25)
 
-def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small", force=False, lmhead_hip=False):
+def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small", force=False, lmhead_lib=False):
     # force: the multi-rank DDP code path even at world size 1 (real collectives per bucket)
-    # lmhead_hip: the LM head's three GEMMs on the hand-written 256x256 kernel (NBD_LMHEAD_HIP),
-    # the table padded to a multiple of 512 for it
+    # lmhead_lib: the LM head's three GEMMs on hipBLASLt (NBD_LMHEAD_HIP=0) instead of the
+    # hand-written 256x256 kernel, the table padded to a multiple of 128 as the library wants
     if impl == "flatgraph" and device.type != "cuda":
         impl = "flat"   # HIP graphs need a GPU
     import nbdistributed_amd.ops.loss as _lm
     prev_hip = _lm.LM_HEAD_HIP
-    _lm.LM_HEAD_HIP = bool(lmhead_hip) or prev_hip
+    if lmhead_lib:
+        _lm.LM_HEAD_HIP = False
     try:
-        return _nbd_gpt2_bench_body(steps, warm, B, T, impl, config, force, 512 if lmhead_hip else 0)
+        return _nbd_gpt2_bench_body(steps, warm, B, T, impl, config, force, 128 if lmhead_lib else 0)
     finally:
         _lm.LM_HEAD_HIP = prev_hip
 
 def _nbd_gpt2_bench_body(steps, warm, B, T, impl, config, force, vocab_pad):
+    # vocab_pad: the table's padding multiple (0: GPT2Config's default)
     torch.manual_seed(0)
     cfg = getattr(GPT2Config, config)()
     if vocab_pad:
@@ -344,21 +346,22 @@ def bench_ddp_graph(session, out: Dict[str, Any], steps: int = 20, warmup: int =
         if isinstance(e, TimeoutError):
             raise
     if bool(session.ready.get(0, {}).get("cuda_available")):
-        # the same graphed step with no library GEMM: the LM head on the hand-written kernels
+        # the same graphed step with the LM head's three GEMMs on hipBLASLt (the only library
+        # GEMMs the step could use) for comparison
         try:
-            _arm_start(out, "graph_lmhead_hip")
+            _arm_start(out, "graph_lmhead_lib")
             r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flatgraph', {config!r}, "
-                                f"lmhead_hip=True)", render=False)
+                                f"lmhead_lib=True)", render=False)
             hms = _max_over_ranks(r)
-            out.update(graph_lmhead_hip_ms_per_step=hms,
-                       graph_lmhead_hip_recipe="as graph, the LM head's forward / input- / weight-gradient GEMMs on "
-                                               "the hand-written 256x256 HIP kernel instead of hipBLASLt "
-                                               "(NBD_LMHEAD_HIP=1; no library GEMM in the step)")
+            out.update(graph_lmhead_lib_ms_per_step=hms,
+                       graph_lmhead_lib_recipe="as graph, the LM head's forward / input- / weight-gradient GEMMs on "
+                                               "hipBLASLt (NBD_LMHEAD_HIP=0) instead of the hand-written 256x256 "
+                                               "HIP kernel")
             rd = _replay_detail(r)
             if rd:
-                out["graph_lmhead_hip_replays"] = rd
+                out["graph_lmhead_lib_replays"] = rd
         except Exception as e:  # noqa: BLE001
-            _record_error(out, "graph_lmhead_hip_error", e)
+            _record_error(out, "graph_lmhead_lib_error", e)
             if isinstance(e, TimeoutError):
                 raise
 

@@ -7,10 +7,10 @@ GEMMs (``ops.gemm_linear`` / ``ops.mlp_gelu``: csrc/kernels/gemm.hip, fused bias
 epilogues, grouped dgrad + wgrad backward writing into the DDP buckets), attention on the HIP
 flash kernels (``ops.attention_qkv``, csrc/kernels/attn.hip), add + LayerNorm on norm.hip and the
 loss on the fused HIP cross-entropy (``ops.linear_cross_entropy``, no fp32 copy of the
-8192 x 50257 logits).  The tied LM-head products (8192 x 50304 x 768, three per step) are the
-one place a library GEMM (hipBLASLt) runs by default: it measured faster than the hand-written
-256x256 kernel on them (docs/FINDINGS.md §10, §29, §33; ``NBD_LMHEAD_HIP=1`` runs them on it,
-1.4 % slower per step).  CPU / fp32: the same model in plain PyTorch.
+8192 x 50257 logits).  The tied LM-head products (8192 x 50688 x 768, three per step) run on the
+hand-written 256x256 kernel (gemm256.hip; the table padded to a multiple of 512 for it) — within
+0.7-1.2 % of hipBLASLt on the step (docs/FINDINGS.md §33; ``NBD_LMHEAD_HIP=0`` runs them on the
+library with a 128-padded table).  CPU / fp32: the same model in plain PyTorch.
 Random init (no checkpoints: no network), GPT-2 initialisation scheme.
 """
 from __future__ import annotations
@@ -42,10 +42,10 @@ class GPT2Config:
     # the token table (and the tied LM head) is stored with its rows padded to a multiple of this
     # from 4096 classes up: zero rows that never receive a gradient, so the LM-head GEMMs run on an
     # aligned vocabulary (hipBLASLt on 50257 vs 50304 columns: 2.18 vs 1.75 ms per GPT-2 step,
-    # docs/FINDINGS.md §16) with no per-step padded copy of the weight.  1 = no padding.  512 with
-    # the hand-written LM head (NBD_LMHEAD_HIP=1): 256x256 tiles over the vocabulary and an input
-    # gradient split 8 ways into whole K-tiles (ops/loss.py _hip_dgrad).
-    vocab_pad: int = 512 if os.environ.get("NBD_LMHEAD_HIP", "0") == "1" else 128
+    # docs/FINDINGS.md §16) with no per-step padded copy of the weight.  1 = no padding.  512 for
+    # the hand-written LM head (the default; 128 with NBD_LMHEAD_HIP=0): 256x256 tiles over the
+    # vocabulary and an input gradient split 8 ways into whole K-tiles (ops/loss.py _hip_dgrad).
+    vocab_pad: int = 128 if os.environ.get("NBD_LMHEAD_HIP", "1") == "0" else 512
 
     @property
     def padded_vocab(self) -> int:

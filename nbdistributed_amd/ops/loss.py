@@ -173,13 +173,14 @@ LM_HEAD_WARM_BYTES = int(float(os.environ.get("NBD_LM_HEAD_WARM_MB", "0")) * (1 
 # rows per LM-head chunk (0 = one [N, Vp] GEMM): GEMM -> in-place loss gradient -> input-gradient
 # GEMM per chunk, so a chunk's logits are re-read from the 256 MB MALL rather than from HBM
 LM_HEAD_CHUNK = int(os.environ.get("NBD_LMHEAD_CHUNK", "0"))
-# NBD_LMHEAD_HIP=1: the head's three products on the hand-written MFMA kernels instead of
-# hipBLASLt — the 256x256 phase-interleaved kernel (gemm256.hip) wherever tokens, padded vocabulary
-# and width are multiples of 256 (GPT2 then pads its table to a multiple of 512, so the input
-# gradient splits 8 ways along the vocabulary: 3 whole rounds of 256 workgroups), else the 128x128
-# 8-wave kernel; the weight gradient is accumulated straight into a DDP bucket slice when one is
-# claimed.  Opt-in: on GPT-2 small it measured slower than the library (docs/FINDINGS.md §33).
-LM_HEAD_HIP = os.environ.get("NBD_LMHEAD_HIP", "0") == "1"
+# The head's three products on the hand-written MFMA kernels (NBD_LMHEAD_HIP=0: hipBLASLt) — the
+# 256x256 phase-interleaved kernel (gemm256.hip) wherever tokens, padded vocabulary and width are
+# multiples of 256 (GPT2 then pads its table to a multiple of 512, so the input gradient splits 8
+# ways along the vocabulary: 3 whole rounds of 256 workgroups), else the 128x128 8-wave kernel;
+# the weight gradient is accumulated straight into a DDP bucket slice when one is claimed.  On the
+# GPT-2 small step within 0.7-1.2 % of the library head (docs/FINDINGS.md §33), with no library
+# GEMM left in the step.
+LM_HEAD_HIP = os.environ.get("NBD_LMHEAD_HIP", "1") != "0"
 # the 256x256 kernel (for the forward with non-temporal C stores, variant 6: the 823 MB of GPT-2
 # logits outgrow every cache on their way out — 660 -> 611 us isolated; the weight gradient, a
 # 77 MB output, measured 643 vs 651 us with them: plain stores), the 128x128 8-wave kernel
@@ -266,9 +267,11 @@ def linear_cross_entropy(h, weight, target, ignore_index: int = -100, reduction:
     """``cross_entropy(h @ weight.T, target)`` for an LM head (``h`` [..., C], ``weight`` [V, C]) —
     the loss's forward and backward fused into one pass over the logits on the GPU path (bf16/fp16,
     V ≤ 65,536: one read and one in-place write of the [N, V] logits instead of two reads and a
-    write), the GEMMs on hipBLASLt.  The logits are not returned.  ``vocab`` < ``weight.shape[0]``:
+    write), the GEMMs on the hand-written MFMA kernels (``NBD_LMHEAD_HIP=0``: hipBLASLt).  The
+    logits are not returned.  ``vocab`` < ``weight.shape[0]``:
     the table's rows past ``vocab`` are zero padding (GPT2 keeps its tied table padded to a
-    multiple of 128) — the loss covers the first ``vocab`` classes only."""
+    multiple of 512; 128 with the library head) — the loss covers the first ``vocab`` classes
+    only."""
     import torch
     import torch.nn.functional as F
 

@@ -53,6 +53,7 @@ def test_linear_cross_entropy_autograd(dev, reduction, V, C, chunk, monkeypatch)
     from nbdistributed_amd.ops import loss as L
 
     monkeypatch.setattr(L, "LM_HEAD_CHUNK", chunk)
+    monkeypatch.setattr(L, "LM_HEAD_HIP", False)  # the library head (its row-chunked form included)
     torch.manual_seed(1)
     N = 512
     h = (torch.randn(N, C, device=dev) * 0.5).to(torch.bfloat16).requires_grad_()
