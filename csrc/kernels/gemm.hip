@@ -410,8 +410,8 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
         }
       }
       const int64_t m = m0 + r, j = n0 / 2 + cn;
-      store8<bf16_t>(reinterpret_cast<bf16_t*>(p.aux_out) + m * p.N + j, g);
-      store8<bf16_t>(reinterpret_cast<bf16_t*>(p.aux_out) + m * p.N + I + j, u);
+      store8_nt<bf16_t>(reinterpret_cast<bf16_t*>(p.aux_out) + m * p.N + j, g);
+      store8_nt<bf16_t>(reinterpret_cast<bf16_t*>(p.aux_out) + m * p.N + I + j, u);
 #pragma unroll
       for (int e = 0; e < 8; ++e) g[e] = g[e] * sigm(g[e]) * u[e];
       store8<bf16_t>(reinterpret_cast<bf16_t*>(p.c) + m * p.ldc + j, g);
@@ -463,7 +463,7 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
       for (int e = 0; e < 8; ++e) v[e] += b[e];
     }
     if constexpr (EPI == EPI_GELU) {
-      store8<bf16_t>(reinterpret_cast<bf16_t*>(p.aux_out) + off, v);
+      store8_nt<bf16_t>(reinterpret_cast<bf16_t*>(p.aux_out) + off, v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
     } else if constexpr (EPI == EPI_DGELU) {
