@@ -627,6 +627,16 @@ static void launch_epi(const Tile& t, const Args& a, dim3 grid, hipStream_t st) 
     // where 128x128 leaves 0.75 / 2.25 rounds
     if constexpr (!A_KM && !B_KN) NBD_GEMM_CASE(128, 96, 1)
   } while (0);
+  // 128x192, 8 waves (forward layout, plain / GELU epilogue): N = 768 forwards are exactly one
+  // round of 256 workgroups (8192 tokens), N = 2304 / 3072 three / four; each wave's 64x48 block
+  // reads 7 fragments per 12 MFMAs (128x128: 6 per 8)
+  if constexpr (!A_KM && !B_KN && (EPI == EPI_NONE || EPI == EPI_GELU)) {
+    if (t.bm == 128 && t.bn == 192 && t.waves == 8 && t.ks == 1) {
+      if (t.stages == 3) NBD_GEMM_K(128, 192, 3, 8, 1);
+      else NBD_GEMM_K(128, 192, 2, 8, 1);
+      return;
+    }
+  }
   if (t.bm == 128 && t.bn == 128 && t.waves == 8 && t.ks == 1) {  // 8 waves: 128x128 only
     if (t.stages == 9) NBD_GEMM_K(128, 128, 103, 8, 1);  // ping-pong, 3-buffer ring
     else if (t.stages == 3) NBD_GEMM_K(128, 128, 3, 8, 1);

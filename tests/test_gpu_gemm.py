@@ -48,11 +48,12 @@ def test_gemm_layouts_and_tiles(layout, tile, shape):
     assert _err(c, _ref(a, b, a_km, b_kn)) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [2128096, 3128096])
+@pytest.mark.parametrize("tile", [2128096, 3128096, 82128192, 83128192])
 @pytest.mark.parametrize("shape", [(256, 576, 320), (384, 192, 192), (128, 384, 64), (512, 768, 1216)])  # N % 192 == 0
 @pytest.mark.parametrize("epi", [0, 1])
 def test_gemm_forward_128x96_tile(tile, shape, epi):
-    """The 128x96 forward tile (row images only), plain and with the bias + GELU epilogue."""
+    """The 128x96 (4 waves) and 128x192 (8 waves) forward tiles (row images only), plain and with
+    the bias + GELU epilogue."""
     M, N, K = shape
     a, b = _operands(M, N, K, False, False, seed=3)
     bias = torch.randn(N, device="cuda").to(torch.bfloat16)
