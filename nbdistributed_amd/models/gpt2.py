@@ -45,7 +45,9 @@ class GPT2Config:
     # docs/FINDINGS.md §16) with no per-step padded copy of the weight.  1 = no padding.  512 for
     # the hand-written LM head (the default; 128 with NBD_LMHEAD_HIP=0): 256x256 tiles over the
     # vocabulary and an input gradient split 8 ways into whole K-tiles (ops/loss.py _hip_dgrad).
-    vocab_pad: int = 128 if os.environ.get("NBD_LMHEAD_HIP", "1") == "0" else 512
+    # NBD_GPT2_VOCAB_PAD overrides (A/B measurements).
+    vocab_pad: int = (int(os.environ.get("NBD_GPT2_VOCAB_PAD", "0"))
+                      or (128 if os.environ.get("NBD_LMHEAD_HIP", "1") == "0" else 512))
 
     @property
     def padded_vocab(self) -> int:
