@@ -3,7 +3,7 @@
 choice (ops/gemm.py ``config``) and torch/hipBLASLt, back-to-back launches timed with HIP events
 (gemm_bench.timeit_pipelined), with a numerics check of each hint against torch.
 
-    python benchmarks/gemm_tile_ab.py [--hints 82128192,83128192] [--gelu]
+    python benchmarks/gemm_tile_ab.py [--hints 82128192,83128192] [--gelu] [--shape M,N,K]
 """
 from __future__ import annotations
 
@@ -26,6 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--hints", default="82128192,83128192")
     ap.add_argument("--gelu", action="store_true", help="bias + GELU epilogue (the c_fc forward's)")
+    ap.add_argument("--shape", default="", help="M,N,K: this product only (e.g. the LM head 8192,50688,768)")
     a = ap.parse_args()
     from nbdistributed_amd import ops
 
@@ -33,7 +34,11 @@ def main():
     dev = torch.device("cuda")
     hints = [int(h) for h in a.hints.split(",") if h]
     epi = G.EPI_GELU if a.gelu else G.EPI_NONE
-    for name, M, N, K in SHAPES:
+    shapes = SHAPES
+    if a.shape:
+        M_, N_, K_ = (int(v) for v in a.shape.split(","))
+        shapes = (("shape", M_, N_, K_),)
+    for name, M, N, K in shapes:
         x = torch.randn(M, K, device=dev).to(torch.bfloat16)
         w = (torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16)
         bias = (torch.randn(N, device=dev) * 0.1).to(torch.bfloat16) if a.gelu else None
