@@ -25,7 +25,10 @@ algbw/busbw and the 1 KiB..1 GiB sweep).  Nothing here may hang silently:
   line with ``"value": null`` and ``"error": "rendezvous: k/N ranks joined"``;
 * past ``NBD_BENCH_HARD_S`` (default 540 s) the line is printed from the last checkpointed phase
   with ``"partial": true``;
-* the exit status is non-zero whenever the line is partial or carries an error.
+* the exit status is non-zero whenever the line is partial or carries an error, and 5 when a
+  data-plane correctness check (``nbdistributed_amd.checks``: collectives against closed-form
+  values, nbd DDP against torch DDP, ZeRO-2, the graphed step, accelerate, ``%%rank`` +
+  broadcast) failed — ``"checks_passed"`` / ``"checks"`` in the line say which.
 """
 from __future__ import annotations
 
@@ -51,6 +54,7 @@ HARD_DEADLINE_S = float(os.environ.get("NBD_BENCH_HARD_S", "540"))
 # a fresh box's first `import torch` alone can take 1-2 minutes
 RENDEZVOUS_S = float(os.environ.get("NBD_BENCH_RENDEZVOUS_S", "300"))
 EXIT_PARTIAL = 3
+EXIT_CHECKS = 5  # the line is complete but a data-plane correctness check failed
 _T0 = time.monotonic()
 
 
@@ -68,6 +72,7 @@ def _args(argv=None):
     ap.add_argument("--ddp-steps", type=int, default=20)
     ap.add_argument("--no-bcast", action="store_true", help="skip the %%%%rank[0] build + broadcast phase (config 3)")
     ap.add_argument("--no-notebook", action="store_true", help="skip the reference notebook workload (SmolLM2)")
+    ap.add_argument("--no-checks", action="store_true", help="skip the data-plane correctness checks")
     ap.add_argument("--backend", default="auto", help="worker backend (auto = rccl on GPUs, gloo on CPU)")
     ap.add_argument("--coordinator", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--endpoint", default=None, help=argparse.SUPPRESS)
@@ -82,7 +87,7 @@ def _log(msg: str) -> None:
 
 def _phases_kw(a) -> dict:
     return dict(allreduce=not a.no_allreduce, sweep=a.sweep, ar_bytes=a.ar_bytes, ddp=not a.no_ddp,
-                ddp_steps=a.ddp_steps, bcast=not a.no_bcast, notebook=not a.no_notebook)
+                ddp_steps=a.ddp_steps, bcast=not a.no_bcast, notebook=not a.no_notebook, checks=not a.no_checks)
 
 
 def _snapshot(out: dict) -> dict:
@@ -135,7 +140,8 @@ class _Printer:
             for k in ("device", "rccl_version", "launch", "init_ready"):
                 if res.get(k) is not None:
                     line[k] = res[k]
-            bad = bool(res.get("partial") or why or line.get("error"))
+            # a failed correctness check makes the run fail (exit status), whatever was timed
+            bad = bool(res.get("partial") or why or line.get("error") or line.get("checks_passed") is False)
             if res.get("partial") or why:
                 line["partial"] = True
                 line["partial_reason"] = why or "coordinator ended before the last phase"
@@ -143,6 +149,8 @@ class _Printer:
             sys.stdout.flush()
             os.write(self.fd, (json.dumps(line) + "\n").encode())
             self.done = True
+            if bad and line.get("checks_passed") is False and not line.get("partial") and not line.get("error"):
+                return EXIT_CHECKS
             return EXIT_PARTIAL if bad else 0
 
 
@@ -258,7 +266,7 @@ def attach_main(a) -> int:
                "--steps", str(a.steps), "--warmup", str(a.warmup), "--out", out_path, "--ar-bytes", str(a.ar_bytes),
                "--ddp-steps", str(a.ddp_steps)]
         for flag, on in (("--no-sweep", not a.sweep), ("--no-allreduce", a.no_allreduce), ("--no-ddp", a.no_ddp),
-                         ("--no-bcast", a.no_bcast), ("--no-notebook", a.no_notebook)):
+                         ("--no-bcast", a.no_bcast), ("--no-notebook", a.no_notebook), ("--no-checks", a.no_checks)):
             if on:
                 cmd.append(flag)
         child = subprocess.Popen(cmd, stdin=subprocess.DEVNULL)

@@ -356,7 +356,11 @@ static void launch_v(const Args& p, bool a_km, bool b_kn, int epi, dim3 grid, hi
 void launch_gemm256(const Args& p, bool a_km, bool b_kn, int epi, dim3 grid, hipStream_t st, int variant) {
   TORCH_CHECK(p.M % 256 == 0 && p.N % 256 == 0 && p.K % BK == 0, "nbd::gemm: 256x256 tiles need M, N % 256 == 0");
   TORCH_CHECK(grid.y == 1 || epi == EPI_NONE, "nbd::gemm: 256x256 split-K only without an epilogue");
-  if (variant == 6) {  // 4 with non-temporal C stores (plain products; split-K slabs stay cached)
+  // every caller of this entry point passes one of the three built layouts; (A [K][M], B [N][K])
+  // has no instantiation (launch_v / launch_nts would run the <true, true> kernel on it)
+  TORCH_CHECK(!(a_km && !b_kn), "nbd::gemm: the 256x256 kernel has no (A [K][M], B [N][K]) layout");
+  if (variant == 6) {  // 4 with non-temporal C stores (plain products; split-K slabs stay cached:
+                       // the slab path returns before the C-tile stores)
     TORCH_CHECK(epi == EPI_NONE, "nbd::gemm: variant 6 stores plain products");
     if (!a_km && !b_kn)
       g256::launch_nts<false, false>(p, grid, st);

@@ -837,7 +837,7 @@ CPU_AR_BYTES = int(os.environ.get("NBD_BENCH_CPU_AR_BYTES", str(1 << 20)))
 def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: bool = False,
             ar_bytes: int = 1 << 30, ddp: bool = True, ddp_steps: int = 20, bcast: bool = True,
             notebook: bool = True, phase_timeout_s: float = 300.0, deadline_s: Optional[float] = None,
-            checkpoint=None) -> Dict[str, Any]:
+            checkpoint=None, checks: bool = True) -> Dict[str, Any]:
     """All phases under one global deadline (``deadline_s`` from now, default
     ``NBD_BENCH_DEADLINE_S`` = 420 s); ``checkpoint(out)`` is called after every phase so the
     caller can persist what has been measured (bench.py writes it where rank 0 reads it, even if
@@ -862,6 +862,17 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
         out: Dict[str, Any] = {"cell": cells}
         ckpt(out)
         _phase(session, out, "world", lambda: bench_world(session), phase_timeout_s, deadline)
+        if checks:
+            # correctness of the data plane at this world size (nbdistributed_amd.checks): every
+            # collective against closed-form values, nbd DDP against torch DDP, the recipe's
+            # cross-rank sync, ZeRO-2, the graphed step, accelerate, %%rank + broadcast
+            _log(f"phase 1a: data-plane correctness checks on {n} rank(s)")
+            from .checks import run_checks
+
+            _phase(session, out, "checks", lambda: run_checks(session, log=_log), phase_timeout_s, deadline, 20.0)
+            ck = out["checks"]
+            _log("checks: " + ("all passed" if ck.get("passed") else f"FAILED {ck.get('failed') or ck.get('error')}"))
+            ckpt(out)
         _log(f"phase 1b: {warmup}+{steps} trivial cells through the magic path (auto mode, ide_sync, renderer)")
         _phase(session, out, "cell_magic", lambda: bench_cells_magic(session, steps, warmup), phase_timeout_s, deadline)
         if "p50_ms" in out["cell_magic"]:
@@ -1020,6 +1031,14 @@ def result_line(res: Dict[str, Any], n: int, steps: int, warmup: int) -> Dict[st
                                      "plane as a Jupyter kernel drives it")
     elif ci and ("error" in ci or "skipped" in ci):
         line["cell_ipython_error"] = ci.get("error") or ci.get("skipped")
+    ck = res.get("checks")
+    if isinstance(ck, dict) and ck:
+        if "passed" in ck:
+            line["checks_passed"] = bool(ck["passed"])
+            line["checks"] = ck
+        else:  # the phase itself failed or was skipped: not a pass
+            line["checks_passed"] = False
+            line["checks"] = {"passed": False, "error": ck.get("error") or ck.get("skipped")}
     wd = res.get("world") or {}
     if "per_rank" in wd:
         line["rccl_world_size"] = {str(r): v["world_size"] for r, v in wd["per_rank"].items()}

@@ -38,6 +38,17 @@ def _copy_into(dst, src):
         raise ValueError("GraphedStep: non-tensor arguments are baked into the graph and must not change")
 
 
+# checks attached to the capture in progress (note_capture_check): objects with before_replay()
+# and after_replay(), e.g. the Llama fused path's attention-mask check (models/llama.py)
+_CAPTURE_CHECKS: list = []
+
+
+def note_capture_check(check) -> None:
+    """Called by a model op whose host-side check cannot run inside a stream capture: the check
+    then runs around every replay of the graph being captured (``GraphedStep``)."""
+    _CAPTURE_CHECKS.append(check)
+
+
 def _drain_collective_watchdog(poll_s: float = 0.35) -> None:
     """ProcessGroupNCCL's watchdog thread polls the events of outstanding collectives (every
     ~100 ms) and retires completed ones.  Warm-up collectives still on its list when capture
@@ -157,7 +168,12 @@ class GraphedStep:
         # watchdog thread keeps querying its events meanwhile, which "global" mode turns into a
         # hipErrorStreamCaptureUnsupported abort (seen intermittently on this stack)
         _take_warm_refs()  # (drop references left by an earlier capture that nobody took)
-        _capture(self.graph, lambda: setattr(self, "static_out", fn(*self.static_args)), pool)
+        del _CAPTURE_CHECKS[:]
+        try:
+            _capture(self.graph, lambda: setattr(self, "static_out", fn(*self.static_args)), pool)
+            self._checks = list(_CAPTURE_CHECKS)
+        finally:
+            del _CAPTURE_CHECKS[:]
         # the captured GEMMs' next-weight warm-up reads (csrc/kernels/gemm.hip, namespace warm)
         # are frozen pointers into those weights' storages: hold them as long as the graph
         self._warm_refs = _take_warm_refs()
@@ -175,8 +191,12 @@ class GraphedStep:
         for dst, src in zip(self.static_args, args):
             _copy_into(dst, src)
         self._sync_hyper()
+        for c in self._checks:
+            c.before_replay()
         self.graph.replay()
         self.replays += 1
+        for c in self._checks:
+            c.after_replay()
         return self.static_out
 
 

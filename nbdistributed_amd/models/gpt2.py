@@ -171,6 +171,31 @@ class GPT2(nn.Module):
             with torch.no_grad():  # the pad rows stay zero: no id reaches them, their gradient is 0
                 self.wte.weight[c.vocab_size:].zero_()
                 self.lm_head.weight[c.vocab_size:].zero_()
+        # the table's padding (vocab_pad) is a storage choice of the process that built the model
+        # (it follows which kernel runs the LM head): a state_dict saved with another padding —
+        # or the unpadded HF layout — loads by zero-padding / trimming the rows past vocab_size
+        self._register_load_state_dict_pre_hook(self._repad_vocab)
+
+    def _repad_vocab(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                     error_msgs) -> None:
+        c = self.config
+        Vp, V = c.padded_vocab, c.vocab_size
+        for name in ("wte.weight", "lm_head.weight"):
+            k = prefix + name
+            t = state_dict.get(k)
+            if not isinstance(t, torch.Tensor) or t.dim() != 2 or t.shape[0] == Vp or t.shape[0] < V:
+                continue
+            if t.shape[1] != c.n_embd:
+                continue  # a genuine mismatch: load_state_dict reports it
+            if t.shape[0] > Vp:
+                extra = t[Vp:]
+                if extra.numel() and bool((extra != 0).any()):
+                    error_msgs.append(f"{k}: rows {Vp}..{t.shape[0] - 1} past the vocabulary ({V}) are not zero; "
+                                      "they cannot be trimmed to this model's padding")
+                    continue
+                state_dict[k] = t[:Vp]
+            else:
+                state_dict[k] = torch.cat([t, t.new_zeros(Vp - t.shape[0], t.shape[1])])
 
     @staticmethod
     def _init(m: nn.Module) -> None:

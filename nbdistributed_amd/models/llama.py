@@ -22,7 +22,9 @@ HF semantics kept by the one-line swap (``native()``):
   padding.  The sequence classifier rotates left-padded rows into right-padded ones in one kernel
   (``ops.seqcls_prep``; RoPE scores depend on position differences only) and re-indexes the
   pooled token; a mask with holes is reported (ValueError at the next call: the check is read
-  without a host sync).  The causal LM needs right padding (reported the same way).
+  without a host sync, so the reported batch has already been applied — ``NBD_MASK_CHECK_SYNC=1``
+  raises on the offending call instead; inside a ``GraphedStep`` the check follows the replays).
+  The causal LM needs right padding (reported the same way).
 * forward (pre-)hooks and backward hooks on the decoder layers or any of their submodules (or
   global module hooks): the model then runs module by module, HF's structure — each layer is
   called as ``layer(hidden_states, ...)`` and returns the residual stream, attention honours the
@@ -279,10 +281,20 @@ def _global_hooks() -> bool:
                 or getattr(_m, "_global_backward_pre_hooks", None))
 
 
+# NBD_MASK_CHECK_SYNC=1: read the mask check right after the prep kernel (one host sync per
+# call) and raise before the batch is used, instead of at the next call
+_MASK_CHECK_SYNC = os.environ.get("NBD_MASK_CHECK_SYNC", "0") == "1"
+
+
 class _MaskCheck:
     """A device-side flag about the attention masks seen (``ops.seqcls_prep``), read one call
     late without a host sync: a pinned copy and an event per call; the next call raises if the
-    flag had a failing bit by then.  Not armed inside a graph capture."""
+    flag had a failing bit by then.  THE REPORTED BATCH HAS ALREADY BEEN APPLIED: its loss and
+    gradients were computed on the fused path (wrong for that mask) and may already have gone
+    through ``optimizer.step()``.  ``NBD_MASK_CHECK_SYNC=1`` checks synchronously instead (the
+    call that got the bad mask raises, before anything uses it).  Inside a HIP graph capture the
+    check is attached to the graph (``graphs.note_capture_check``): ``GraphedStep`` copies the
+    flag after every replay and raises at the next replay."""
 
     def __init__(self):
         self.dev = None
@@ -296,27 +308,56 @@ class _MaskCheck:
             self.ev = None
         return self.dev
 
+    def _raise(self, what: str, late: bool) -> None:
+        self.dev.zero_()
+        if late:
+            raise ValueError(f"nbd Llama: an attention_mask {what}.  It was seen in an EARLIER call, whose batch has "
+                             "already been applied (its loss and gradients were computed on the fused path without "
+                             "that mask, and may have gone through optimizer.step()).  NBD_MASK_CHECK_SYNC=1 raises "
+                             "on the offending call instead; register a forward hook on the model to run the module "
+                             "path, which honours any mask (models/llama.py module docstring)")
+        raise ValueError(f"nbd Llama: attention_mask {what} (nothing of this batch was applied; register a forward "
+                         "hook on the model to run the module path, which honours any mask)")
+
     def poll(self, fail_bits: int, what: str) -> None:
         if self.ev is not None and not torch.cuda.is_current_stream_capturing() and self.ev.query():
             v = int(self.host[0])
             self.ev = None
             if v & fail_bits:
-                self.dev.zero_()
-                raise ValueError(f"nbd Llama: an attention_mask {what} (a batch of an earlier call; the fused path "
-                                 "checks masks without synchronising) — register no hooks to keep the fused path, "
-                                 "or see models/llama.py's module docstring")
+                self._raise(what, late=True)
 
     def arm(self, fail_bits: int, what: str) -> None:
         if self.dev.device.type != "cuda":
             if int(self.dev[0]) & fail_bits:
-                self.dev.zero_()
-                raise ValueError(f"nbd Llama: attention_mask {what}")
+                self._raise(what, late=False)
             return
         if torch.cuda.is_current_stream_capturing():
+            from ..graphs import note_capture_check
+
+            note_capture_check(_CapturedMaskCheck(self, fail_bits, what))
+            return
+        if _MASK_CHECK_SYNC:
+            if int(self.dev[0]) & fail_bits:  # (a host sync: opt-in)
+                self._raise(what, late=False)
             return
         self.host.copy_(self.dev, non_blocking=True)
         self.ev = torch.cuda.Event()
         self.ev.record()
+
+
+class _CapturedMaskCheck:
+    """A mask check captured into a HIP graph: the prep kernel (and its flag update) replays with
+    the graph, so ``GraphedStep`` arms the flag's copy after each replay and polls it before the
+    next one."""
+
+    def __init__(self, chk: _MaskCheck, fail_bits: int, what: str):
+        self.chk, self.fail_bits, self.what = chk, fail_bits, what
+
+    def before_replay(self) -> None:
+        self.chk.poll(self.fail_bits, self.what)
+
+    def after_replay(self) -> None:
+        self.chk.arm(self.fail_bits, self.what)
 
 
 class LlamaModel(nn.Module):

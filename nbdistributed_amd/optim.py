@@ -249,9 +249,13 @@ _FALLBACK_KEYS = ("amsgrad", "maximize", "capturable", "differentiable")
 
 
 def _fast_adamw_ok(opt) -> bool:
-    """Every condition under which the HIP step is torch's update exactly (else torch's step
-    runs): plain hyper-parameters, no step hooks, no graph capture, contiguous fp32 GPU
-    parameters / gradients, fused-style (device, fp32) step counts in any existing state."""
+    """Every condition under which the HIP step computes torch's update (else torch's step
+    runs): plain hyper-parameters, no step hooks, no graph capture, contiguous fp32 parameters /
+    gradients all on ONE GPU (the kernel takes one device's tensor table), fused-style (device,
+    fp32) step counts in any existing state.  The update then equals torch's within rounding, not
+    bitwise: the kernel forms the bias corrections from the device step count in fp32 (powf),
+    torch's fused AdamW in double, and the fp32 operations are ordered differently — parameters
+    and moments agree to ~1e-6 relative (tests/test_gpu_swap_semantics.py)."""
     from torch.optim import optimizer as _topt
 
     if (getattr(opt, "_optimizer_step_pre_hooks", None) or getattr(opt, "_optimizer_step_post_hooks", None)
@@ -259,6 +263,7 @@ def _fast_adamw_ok(opt) -> bool:
         return False
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
         return False
+    dev = None
     for group in opt.param_groups:
         if any(group.get(k) for k in _FALLBACK_KEYS) or torch.is_tensor(group["lr"]):
             return False
@@ -271,10 +276,15 @@ def _fast_adamw_ok(opt) -> bool:
             if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and g.dtype == torch.float32
                     and not g.is_sparse and g.is_contiguous() and g.device == p.device):
                 return False
+            if dev is None:
+                dev = p.device
+            elif p.device != dev:  # a model split across GPUs: torch's step
+                return False
             st = opt.state.get(p)
             if st:
                 s_ = st.get("step")
                 if not (torch.is_tensor(s_) and s_.is_cuda and s_.dtype == torch.float32 and s_.numel() == 1
+                        and s_.device == p.device and st["exp_avg"].device == p.device
                         and st["exp_avg"].is_contiguous() and st["exp_avg_sq"].is_contiguous()):
                     return False
     return True

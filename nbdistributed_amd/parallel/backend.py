@@ -97,8 +97,11 @@ def init_data_plane(backend: str, rank: int, world_size: int, device, timeout_s:
     kw = {}
     if timeout_s:
         kw["timeout"] = datetime.timedelta(seconds=timeout_s)
-    if backend == "nccl" and device is not None and device.type == "cuda":
-        kw["device_id"] = device  # torch eagerly creates the communicator itself
+    if backend in ("nccl", "rccl") and device is not None and device.type == "cuda":
+        # bound device (both names are RCCL here): torch creates the communicator eagerly on it
+        # (ProcessGroupNCCL.eager_connect_single_device) and every later device-less call —
+        # a cell's plain dist.barrier(), new_group splits — uses it instead of guessing
+        kw["device_id"] = device
     dist.init_process_group(backend=backend, rank=rank, world_size=world_size,
                             init_method=init_method or "env://", **kw)
     if eager:

@@ -60,6 +60,9 @@ import torch.distributed as dist
 
 from .. import ops
 
+# NBD_FAULT_DDP_GRAD_SCALE (tests only): rank 0 scales each bucket by this before its collective
+_FAULT_GRAD_SCALE = float(os.environ.get("NBD_FAULT_DDP_GRAD_SCALE", "1") or "1")
+
 
 @dataclass
 class _Bucket:
@@ -366,6 +369,11 @@ class DistributedDataParallel(torch.nn.Module):
         # (forced at world 1: the average over one rank is the sum — RCCL would run AVG as a
         # separate pre-multiply pass over the bucket there, an artefact no N-GPU run has)
         op = dist.ReduceOp.AVG if avg and self.world > 1 else dist.ReduceOp.SUM
+        if _FAULT_GRAD_SCALE != 1.0 and self.rank == 0:
+            # fault injection (tests only): a broken gradient hook — rank 0 contributes a scaled
+            # bucket, so the averaged gradient is wrong by a small factor and nothing else fails
+            # (what nbdistributed_amd.checks' DDP-parity check must catch)
+            b.buffer.mul_(_FAULT_GRAD_SCALE)
         if self.shard:  # ZeRO-2: this rank keeps the averaged gradient of its slice only
             return dist.reduce_scatter_tensor(b.grad_shard, b.buffer, op=op, group=self.pg, async_op=True)
         return dist.all_reduce(b.buffer, op=op, group=self.pg, async_op=True)

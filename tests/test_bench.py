@@ -134,6 +134,27 @@ def test_bench_py_self_launch(n):
     assert d["rccl_world_size"] == {str(r): n for r in range(n)}
     assert d["allreduce_busbw_GBps"] is not None and d["allreduce_busbw_GBps"] > 0 and d["allreduce_correct"]
     assert d["allreduce_peak_busbw_GBps"] > 0 and d["launch"].startswith("self")
+    # every data-plane correctness check ran at this world size and passed
+    ck = d["checks"]
+    assert d["checks_passed"] is True and ck["passed"] and ck["world_size"] == n and not ck["failed"], ck
+    for k in ("ddp_vs_torch", "recipe_sync", "zero2", "accelerate", "rank_broadcast"):
+        assert ck["results"][k] is True, (k, ck)
+    for op in ("all_reduce", "broadcast", "all_gather", "reduce_scatter", "all_to_all", "send_recv",
+               "batch_isend_irecv"):
+        for dt in ("float32", "bfloat16"):
+            assert ck["results"][f"{op}_{dt}_1024"] is True, (op, dt, ck)
+
+
+def test_bench_py_broken_ddp_hook_fails_the_run():
+    """A deliberately broken gradient hook (rank 0 scales its buckets by 1.5 before the
+    collective: ``NBD_FAULT_DDP_GRAD_SCALE``) trains without any error — only the DDP-parity
+    check against torch DDP sees it, and the bench then exits non-zero."""
+    res, lines = _selflaunch(2, env_extra={"NBD_FAULT_DDP_GRAD_SCALE": "1.5"}, args=("--no-sweep",))
+    assert len(lines) == 1, res.stdout[-2000:] + res.stderr[-3000:]
+    d = json.loads(lines[0])
+    assert res.returncode == 5, (res.returncode, d.get("checks"))
+    assert d["checks_passed"] is False and "ddp_vs_torch" in d["checks"]["failed"]
+    assert d["checks"]["results"]["all_reduce_float32_1024"] is True  # the collectives themselves are fine
 
 
 def test_bench_py_rank_that_never_joins_is_reported():

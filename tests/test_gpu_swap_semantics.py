@@ -117,6 +117,38 @@ def test_native_mask_with_holes_raises_next_call(dev):
         m(input_ids=ids, attention_mask=torch.ones_like(mask), labels=labels)
 
 
+def test_native_mask_check_sync_raises_on_the_offending_call(dev, monkeypatch):
+    """NBD_MASK_CHECK_SYNC=1: the call that gets the bad mask raises (nothing of it applied)."""
+    from nbdistributed_amd.models import llama
+
+    monkeypatch.setattr(llama, "_MASK_CHECK_SYNC", True)
+    hf, m = _hf_and_native(dev)
+    ids, mask, labels = _batch(dev, False)
+    m(input_ids=ids, attention_mask=mask, labels=labels)  # a good mask: fine
+    mask[1, 5] = 0
+    with pytest.raises(ValueError, match="nothing of this batch was applied"):
+        m(input_ids=ids, attention_mask=mask, labels=labels)
+
+
+def test_native_mask_check_follows_graph_replays(dev):
+    """A mask check captured into a GraphedStep: a replay on a mask with holes is reported at the
+    next replay (the capture-time check alone would never see replayed batches)."""
+    from nbdistributed_amd.graphs import GraphedStep
+
+    hf, m = _hf_and_native(dev)
+    ids, mask, labels = _batch(dev, False)
+    with torch.no_grad():
+        g = GraphedStep(lambda i, k: m(input_ids=i, attention_mask=k).logits, (ids, mask), warmup=2)
+        g(ids, mask)
+        g(ids, mask)
+        holes = mask.clone()
+        holes[1, 5] = 0
+        g(ids, holes)
+        torch.cuda.synchronize()
+        with pytest.raises(ValueError, match="EARLIER call"):
+            g(ids, mask)
+
+
 def test_native_layer_hook_fires_with_hf_activations(dev):
     hf, m = _hf_and_native(dev, layers=4)
     ids, mask, labels = _batch(dev, True)

@@ -58,8 +58,15 @@ def test_pip_install_read_only_ipython():
     env = dict(os.environ)
     if not N._fresh(N.OPS_LIB, N._ops_deps(), N._ops_salt()):
         env["NBD_SKIP_OPS_BUILD"] = "1"  # (no multi-minute hipcc build inside a unit test)
+    # pip builds from a copy of the tree: setuptools writes its build/ and *.egg-info next to
+    # setup.py, and the source tree must never be written by a test (a stale build/lib beside the
+    # package is a trap).  copy2 keeps mtimes, so the in-tree native libraries stay "fresh".
+    src = tmp_path / "src"
+    shutil.copytree(ROOT, src, ignore=shutil.ignore_patterns(
+        ".git", "build", "gpurun_out", "gpurun_ab", "profiles", "benchmarks", "docs", "tests", "examples",
+        "*.egg-info", "__pycache__", ".pytest_cache", ".hypothesis", "*.json", "*.log"))
     p = subprocess.run([sys.executable, "-m", "pip", "install", "--no-build-isolation", "--no-deps", "--target",
-                        str(target), ROOT], capture_output=True, text=True, timeout=600, env=env)
+                        str(target), str(src)], capture_output=True, text=True, timeout=600, env=env, cwd=str(tmp_path))
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     pkg = target / "nbdistributed_amd"
     assert (pkg / "_native" / "libnbd_transport.so").exists()
