@@ -869,17 +869,76 @@ static Tile pick_tile(int M, int N, int64_t tile_hint) {
   return cands[best];
 }
 
+// Column split (tile hint >= kColSplit: hint - kColSplit = the tail's tile): the product's first
+// N0 columns — as many as make WHOLE rounds of 256x256 tiles, one workgroup per CU — run on the
+// 8-phase 256x256 kernel (gemm256.hip), the remaining N - N0 columns on the tail tile, as a second
+// launch writing the same C (row stride N).  GPT-2 small's q|k|v (N = 2304 = 2048 + 256) and c_fc
+// (N = 3072 = 2048 + 1024) forwards at 8192 tokens: 1.125 / 1.5 rounds of 256x256 tiles as one
+// kernel, 2.25 / 3 rounds of 128x128 at two per CU (benchmarks/gemm_colsplit.py).  N0 = 0 when M
+// is not a multiple of 256 or no whole round fits: the tail tile then runs the whole product.
+constexpr int64_t kColSplit = 1000000000;
+constexpr int kCUs = 256;
+
+static int colsplit_head(int M, int N) {
+  if (M % 256 != 0) return 0;
+  const int64_t tm = M / 256;
+  // columns per round of kCUs tiles; whole rounds only
+  if ((int64_t)kCUs % tm != 0) return 0;
+  const int per_round = (int)(kCUs / tm) * 256;
+  return N / per_round * per_round;
+}
+
+void gemm_hip_one(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_km, bool b_kn,
+                  const c10::optional<at::Tensor>& bias, int64_t epi, const c10::optional<at::Tensor>& aux_in,
+                  const c10::optional<at::Tensor>& aux_out, int64_t splits, int64_t tile_hint, int64_t accum);
+
 // c = A·B with the layouts above; c is [M][N] bf16 (contiguous).
 void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_km, bool b_kn,
               const c10::optional<at::Tensor>& bias, int64_t epi, const c10::optional<at::Tensor>& aux_in,
               const c10::optional<at::Tensor>& aux_out, int64_t splits, int64_t tile_hint, int64_t accum) {
+  if (tile_hint >= kColSplit) {
+    const int64_t tail = tile_hint - kColSplit;
+    const int M = a_km ? a.size(1) : a.size(0);
+    const int N = b_kn ? b.size(1) : b.size(0);
+    const int N0 = (!a_km && (epi == EPI_NONE || epi == EPI_GELU || epi == EPI_DGELU) && splits <= 1 && accum == 0)
+                       ? colsplit_head(M, N) : 0;
+    if (N0 == 0 || N0 == N) {
+      gemm_hip_one(a, b, c, a_km, b_kn, bias, epi, aux_in, aux_out, splits, N0 == N ? 86256256 : tail, accum);
+      return;
+    }
+    // column blocks of B (rows of W [N][K], or columns of W as [K][N]), of C / the aux tensors
+    // (row stride N) and of the bias
+    auto cols = [&](const at::Tensor& t, int64_t lo, int64_t n) { return t.narrow(1, lo, n); };
+    const at::Tensor b0 = b_kn ? cols(b, 0, N0) : b.narrow(0, 0, N0);
+    const at::Tensor b1 = b_kn ? cols(b, N0, N - N0) : b.narrow(0, N0, N - N0);
+    auto part = [&](const c10::optional<at::Tensor>& t, int64_t lo, int64_t n) -> c10::optional<at::Tensor> {
+      if (!t) return c10::nullopt;
+      return t->dim() == 1 ? t->narrow(0, lo, n) : cols(*t, lo, n);
+    };
+    gemm_hip_one(a, b0, cols(c, 0, N0), false, b_kn, part(bias, 0, N0), epi, part(aux_in, 0, N0),
+                 part(aux_out, 0, N0), 1, 86256256, 0);
+    gemm_hip_one(a, b1, cols(c, N0, N - N0), false, b_kn, part(bias, N0, N - N0), epi, part(aux_in, N0, N - N0),
+                 part(aux_out, N0, N - N0), 1, tail, 0);
+    return;
+  }
+  gemm_hip_one(a, b, c, a_km, b_kn, bias, epi, aux_in, aux_out, splits, tile_hint, accum);
+}
+
+// one launch (plus its split-K reduce).  C (and the aux tensors, which share its layout) may be a
+// column block of a wider row-major matrix (unit inner stride, row stride >= N: the column split
+// above) when there is no split-K; B [N][K] a row block, B as [K][N] a column block.
+void gemm_hip_one(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_km, bool b_kn,
+                  const c10::optional<at::Tensor>& bias, int64_t epi, const c10::optional<at::Tensor>& aux_in,
+                  const c10::optional<at::Tensor>& aux_out, int64_t splits, int64_t tile_hint, int64_t accum) {
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "nbd::gemm: 2-D operands");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kBFloat16,
               "nbd::gemm: bf16 operands");
   // A may be a row-strided view (unit inner stride, row stride >= its width: a column block of a
   // wider matrix, e.g. the LM head's weight gradient split by vocabulary rows); B and C contiguous
-  TORCH_CHECK(a.stride(1) == 1 && a.stride(0) >= a.size(1) && b.is_contiguous() && c.is_contiguous(),
-              "nbd::gemm: contiguous operands (A: unit inner stride)");
+  TORCH_CHECK(a.stride(1) == 1 && a.stride(0) >= a.size(1) && b.stride(1) == 1 && b.stride(0) >= b.size(1) &&
+                  c.stride(1) == 1 && c.stride(0) >= c.size(1),
+              "nbd::gemm: operands need a unit inner stride (row-strided blocks of wider matrices allowed)");
+  const bool c_dense = c.is_contiguous();
   const int M = a_km ? a.size(1) : a.size(0);
   const int K = a_km ? a.size(0) : a.size(1);
   const int N = b_kn ? b.size(1) : b.size(0);
@@ -896,12 +955,15 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
     TORCH_CHECK(bias->is_contiguous() && bias->numel() == N && bias->scalar_type() == at::kBFloat16, "nbd::gemm: bias");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0, "nbd::gemm: bias alignment");
   }
+  // (the GELU / GELU′ operands are indexed with C's row stride)
   if (epi == EPI_GELU)
-    TORCH_CHECK(aux_out && aux_out->sizes() == c.sizes() && aux_out->is_contiguous() &&
+    TORCH_CHECK(aux_out && aux_out->sizes() == c.sizes() && aux_out->strides() == c.strides() &&
                     aux_out->scalar_type() == at::kBFloat16, "nbd::gemm: aux_out");
   if (epi == EPI_DGELU)
-    TORCH_CHECK(aux_in && aux_in->sizes() == c.sizes() && aux_in->is_contiguous() &&
+    TORCH_CHECK(aux_in && aux_in->sizes() == c.sizes() && aux_in->strides() == c.strides() &&
                     aux_in->scalar_type() == at::kBFloat16, "nbd::gemm: aux_in");
+  TORCH_CHECK(c_dense || (epi == EPI_NONE || epi == EPI_GELU || epi == EPI_DGELU),
+              "nbd::gemm: a row-strided C only with the plain / GELU / GELU' epilogues");
   if (epi == EPI_ROWSUM)
     TORCH_CHECK(aux_out && aux_out->numel() == M && aux_out->is_contiguous() &&
                     aux_out->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(aux_out->data_ptr()) % 16 == 0,
@@ -925,7 +987,7 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   // per-lane DMA offsets are 32-bit byte offsets within one tile's rows (gemm_common.h Pieces)
   {
     const int64_t ra = a_km ? BK : t.bm, rb = b_kn ? BK : (epi == EPI_SWIGLU ? N / 2 + t.bn : t.bn);
-    TORCH_CHECK(ra * a.stride(0) * 2 < (1LL << 32) && rb * b.size(1) * 2 < (1LL << 32),
+    TORCH_CHECK(ra * a.stride(0) * 2 < (1LL << 32) && rb * b.stride(0) * 2 < (1LL << 32),
                 "nbd::gemm: row stride too large for 32-bit DMA offsets");
   }
   const int tiles = (M / t.bm) * (N / t.bn);
@@ -933,6 +995,8 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   TORCH_CHECK(K % (BK * S * t.ks) == 0, "nbd::gemm: K not divisible into ", S, " splits x ", t.ks, " K-groups");
   TORCH_CHECK(S == 1 || ((epi == EPI_NONE || epi == EPI_ROWSUM) && !bias),
               "nbd::gemm: split-K only without an elementwise epilogue");
+  TORCH_CHECK(S == 1 || c_dense, "nbd::gemm: split-K writes a contiguous C");
+  TORCH_CHECK(c.stride(0) < (1LL << 31) && b.stride(0) < (1LL << 31), "nbd::gemm: row stride too large");
 
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
@@ -946,8 +1010,8 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
   p.N = N;
   p.K = K / S;
   p.lda = a.stride(0);
-  p.ldb = b.size(1);
-  p.ldc = cN;
+  p.ldb = b.stride(0);
+  p.ldc = c.stride(0);  // = cN when C is contiguous
   p.tiles_m = M / t.bm;
   p.tiles_n = N / t.bn;
   p.accum = (int)accum;

@@ -101,20 +101,23 @@ def _nbd_wrap(m, impl, **kw):
         return _NbdDDP(m, **kw)
     return _TorchDDP(m, device_ids=[device.index] if device.type == "cuda" else None, bucket_cap_mb=25)
 
-def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small", force=False, lmhead_lib=False):
+def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small", force=False, lmhead_lib=False, lmhead_hip=False):
     # force: the multi-rank DDP code path even at world size 1 (real collectives per bucket)
-    # lmhead_lib: the LM head's three GEMMs on hipBLASLt (NBD_LMHEAD_HIP=0) instead of the
-    # hand-written 256x256 kernel, the table padded to a multiple of 128 as the library wants
+    # lmhead_lib: the LM head's three GEMMs on hipBLASLt (NBD_LMHEAD_HIP=0), the table padded to a
+    # multiple of 128 as the library wants; lmhead_hip: all three on the hand-written kernels
+    # (NBD_LMHEAD_HIP=1); neither: the default per-product plan (ops.loss.HEAD_PRODUCTS)
     if impl == "flatgraph" and device.type != "cuda":
         impl = "flat"   # HIP graphs need a GPU
     import nbdistributed_amd.ops.loss as _lm
-    prev_hip = _lm.LM_HEAD_HIP
+    prev_hip, prev_products = _lm.LM_HEAD_HIP, _lm.HEAD_PRODUCTS
     if lmhead_lib:
         _lm.LM_HEAD_HIP = False
+    if lmhead_hip:
+        _lm.LM_HEAD_HIP, _lm.HEAD_PRODUCTS = True, {"fwd": True, "dgrad": True, "wgrad": True}
     try:
         return _nbd_gpt2_bench_body(steps, warm, B, T, impl, config, force, 128 if lmhead_lib else 0)
     finally:
-        _lm.LM_HEAD_HIP = prev_hip
+        _lm.LM_HEAD_HIP, _lm.HEAD_PRODUCTS = prev_hip, prev_products
 
 def _nbd_gpt2_bench_body(steps, warm, B, T, impl, config, force, vocab_pad):
     # vocab_pad: the table's padding multiple (0: GPT2Config's default)
@@ -350,24 +353,31 @@ def bench_ddp_graph(session, out: Dict[str, Any], steps: int = 20, warmup: int =
         # N = 2 rehearsal): a second capture in the same workers would only fail the same way
         out["graph_lmhead_lib_error"] = "skipped: the graph arm failed"
     elif bool(session.ready.get(0, {}).get("cuda_available")):
-        # the same graphed step with the LM head's three GEMMs on hipBLASLt (the only library
-        # GEMMs the step could use) for comparison
-        try:
-            _arm_start(out, "graph_lmhead_lib")
-            r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flatgraph', {config!r}, "
-                                f"lmhead_lib=True)", render=False)
-            hms = _max_over_ranks(r)
-            out.update(graph_lmhead_lib_ms_per_step=hms,
-                       graph_lmhead_lib_recipe="as graph, the LM head's forward / input- / weight-gradient GEMMs on "
-                                               "hipBLASLt (NBD_LMHEAD_HIP=0) instead of the hand-written 256x256 "
-                                               "HIP kernel")
-            rd = _replay_detail(r)
-            if rd:
-                out["graph_lmhead_lib_replays"] = rd
-        except Exception as e:  # noqa: BLE001
-            _record_error(out, "graph_lmhead_lib_error", e)
-            if isinstance(e, TimeoutError):
-                raise
+        # the same graphed step with the LM head's three GEMMs all on hipBLASLt, and all on the
+        # hand-written kernels, for comparison with the default per-product plan
+        # (ops.loss.HEAD_PRODUCTS: input gradient hand-written, forward / weight gradient library)
+        out["graph_lmhead_plan"] = "per-product (ops.loss.HEAD_PRODUCTS): " + session.execute(
+            "import nbdistributed_amd.ops.loss as _lm2; str(_lm2.HEAD_PRODUCTS if _lm2.LM_HEAD_HIP else 'library')",
+            render=False).results[0].get("echo", "")
+        for key, kw, recipe in (("graph_lmhead_lib", "lmhead_lib=True",
+                                 "as graph, the LM head's forward / input- / weight-gradient GEMMs all on hipBLASLt "
+                                 "(NBD_LMHEAD_HIP=0)"),
+                                ("graph_lmhead_hip", "lmhead_hip=True",
+                                 "as graph, the LM head's three GEMMs all on the hand-written 256x256 kernel "
+                                 "(NBD_LMHEAD_HIP=1: no library GEMM in the step)")):
+            try:
+                _arm_start(out, key)
+                r = session.execute(f"_nbd_gpt2_bench({steps}, {warmup}, {B}, {T}, 'flatgraph', {config!r}, {kw})",
+                                    render=False)
+                out[key + "_ms_per_step"] = _max_over_ranks(r)
+                out[key + "_recipe"] = recipe
+                rd = _replay_detail(r)
+                if rd:
+                    out[key + "_replays"] = rd
+            except Exception as e:  # noqa: BLE001
+                _record_error(out, key + "_error", e)
+                if isinstance(e, TimeoutError):
+                    raise
 
 
 def _log(msg: str) -> None:
@@ -862,17 +872,6 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
         out: Dict[str, Any] = {"cell": cells}
         ckpt(out)
         _phase(session, out, "world", lambda: bench_world(session), phase_timeout_s, deadline)
-        if checks:
-            # correctness of the data plane at this world size (nbdistributed_amd.checks): every
-            # collective against closed-form values, nbd DDP against torch DDP, the recipe's
-            # cross-rank sync, ZeRO-2, the graphed step, accelerate, %%rank + broadcast
-            _log(f"phase 1a: data-plane correctness checks on {n} rank(s)")
-            from .checks import run_checks
-
-            _phase(session, out, "checks", lambda: run_checks(session, log=_log), phase_timeout_s, deadline, 20.0)
-            ck = out["checks"]
-            _log("checks: " + ("all passed" if ck.get("passed") else f"FAILED {ck.get('failed') or ck.get('error')}"))
-            ckpt(out)
         _log(f"phase 1b: {warmup}+{steps} trivial cells through the magic path (auto mode, ide_sync, renderer)")
         _phase(session, out, "cell_magic", lambda: bench_cells_magic(session, steps, warmup), phase_timeout_s, deadline)
         if "p50_ms" in out["cell_magic"]:
@@ -954,6 +953,19 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
                        lambda: bench_notebook_graph(session, out["notebook"], steps=ddp_steps, tick=lambda: ckpt(out))
                        and None, phase_timeout_s, deadline, 60.0)
                 ckpt(out)
+        if checks:
+            # correctness of the data plane at this world size (nbdistributed_amd.checks): every
+            # collective against closed-form values, nbd DDP against torch DDP, the recipe's
+            # cross-rank sync, ZeRO-2, the graphed step, accelerate, %%rank + broadcast.  Last:
+            # a check that hangs (aborting the phase) must not cost the measured numbers.
+            _log(f"phase 7: data-plane correctness checks on {n} rank(s)")
+            from .checks import run_checks
+
+            _phase(session, out, "checks", lambda: run_checks(session, log=_log), phase_timeout_s, deadline, 30.0)
+            ck = out["checks"]
+            _log("checks: " + ("all passed" if ck.get("passed") else
+                               f"NOT PASSED {ck.get('failed') or ck.get('error') or ck.get('skipped')}"))
+            ckpt(out)
         return out
     finally:
         session.deadline = prev_deadline
@@ -1036,9 +1048,12 @@ def result_line(res: Dict[str, Any], n: int, steps: int, warmup: int) -> Dict[st
         if "passed" in ck:
             line["checks_passed"] = bool(ck["passed"])
             line["checks"] = ck
-        else:  # the phase itself failed or was skipped: not a pass
+        elif "skipped" in ck:  # not run (bench deadline / an earlier phase aborted): no verdict
+            line["checks_passed"] = None
+            line["checks"] = {"passed": None, "skipped": ck["skipped"]}
+        else:  # the phase itself failed (raised or timed out): not a pass
             line["checks_passed"] = False
-            line["checks"] = {"passed": False, "error": ck.get("error") or ck.get("skipped")}
+            line["checks"] = {"passed": False, "error": ck.get("error")}
     wd = res.get("world") or {}
     if "per_rank" in wd:
         line["rccl_world_size"] = {str(r): v["world_size"] for r, v in wd["per_rank"].items()}

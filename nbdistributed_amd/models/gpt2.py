@@ -7,10 +7,12 @@ GEMMs (``ops.gemm_linear`` / ``ops.mlp_gelu``: csrc/kernels/gemm.hip, fused bias
 epilogues, grouped dgrad + wgrad backward writing into the DDP buckets), attention on the HIP
 flash kernels (``ops.attention_qkv``, csrc/kernels/attn.hip), add + LayerNorm on norm.hip and the
 loss on the fused HIP cross-entropy (``ops.linear_cross_entropy``, no fp32 copy of the
-8192 x 50257 logits).  The tied LM-head products (8192 x 50688 x 768, three per step) run on the
-hand-written 256x256 kernel (gemm256.hip; the table padded to a multiple of 512 for it) — within
-0.7-1.2 % of hipBLASLt on the step (docs/FINDINGS.md §33; ``NBD_LMHEAD_HIP=0`` runs them on the
-library with a 128-padded table).  CPU / fp32: the same model in plain PyTorch.
+8192 x 50257 logits).  The tied LM-head products (8192 x 50688 x 768, three per step) each run on
+whichever kernel measured faster for that product (``ops.loss.HEAD_PRODUCTS``): the input gradient
+on the hand-written 256x256 kernel (gemm256.hip, split 8 ways; the table padded to a multiple of
+512 for it), the forward and weight gradient on hipBLASLt (docs/FINDINGS.md §35;
+``NBD_LMHEAD_HIP=1`` all three hand-written, ``=0`` all three on the library with a 128-padded
+table).  CPU / fp32: the same model in plain PyTorch.
 Random init (no checkpoints: no network), GPT-2 initialisation scheme.
 """
 from __future__ import annotations
@@ -47,7 +49,7 @@ class GPT2Config:
     # vocabulary and an input gradient split 8 ways into whole K-tiles (ops/loss.py _hip_dgrad).
     # NBD_GPT2_VOCAB_PAD overrides (A/B measurements).
     vocab_pad: int = (int(os.environ.get("NBD_GPT2_VOCAB_PAD", "0"))
-                      or (128 if os.environ.get("NBD_LMHEAD_HIP", "1") == "0" else 512))
+                      or (128 if os.environ.get("NBD_LMHEAD_HIP", "auto") == "0" else 512))
 
     @property
     def padded_vocab(self) -> int:

@@ -583,7 +583,13 @@ class LlamaForSequenceClassification(_LlamaPreTrained):
         # gather (backward = scatter-add: no sort, graph-safe) instead of advanced indexing
         pooled = torch.gather(h, 1, last.view(B, 1, 1).expand(B, 1, C)).squeeze(1)
         w = self.score.weight
-        logits = self.score(pooled) if w.dtype == pooled.dtype else F.linear(pooled, w.to(pooled.dtype))
+        if (pooled.is_cuda and self.score.bias is None and not self.score._forward_hooks
+                and not self.score._forward_pre_hooks and ops.tiny.shape_ok(pooled, w.shape[0], w.shape[1])):
+            # the classifier head (N = num_labels) on the tiny-linear HIP kernels: one launch
+            # forward, one backward (dx, dW together) instead of three library GEMMs
+            logits = ops.linear_tiny(pooled, w if w.dtype == pooled.dtype else w.to(pooled.dtype))
+        else:
+            logits = self.score(pooled) if w.dtype == pooled.dtype else F.linear(pooled, w.to(pooled.dtype))
         loss = None
         if labels is not None:
             loss = F.cross_entropy(logits.float(), labels.view(-1))

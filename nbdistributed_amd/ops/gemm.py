@@ -157,7 +157,9 @@ def gemm_ok(M: int, N: int, K: int) -> bool:
 # benchmarks/gemm_bench.py --sweep
 # (profiles/gemm_bench_r1.txt; split-K only where it beats the best unsplit kernel by > 5 %).
 _TUNED = {
-    (False, False, 8192, 2304, 768): (82128128, 1),  # gpt2.c_attn fwd 44.5 us
+    # gpt2.c_attn fwd: columns 0..2047 on the 256x256 8-phase kernel (one round), 2048..2303 on
+    # 128x128 — 41.1-41.3 us vs 44.7 for 128x128 alone, hipBLASLt 40.0 (profiles/gemm_colsplit_r6.txt)
+    (False, False, 8192, 2304, 768): (1082128128, 1),
     (False, True, 8192, 768, 2304): (82128128, 1),  # gpt2.c_attn dgrad 42.3 us
     (True, True, 2304, 768, 8192): (203128064, 1),  # gpt2.c_attn wgrad 49.7 us (K-split groups)
     (False, False, 8192, 768, 768): (2128096, 1),  # gpt2.attn.c_proj fwd 14.8 us (128x128/8 waves 16.5: 512 tiles = one round)
@@ -186,6 +188,13 @@ _TUNED = {
     (True, True, 576, 1536, 2048): (203064064, 1),  # smollm2.down wgrad 13.7 us (15.6)
 }
 
+# epilogue-specific entries, checked first: (a_km, b_kn, M, N, K, epi)
+_TUNED_EPI = {
+    # gpt2.c_fc fwd + GELU: column split as c_attn (2048 + 1024 columns): 53.4 vs 57.2 us, hipBLASLt +
+    # a GELU pass 71.9 (profiles/gemm_colsplit_r6.txt); the plain product keeps 128x128 (43.5 vs 45.0)
+    (False, False, 8192, 3072, 768, EPI_GELU): (1082128128, 1),
+}
+
 _TILES = (128128, 128064, 64128, 64064)  # (+ 128096: forward only, tuned entries)
 
 
@@ -200,6 +209,9 @@ def _ntiles(tile: int, M: int, N: int) -> int:
 # (Llama-1B q|k|v, 384 tiles) lose: docs/FINDINGS.md §10); its epilogues: none / bias / GELU
 G256 = 86256256
 G256_EPIS = (EPI_NONE, EPI_GELU)
+# column split (gemm.hip kColSplit): COLSPLIT + tail tile runs the columns that make whole rounds
+# of 256x256 tiles on the 8-phase kernel and the rest on the tail tile (two launches, one C)
+COLSPLIT = 1000000000
 # Plain products at least this large (FLOPs) with no tuned entry go to hipBLASLt: it measured
 # 1.16-1.61 PF on them, 15-30 % ahead of both hand-written families (profiles/gemm256_bench_r2.txt);
 # the hand-written kernels keep the fused epilogues and the workload shapes they win on.
@@ -217,7 +229,7 @@ def config(a_km: bool, b_kn: bool, M: int, N: int, K: int, can_split: bool = Tru
     < 512 workgroups (one per CU cannot hide a drained pipeline); long-K products with < 400
     workgroups split K (the largest tile needing <= 8 splits, each >= 512 deep) — split-K (a
     second, reducing kernel) only without an epilogue."""
-    hit = _TUNED.get((a_km, b_kn, M, N, K))
+    hit = _TUNED_EPI.get((a_km, b_kn, M, N, K, epi)) or _TUNED.get((a_km, b_kn, M, N, K))
     if hit is not None and (can_split or hit[1] == 1):
         return hit if KSPLIT else (hit[0] % 100000000, hit[1])
     t256 = (M // 256) * (N // 256)
@@ -603,8 +615,13 @@ def linear_any(x, weight, bias=None):
 
     if _fast(x, weight) and _native(bias):
         return gemm_linear(x, weight, bias)
-    # (bf16 shapes the HIP GEMMs cannot tile stay on F.linear: the node's bias-gradient row sums
-    # need the HIP kernel)
+    # bf16 heads with a tiny output dimension (classifiers: N <= 64): the tiny-linear kernels
+    from .tiny import linear_tiny, supported as _tiny_ok
+
+    if _tiny_ok(x, weight, bias):
+        return linear_tiny(x, weight, bias)
+    # (other bf16 shapes the HIP GEMMs cannot tile stay on F.linear: the node's bias-gradient row
+    # sums need the HIP kernel)
     if (x.is_cuda and x.dtype == weight.dtype and x.dtype in (torch.float32, torch.float16)
             and (bias is None or bias.dtype == weight.dtype) and NATIVE_AUTOGRAD):
         _require()

@@ -78,11 +78,11 @@ def _xent_fn():
             N = h2.shape[0]
             chunk = LM_HEAD_CHUNK if 0 < LM_HEAD_CHUNK < N else N
             dh = None
-            hip = _hip_ok(h2, wp)
-            if hip:
+            plan = head_plan(h2, wp)
+            if any(plan.values()):
                 chunk = N  # (row chunks are a hipBLASLt experiment)
             if chunk == N:
-                logits_p = _hip_logits(h2, wp) if hip else torch.mm(h2, wp.t())
+                logits_p = _hip_logits(h2, wp) if plan["fwd"] else torch.mm(h2, wp.t())
                 loss_rows, _ = torch.ops.nbd.xent_fused(logits_p[:, :V] if Vp != V else logits_p, target,
                                                         ignore_index, scale)
             else:
@@ -104,7 +104,7 @@ def _xent_fn():
                         torch.mm(lc, wp, out=dh[r0:r1])
             # logits now hold d(loss)/d(logits) for grad_out = 1 (and dh = dlogits·W, if fused)
             ctx.save_for_backward(h2, wp, logits_p, w, dh)
-            ctx.hip = hip
+            ctx.plan = plan
             ctx.rows = w.shape[0]
             ctx.copied = wp is not w
             return loss_rows.sum() * scale[0]
@@ -120,13 +120,13 @@ def _xent_fn():
                 if dh_fused is not None:
                     dh = dh_fused.mul_(g)
                 else:
-                    dh = (_hip_dgrad(dlogits, wp) if ctx.hip else torch.mm(dlogits, wp)).mul_(g)
+                    dh = (_hip_dgrad(dlogits, wp) if ctx.plan["dgrad"] else torch.mm(dlogits, wp)).mul_(g)
             dw = None
             if ctx.needs_input_grad[1]:
                 hg = h2 * g
                 dst, acc = graddst.claim(w) if not ctx.copied else (None, False)
                 if dst is not None:  # straight into the DDP bucket slice (graddst.py)
-                    if ctx.hip:
+                    if ctx.plan["wgrad"]:
                         _hip_wgrad(dlogits, hg, out=dst, accum=acc)
                     elif acc:
                         dst.addmm_(dlogits.t(), hg)
@@ -134,7 +134,7 @@ def _xent_fn():
                         torch.mm(dlogits.t(), hg, out=dst)
                     dw = graddst.hand_back(w, dst, acc)
                 else:
-                    dw = (_hip_wgrad(dlogits, hg) if ctx.hip else torch.mm(dlogits.t(), hg))[:ctx.rows]
+                    dw = (_hip_wgrad(dlogits, hg) if ctx.plan["wgrad"] else torch.mm(dlogits.t(), hg))[:ctx.rows]
             return dh, dw, None, None, None, None, None
 
     _XentFn = (_FusedCrossEntropy, _LinearCrossEntropy)
@@ -180,7 +180,22 @@ LM_HEAD_CHUNK = int(os.environ.get("NBD_LMHEAD_CHUNK", "0"))
 # the weight gradient is accumulated straight into a DDP bucket slice when one is claimed.  On the
 # GPT-2 small step within 0.7-1.2 % of the library head (docs/FINDINGS.md §33), with no library
 # GEMM left in the step.
-LM_HEAD_HIP = os.environ.get("NBD_LMHEAD_HIP", "1") != "0"
+LM_HEAD_HIP = os.environ.get("NBD_LMHEAD_HIP", "auto") != "0"
+# Which of the three products run hand-written when LM_HEAD_HIP is on.  NBD_LMHEAD_HIP=1: all
+# three; "auto" (default): the measured faster kernel per product on the GPT-2 small head (8192 x
+# 50688 x 768, back-to-back on one MI355X: profiles/lmhead_products_r6.txt) — the input gradient
+# on gemm256 split 8 ways (515 vs 576 µs for hipBLASLt), the forward (600 vs 568) and the weight
+# gradient (565 vs 505) on hipBLASLt, whose persistent kernels fit these shapes' tile
+# quantisation better (2.3 rounds of 256x256 tiles for the weight gradient); or a list such as
+# "fwd,dgrad".  The bench line carries the graphed step with every product on each side.
+_HEAD_SPEC = os.environ.get("NBD_LMHEAD_HIP", "auto")
+HEAD_PRODUCTS = ({"fwd": False, "dgrad": True, "wgrad": False} if _HEAD_SPEC == "auto" else
+                 {p: _HEAD_SPEC not in ("0",) and (_HEAD_SPEC == "1" or p in _HEAD_SPEC.split(","))
+                  for p in ("fwd", "dgrad", "wgrad")})
+
+
+def _use_hip(product: str) -> bool:
+    return LM_HEAD_HIP and HEAD_PRODUCTS.get(product, False)
 # the 256x256 kernel (for the forward with non-temporal C stores, variant 6: the 823 MB of GPT-2
 # logits outgrow every cache on their way out — 660 -> 611 us isolated; the weight gradient, a
 # 77 MB output, measured 643 vs 651 us with them: plain stores), the 128x128 8-wave kernel
@@ -193,6 +208,12 @@ def _hip_ok(h2, wp) -> bool:
     N, C = h2.shape
     return (LM_HEAD_HIP and h2.is_cuda and h2.dtype == torch.bfloat16 and wp.dtype == torch.bfloat16
             and N % 128 == 0 and wp.shape[0] % 128 == 0 and C % 128 == 0)
+
+
+def head_plan(h2, wp) -> dict:
+    """{fwd, dgrad, wgrad}: True where that product of the head runs hand-written."""
+    ok = _hip_ok(h2, wp)
+    return {p: ok and _use_hip(p) for p in ("fwd", "dgrad", "wgrad")}
 
 
 def _big(*dims) -> bool:

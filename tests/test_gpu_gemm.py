@@ -394,3 +394,36 @@ def test_gemm_next_weight_warm_up(monkeypatch):
     assert torch.equal(G.matmul(x, w2, splits=1), ref[1])
     torch.cuda.synchronize()
 
+
+
+# column split (gemm.hip kColSplit): the columns that make whole rounds of 256x256 tiles on the
+# 8-phase kernel, the rest on the tail tile, both writing one C; M = 8192 -> 2048 columns a round
+@pytest.mark.parametrize("N,tail", [(2304, 82128128), (3072, 82128128), (3072, 2128128), (2048, 82128128),
+                                    (768, 82128128)])
+@pytest.mark.parametrize("epi", [G.EPI_NONE, G.EPI_GELU])
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemm_column_split(N, tail, epi, bias):
+    M, K = 8192, 256
+    a, b = _operands(M, N, K, False, False, seed=N + epi)
+    bb = (torch.randn(N, device="cuda") * 0.5).to(torch.bfloat16) if bias else None
+    ref = _ref(a, b, False, False) + (bb.float() if bias else 0.0)
+    out = G.matmul(a, b, bias=bb, epi=epi, tile=G.COLSPLIT + tail, splits=1)
+    if epi == G.EPI_GELU:
+        g, pre = out
+        assert _err(pre, ref) < 1e-2
+        assert _err(g, torch.nn.functional.gelu(ref, approximate="tanh")) < 1e-2
+    else:
+        assert _err(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("N", [2304, 3072])
+def test_gemm_column_split_dgrad_layout(N):
+    """The split on the input-gradient layout (B as [K][N]: column blocks), with GELU'."""
+    M, K = 8192, 256
+    a, b = _operands(M, N, K, False, True, seed=N)
+    ref = _ref(a, b, False, True)
+    assert _err(G.matmul(a, b, b_kn=True, tile=G.COLSPLIT + 82128128, splits=1), ref) < 1e-2
+    pre = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    want = G._dgelu_ref(ref.to(torch.bfloat16), pre).float()
+    got = G.matmul(a, b, b_kn=True, epi=G.EPI_DGELU, aux=pre, tile=G.COLSPLIT + 82128128, splits=1)
+    assert _err(got, want) < 2e-2

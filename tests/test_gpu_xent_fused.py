@@ -102,6 +102,7 @@ def test_linear_cross_entropy_hand_written_products(dev, reduction, V, C, N, mon
     from nbdistributed_amd.ops import loss as L
 
     monkeypatch.setattr(L, "LM_HEAD_HIP", True)
+    monkeypatch.setattr(L, "HEAD_PRODUCTS", {"fwd": True, "dgrad": True, "wgrad": True})
     torch.manual_seed(3)
     h = (torch.randn(N, C, device=dev) * 0.5).to(torch.bfloat16).requires_grad_()
     w = (torch.randn(V, C, device=dev) * 0.05).to(torch.bfloat16).requires_grad_()
@@ -118,10 +119,11 @@ def test_linear_cross_entropy_hand_written_products(dev, reduction, V, C, N, mon
 
 
 def test_hand_written_head_runs_no_library_gemm(dev, monkeypatch):
-    """With NBD_LMHEAD_HIP the head issues only nbd kernels: torch.mm is never called."""
+    """With NBD_LMHEAD_HIP=1 the head issues only nbd kernels: torch.mm is never called."""
     from nbdistributed_amd.ops import loss as L
 
     monkeypatch.setattr(L, "LM_HEAD_HIP", True)
+    monkeypatch.setattr(L, "HEAD_PRODUCTS", {"fwd": True, "dgrad": True, "wgrad": True})
     calls = []
     real_mm = torch.mm
 
@@ -137,3 +139,29 @@ def test_hand_written_head_runs_no_library_gemm(dev, monkeypatch):
     torch.cuda.synchronize()
     assert calls == []
     assert h.grad is not None and w.grad is not None
+
+
+@pytest.mark.parametrize("products", [{"fwd": False, "dgrad": True, "wgrad": False},
+                                      {"fwd": True, "dgrad": False, "wgrad": True}])
+def test_linear_cross_entropy_mixed_products(dev, products, monkeypatch):
+    """The head's products chosen one by one (the default "auto" plan: the input gradient
+    hand-written, forward and weight gradient on the library) give the same loss / gradients as
+    fp32 torch, and the library is called for exactly the library products."""
+    from nbdistributed_amd.ops import loss as L
+
+    monkeypatch.setattr(L, "LM_HEAD_HIP", True)
+    monkeypatch.setattr(L, "HEAD_PRODUCTS", products)
+    calls = []
+    real_mm = torch.mm
+    monkeypatch.setattr(torch, "mm", lambda *a, **k: calls.append(1) or real_mm(*a, **k))
+    torch.manual_seed(5)
+    V, C, N = 50257, 768, 512
+    h = (torch.randn(N, C, device=dev) * 0.5).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(V, C, device=dev) * 0.05).to(torch.bfloat16).requires_grad_()
+    tgt = torch.randint(0, V, (N,), device=dev)
+    loss = ops.linear_cross_entropy(h, w, tgt)
+    loss.backward()
+    hr, wr = h.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    F.cross_entropy(F.linear(hr, wr), tgt).backward()
+    assert _rel(h.grad, hr.grad) < 3e-2 and _rel(w.grad, wr.grad) < 3e-2
+    assert len(calls) == sum(not v for v in products.values())
