@@ -14,6 +14,7 @@
 #   bench [ARGS...]         python bench.py ARGS            -> gpurun_out/TAG_bench.json / .log
 #   py SCRIPT [ARGS...]     python SCRIPT ARGS              -> gpurun_out/TAG_<script>.txt
 #   prof SCRIPT [ARGS...]   rocprofv3 --kernel-trace --stats around SCRIPT -> gpurun_out/TAG_prof/
+#   sh SCRIPT [ARGS...]     bash SCRIPT ARGS (e.g. benchmarks/prof_gpt2_graph.sh: profile + summary)
 #   ab VAR V1,V2 ROUNDS SCRIPT [ARGS...]
 #                           interleaved A/B: ROUNDS x (VAR=V1, VAR=V2, ...) python SCRIPT ARGS
 #                           -> gpurun_out/TAG_ab_<VAR>.txt (cdna_hip_programming.md §5.4 rule 24)
@@ -50,6 +51,9 @@ run_step() {
       base=$(basename "$1" .py)
       timeout -k 10 "$STEP_S" rocprofv3 --kernel-trace --stats -d "gpurun_out/${TAG}_prof" -o "$base" \
         -- python3 -u "$@" > "gpurun_out/${TAG}_prof_${base}.txt" 2>&1 ;;
+    sh)
+      base=$(basename "$1" .sh)
+      timeout -k 10 "$STEP_S" bash "$@" > "gpurun_out/${TAG}_${base}.txt" 2>&1 ;;
     ab)
       local var=$1 vals=$2 rounds=$3
       shift 3

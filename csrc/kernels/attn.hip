@@ -243,22 +243,36 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
     // one tile; DIAG = the causal mask cuts through it (only those tiles pay for the compares)
     auto tile_body = [&](auto diag_c) {
       constexpr bool DIAG = decltype(diag_c)::value;
+      // DIAG: the tile's second 32-key block lies wholly past this wave's queries for waves whose
+      // diagonal falls in the first (skip1: no S / P·V MFMAs, P = 0), and a block wholly before
+      // them needs no mask — only the block the diagonal crosses pays the compares (wave-uniform)
+      const bool skip1 = DIAG && k0 + 32 > q0 + 31;
       f16x sacc[2] = {zero16(), zero16()};
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb) {
+        if (kb == 1 && skip1) break;
 #pragma unroll
         for (int s = 0; s < 4; ++s) sacc[kb] = mfma(ld16(Ks + (kb * 32 + r) * RS + 16 * s + 8 * h), qf[s], sacc[kb]);
+      }
       // running max on the raw scores (sc2 > 0), scaled once; p = exp2(s·sc2 − m) as one FMA + exp
       float mt = -INFINITY;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb) {
+        if constexpr (DIAG) {
+          if (kb == 1 && skip1) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if constexpr (DIAG) {
-            if (k0 + kb * 32 + crow(i, h) > qi) sacc[kb][i] = -INFINITY;
+            for (int i = 0; i < 16; ++i) sacc[1][i] = -INFINITY;
+            continue;
           }
-          mt = fmaxf(mt, sacc[kb][i]);
+          if (k0 + kb * 32 + 31 > q0) {  // the diagonal crosses this block
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (k0 + kb * 32 + crow(i, h) > qi) sacc[kb][i] = -INFINITY;
+          }
         }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[kb][i]);
+      }
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
       // deferred rescale (cdna_hip_programming.md T13): the O / l rescale by exp2(m − m') runs
       // only when some query of the wave saw its running max grow by more than kDeferLog2;
@@ -292,7 +306,8 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
       l += rs;
       // O^T[d][q] += V^T[d][key] . P[key][q]
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb) {
+        if (kb == 1 && skip1) break;  // P = 0 there
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const s8v pb = pack_half(sacc[kb], s);
@@ -303,6 +318,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MVie
             acc_o[db] = mfma(cat(tr4(base), tr4(base + 8 * RSV)), pb, acc_o[db]);
           }
         }
+      }
     };
     if (!CAUSAL || k0 <= q0 + 31) {
       if (CAUSAL && k0 + TILE - 1 > q0)
@@ -569,6 +585,10 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
     if (!CAUSAL || k0 <= q0 + 31) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
+        const int kr0 = k0 + kb * 32;
+        // a 32-key block wholly past this wave's queries contributes nothing (P = 0): skipped
+        // (wave-uniform; the tile's first block always holds some key <= the wave's last query)
+        if (CAUSAL && kb == 1 && __builtin_amdgcn_readfirstlane((int)(kr0 > q0 + 31))) break;
         f16x sacc = zero16(), dp = ndl;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -577,7 +597,6 @@ __device__ __forceinline__ void dq_body(int blk, int nblocks, View q, View k, Vi
         }
         // causal mask only where this 32-key block crosses the wave's queries (wave-uniform
         // branch; keys past every query of the wave were skipped with the whole tile)
-        const int kr0 = k0 + kb * 32;
         if (CAUSAL && __builtin_amdgcn_readfirstlane((int)(kr0 + 31 > q0))) {
           const int thr = qi - kr0 - 4 * h;  // masked where (i&3) + 8(i>>2) > thr
 #pragma unroll

@@ -57,7 +57,16 @@ def _nbd_pat(n, dtype, k, scale=1, offset=0):
 
 def _nbd_chk_collectives(sizes, dtypes):
     W, r = world_size, rank
-    res = {}
+    res, errs = {}, {}
+
+    def run(key, fn):
+        # one collective: a raise is recorded as a failure of that op only (the others still run)
+        try:
+            res[key] = bool(fn())
+        except Exception as e:  # noqa: BLE001
+            res[key] = False
+            errs[key] = (type(e).__name__ + ": " + str(e))[:300]
+
     for dt in dtypes:
         dtype = getattr(torch, dt)
         esz = torch.tensor([], dtype=dtype).element_size()
@@ -65,52 +74,68 @@ def _nbd_chk_collectives(sizes, dtypes):
             tag = dt + "_" + str(nbytes)
             n = max(64 * W, nbytes // esz // (8 * W) * (8 * W))   # elements, a multiple of 8 W
             c = n // W
-            # all_reduce SUM: Σ_r (r + 1) · p = W(W+1)/2 · p
-            x = _nbd_pat(n, dtype, 5, r + 1)
-            dist.all_reduce(x)
-            res["all_reduce_" + tag] = bool(torch.equal(x, _nbd_pat(n, dtype, 5, W * (W + 1) // 2)))
-            # broadcast from the last rank (a non-zero source)
-            src = W - 1
-            x = _nbd_pat(n, dtype, 7, 1, r) if r == src else torch.zeros(n, dtype=dtype, device=device)
-            dist.broadcast(x, src=src)
-            res["broadcast_" + tag] = bool(torch.equal(x, _nbd_pat(n, dtype, 7, 1, src)))
-            # all_gather_into_tensor: chunk s = (s + 1) · p
-            x = _nbd_pat(c, dtype, 3, r + 1)
-            out = torch.empty(n, dtype=dtype, device=device)
-            dist.all_gather_into_tensor(out, x)
-            want = torch.cat([_nbd_pat(c, dtype, 3, s + 1) for s in range(W)])
-            res["all_gather_" + tag] = bool(torch.equal(out, want))
-            # reduce_scatter_tensor SUM: this rank's chunk of W(W+1)/2 · p
-            x = _nbd_pat(n, dtype, 5, r + 1)
-            out = torch.empty(c, dtype=dtype, device=device)
-            dist.reduce_scatter_tensor(out, x)
-            res["reduce_scatter_" + tag] = bool(torch.equal(out, _nbd_pat(n, dtype, 5, W * (W + 1) // 2)[r * c:(r + 1) * c]))
-            # all_to_all_single: the chunk sent to rank j is r·W + j + 1; received chunk s = s·W + r + 1
-            x = torch.cat([torch.full((c,), r * W + j + 1, dtype=dtype, device=device) for j in range(W)])
-            out = torch.empty(n, dtype=dtype, device=device)
-            dist.all_to_all_single(out, x)
-            want = torch.cat([torch.full((c,), s * W + r + 1, dtype=dtype, device=device) for s in range(W)])
-            res["all_to_all_" + tag] = bool(torch.equal(out, want))
+
+            def all_reduce():  # SUM: Σ_r (r + 1) · p = W(W+1)/2 · p
+                x = _nbd_pat(n, dtype, 5, r + 1)
+                dist.all_reduce(x)
+                return torch.equal(x, _nbd_pat(n, dtype, 5, W * (W + 1) // 2))
+
+            def broadcast():  # from the last rank (a non-zero source)
+                src = W - 1
+                x = _nbd_pat(n, dtype, 7, 1, r) if r == src else torch.zeros(n, dtype=dtype, device=device)
+                dist.broadcast(x, src=src)
+                return torch.equal(x, _nbd_pat(n, dtype, 7, 1, src))
+
+            def all_gather():  # chunk s = (s + 1) · p
+                out = torch.empty(n, dtype=dtype, device=device)
+                dist.all_gather_into_tensor(out, _nbd_pat(c, dtype, 3, r + 1))
+                return torch.equal(out, torch.cat([_nbd_pat(c, dtype, 3, s + 1) for s in range(W)]))
+
+            def reduce_scatter():  # SUM: this rank's chunk of W(W+1)/2 · p
+                out = torch.empty(c, dtype=dtype, device=device)
+                dist.reduce_scatter_tensor(out, _nbd_pat(n, dtype, 5, r + 1))
+                return torch.equal(out, _nbd_pat(n, dtype, 5, W * (W + 1) // 2)[r * c:(r + 1) * c])
+
+            def all_to_all():  # the chunk sent to rank j is r·W + j + 1; received chunk s = s·W + r + 1
+                x = torch.cat([torch.full((c,), r * W + j + 1, dtype=dtype, device=device) for j in range(W)])
+                out = torch.empty(n, dtype=dtype, device=device)
+                dist.all_to_all_single(out, x)
+                return torch.equal(out, torch.cat([torch.full((c,), s * W + r + 1, dtype=dtype, device=device)
+                                                   for s in range(W)]))
+
+            run("all_reduce_" + tag, all_reduce)
+            run("broadcast_" + tag, broadcast)
+            run("all_gather_" + tag, all_gather)
+            run("reduce_scatter_" + tag, reduce_scatter)
+            run("all_to_all_" + tag, all_to_all)
             if W > 1:   # point to point around the ring (even ranks send first: no deadlock)
                 nxt, prv = (r + 1) % W, (r - 1) % W
-                s_ = _nbd_pat(n, dtype, 7, 1, r)
-                rb = torch.zeros(n, dtype=dtype, device=device)
-                if r % 2 == 0:
-                    dist.send(s_, nxt); dist.recv(rb, prv)
-                else:
-                    dist.recv(rb, prv); dist.send(s_, nxt)
-                res["send_recv_" + tag] = bool(torch.equal(rb, _nbd_pat(n, dtype, 7, 1, prv)))
-                fw = torch.zeros(n, dtype=dtype, device=device)
-                bw = torch.zeros(n, dtype=dtype, device=device)
-                ops_ = [dist.P2POp(dist.isend, s_, nxt), dist.P2POp(dist.irecv, fw, prv),
-                        dist.P2POp(dist.isend, s_, prv), dist.P2POp(dist.irecv, bw, nxt)]
-                for q in dist.batch_isend_irecv(ops_):
-                    q.wait()
-                res["batch_isend_irecv_" + tag] = bool(torch.equal(fw, _nbd_pat(n, dtype, 7, 1, prv))
-                                                       and torch.equal(bw, _nbd_pat(n, dtype, 7, 1, nxt)))
-            del x, out
+
+                def send_recv():
+                    s_ = _nbd_pat(n, dtype, 7, 1, r)
+                    rb = torch.zeros(n, dtype=dtype, device=device)
+                    if r % 2 == 0:
+                        dist.send(s_, nxt); dist.recv(rb, prv)
+                    else:
+                        dist.recv(rb, prv); dist.send(s_, nxt)
+                    return torch.equal(rb, _nbd_pat(n, dtype, 7, 1, prv))
+
+                def batch_p2p():  # both directions at once
+                    s_ = _nbd_pat(n, dtype, 7, 1, r)
+                    fw = torch.zeros(n, dtype=dtype, device=device)
+                    bw = torch.zeros(n, dtype=dtype, device=device)
+                    ops_ = [dist.P2POp(dist.isend, s_, nxt), dist.P2POp(dist.irecv, fw, prv),
+                            dist.P2POp(dist.isend, s_, prv), dist.P2POp(dist.irecv, bw, nxt)]
+                    for q in dist.batch_isend_irecv(ops_):
+                        q.wait()
+                    return torch.equal(fw, _nbd_pat(n, dtype, 7, 1, prv)) and torch.equal(bw, _nbd_pat(n, dtype, 7, 1, nxt))
+
+                run("send_recv_" + tag, send_recv)
+                run("batch_isend_irecv_" + tag, batch_p2p)
     if device.type == "cuda":
         torch.cuda.synchronize()
+    if errs:
+        res["detail"] = {"collective_errors": errs}
     return res
 
 def _nbd_same_on_all_ranks(t):

@@ -603,6 +603,36 @@ class MagicCore:
         what = ", ".join(args.names) if args.names else "all names in the checkpoint"
         self.p(f"✓ {verb} {what} on {len(res.ranks)} ranks ({path}, {time.perf_counter() - t0:.2f}s)")
 
+    def dist_check(self, line: str = "") -> None:
+        """``%dist_check [--only collectives,ddp,recipe,graph,accelerate,rank_broadcast] [--big BYTES]``:
+        verify the data plane on the live ranks (``nbdistributed_amd.checks``): every collective
+        against closed-form values, nbd DDP against torch DDP, ZeRO-2, the graphed step,
+        accelerate, ``%%rank`` + broadcast.  Prints one line per failed check (or all passed)."""
+        import argparse
+        import shlex
+
+        from .checks import run_checks
+
+        if not self.session.active:
+            self.p("No distributed workers running. Use %dist_init first.")
+            return
+        ap = argparse.ArgumentParser(prog="%dist_check", add_help=False)
+        ap.add_argument("--only", default="")
+        ap.add_argument("--big", type=int, default=None)
+        args = ap.parse_args(shlex.split(line))
+        only = [x for x in args.only.split(",") if x] or None
+        out = run_checks(self.session, big_bytes=args.big, only=only, log=lambda m: None)
+        res = out["results"]
+        if out["passed"]:
+            self.p(f"✓ {len(res)} data-plane checks passed on {out['world_size']} rank(s) ({out['seconds']:.1f}s)")
+            return
+        self.p(f"✗ {len(out['failed'])} of {len(res)} checks FAILED on {out['world_size']} rank(s):")
+        for k in out["failed"]:
+            self.p(f"  {k}: {out.get('errors', {}).get(k, 'wrong result')}")
+        for r, d in sorted(out.get("detail", {}).items()):
+            if r.startswith("rank") and isinstance(d, dict):
+                self.p(f"  {r}: {d}")
+
     def dist_topology(self, line: str = "") -> None:
         """xGMI / PCIe link table between the GPUs of this node (KFD topology)."""
         from .utils.devices import kfd_gpus, xgmi_matrix
@@ -634,7 +664,7 @@ class MagicCore:
 LINE_MAGICS = ["dist_init", "sync", "dist_status", "dist_mode", "dist_shutdown", "dist_reset", "dist_debug",
                "dist_sync_ide", "timeline_save", "timeline_debug", "timeline_clear", "dist_interrupt",
                "dist_recover", "dist_pull", "dist_push", "dist_profile", "dist_checkpoint", "dist_topology",
-               "dist_fault"]
+               "dist_fault", "dist_check"]
 CELL_MAGICS = ["distributed", "rank"]
 
 

@@ -180,6 +180,16 @@ def test_sync_status_debug_mode_timeline(nb, tmp_path):
     assert "Cleared" in cap.take()
 
 
+def test_dist_check_magic(nb):
+    """%dist_check verifies the data plane on the live ranks (nbdistributed_amd.checks)."""
+    sh, core, cap = nb
+    cap.take()
+    r = sh.run_cell("%dist_check --only collectives,ddp,rank_broadcast")
+    assert r.success
+    out = cap.take()
+    assert "data-plane checks passed on 2 rank(s)" in out, out
+
+
 def test_pull_push(nb):
     sh, core, cap = nb
     sh.run_cell("arr = torch.arange(6.).reshape(2, 3) + rank")
