@@ -34,6 +34,9 @@ def bench(fn, reps=10, rounds=5, warm=3):
 
 
 def main():
+    from nbdistributed_amd import ops
+
+    ops._require()
     N, V, C = 8192, 50688, 768
     torch.manual_seed(0)
     h = (torch.randn(N, C, device="cuda") * 0.5).to(torch.bfloat16)

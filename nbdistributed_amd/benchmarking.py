@@ -961,7 +961,9 @@ def run_all(session, steps: int, warmup: int, allreduce: bool = True, sweep: boo
             _log(f"phase 7: data-plane correctness checks on {n} rank(s)")
             from .checks import run_checks
 
-            _phase(session, out, "checks", lambda: run_checks(session, log=_log), phase_timeout_s, deadline, 30.0)
+            # (150 s per cell at most: at N = 8 the whole phase takes seconds; a hang in it ends early)
+            _phase(session, out, "checks", lambda: run_checks(session, log=_log), min(phase_timeout_s, 150.0),
+                   deadline, 30.0)
             ck = out["checks"]
             _log("checks: " + ("all passed" if ck.get("passed") else
                                f"NOT PASSED {ck.get('failed') or ck.get('error') or ck.get('skipped')}"))

@@ -19,6 +19,8 @@ from ._lib import _require
 # NBD_HIP_GEMM=0 routes gemm_linear / mlp_gelu to PyTorch (hipBLASLt) — for A/B measurements
 ENABLED = os.environ.get("NBD_HIP_GEMM", "1") != "0"
 KSPLIT = os.environ.get("NBD_GEMM_KSPLIT", "1") != "0"
+# NBD_GEMM_COLSPLIT=0: the column-split tuned entries run their tail tile over all columns (A/B)
+COLSPLIT_ON = os.environ.get("NBD_GEMM_COLSPLIT", "1") != "0"
 FUSED_SWIGLU = os.environ.get("NBD_FUSED_SWIGLU", "1") != "0"  # 0: separate swiglu kernels (A/B)
 # backward: a Linear's input- and weight-gradient GEMMs as one grouped launch (nbd::gemm_pair,
 # 128x128 tiles): the weight-gradient tiles fill the CUs the input-gradient grid leaves idle
@@ -230,6 +232,8 @@ def config(a_km: bool, b_kn: bool, M: int, N: int, K: int, can_split: bool = Tru
     workgroups split K (the largest tile needing <= 8 splits, each >= 512 deep) — split-K (a
     second, reducing kernel) only without an epilogue."""
     hit = _TUNED_EPI.get((a_km, b_kn, M, N, K, epi)) or _TUNED.get((a_km, b_kn, M, N, K))
+    if hit is not None and hit[0] >= COLSPLIT and not COLSPLIT_ON:
+        hit = (hit[0] - COLSPLIT, hit[1])
     if hit is not None and (can_split or hit[1] == 1):
         return hit if KSPLIT else (hit[0] % 100000000, hit[1])
     t256 = (M // 256) * (N // 256)

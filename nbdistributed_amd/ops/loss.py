@@ -190,7 +190,7 @@ LM_HEAD_HIP = os.environ.get("NBD_LMHEAD_HIP", "auto") != "0"
 # "fwd,dgrad".  The bench line carries the graphed step with every product on each side.
 _HEAD_SPEC = os.environ.get("NBD_LMHEAD_HIP", "auto")
 HEAD_PRODUCTS = ({"fwd": False, "dgrad": True, "wgrad": False} if _HEAD_SPEC == "auto" else
-                 {p: _HEAD_SPEC not in ("0",) and (_HEAD_SPEC == "1" or p in _HEAD_SPEC.split(","))
+                 {p: _HEAD_SPEC not in ("0",) and (_HEAD_SPEC == "1" or p in _HEAD_SPEC.replace("+", ",").split(","))
                   for p in ("fwd", "dgrad", "wgrad")})
 
 

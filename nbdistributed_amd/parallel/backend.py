@@ -100,8 +100,9 @@ def init_data_plane(backend: str, rank: int, world_size: int, device, timeout_s:
     if backend in ("nccl", "rccl") and device is not None and device.type == "cuda":
         # bound device (both names are RCCL here): torch creates the communicator eagerly on it
         # (ProcessGroupNCCL.eager_connect_single_device) and every later device-less call —
-        # a cell's plain dist.barrier(), new_group splits — uses it instead of guessing
-        kw["device_id"] = device
+        # a cell's plain dist.barrier(), new_group splits — uses it instead of guessing.  A bare
+        # torch.device("cuda") means the current device (torch wants an index).
+        kw["device_id"] = device if device.index is not None else torch.device("cuda", torch.cuda.current_device())
     dist.init_process_group(backend=backend, rank=rank, world_size=world_size,
                             init_method=init_method or "env://", **kw)
     if eager:
