@@ -115,7 +115,10 @@ def _nbd_gpt2_bench(steps, warm, B, T, impl, config="small", force=False, lmhead
     if lmhead_hip:
         _lm.LM_HEAD_HIP, _lm.HEAD_PRODUCTS = True, {"fwd": True, "dgrad": True, "wgrad": True}
     try:
-        return _nbd_gpt2_bench_body(steps, warm, B, T, impl, config, force, 128 if lmhead_lib else 0)
+        # the table padded as each plan wants it (ops.loss.table_pad): 128 for the library, 512 with
+        # the hand-written input gradient, the default plan's own otherwise
+        return _nbd_gpt2_bench_body(steps, warm, B, T, impl, config, force,
+                                    128 if lmhead_lib else 512 if lmhead_hip else 0)
     finally:
         _lm.LM_HEAD_HIP, _lm.HEAD_PRODUCTS = prev_hip, prev_products
 
@@ -355,7 +358,7 @@ def bench_ddp_graph(session, out: Dict[str, Any], steps: int = 20, warmup: int =
     elif bool(session.ready.get(0, {}).get("cuda_available")):
         # the same graphed step with the LM head's three GEMMs all on hipBLASLt, and all on the
         # hand-written kernels, for comparison with the default per-product plan
-        # (ops.loss.HEAD_PRODUCTS: input gradient hand-written, forward / weight gradient library)
+        # (ops.loss.HEAD_PRODUCTS: weight gradient hand-written, forward / input gradient library)
         out["graph_lmhead_plan"] = "per-product (ops.loss.HEAD_PRODUCTS): " + session.execute(
             "import nbdistributed_amd.ops.loss as _lm2; str(_lm2.HEAD_PRODUCTS if _lm2.LM_HEAD_HIP else 'library')",
             render=False).results[0].get("echo", "")

@@ -7,24 +7,30 @@ GEMMs (``ops.gemm_linear`` / ``ops.mlp_gelu``: csrc/kernels/gemm.hip, fused bias
 epilogues, grouped dgrad + wgrad backward writing into the DDP buckets), attention on the HIP
 flash kernels (``ops.attention_qkv``, csrc/kernels/attn.hip), add + LayerNorm on norm.hip and the
 loss on the fused HIP cross-entropy (``ops.linear_cross_entropy``, no fp32 copy of the
-8192 x 50257 logits).  The tied LM-head products (8192 x 50688 x 768, three per step) each run on
-whichever kernel measured faster for that product (``ops.loss.HEAD_PRODUCTS``): the input gradient
-on the hand-written 256x256 kernel (gemm256.hip, split 8 ways; the table padded to a multiple of
-512 for it), the forward and weight gradient on hipBLASLt (docs/FINDINGS.md §35;
-``NBD_LMHEAD_HIP=1`` all three hand-written, ``=0`` all three on the library with a 128-padded
-table).  CPU / fp32: the same model in plain PyTorch.
+8192 x 50257 logits).  The tied LM-head products (8192 x 50432 x 768, three per step) follow the
+plan the step measured fastest (``ops.loss.HEAD_PRODUCTS``): the weight gradient on the
+hand-written 256x256 kernel (gemm256.hip; the table padded to a multiple of 256 for it), the
+forward and input gradient on hipBLASLt (docs/FINDINGS.md §35; ``NBD_LMHEAD_HIP=1`` all three
+hand-written, ``=0`` all three on the library with a 128-padded table).  CPU / fp32: the same
+model in plain PyTorch.
 Random init (no checkpoints: no network), GPT-2 initialisation scheme.
 """
 from __future__ import annotations
 
 import math
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Optional
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+
+def _table_pad() -> int:
+    from ..ops.loss import table_pad
+
+    return table_pad()
 
 
 @dataclass
@@ -44,12 +50,11 @@ class GPT2Config:
     # the token table (and the tied LM head) is stored with its rows padded to a multiple of this
     # from 4096 classes up: zero rows that never receive a gradient, so the LM-head GEMMs run on an
     # aligned vocabulary (hipBLASLt on 50257 vs 50304 columns: 2.18 vs 1.75 ms per GPT-2 step,
-    # docs/FINDINGS.md §16) with no per-step padded copy of the weight.  1 = no padding.  512 for
-    # the hand-written LM head (the default; 128 with NBD_LMHEAD_HIP=0): 256x256 tiles over the
-    # vocabulary and an input gradient split 8 ways into whole K-tiles (ops/loss.py _hip_dgrad).
-    # NBD_GPT2_VOCAB_PAD overrides (A/B measurements).
-    vocab_pad: int = (int(os.environ.get("NBD_GPT2_VOCAB_PAD", "0"))
-                      or (128 if os.environ.get("NBD_LMHEAD_HIP", "auto") == "0" else 512))
+    # docs/FINDINGS.md §16) with no per-step padded copy of the weight.  1 = no padding.  The
+    # multiple follows the LM head's kernel plan (ops.loss.table_pad: 256 for the default plan's
+    # hand-written weight gradient on 256x256 tiles, 512 when the input gradient is hand-written too,
+    # 128 for hipBLASLt alone); NBD_GPT2_VOCAB_PAD overrides (A/B measurements).
+    vocab_pad: int = field(default_factory=lambda: int(os.environ.get("NBD_GPT2_VOCAB_PAD", "0")) or _table_pad())
 
     @property
     def padded_vocab(self) -> int:

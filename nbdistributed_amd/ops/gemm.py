@@ -159,9 +159,9 @@ def gemm_ok(M: int, N: int, K: int) -> bool:
 # benchmarks/gemm_bench.py --sweep
 # (profiles/gemm_bench_r1.txt; split-K only where it beats the best unsplit kernel by > 5 %).
 _TUNED = {
-    # gpt2.c_attn fwd: columns 0..2047 on the 256x256 8-phase kernel (one round), 2048..2303 on
-    # 128x128 — 41.1-41.3 us vs 44.7 for 128x128 alone, hipBLASLt 40.0 (profiles/gemm_colsplit_r6.txt)
-    (False, False, 8192, 2304, 768): (1082128128, 1),
+    # gpt2.c_attn fwd 44.5 us.  (A column split — columns 0..2047 on the 256x256 kernel, one round,
+    # the rest on 128x128: 41.1 us isolated — made the graphed step 0.12 ms slower: COLSPLIT below)
+    (False, False, 8192, 2304, 768): (82128128, 1),
     (False, True, 8192, 768, 2304): (82128128, 1),  # gpt2.c_attn dgrad 42.3 us
     (True, True, 2304, 768, 8192): (203128064, 1),  # gpt2.c_attn wgrad 49.7 us (K-split groups)
     (False, False, 8192, 768, 768): (2128096, 1),  # gpt2.attn.c_proj fwd 14.8 us (128x128/8 waves 16.5: 512 tiles = one round)
@@ -190,12 +190,13 @@ _TUNED = {
     (True, True, 576, 1536, 2048): (203064064, 1),  # smollm2.down wgrad 13.7 us (15.6)
 }
 
-# epilogue-specific entries, checked first: (a_km, b_kn, M, N, K, epi)
-_TUNED_EPI = {
-    # gpt2.c_fc fwd + GELU: column split as c_attn (2048 + 1024 columns): 53.4 vs 57.2 us, hipBLASLt +
-    # a GELU pass 71.9 (profiles/gemm_colsplit_r6.txt); the plain product keeps 128x128 (43.5 vs 45.0)
-    (False, False, 8192, 3072, 768, EPI_GELU): (1082128128, 1),
-}
+# epilogue-specific entries, checked first: (a_km, b_kn, M, N, K, epi).  (The column split of c_fc +
+# GELU — 53.4 vs 57.2 us isolated, profiles/gemm_colsplit_r6.txt — lost in the step with q|k|v's:
+# graphed GPT-2 10.53-10.58 vs 10.41-10.44 ms, eager 10.73-10.75 vs 10.60-10.66,
+# profiles/colsplit_step_ab_r6.txt: the 256x256 head launch has no next-weight warm-up and the
+# two launches each pay a ramp; in the step each product measured 43.1 / 56.4 us split vs 43.1 /
+# 57.4 whole, profiles/gpt2_graph_prof_r6a.md)
+_TUNED_EPI: dict = {}
 
 _TILES = (128128, 128064, 64128, 64064)  # (+ 128096: forward only, tuned entries)
 
@@ -212,7 +213,8 @@ def _ntiles(tile: int, M: int, N: int) -> int:
 G256 = 86256256
 G256_EPIS = (EPI_NONE, EPI_GELU)
 # column split (gemm.hip kColSplit): COLSPLIT + tail tile runs the columns that make whole rounds
-# of 256x256 tiles on the 8-phase kernel and the rest on the tail tile (two launches, one C)
+# of 256x256 tiles on the 8-phase kernel and the rest on the tail tile (two launches, one C) —
+# available as a tile hint, in no tuned entry (slower in the GPT-2 step, _TUNED_EPI note)
 COLSPLIT = 1000000000
 # Plain products at least this large (FLOPs) with no tuned entry go to hipBLASLt: it measured
 # 1.16-1.61 PF on them, 15-30 % ahead of both hand-written families (profiles/gemm256_bench_r2.txt);

@@ -182,16 +182,27 @@ LM_HEAD_CHUNK = int(os.environ.get("NBD_LMHEAD_CHUNK", "0"))
 # GEMM left in the step.
 LM_HEAD_HIP = os.environ.get("NBD_LMHEAD_HIP", "auto") != "0"
 # Which of the three products run hand-written when LM_HEAD_HIP is on.  NBD_LMHEAD_HIP=1: all
-# three; "auto" (default): the measured faster kernel per product on the GPT-2 small head (8192 x
-# 50688 x 768, back-to-back on one MI355X: profiles/lmhead_products_r6.txt) — the input gradient
-# on gemm256 split 8 ways (515 vs 576 µs for hipBLASLt), the forward (600 vs 568) and the weight
-# gradient (565 vs 505) on hipBLASLt, whose persistent kernels fit these shapes' tile
-# quantisation better (2.3 rounds of 256x256 tiles for the weight gradient); or a list such as
-# "fwd,dgrad".  The bench line carries the graphed step with every product on each side.
+# three; "auto" (default): the plan the GPT-2 small step measured fastest (interleaved A/B of every
+# plan in the graphed step, one box: profiles/lmhead_plan_ab_r6a.txt, lmhead_plan_ab_r6b.txt) — the
+# weight gradient on the 256x256 kernel (whole rounds + a token-split tail: 10.36-10.40 ms, tied
+# with all-hipBLASLt 10.36-10.39), the forward and input gradient on hipBLASLt (hand-written: +0.10
+# and +0.15 ms in the step, though the isolated kernels swap places from box to box:
+# profiles/lmhead_products_r6.txt); or a list such as "fwd+wgrad".
 _HEAD_SPEC = os.environ.get("NBD_LMHEAD_HIP", "auto")
-HEAD_PRODUCTS = ({"fwd": False, "dgrad": True, "wgrad": False} if _HEAD_SPEC == "auto" else
+HEAD_PRODUCTS = ({"fwd": False, "dgrad": False, "wgrad": True} if _HEAD_SPEC == "auto" else
                  {p: _HEAD_SPEC not in ("0",) and (_HEAD_SPEC == "1" or p in _HEAD_SPEC.replace("+", ",").split(","))
                   for p in ("fwd", "dgrad", "wgrad")})
+
+
+def table_pad() -> int:
+    """Row padding of an LM-head table for this process's plan: 512 when the input gradient is
+    hand-written (split 8 ways into whole K-tiles), 256 when the forward or the weight gradient is
+    (256x256 tiles over the vocabulary), else 128 (hipBLASLt's alignment)."""
+    if not LM_HEAD_HIP:
+        return 128
+    if HEAD_PRODUCTS.get("dgrad"):
+        return 512
+    return 256 if HEAD_PRODUCTS.get("fwd") or HEAD_PRODUCTS.get("wgrad") else 128
 
 
 def _use_hip(product: str) -> bool:
