@@ -38,8 +38,14 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <numeric>
+#include <queue>
 #include <tuple>
+#include <vector>
 #include <type_traits>
 
 #include "nbd_common.h"
@@ -209,11 +215,14 @@ struct Stage2 {
 // ============================================================================ forward
 template <bool CAUSAL>
 __global__ __launch_bounds__(NT, 2) void fwd_kernel(View q, View k, View v, MView o, float* __restrict__ lse,
-                                                     int H, int T, int nblk, float sc2, int group, Rope rp) {
+                                                     int H, int T, int nblk, float sc2, int group, Rope rp,
+                                                     const int* __restrict__ order) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[TILE * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[TILE * RSV];
-  const int bh = blockIdx.x % (gridDim.x / nblk);
-  const int qb = CAUSAL ? nblk - 1 - blockIdx.x / (gridDim.x / nblk) : blockIdx.x / (gridDim.x / nblk);
+  // work item (heaviest first under a causal mask); `order` places the items on the CUs (host: block_order)
+  const int item = order != nullptr ? order[blockIdx.x] : (int)blockIdx.x;
+  const int bh = item % (gridDim.x / nblk);
+  const int qb = CAUSAL ? nblk - 1 - item / (gridDim.x / nblk) : item / (gridDim.x / nblk);
   const int b = bh / H, hh = bh % H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
   const int q0 = qb * BLK + w * 32;  // this wave's first query
@@ -647,12 +656,14 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(View q, View k, View v, View
                                                      const float* __restrict__ lse,
                                                      const float* __restrict__ delta, MView dq, MView dk, MView dv,
                                                      int Hq, int Hkv, int T, int nblk, float sc2, float scale,
-                                                     int group, Rope rp, int nkv, int gsplit, int64_t split_stride) {
-  if ((int)blockIdx.x < nkv)
-    dkdv_body<CAUSAL, FD>(blockIdx.x, nkv, q, k, v, dout, out, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale, group, rp,
+                                                     int group, Rope rp, int nkv, int gsplit, int64_t split_stride,
+                                                     const int* __restrict__ order) {
+  const int item = order != nullptr ? order[blockIdx.x] : (int)blockIdx.x;
+  if (item < nkv)
+    dkdv_body<CAUSAL, FD>(item, nkv, q, k, v, dout, out, lse, delta, dk, dv, Hkv, T, nblk, sc2, scale, group, rp,
                           gsplit, split_stride);
   else
-    dq_body<CAUSAL, FD>(blockIdx.x - nkv, gridDim.x - nkv, q, k, v, dout, out, lse, delta, dq, Hq, T, nblk, sc2, scale,
+    dq_body<CAUSAL, FD>(item - nkv, gridDim.x - nkv, q, k, v, dout, out, lse, delta, dq, Hq, T, nblk, sc2, scale,
                         group, rp);
 }
 
@@ -694,6 +705,109 @@ static int fwd_pad() {
 static int bwd_pad() {
   static const int v = lds_pad("NBD_ATTN_BWD_LDS_PAD");
   return v;
+}
+
+// Block order for a causal grid (NBD_ATTN_ORDER=0: the plain heaviest-first order, A/B).
+//
+// A grid that the chip holds at once is placed round-robin: block w goes to CU w mod R (R = the
+// CU count), so a CU's blocks are w, w + R, w + 2R, ... (benchmarks/dispatch_probe.hip,
+// profiles/dispatch_probe_r6.txt: every CU, every grid size probed).  With causal work items of
+// unequal cost, the time of such a grid is the most loaded CU's sum: GPT-2's forward (768
+// blocks, 3 per CU) in the plain order puts 34 key tiles on its most loaded CU against a mean of
+// 27.  The table maps block -> work item so that the first fill is an LPT assignment (heaviest
+// item to the least loaded CU that still has a slot; 28 tiles there), and the blocks past the
+// first fill keep the heaviest-first order for the dispatcher to hand out as slots free up.
+// Built on the host once per (weights, slots) and kept in device memory; under stream capture
+// an order not built yet is not built (a memcpy cannot be captured) and the plain order runs.
+static bool order_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NBD_ATTN_ORDER");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
+static int cu_count(int dev) {
+  static int n[64] = {0};
+  if (dev < 0 || dev >= 64) return 0;
+  if (n[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) v = -1;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+
+// weight[k] = cost of work item k (items indexed as the kernel reads them); slots = resident
+// blocks per CU.  Returns nullptr when the plain order is as good (equal weights) or unavailable.
+static const int* block_order(const std::vector<int>& weight, int slots, int dev, hipStream_t st) {
+  if (!order_enabled() || slots < 1 || weight.empty()) return nullptr;
+  if (std::all_of(weight.begin(), weight.end(), [&](int x) { return x == weight[0]; })) return nullptr;
+  const int R = cu_count(dev);
+  if (R < 1) return nullptr;
+  static std::mutex mu;
+  static std::map<std::vector<int>, int*> cache;
+  std::vector<int> key(weight);
+  key.push_back(slots);
+  key.push_back(R);
+  key.push_back(dev);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  const int G = (int)weight.size();
+  std::vector<int> items(G);
+  std::iota(items.begin(), items.end(), 0);
+  std::stable_sort(items.begin(), items.end(), [&](int a, int b) { return weight[a] > weight[b]; });
+  const int F = std::min<int64_t>(G, (int64_t)R * slots);  // the first fill
+  // CU c holds the first-fill blocks c, c + R, ... (< F): cap[c] of them
+  std::vector<int> cap(R), load(R, 0);
+  std::vector<std::vector<int>> held(R);
+  for (int c = 0; c < R; ++c) cap[c] = F / R + (c < F % R ? 1 : 0);
+  using E = std::pair<int, int>;  // (load, cu)
+  std::priority_queue<E, std::vector<E>, std::greater<E>> pq;
+  for (int c = 0; c < R; ++c)
+    if (cap[c] > 0) pq.push({0, c});
+  for (int i = 0; i < F; ++i) {
+    const E e = pq.top();
+    pq.pop();
+    const int c = e.second;
+    held[c].push_back(items[i]);
+    load[c] += weight[items[i]];
+    if ((int)held[c].size() < cap[c]) pq.push({load[c], c});
+  }
+  std::vector<int> perm(G);
+  for (int c = 0; c < R; ++c)
+    for (size_t r = 0; r < held[c].size(); ++r) perm[c + (int64_t)r * R] = held[c][r];
+  for (int i = F; i < G; ++i) perm[i] = items[i];
+  int* d = nullptr;
+  if (hipMalloc(&d, sizeof(int) * G) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, perm.data(), sizeof(int) * G, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  cache.emplace(std::move(key), d);
+  if (const char* lg = std::getenv("NBD_ATTN_ORDER_LOG"); lg != nullptr && lg[0] == '1') {
+    int plain = 0;  // the most loaded CU under the plain order (first fill)
+    for (int c = 0; c < R; ++c) {
+      int sum = 0;
+      for (int64_t b = c; b < F; b += R) sum += weight[b];
+      plain = std::max(plain, sum);
+    }
+    std::fprintf(stderr, "nbd attn block order: %d items, %d per CU x %d CUs, most loaded CU %d (plain order %d)\n", G,
+                 slots, R, *std::max_element(load.begin(), load.end()), plain);
+  }
+  return d;
+}
+
+template <typename K>
+static int resident_blocks(K kernel, int lds_bytes) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel), NT, lds_bytes) !=
+      hipSuccess)
+    return 0;
+  return n;
 }
 
 static View view_of(const at::Tensor& t, const char* name) {
@@ -745,12 +859,21 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::T
   const dim3 grid((unsigned)(B * H * nblk));
   const float sc2 = (float)scale * kLog2e;
   const int group = H / (int)k.size(1);
-  if (causal)
+  if (causal) {
+    // item k: query block nblk - 1 - k / (B·H), 2·(that + 1) key tiles
+    const int* order = nullptr;
+    if (nblk > 1) {
+      static const int slots = resident_blocks(fwd_kernel<true>, fwd_pad());
+      std::vector<int> w((size_t)B * H * nblk);
+      for (size_t i = 0; i < w.size(); ++i) w[i] = 2 * (nblk - (int)(i / ((size_t)B * H)));
+      order = block_order(w, slots, q.get_device(), st);
+    }
     hipLaunchKernelGGL((fwd_kernel<true>), grid, dim3(NT), fwd_pad(), st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
-                       sc2, group, rp);
-  else
+                       sc2, group, rp, order);
+  } else {
     hipLaunchKernelGGL((fwd_kernel<false>), grid, dim3(NT), fwd_pad(), st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
-                       sc2, group, rp);
+                       sc2, group, rp, static_cast<const int*>(nullptr));
+  }
   C10_HIP_KERNEL_LAUNCH_CHECK();
   return {o, lse};
 }
@@ -809,16 +932,28 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     dkw = MView{static_cast<uint16_t*>(pk.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
     dvw = MView{static_cast<uint16_t*>(pv.data_ptr()), (int64_t)Hkv * T * D, (int64_t)T * D, D};
   }
-#define NBD_BWD(C_, F_)                                                                                      \
+  // causal items: dK/dV of key block kb sweeps (nblk - kb)·2 query tiles of gpw heads, ≈ 4 MFMA
+  // products per tile; dQ of query block qb sweeps (qb + 1)·2 key tiles, 3 products per tile
+  auto causal_order = [&](auto kernel) -> const int* {
+    if (nblk <= 1) return nullptr;
+    static const int slots = resident_blocks(kernel, bwd_pad());
+    std::vector<int> w((size_t)nkv + nq);
+    const int gpw = group / gsplit, per_kv = nkv / nblk, per_q = nq / nblk;
+    for (int i = 0; i < nkv; ++i) w[i] = 4 * 2 * (nblk - i / per_kv) * gpw;
+    for (int i = 0; i < nq; ++i) w[nkv + i] = 3 * 2 * (nblk - i / per_q);
+    return block_order(w, slots, q.get_device(), st);
+  };
+#define NBD_BWD(C_, F_, O_)                                                                                  \
   hipLaunchKernelGGL((bwd_kernel<C_, F_>), dim3((unsigned)(nkv + nq)), dim3(NT), bwd_pad(), st, qv, kv, vv, dov, ov,   \
                      lse.data_ptr<float>(), dptr, dqv, dkw, dvw, H, Hkv, T, nblk, sc2, (float)scale, group, rp, nkv, \
-                     gsplit, split_stride)
+                     gsplit, split_stride, O_)
+  const int* none = nullptr;
   if (causal) {
-    if (fd) NBD_BWD(true, true);
-    else NBD_BWD(true, false);
+    if (fd) NBD_BWD(true, true, causal_order(bwd_kernel<true, true>));
+    else NBD_BWD(true, false, causal_order(bwd_kernel<true, false>));
   } else {
-    if (fd) NBD_BWD(false, true);
-    else NBD_BWD(false, false);
+    if (fd) NBD_BWD(false, true, none);
+    else NBD_BWD(false, false, none);
   }
 #undef NBD_BWD
   C10_HIP_KERNEL_LAUNCH_CHECK();
