@@ -157,12 +157,16 @@ def _nbd_gpt2_bench_body(steps, warm, B, T, impl, config, force, vocab_pad):
         torch.cuda.empty_cache()
     return res
 
-def _nbd_linear_bench(steps, warm, rows, impl, dim=4096):
+def _nbd_linear_bench(steps, warm, rows, impl, dim=4096, bf16=False):
+    # bf16: the same step on a bf16 Linear (nbd: flat bf16 parameters in the DDP buckets, the
+    # forward / input gradient / weight gradient + bias row sums on the HIP GEMMs, the weight
+    # gradient written into its bucket slice; torch: DDP over the bf16 module, hipBLASLt)
     torch.manual_seed(0)
-    m = torch.nn.Linear(dim, dim).to(device)
-    model = _nbd_wrap(m, impl)
+    dt = torch.bfloat16 if bf16 and device.type == "cuda" else torch.float32
+    m = torch.nn.Linear(dim, dim).to(device, dt)
+    model = _nbd_wrap(m, impl, **({"flat_params": True, "grad_mode": "bucket"} if bf16 and impl == "nbd" else {}))
     opt = torch.optim.SGD(m.parameters(), lr=1e-3)
-    x = torch.randn(rows, dim, device=device)
+    x = torch.randn(rows, dim, device=device).to(dt)
     def step():
         loss = model(x).square().mean()
         loss.backward()
@@ -304,6 +308,19 @@ def bench_ddp(session, steps: int = 20, warmup: int = 5, B: int = 8, T: int = 10
     if compare_torch:
         r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'torch', {linear_dim})", render=False)
         lin["torch_ddp_ms_per_step"] = _max_over_ranks(r)
+    lin["recipe"] = "fp32 Linear (the reference README's module as written), SGD; both arms' GEMMs on hipBLASLt"
+    # the same step in bf16: the module on the HIP GEMMs (no library GEMM) against torch DDP on hipBLASLt
+    r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'nbd', {linear_dim}, bf16=True)",
+                        render=False)
+    lb = {"ms_per_step": _max_over_ranks(r),
+          "recipe": "bf16 Linear, SGD; nbd: flat bf16 params in DDP buckets, HIP GEMMs (bias add and bias-gradient "
+                    "row sums fused, weight gradient written into its bucket slice); torch: DDP, hipBLASLt"}
+    if compare_torch:
+        r = session.execute(f"_nbd_linear_bench({steps}, {warmup}, {linear_rows}, 'torch', {linear_dim}, bf16=True)",
+                            render=False)
+        lb["torch_ddp_ms_per_step"] = _max_over_ranks(r)
+        lb["speedup_vs_torch_ddp"] = lb["torch_ddp_ms_per_step"] / lb["ms_per_step"]
+    lin["bf16"] = lb
     tick()
     if _graph_arms(n) if graph is None else graph:
         bench_ddp_graph(session, out, steps, warmup, B, T, config)

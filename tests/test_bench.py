@@ -32,6 +32,8 @@ def test_ddp_phase_multi_rank(sess):
     assert r["ms_per_step"] > 0 and r["tokens_per_s"] > 0 and r["global_batch"] == 4
     assert r["amp_ms_per_step"] > 0 and "FlatAdamW" in r["recipe"]
     assert r["torch_ddp_ms_per_step"] > 0 and r["linear4096"]["ms_per_step"] > 0
+    lb = r["linear4096"]["bf16"]  # the bf16 arm (fp32 on the CPU): both implementations timed
+    assert lb["ms_per_step"] > 0 and lb["torch_ddp_ms_per_step"] > 0 and lb["speedup_vs_torch_ddp"] > 0
 
 
 def test_allreduce_sweep_multi_rank(sess):
