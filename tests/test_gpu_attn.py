@@ -29,8 +29,10 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("B,H,T", [(1, 1, 128), (2, 3, 256), (1, 2, 384)])
+@pytest.mark.parametrize("B,H,T", [(1, 1, 128), (2, 3, 256), (1, 2, 384), (1, 2, 640), (2, 2, 1024)])
 def test_flash_forward_backward(dev, causal, B, H, T):
+    """T >= 256 causal: the forward's heavier query blocks run split along the keys
+    (fwd_split_kernel, merged through LDS); odd block counts (384, 640) leave an uneven split."""
     g = torch.Generator(device="cpu").manual_seed(T + H)
     q, k, v, do = (torch.randn(B, H, T, 64, generator=g).to(dev, torch.bfloat16) for _ in range(4))
     scale = 0.125
