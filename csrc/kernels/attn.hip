@@ -738,24 +738,29 @@ static int cu_count(int dev) {
   return n[dev];
 }
 
-// weight[k] = cost of work item k (items indexed as the kernel reads them); slots = resident
-// blocks per CU.  Returns nullptr when the plain order is as good (equal weights) or unavailable.
-static const int* block_order(const std::vector<int>& weight, int slots, int dev, hipStream_t st) {
-  if (!order_enabled() || slots < 1 || weight.empty()) return nullptr;
-  if (std::all_of(weight.begin(), weight.end(), [&](int x) { return x == weight[0]; })) return nullptr;
+// weights() = cost of each work item k (items indexed as the kernel reads them), called only
+// when `shape` (everything the weights depend on) has no table yet; slots = resident blocks per
+// CU.  Returns nullptr when the plain order is as good (equal weights) or unavailable.
+template <typename W>
+static const int* block_order(std::vector<int64_t> shape, W weights, int slots, int dev, hipStream_t st) {
+  if (!order_enabled() || slots < 1) return nullptr;
   const int R = cu_count(dev);
   if (R < 1) return nullptr;
   static std::mutex mu;
-  static std::map<std::vector<int>, int*> cache;
-  std::vector<int> key(weight);
-  key.push_back(slots);
-  key.push_back(R);
-  key.push_back(dev);
+  static std::map<std::vector<int64_t>, int*> cache;  // (nullptr: the plain order)
+  shape.push_back(slots);
+  shape.push_back(R);
+  shape.push_back(dev);
   std::lock_guard<std::mutex> lock(mu);
-  auto it = cache.find(key);
+  auto it = cache.find(shape);
   if (it != cache.end()) return it->second;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  const std::vector<int> weight = weights();
+  if (weight.empty() || std::all_of(weight.begin(), weight.end(), [&](int x) { return x == weight[0]; })) {
+    cache.emplace(std::move(shape), nullptr);
+    return nullptr;
+  }
   const int G = (int)weight.size();
   std::vector<int> items(G);
   std::iota(items.begin(), items.end(), 0);
@@ -787,7 +792,7 @@ static const int* block_order(const std::vector<int>& weight, int slots, int dev
     (void)hipFree(d);
     return nullptr;
   }
-  cache.emplace(std::move(key), d);
+  cache.emplace(std::move(shape), d);
   if (const char* lg = std::getenv("NBD_ATTN_ORDER_LOG"); lg != nullptr && lg[0] == '1') {
     int plain = 0;  // the most loaded CU under the plain order (first fill)
     for (int c = 0; c < R; ++c) {
@@ -802,7 +807,11 @@ static const int* block_order(const std::vector<int>& weight, int slots, int dev
 }
 
 template <typename K>
-static int resident_blocks(K kernel, int lds_bytes) {
+static int resident_blocks(K kernel, int lds_bytes, const char* env = nullptr) {
+  if (env != nullptr) {  // override for A/B runs
+    const char* e = std::getenv(env);
+    if (e != nullptr && std::atoi(e) > 0) return std::atoi(e);
+  }
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel), NT, lds_bytes) !=
       hipSuccess)
@@ -863,10 +872,16 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::T
     // item k: query block nblk - 1 - k / (B·H), 2·(that + 1) key tiles
     const int* order = nullptr;
     if (nblk > 1) {
-      static const int slots = resident_blocks(fwd_kernel<true>, fwd_pad());
-      std::vector<int> w((size_t)B * H * nblk);
-      for (size_t i = 0; i < w.size(); ++i) w[i] = 2 * (nblk - (int)(i / ((size_t)B * H)));
-      order = block_order(w, slots, q.get_device(), st);
+      static const int slots = resident_blocks(fwd_kernel<true>, fwd_pad(), "NBD_ATTN_FWD_SLOTS");
+      const int BH = B * H;
+      order = block_order(
+          {0, BH, nblk},
+          [&] {
+            std::vector<int> w((size_t)BH * nblk);
+            for (size_t i = 0; i < w.size(); ++i) w[i] = 2 * (nblk - (int)(i / BH));
+            return w;
+          },
+          slots, q.get_device(), st);
     }
     hipLaunchKernelGGL((fwd_kernel<true>), grid, dim3(NT), fwd_pad(), st, qv, kv, vv, ov, lse.data_ptr<float>(), H, T, nblk,
                        sc2, group, rp, order);
@@ -936,12 +951,18 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
   // products per tile; dQ of query block qb sweeps (qb + 1)·2 key tiles, 3 products per tile
   auto causal_order = [&](auto kernel) -> const int* {
     if (nblk <= 1) return nullptr;
-    static const int slots = resident_blocks(kernel, bwd_pad());
-    std::vector<int> w((size_t)nkv + nq);
-    const int gpw = group / gsplit, per_kv = nkv / nblk, per_q = nq / nblk;
-    for (int i = 0; i < nkv; ++i) w[i] = 4 * 2 * (nblk - i / per_kv) * gpw;
-    for (int i = 0; i < nq; ++i) w[nkv + i] = 3 * 2 * (nblk - i / per_q);
-    return block_order(w, slots, q.get_device(), st);
+    static const int slots = resident_blocks(kernel, bwd_pad(), "NBD_ATTN_BWD_SLOTS");
+    const int gpw = group / gsplit;
+    return block_order(
+        {1, nkv, nq, nblk, gpw},
+        [&] {
+          std::vector<int> w((size_t)nkv + nq);
+          const int per_kv = nkv / nblk, per_q = nq / nblk;
+          for (int i = 0; i < nkv; ++i) w[i] = 4 * 2 * (nblk - i / per_kv) * gpw;
+          for (int i = 0; i < nq; ++i) w[nkv + i] = 3 * 2 * (nblk - i / per_q);
+          return w;
+        },
+        slots, q.get_device(), st);
   };
 #define NBD_BWD(C_, F_, O_)                                                                                  \
   hipLaunchKernelGGL((bwd_kernel<C_, F_>), dim3((unsigned)(nkv + nq)), dim3(NT), bwd_pad(), st, qv, kv, vv, dov, ov,   \
