@@ -33,6 +33,8 @@ TORCH_LIBRARY(nbd, m) {
   m.def("xent_fwd(Tensor logits, Tensor target, int ignore_index) -> (Tensor, Tensor)");
   m.def("xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor scale, int ignore_index, Tensor(a!) dlogits) -> ()");
   m.def("xent_fused(Tensor(a!) logits, Tensor target, int ignore_index, Tensor scale) -> (Tensor, Tensor)");
+  m.def("xent_mean_scale(Tensor target, int ignore_index) -> Tensor");
+  m.def("xent_loss_total(Tensor rows, Tensor scale) -> Tensor");
   m.def("gemm(Tensor a, Tensor b, Tensor(a!) c, bool a_km, bool b_kn, Tensor? bias, int epi, Tensor? aux_in, "
         "Tensor(b!)? aux_out, int splits, int tile, int accum=0) -> ()");
   m.def("gemm_pair(Tensor a1, Tensor b1, Tensor(a!) c1, int epi1, Tensor? aux_in1, Tensor a2, Tensor b2, "

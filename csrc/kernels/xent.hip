@@ -410,10 +410,76 @@ std::tuple<at::Tensor, at::Tensor> xent_fused_hip(const at::Tensor& logits, cons
   return {loss, lse};
 }
 
+// The mean reduction's two scalars, one launch each instead of torch's compare / sum / cast /
+// reciprocal and sum / multiply chains (six small kernels around the GPT-2 LM head, ≈ 35 µs per
+// step: docs/FINDINGS.md §36).  One 1024-thread workgroup; fixed summation order (deterministic).
+constexpr int kScalarThreads = 1024;
+
+__device__ __forceinline__ float block_sum_1024(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < kScalarThreads / 64; ++i) t += red[i];
+  return t;  // (valid in thread 0)
+}
+
+// scale[0] = 1 / #(target != ignore_index)  (+inf when every row is ignored: the loss is then nan, as torch)
+__global__ __launch_bounds__(kScalarThreads) void xent_mean_scale_kernel(const int64_t* __restrict__ target, int64_t n,
+                                                                         int64_t ignore_index, float* __restrict__ scale) {
+  __shared__ float red[kScalarThreads / 64];
+  float c = 0.f;  // exact: counts < 2^24
+  for (int64_t i = threadIdx.x; i < n; i += kScalarThreads) c += target[i] != ignore_index ? 1.f : 0.f;
+  const float t = block_sum_1024(c, red);
+  if (threadIdx.x == 0) scale[0] = 1.f / t;
+}
+
+// loss = Σ rows · scale[0]
+__global__ __launch_bounds__(kScalarThreads) void xent_loss_total_kernel(const float* __restrict__ rows, int64_t n,
+                                                                         const float* __restrict__ scale,
+                                                                         float* __restrict__ out) {
+  __shared__ float red[kScalarThreads / 64];
+  float c = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += kScalarThreads) c += rows[i];
+  const float t = block_sum_1024(c, red);
+  if (threadIdx.x == 0) out[0] = t * scale[0];
+}
+
+at::Tensor xent_mean_scale_hip(const at::Tensor& target, int64_t ignore_index) {
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == at::kLong && target.is_contiguous(),
+              "xent_mean_scale: contiguous int64 GPU targets expected");
+  at::Tensor scale = at::empty({1}, target.options().dtype(at::kFloat));
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(target.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  hipLaunchKernelGGL(xent_mean_scale_kernel, dim3(1), dim3(kScalarThreads), 0, st, target.data_ptr<int64_t>(),
+                     target.numel(), ignore_index, scale.data_ptr<float>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return scale;
+}
+
+at::Tensor xent_loss_total_hip(const at::Tensor& rows, const at::Tensor& scale) {
+  TORCH_CHECK(rows.is_cuda() && rows.scalar_type() == at::kFloat && rows.is_contiguous(),
+              "xent_loss_total: contiguous float32 GPU rows expected");
+  TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() == 1,
+              "xent_loss_total: scale must be a 1-element float32 GPU tensor");
+  at::Tensor out = at::empty({}, rows.options());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(rows.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  hipLaunchKernelGGL(xent_loss_total_kernel, dim3(1), dim3(kScalarThreads), 0, st, rows.data_ptr<float>(), rows.numel(),
+                     scale.data_ptr<float>(), out.data_ptr<float>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return out;
+}
+
 }  // namespace nbd
 
 TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
   m.impl("xent_fwd", &nbd::xent_fwd_hip);
   m.impl("xent_bwd", &nbd::xent_bwd_hip);
   m.impl("xent_fused", &nbd::xent_fused_hip);
+  m.impl("xent_mean_scale", &nbd::xent_mean_scale_hip);
+  m.impl("xent_loss_total", &nbd::xent_loss_total_hip);
 }

@@ -71,8 +71,8 @@ def _xent_fn():
                 # (csrc/kernels/gemm.hip "next-weight warm-up"; docs/FINDINGS.md §23)
                 if LM_HEAD_WARM_BYTES > 0 and wp.is_cuda and hasattr(torch.ops.nbd, "gemm_warm_hint"):
                     torch.ops.nbd.gemm_warm_hint(wp, False, LM_HEAD_WARM_BYTES)
-            if reduction == "mean":
-                scale = (1.0 / (target != ignore_index).sum().float()).reshape(1)  # inf (-> nan loss) if none
+            if reduction == "mean":  # 1 / #(non-ignored rows), one launch (inf -> nan loss if none)
+                scale = torch.ops.nbd.xent_mean_scale(target, ignore_index)
             else:
                 scale = torch.ones(1, dtype=torch.float32, device=h2.device)
             N = h2.shape[0]
@@ -107,23 +107,28 @@ def _xent_fn():
             ctx.plan = plan
             ctx.rows = w.shape[0]
             ctx.copied = wp is not w
-            return loss_rows.sum() * scale[0]
+            return torch.ops.nbd.xent_loss_total(loss_rows, scale)  # Σ rows · scale, one launch
 
         @staticmethod
         def backward(ctx, grad):
             from . import graddst
 
             h2, wp, dlogits, w, dh_fused = ctx.saved_tensors
-            g = grad.to(h2.dtype)
-            dh = None
-            if ctx.needs_input_grad[0]:
-                if dh_fused is not None:
-                    dh = dh_fused.mul_(g)
-                else:
-                    dh = (_hip_dgrad(dlogits, wp) if ctx.plan["dgrad"] else torch.mm(dlogits, wp)).mul_(g)
+            need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+            dh = hg = None
+            if need_h:
+                dh = dh_fused if dh_fused is not None else (
+                    _hip_dgrad(dlogits, wp) if ctx.plan["dgrad"] else torch.mm(dlogits, wp))
+            # the incoming gradient (1 after loss.backward()) scales dh and the weight gradient's
+            # operand: one multi-tensor launch for both, by the fp32 scalar as it arrives
+            if need_h and need_w:
+                dh, hg = torch._foreach_mul([dh, h2], grad)
+            elif need_h:
+                dh = dh.mul_(grad)
+            elif need_w:
+                hg = h2 * grad
             dw = None
-            if ctx.needs_input_grad[1]:
-                hg = h2 * g
+            if need_w:
                 dst, acc = graddst.claim(w) if not ctx.copied else (None, False)
                 if dst is not None:  # straight into the DDP bucket slice (graddst.py)
                     if ctx.plan["wgrad"]:
