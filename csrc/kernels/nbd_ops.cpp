@@ -26,6 +26,7 @@ TORCH_LIBRARY(nbd, m) {
   m.def("rms_bwd(Tensor x, Tensor dy, Tensor? dres, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
   m.def("embedding_bwd(Tensor dy, Tensor idx, int V, Tensor(a!)? grad_out=None, bool accumulate=False) -> Tensor");
   m.def("embedding_tokpos(Tensor idx, Tensor wte, Tensor pos, Tensor wpe, int vocab=-1, Tensor(a!)? err=None) -> Tensor");
+  m.def("embedding_pos_bwd(Tensor dy, Tensor pos, int P, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, int n_rot, int head_dim, bool inverse) -> ()");
   m.def("seqcls_prep(Tensor ids, Tensor? mask, int pad_id, bool has_pad, Tensor(a!) bad) -> (Tensor, Tensor)");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
@@ -35,6 +36,7 @@ TORCH_LIBRARY(nbd, m) {
   m.def("xent_fused(Tensor(a!) logits, Tensor target, int ignore_index, Tensor scale) -> (Tensor, Tensor)");
   m.def("xent_mean_scale(Tensor target, int ignore_index) -> Tensor");
   m.def("xent_loss_total(Tensor rows, Tensor scale) -> Tensor");
+  m.def("scale_pair_(Tensor(a!) a, Tensor b, Tensor g) -> Tensor");
   m.def("gemm(Tensor a, Tensor b, Tensor(a!) c, bool a_km, bool b_kn, Tensor? bias, int epi, Tensor? aux_in, "
         "Tensor(b!)? aux_out, int splits, int tile, int accum=0) -> ()");
   m.def("gemm_pair(Tensor a1, Tensor b1, Tensor(a!) c1, int epi1, Tensor? aux_in1, Tensor a2, Tensor b2, "

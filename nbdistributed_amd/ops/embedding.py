@@ -97,6 +97,9 @@ def _tokpos_fn():
             @staticmethod
             def forward(ctx, idx, wte, pos, wpe, vocab):
                 ctx.save_for_backward(idx, pos, wte)
+                # (the parameter itself, for its DDP bucket slice; a plain reference, not a saved
+                # tensor: its value is never read)
+                ctx.wpe = wpe if isinstance(wpe, torch.nn.Parameter) else None
                 V = vocab if 0 < vocab < wte.shape[0] else wte.shape[0]
                 ctx.shapes = (V, wpe.shape[0])
                 return torch.ops.nbd.embedding_tokpos(idx, wte, pos, wpe, V, _poll_ids(wte.device))
@@ -130,11 +133,20 @@ def _tokpos_fn():
                             d_wte = torch.ops.nbd.embedding_bwd(dy2, ids, V)
                 d_wpe = None
                 if ctx.needs_input_grad[3]:
-                    # positions repeat every T rows: sum the batch first (fp32), then place the T
-                    # rows (unique positions: index_add_ without collisions — deterministic)
-                    T = pos.numel()
-                    s = dy2.view(-1, T, C).sum(0, dtype=torch.float32)
-                    d_wpe = torch.zeros(P, C, dtype=torch.float32, device=dy.device).index_add_(0, pos, s).to(dy.dtype)
+                    # positions repeat every T rows: the batch summed per position in fp32 and
+                    # placed at its (unique) row — one launch, straight into the DDP bucket slice
+                    # when DDP registered one (graddst.py)
+                    wpe = ctx.wpe
+                    dst, acc = graddst.claim(wpe) if wpe is not None else (None, False)
+                    if dst is not None and (dst.dtype != dy2.dtype or tuple(dst.shape) != (P, C)):
+                        dst = dst.view(P, C) if dst.numel() == P * C and dst.dtype == dy2.dtype else None
+                        if dst is None:  # (a slice this op cannot write: return the gradient instead)
+                            raise RuntimeError("embedding_pos_bwd: unexpected DDP gradient slice for the position table")
+                    if dst is not None:
+                        torch.ops.nbd.embedding_pos_bwd(dy2, pos, P, dst, acc)
+                        d_wpe = graddst.hand_back(wpe, dst, acc)
+                    else:
+                        d_wpe = torch.ops.nbd.embedding_pos_bwd(dy2, pos, P)
                 return None, d_wte, None, d_wpe, None
 
         _TokPosFn = _TokPos

@@ -120,13 +120,15 @@ def _xent_fn():
                 dh = dh_fused if dh_fused is not None else (
                     _hip_dgrad(dlogits, wp) if ctx.plan["dgrad"] else torch.mm(dlogits, wp))
             # the incoming gradient (1 after loss.backward()) scales dh and the weight gradient's
-            # operand: one multi-tensor launch for both, by the fp32 scalar as it arrives
-            if need_h and need_w:
-                dh, hg = torch._foreach_mul([dh, h2], grad)
-            elif need_h:
-                dh = dh.mul_(grad)
-            elif need_w:
-                hg = h2 * grad
+            # operand: one launch for both (dh in place, hg = h2·g), by the fp32 scalar as it arrives
+            if need_h and need_w and dh.is_contiguous() and dh.numel() % 8 == 0 and h2.numel() % 8 == 0:
+                hg = torch.ops.nbd.scale_pair_(dh, h2, grad.float().reshape(1))
+            else:
+                g = grad.to(h2.dtype)
+                if need_h:
+                    dh = dh.mul_(g)
+                if need_w:
+                    hg = h2 * g
             dw = None
             if need_w:
                 dst, acc = graddst.claim(w) if not ctx.copied else (None, False)

@@ -211,3 +211,30 @@ def test_embedding_tok_pos_matches_two_lookups(dtype):
     assert (gt.float() - rt.float()).abs().max() <= tol * rt.float().abs().max()
     assert (gp.float() - rp.float()).abs().max() <= tol * rp.float().abs().max()
     assert float(gp[:64].float().abs().max()) == 0.0 and float(gp[64 + T:].float().abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_embedding_pos_bwd_op(dtype):
+    """The position table's gradient in one launch: permuted positions covering every row (no
+    zero fill), a partial cover (rows left zero), and accumulation into a given buffer — against
+    fp32 sum + index_add."""
+    g = torch.Generator(device="cuda").manual_seed(1)
+    B, T, C = 4, 96, 256
+    dy = torch.randn(B * T, C, device="cuda", generator=g).to(dtype)
+    ref_rows = dy.float().view(B, T, C).sum(0)
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    pos = torch.randperm(T, device="cuda", generator=g)
+    got = torch.ops.nbd.embedding_pos_bwd(dy, pos, T)
+    ref = torch.zeros(T, C, device="cuda").index_add_(0, pos, ref_rows)
+    assert (got.float() - ref).abs().max() <= tol * ref.abs().max()
+    P = 200
+    pos2 = torch.arange(50, 50 + T, device="cuda")
+    got2 = torch.ops.nbd.embedding_pos_bwd(dy, pos2, P)
+    ref2 = torch.zeros(P, C, device="cuda").index_add_(0, pos2, ref_rows)
+    assert (got2.float() - ref2).abs().max() <= tol * ref2.abs().max()
+    assert float(got2[:50].float().abs().max()) == 0.0 and float(got2[50 + T:].float().abs().max()) == 0.0
+    base = torch.randn(P, C, device="cuda", generator=g).to(dtype)
+    acc = base.clone()
+    torch.ops.nbd.embedding_pos_bwd(dy, pos2, P, acc, True)
+    ref3 = base.float() + ref2
+    assert (acc.float() - ref3).abs().max() <= 2 * tol * ref3.abs().max()

@@ -165,3 +165,31 @@ def test_linear_cross_entropy_mixed_products(dev, products, monkeypatch):
     F.cross_entropy(F.linear(hr, wr), tgt).backward()
     assert _rel(h.grad, hr.grad) < 3e-2 and _rel(w.grad, wr.grad) < 3e-2
     assert len(calls) == sum(not v for v in products.values())
+
+
+@pytest.mark.parametrize("n", [1, 96, 8192, 70001])
+def test_loss_scalar_ops(dev, n):
+    """xent_mean_scale / xent_loss_total (the mean reduction's two one-launch scalars) and
+    scale_pair_ (the backward's dh *= g, h·g) against fp32 PyTorch."""
+    torch.manual_seed(n)
+    tgt = torch.randint(0, 50, (n,), device=dev)
+    tgt[::3] = -100
+    valid = int((tgt != -100).sum())
+    s = torch.ops.nbd.xent_mean_scale(tgt, -100)
+    assert s.shape == (1,) and s.dtype == torch.float32
+    assert (float(s) == float("inf")) if valid == 0 else abs(float(s) * valid - 1.0) < 1e-6  # fp32 reciprocal
+    rows = torch.randn(n, device=dev)
+    tot = torch.ops.nbd.xent_loss_total(rows, s if valid else torch.ones(1, device=dev))
+    ref = rows.double().sum() * (float(s) if valid else 1.0)
+    assert tot.dim() == 0 and abs(float(tot) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
+    a = torch.randn(n * 8, device=dev).to(torch.bfloat16)
+    b = torch.randn(n * 8, device=dev).to(torch.bfloat16)
+    g = torch.tensor([0.37], device=dev)
+    a_ref, b_ref = (a.float() * 0.37).to(torch.bfloat16), (b.float() * 0.37).to(torch.bfloat16)
+    out = torch.ops.nbd.scale_pair_(a, b, g)
+    assert torch.equal(a, a_ref) and torch.equal(out, b_ref)
+
+
+def test_mean_scale_all_ignored(dev):
+    tgt = torch.full((64,), -100, device=dev)
+    assert float(torch.ops.nbd.xent_mean_scale(tgt, -100)) == float("inf")
