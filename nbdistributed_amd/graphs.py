@@ -188,8 +188,18 @@ class GraphedStep:
     def __call__(self, *args):
         if len(args) != len(self.static_args):
             raise ValueError(f"GraphedStep: expected {len(self.static_args)} arguments, got {len(args)}")
+        dsts, srcs = [], []
         for dst, src in zip(self.static_args, args):
-            _copy_into(dst, src)
+            if isinstance(dst, torch.Tensor) and isinstance(src, torch.Tensor) and src.device == dst.device:
+                if src.shape != dst.shape or src.dtype != dst.dtype:
+                    _copy_into(dst, src)  # (raises with the mismatch)
+                if src.data_ptr() != dst.data_ptr():
+                    dsts.append(dst)
+                    srcs.append(src)
+            else:
+                _copy_into(dst, src)
+        if dsts:  # the step's device inputs in one multi-tensor launch, not one copy each
+            torch._foreach_copy_(dsts, srcs, non_blocking=True)
         self._sync_hyper()
         for c in self._checks:
             c.before_replay()

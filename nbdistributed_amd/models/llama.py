@@ -580,11 +580,18 @@ class LlamaForSequenceClassification(_LlamaPreTrained):
             chk.arm(1, "with holes (not one contiguous run per row) is not supported by the fused path")
             h = self.model(ids)
         B, T, C = h.shape
+        w = self.score.weight
+        no_hooks = not self.score._forward_hooks and not self.score._forward_pre_hooks
+        if (labels is not None and self.score.bias is None and no_hooks and w.dtype == h.dtype
+                and ops.tiny.seqcls_ok(h, w, labels.view(-1))):
+            # the whole tail (pooling gather, score head, mean cross-entropy) in one HIP launch,
+            # its backward in one (csrc/kernels/tiny.hip seqcls): ≈ 14 torch / library launches less
+            loss, logits = ops.tiny.seqcls_head_loss(h, last, w, labels.view(-1))
+            return SequenceClassifierOutput(loss, logits)
         # gather (backward = scatter-add: no sort, graph-safe) instead of advanced indexing
         pooled = torch.gather(h, 1, last.view(B, 1, 1).expand(B, 1, C)).squeeze(1)
-        w = self.score.weight
-        if (pooled.is_cuda and self.score.bias is None and not self.score._forward_hooks
-                and not self.score._forward_pre_hooks and ops.tiny.shape_ok(pooled, w.shape[0], w.shape[1])):
+        if (pooled.is_cuda and self.score.bias is None and no_hooks
+                and ops.tiny.shape_ok(pooled, w.shape[0], w.shape[1])):
             # the classifier head (N = num_labels) on the tiny-linear HIP kernels: one launch
             # forward, one backward (dx, dW together) instead of three library GEMMs
             logits = ops.linear_tiny(pooled, w if w.dtype == pooled.dtype else w.to(pooled.dtype))

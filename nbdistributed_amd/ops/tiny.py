@@ -79,3 +79,70 @@ def linear_tiny(x, weight, bias=None):
     import torch.nn.functional as F
 
     return F.linear(x, weight, bias)
+
+
+# ---- the sequence-classification tail, fused (pooled row -> score -> mean cross-entropy) ------
+_SeqFn = None
+MAX_ROWS = 64
+
+
+def seqcls_ok(h, weight, labels) -> bool:
+    """h [B, T, C] bf16 (GPU, contiguous), ``weight`` [N, C] bf16, integer ``labels`` [B]: fits
+    ``nbd::seqcls_head`` (B <= 64, N <= 64, B·N <= 1024, C % 8 == 0)."""
+    import torch
+
+    return bool(ENABLED and h.is_cuda and h.dim() == 3 and h.dtype == torch.bfloat16 and weight.dim() == 2
+                and weight.dtype == torch.bfloat16 and weight.shape[1] == h.shape[2] and h.shape[2] % 8 == 0
+                and 1 <= h.shape[0] <= MAX_ROWS and 1 <= weight.shape[0] <= MAX_N
+                and h.shape[0] * weight.shape[0] <= 1024 and labels is not None
+                and labels.dtype in (torch.int64, torch.int32) and labels.numel() == h.shape[0])
+
+
+def _seq_fn():
+    global _SeqFn
+    if _SeqFn is not None:
+        return _SeqFn
+    import torch
+
+    class _SeqClsHead(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, h, last, w, labels, ignore_index):
+            h = h if h.is_contiguous() and h.data_ptr() % 16 == 0 else h.contiguous()
+            w2 = w if w.is_contiguous() and w.data_ptr() % 16 == 0 else w.contiguous()
+            loss, logits, dl = torch.ops.nbd.seqcls_head(h, last, w2, labels, int(ignore_index))
+            ctx.save_for_backward(h, last, w2, dl)
+            ctx.set_materialize_grads(False)  # an unused output's gradient arrives as None, not a zero fill
+            ctx.param = w if isinstance(w, torch.nn.Parameter) else None
+            return loss, logits
+
+        @staticmethod
+        def backward(ctx, g_loss, g_logits):
+            from . import graddst
+
+            h, last, w2, dl = ctx.saved_tensors
+            need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[2]
+            if not (need_h or need_w):
+                return None, None, None, None, None
+            g = (g_loss.float().reshape(1) if g_loss is not None
+                 else torch.zeros(1, dtype=torch.float32, device=h.device))
+            glog = g_logits.to(torch.bfloat16).contiguous() if g_logits is not None else None
+            dst, acc = graddst.claim(ctx.param) if need_w and ctx.param is not None else (None, False)
+            if dst is not None and (dst.dtype != torch.bfloat16 or dst.shape != w2.shape or not dst.is_contiguous()):
+                raise RuntimeError("seqcls_head: unexpected DDP gradient slice for the score weight")
+            dh, dw = torch.ops.nbd.seqcls_head_bwd(h, last, w2, dl, g, glog, dst, acc)
+            if dst is not None:
+                dw = graddst.hand_back(ctx.param, dst, acc)
+            return (dh if need_h else None), None, (dw if need_w else None), None, None
+
+    _SeqFn = _SeqClsHead
+    return _SeqFn
+
+
+def seqcls_head_loss(h, last, weight, labels, ignore_index: int = -100):
+    """(loss, logits) of a sequence classifier's tail — ``pooled = h[b, last[b]]``, ``logits =
+    pooled·weightᵀ`` (bf16, as ``F.linear``), ``loss = F.cross_entropy(logits.float(), labels)``
+    (mean over rows whose label is not ``ignore_index``) — in one HIP launch forward and one
+    backward (``csrc/kernels/tiny.hip`` seqcls); the caller checks ``seqcls_ok`` first."""
+    _require()
+    return _seq_fn().apply(h, last.reshape(-1).long().contiguous(), weight, labels.reshape(-1).long().contiguous(),
+                           int(ignore_index))
