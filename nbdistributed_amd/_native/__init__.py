@@ -83,14 +83,18 @@ def _hash_file(lib: Path) -> Path:
 
 
 def _fresh(lib: Path, deps: List[Path], salt: str) -> bool:
+    """Built from exactly these sources: no source newer than the library, and — when the build
+    left its source hash — the same set of files (a deleted or added source changes the hash
+    without changing any mtime)."""
     if not lib.exists():
         return False
-    if not _stale(lib, deps):
-        return True
     try:
-        return _hash_file(lib).read_text().strip() == source_hash(deps, salt)
+        stored = _hash_file(lib).read_text().strip()
     except OSError:
-        return False
+        stored = None
+    if not _stale(lib, deps):
+        return stored is None or stored == source_hash(deps, salt)
+    return stored is not None and stored == source_hash(deps, salt)
 
 
 def _writable(d: Path) -> bool:

@@ -95,3 +95,28 @@ def test_pip_install_read_only_ipython():
     finally:
         subprocess.run(["chmod", "-R", "u+w", str(target)])
         shutil.rmtree(tmp_path, ignore_errors=True)
+
+
+def test_fresh_detects_added_and_removed_sources(tmp_path):
+    """A library is fresh only for the exact source set it was built from: deleting (or adding)
+    a source changes the stored hash although no remaining file is newer than the library."""
+    import os
+    import time
+
+    from nbdistributed_amd import _native as N
+
+    srcs = [tmp_path / f"k{i}.hip" for i in range(3)]
+    for i, p in enumerate(srcs):
+        p.write_text(f"// kernel {i}\n")
+    lib = tmp_path / "libx.so"
+    time.sleep(0.01)
+    lib.write_bytes(b"\0")
+    N._hash_file(lib).write_text(N.source_hash(srcs, "salt") + "\n")
+    assert N._fresh(lib, srcs, "salt")
+    assert not N._fresh(lib, srcs[:2], "salt")  # a source removed since the build
+    extra = tmp_path / "k9.hip"
+    extra.write_text("// new\n")
+    os.utime(extra, (lib.stat().st_mtime - 10, lib.stat().st_mtime - 10))  # older than the library
+    assert not N._fresh(lib, srcs + [extra], "salt")  # a source added since the build
+    N._hash_file(lib).unlink()
+    assert N._fresh(lib, srcs, "salt")  # no stored hash: the mtimes decide
