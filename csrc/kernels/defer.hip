@@ -206,7 +206,33 @@ void launch_col(const std::vector<const Item*>& items) {
   }
 }
 
+// ---- the carried split-K reduce (graddst.h push_carry / take_carry): one slot
+bool carry_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NBD_GEMM_CARRY");  // 0: launch large reduces at once (A/B)
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+bool c_has = false;
+Item c_item;
+hipStream_t c_stream = nullptr;
+int c_device = -1;
+bool c_capturing = false;
+
+void flush_carry_locked() {
+  if (!c_has) return;
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)c_device));
+  hipStream_t prev = q_stream;
+  q_stream = c_stream;
+  launch_split({&c_item});
+  q_stream = prev;
+  c_item = Item{};
+  c_has = false;
+}
+
 void flush_locked() {
+  flush_carry_locked();
   if (q_items.empty()) return;
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)q_device));
   std::vector<const Item*> split, col;
@@ -276,7 +302,7 @@ void flush() {
 
 int64_t pending() {
   std::lock_guard<std::mutex> lk(q_mu);
-  return (int64_t)q_items.size();
+  return (int64_t)q_items.size() + (c_has ? 1 : 0);
 }
 
 // A captured graph's deferred reductions: recorded at capture instead of queued (their partial
@@ -304,6 +330,53 @@ void replay(const std::shared_ptr<void>& rec, void* stream) {
 bool push_splitk(const at::Tensor& ws, int splits, int64_t n8, int64_t m8, int64_t slab, uint16_t* out,
                  uint16_t* rs_out, int accum, void* stream) {
   return push(Item{0, ws, out, rs_out, n8, m8, slab, splits, accum}, stream);
+}
+
+bool push_carry(const at::Tensor& ws, int splits, int64_t n8, int64_t m8, int64_t slab, uint16_t* out,
+                uint16_t* rs_out, int accum, void* stream) {
+  if (!carry_enabled() || t_record != nullptr) return false;  // (block-graph records: launch at once)
+  std::lock_guard<std::mutex> lk(q_mu);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  C10_HIP_CHECK(hipStreamIsCapturing(st, &cs));
+  flush_carry_locked();  // (one slot: a carry nobody took goes now)
+  c_item = Item{0, ws, out, rs_out, n8, m8, slab, splits, accum};
+  c_stream = st;
+  c_device = ws.get_device();
+  c_capturing = cs == hipStreamCaptureStatusActive;
+  c_has = true;
+  if (!q_callback) {  // finished by the end of this backward at the latest (as push)
+    try {
+      torch::autograd::Engine::get_default_engine().queue_callback([] { flush(); });
+      q_callback = true;
+    } catch (const std::exception&) {
+      flush_carry_locked();
+    }
+  }
+  return true;
+}
+
+bool take_carry(void* stream, Carry* c) {
+  std::lock_guard<std::mutex> lk(q_mu);
+  if (!c_has) return false;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  C10_HIP_CHECK(hipStreamIsCapturing(st, &cs));
+  if (st != c_stream || (cs == hipStreamCaptureStatusActive) != c_capturing) {
+    flush_carry_locked();  // another stream / capture state: launch it on its own
+    return false;
+  }
+  c->buf = std::move(c_item.buf);
+  c->out = c_item.out0;
+  c->rs_out = c_item.out1;
+  c->n8 = c_item.a;
+  c->m8 = c_item.b;
+  c->slab = c_item.c;
+  c->splits = c_item.d;
+  c->accum = c_item.accum;
+  c_item = Item{};
+  c_has = false;
+  return true;
 }
 
 bool push_colred(const at::Tensor& part, int nparts, int ld, int W, int C, uint16_t* out0, uint16_t* out1, int accum,

@@ -535,13 +535,54 @@ __global__ __launch_bounds__(64 * W * KS, KS == 1 ? 2 : 1) void gemm_kernel(Args
 // dispatcher hands out blocks in id order as slots free up, so the half with the longer units
 // goes first (longest-processing-time order): a short-unit half dispatched first leaves the
 // long units as a serial tail once it drains (ops/gemm.py pair_plan).
+// A split-K reduce carried into a launch (graddst.h defer::take_carry): out[i] (+)= Σ_s ws[s][i]
+// over the launch's last `blocks` workgroups — reduce_kernel's sums, in its order.
+struct Red {
+  const float* ws;
+  uint16_t* out;
+  uint16_t* rs_out;
+  int64_t n8, m8, slab;
+  int splits, accum, blocks;
+};
+
+__device__ __forceinline__ void reduce_body(const Red& r, int blk, int nthreads) {
+  for (int64_t i = (int64_t)blk * nthreads + threadIdx.x; i < r.n8 + r.m8; i += (int64_t)r.blocks * nthreads) {
+    const bool rs = i >= r.n8;
+    const float* src = rs ? r.ws + r.splits * r.slab + 8 * (i - r.n8) : r.ws + 8 * i;
+    const int64_t stride = rs ? r.m8 * 8 : r.slab;
+    float v[8];
+    load8<float>(src, v);
+    for (int s = 1; s < r.splits; ++s) {
+      float w[8];
+      load8<float>(src + s * stride, w);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += w[e];
+    }
+    bf16_t* dst = reinterpret_cast<bf16_t*>(rs ? r.rs_out : r.out) + 8 * (rs ? i - r.n8 : i);
+    if (r.accum & (rs ? 2 : 1)) {
+      float o[8];
+      load8<bf16_t>(dst, o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += o[e];
+    }
+    store8<bf16_t>(dst, v);
+  }
+}
+
 template <int BM, int BN, int W, int STAGES, int EPI1, int EPI2>
 __global__ __launch_bounds__(64 * W, W == 8 ? 2 : 2) void pair_kernel(Args p1, int t1, int first, Args p2, int t2, int s2,
-                                                                      int wfirst) {
+                                                                      int wfirst, Red red) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<BM, BN, STAGES, 1>::BYTES];
   const int b = (int)blockIdx.x - p1.warm_blocks;  // warm-up blocks first (gemm_kernel)
   if (b < 0) {
     warm_lines<64 * W>(p1, blockIdx.x, p1.warm_blocks);
+    return;
+  }
+  // the carried reduce in the grid's last workgroups: dispatched after every tile, they fill the
+  // CUs the tail round leaves idle
+  const int nmain = (int)gridDim.x - p1.warm_blocks - red.blocks;
+  if (b >= nmain) {
+    reduce_body(red, b - nmain, 64 * W);
     return;
   }
   const bool dgrad = wfirst ? b >= first : b < first;
@@ -588,7 +629,9 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ w
 // gradient written into its claimed bucket slice, autograd.hip), else launched now
 static void splitk_reduce(const at::Tensor& ws, int S, int64_t n8, int64_t slab, uint16_t* out, int64_t m8,
                           uint16_t* rs_out, int accum, hipStream_t st) {
-  if (defer::want() && defer::push_splitk(ws, S, n8, m8, slab, out, rs_out, accum, st)) return;
+  if (defer::want() && (defer::push_splitk(ws, S, n8, m8, slab, out, rs_out, accum, st) ||
+                         defer::push_carry(ws, S, n8, m8, slab, out, rs_out, accum, st)))
+    return;
   const int blocks = (int)std::min<int64_t>((n8 + m8 + 255) / 256, 2048);
   hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, st, ws.data_ptr<float>(), S, n8, slab, out, m8,
                      rs_out, accum);
@@ -1126,7 +1169,16 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
       p1.warm_blocks = warm::blocks_for(p1.pf_lines, big ? 512 : 256);
     }
   }
-  const int64_t nblocks = (int64_t)p1.warm_blocks + nb1 + nb2;
+  // a previous product's large split-K reduce rides in this grid's tail (defer::take_carry)
+  Red red{};
+  defer::Carry carried;
+  if (defer::take_carry(st, &carried)) {
+    red = Red{carried.buf.data_ptr<float>(), carried.out, carried.rs_out, carried.n8, carried.m8, carried.slab,
+              carried.splits, carried.accum, 0};
+    const int nt = big ? 512 : 256;  // threads per workgroup of this launch
+    red.blocks = (int)std::min<int64_t>((carried.n8 + carried.m8 + 4LL * nt - 1) / (4LL * nt), 1024);
+  }
+  const int64_t nblocks = (int64_t)p1.warm_blocks + nb1 + nb2 + red.blocks;
   TORCH_CHECK(nblocks < (1LL << 31), "nbd::gemm_pair: grid too large");
   const dim3 grid((unsigned)nblocks);
   // NBD_GEMM_PAIR_PP=1: the 128x128 halves on the ping-pong schedule (one workgroup per CU)
@@ -1135,11 +1187,14 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   auto launch = [&](auto e1, auto e2) {
     constexpr int E1 = decltype(e1)::value, E2 = decltype(e2)::value;
     if (big && pp)
-      hipLaunchKernelGGL((pair_kernel<128, 128, 8, 103, E1, E2>), grid, dim3(512), 0, st, p1, t1, first, p2, t2, S, wfirst);
+      hipLaunchKernelGGL((pair_kernel<128, 128, 8, 103, E1, E2>), grid, dim3(512), 0, st, p1, t1, first, p2, t2, S, wfirst,
+                         red);
     else if (big)
-      hipLaunchKernelGGL((pair_kernel<128, 128, 8, 2, E1, E2>), grid, dim3(512), 0, st, p1, t1, first, p2, t2, S, wfirst);
+      hipLaunchKernelGGL((pair_kernel<128, 128, 8, 2, E1, E2>), grid, dim3(512), 0, st, p1, t1, first, p2, t2, S, wfirst,
+                         red);
     else
-      hipLaunchKernelGGL((pair_kernel<64, 64, 4, 3, E1, E2>), grid, dim3(256), 0, st, p1, t1, first, p2, t2, S, wfirst);
+      hipLaunchKernelGGL((pair_kernel<64, 64, 4, 3, E1, E2>), grid, dim3(256), 0, st, p1, t1, first, p2, t2, S, wfirst,
+                         red);
   };
   using I0 = std::integral_constant<int, EPI_NONE>;
   using I2 = std::integral_constant<int, EPI_DGELU>;

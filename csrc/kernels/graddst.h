@@ -80,6 +80,19 @@ bool push_colred(const at::Tensor& part, int nparts, int ld, int W, int C, uint1
                  void* stream);
 void flush();
 int64_t pending();
+// A split-K reduce too large to queue (its slabs are read best while still in the MALL) can ride
+// in the NEXT grouped GEMM launch on the same stream as extra workgroups (gemm.hip pair_kernel's
+// tail) instead of a launch of its own; flush() and every flush point above launch it alone.
+struct Carry {
+  at::Tensor buf;  // the fp32 slabs (kept alive until the launch that reads them is enqueued)
+  uint16_t* out;
+  uint16_t* rs_out;
+  int64_t n8, m8, slab;
+  int splits, accum;
+};
+bool push_carry(const at::Tensor& ws, int splits, int64_t n8, int64_t m8, int64_t slab, uint16_t* out,
+                uint16_t* rs_out, int accum, void* stream);
+bool take_carry(void* stream, Carry* c);  // the pending carry for a launch on `stream` (false: none)
 // Recording (this thread, around a graph capture): pushes are kept in the record, not queued;
 // replay() queues the recorded reductions on `stream` (after each replay of that graph).
 void record_begin();
