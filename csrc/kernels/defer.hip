@@ -356,27 +356,47 @@ bool push_carry(const at::Tensor& ws, int splits, int64_t n8, int64_t m8, int64_
   return true;
 }
 
-bool take_carry(void* stream, Carry* c) {
+static void to_carry(Item& it, Carry* c) {
+  c->buf = std::move(it.buf);
+  c->out = it.out0;
+  c->rs_out = it.out1;
+  c->n8 = it.a;
+  c->m8 = it.b;
+  c->slab = it.c;
+  c->splits = it.d;
+  c->accum = it.accum;
+}
+
+int take_carry(void* stream, Carry* c, int max) {
   std::lock_guard<std::mutex> lk(q_mu);
-  if (!c_has) return false;
+  if (max <= 0 || (!c_has && q_items.empty())) return 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   C10_HIP_CHECK(hipStreamIsCapturing(st, &cs));
-  if (st != c_stream || (cs == hipStreamCaptureStatusActive) != c_capturing) {
-    flush_carry_locked();  // another stream / capture state: launch it on its own
-    return false;
+  const bool capturing = cs == hipStreamCaptureStatusActive;
+  int n = 0;
+  if (c_has) {
+    if (st != c_stream || capturing != c_capturing) {
+      flush_carry_locked();  // another stream / capture state: launch it on its own
+    } else {
+      to_carry(c_item, &c[n++]);
+      c_item = Item{};
+      c_has = false;
+    }
   }
-  c->buf = std::move(c_item.buf);
-  c->out = c_item.out0;
-  c->rs_out = c_item.out1;
-  c->n8 = c_item.a;
-  c->m8 = c_item.b;
-  c->slab = c_item.c;
-  c->splits = c_item.d;
-  c->accum = c_item.accum;
-  c_item = Item{};
-  c_has = false;
-  return true;
+  // queued split-K reduces of this stream and capture state, oldest first
+  if (!q_items.empty() && st == q_stream && capturing == q_capturing) {
+    for (size_t i = 0; i < q_items.size() && n < max;) {
+      if (q_items[i].kind != 0) {
+        ++i;
+        continue;
+      }
+      q_bytes -= (int64_t)q_items[i].buf.numel() * (int64_t)q_items[i].buf.element_size();
+      to_carry(q_items[i], &c[n++]);
+      q_items.erase(q_items.begin() + (int64_t)i);
+    }
+  }
+  return n;
 }
 
 bool push_colred(const at::Tensor& part, int nparts, int ld, int W, int C, uint16_t* out0, uint16_t* out1, int accum,

@@ -544,6 +544,11 @@ struct Red {
   int64_t n8, m8, slab;
   int splits, accum, blocks;
 };
+constexpr int kRedMax = 4;  // reduces per launch (kernel-argument table)
+struct RedTable {
+  Red d[kRedMax];
+  int n, blocks;  // descriptors, their workgroups in total
+};
 
 __device__ __forceinline__ void reduce_body(const Red& r, int blk, int nthreads) {
   for (int64_t i = (int64_t)blk * nthreads + threadIdx.x; i < r.n8 + r.m8; i += (int64_t)r.blocks * nthreads) {
@@ -571,7 +576,7 @@ __device__ __forceinline__ void reduce_body(const Red& r, int blk, int nthreads)
 
 template <int BM, int BN, int W, int STAGES, int EPI1, int EPI2>
 __global__ __launch_bounds__(64 * W, W == 8 ? 2 : 2) void pair_kernel(Args p1, int t1, int first, Args p2, int t2, int s2,
-                                                                      int wfirst, Red red) {
+                                                                      int wfirst, RedTable red) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem_all[Smem<BM, BN, STAGES, 1>::BYTES];
   const int b = (int)blockIdx.x - p1.warm_blocks;  // warm-up blocks first (gemm_kernel)
   if (b < 0) {
@@ -582,7 +587,9 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : 2) void pair_kernel(Args p1, i
   // CUs the tail round leaves idle
   const int nmain = (int)gridDim.x - p1.warm_blocks - red.blocks;
   if (b >= nmain) {
-    reduce_body(red, b - nmain, 64 * W);
+    int r = b - nmain, d = 0;
+    while (d + 1 < red.n && r >= red.d[d].blocks) r -= red.d[d++].blocks;  // (block-uniform)
+    reduce_body(red.d[d], r, 64 * W);
     return;
   }
   const bool dgrad = wfirst ? b >= first : b < first;
@@ -1170,13 +1177,21 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
     }
   }
   // a previous product's large split-K reduce rides in this grid's tail (defer::take_carry)
-  Red red{};
-  defer::Carry carried;
-  if (defer::take_carry(st, &carried)) {
-    red = Red{carried.buf.data_ptr<float>(), carried.out, carried.rs_out, carried.n8, carried.m8, carried.slab,
-              carried.splits, carried.accum, 0};
+  // (NBD_GEMM_CARRY_QUEUED=1: also up to kRedMax - 1 queued small ones, which then need no flush
+  // launch — measured no faster on the notebook step, whose flushes are few: FINDINGS §36)
+  static const int take_max = [] {
+    const char* e = std::getenv("NBD_GEMM_CARRY_QUEUED");
+    return e != nullptr && e[0] == '1' ? kRedMax : 1;
+  }();
+  RedTable red{};
+  defer::Carry carried[kRedMax];
+  red.n = defer::take_carry(st, carried, take_max);
+  for (int i = 0; i < red.n; ++i) {
+    const defer::Carry& c = carried[i];
     const int nt = big ? 512 : 256;  // threads per workgroup of this launch
-    red.blocks = (int)std::min<int64_t>((carried.n8 + carried.m8 + 4LL * nt - 1) / (4LL * nt), 1024);
+    red.d[i] = Red{c.buf.data_ptr<float>(), c.out, c.rs_out, c.n8, c.m8, c.slab, c.splits, c.accum,
+                   (int)std::max<int64_t>(1, std::min<int64_t>((c.n8 + c.m8 + 4LL * nt - 1) / (4LL * nt), 1024))};
+    red.blocks += red.d[i].blocks;
   }
   const int64_t nblocks = (int64_t)p1.warm_blocks + nb1 + nb2 + red.blocks;
   TORCH_CHECK(nblocks < (1LL << 31), "nbd::gemm_pair: grid too large");

@@ -92,7 +92,9 @@ struct Carry {
 };
 bool push_carry(const at::Tensor& ws, int splits, int64_t n8, int64_t m8, int64_t slab, uint16_t* out,
                 uint16_t* rs_out, int accum, void* stream);
-bool take_carry(void* stream, Carry* c);  // the pending carry for a launch on `stream` (false: none)
+// up to `max` reduces for a launch on `stream`: the carry first, then queued split-K reduces
+// (theirs are small; summed in a grid's tail they need no flush launch); returns how many
+int take_carry(void* stream, Carry* c, int max);
 // Recording (this thread, around a graph capture): pushes are kept in the record, not queued;
 // replay() queues the recorded reductions on `stream` (after each replay of that graph).
 void record_begin();
