@@ -198,6 +198,21 @@ _TUNED = {
 # 57.4 whole, profiles/gpt2_graph_prof_r6a.md)
 _TUNED_EPI: dict = {}
 
+
+def _env_tuned(spec: str) -> dict:
+    """NBD_GEMM_TUNE (in-step A/B runs): entries "a_km:b_kn:M:N:K=tile:splits" joined by "+",
+    e.g. "0:0:2048:576:576=203064064:1", overriding the measured table."""
+    out = {}
+    for ent in filter(None, (e.strip() for e in spec.split("+"))):
+        key, val = ent.split("=")
+        a, b, m, n, k = (int(v) for v in key.split(":"))
+        t, sp = (int(v) for v in val.split(":"))
+        out[(bool(a), bool(b), m, n, k)] = (t, sp)
+    return out
+
+
+_TUNED.update(_env_tuned(os.environ.get("NBD_GEMM_TUNE", "")))
+
 _TILES = (128128, 128064, 64128, 64064)  # (+ 128096: forward only, tuned entries)
 
 
