@@ -566,8 +566,38 @@ def _fast(x, *ws) -> bool:
     return all(w.dtype == torch.bfloat16 and w.shape[-1] % 64 == 0 and w.shape[0] % 64 == 0 for w in ws)
 
 
+# rows (tokens) not a multiple of 64: pad them with zero rows for the HIP kernels instead of
+# falling back to the library (NBD_GEMM_PAD_ROWS=0: the library for such shapes)
+PAD_ROWS = os.environ.get("NBD_GEMM_PAD_ROWS", "1") != "0"
+
+
+def _pad_rows(x, *ws):
+    """(x as [M64, K] with zero rows appended, M) when only the row count keeps ``x`` off the HIP
+    kernels (the weights' dims are multiples of 64), else None.  Autograd sees a pad and a slice:
+    the padded rows' gradients are dropped, and zero rows add nothing to a weight gradient."""
+    import torch
+
+    if not (PAD_ROWS and ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and not torch.is_autocast_enabled()
+            and x.dim() >= 1 and x.shape[-1] % 64 == 0):
+        return None
+    M = x.numel() // max(1, x.shape[-1])
+    if M == 0 or M % 64 == 0:
+        return None
+    if not all(w.dtype == torch.bfloat16 and w.shape[-1] % 64 == 0 and w.shape[0] % 64 == 0 for w in ws):
+        return None
+    import torch.nn.functional as F
+
+    # to a multiple of 256, not 64: the measured table and the 128-row tiles are for such counts
+    # (M = 8100 padded to 8128 ran 10-40 % slower than to 8192: profiles/odd_rows_r6.txt)
+    return F.pad(x.reshape(M, x.shape[-1]), (0, 0, 0, (-M) % 256)), M
+
+
 def gemm_linear(x, weight, bias=None):
-    """``F.linear`` on the HIP MFMA GEMM (bf16, dims multiple of 64); PyTorch otherwise."""
+    """``F.linear`` on the HIP MFMA GEMM (bf16; weight dims multiples of 64, a row count that is
+    not is padded); PyTorch otherwise."""
+    pr = _pad_rows(x, weight)
+    if pr is not None:
+        return gemm_linear(pr[0], weight, bias)[:pr[1]].reshape(*x.shape[:-1], weight.shape[0])
     if _fast(x, weight):
         if _native(bias):
             import torch
@@ -582,6 +612,9 @@ def gemm_linear(x, weight, bias=None):
 
 def mlp_gelu(x, w1, b1, w2, b2):
     """``F.linear(gelu_tanh(F.linear(x, w1, b1)), w2, b2)`` with the activation fused into the GEMMs."""
+    pr = _pad_rows(x, w1, w2)
+    if pr is not None:
+        return mlp_gelu(pr[0], w1, b1, w2, b2)[:pr[1]].reshape(*x.shape[:-1], w2.shape[0])
     if _fast(x, w1, w2):
         if _native(b1, b2):
             import torch
@@ -597,6 +630,9 @@ def mlp_gelu(x, w1, b1, w2, b2):
 def mlp_swiglu(x, w_gu, w_down):
     """Llama MLP ``down(silu(g)·u)`` with ``[g|u] = F.linear(x, w_gu)`` (``w_gu`` = [gate; up],
     [2I, H]) — SwiGLU and its backward fused into the GEMM epilogues on the GPU path."""
+    pr = _pad_rows(x, w_gu, w_down) if FUSED_SWIGLU else None
+    if pr is not None:
+        return mlp_swiglu(pr[0], w_gu, w_down)[:pr[1]].reshape(*x.shape[:-1], w_down.shape[0])
     if FUSED_SWIGLU and _fast(x, w_gu, w_down):
         if _native():
             import torch
@@ -634,8 +670,8 @@ def linear_any(x, weight, bias=None):
     is the forward ``parallel.DistributedDataParallel(fused_linear=True)`` gives ``nn.Linear``."""
     import torch
 
-    if _fast(x, weight) and _native(bias):
-        return gemm_linear(x, weight, bias)
+    if (_fast(x, weight) or _pad_rows(x, weight) is not None) and _native(bias):
+        return gemm_linear(x, weight, bias)  # (a row count off the 64-grid is padded there)
     # bf16 heads with a tiny output dimension (classifiers: N <= 64): the tiny-linear kernels
     from .tiny import linear_tiny, supported as _tiny_ok
 

@@ -427,3 +427,34 @@ def test_gemm_column_split_dgrad_layout(N):
     want = G._dgelu_ref(ref.to(torch.bfloat16), pre).float()
     got = G.matmul(a, b, b_kn=True, epi=G.EPI_DGELU, aux=pre, tile=G.COLSPLIT + 82128128, splits=1)
     assert _err(got, want) < 2e-2
+
+
+@pytest.mark.parametrize("M", [1, 63, 1000, 8001])
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemm_linear_odd_rows_padded(M, bias):
+    """A row count off the 64-grid runs on the HIP kernels with zero rows appended (no library
+    GEMM): output, input / weight / bias gradients against fp32."""
+    import torch.nn.functional as F
+
+    from nbdistributed_amd.ops import gemm as G
+
+    torch.manual_seed(M)
+    x = torch.randn(M, 256, device="cuda").to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(192, 256, device="cuda") * 0.05).to(torch.bfloat16).requires_grad_()
+    b = (torch.randn(192, device="cuda") * 0.1).to(torch.bfloat16).requires_grad_() if bias else None
+    assert G._pad_rows(x, w) is not None
+    y = G.gemm_linear(x, w, b)
+    assert y.shape == (M, 192)
+    dy = torch.randn(M, 192, device="cuda").to(torch.bfloat16)
+    y.backward(dy)
+    xf, wf = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    bf = b.detach().float().requires_grad_() if bias else None
+    yf = F.linear(xf, wf, bf)
+    yf.backward(dy.float())
+
+    def rel(a, r):
+        return float((a.float() - r).abs().max() / r.abs().max().clamp_min(1e-6))
+
+    assert rel(y, yf) < 1e-2 and rel(x.grad, xf.grad) < 1e-2 and rel(w.grad, wf.grad) < 2e-2
+    if bias:
+        assert rel(b.grad, bf.grad) < 2e-2
