@@ -87,6 +87,14 @@ _PAIR_TUNED = {
 }
 
 
+# NBD_GEMM_PAIR_TUNE (in-step A/B runs): entries "M:N:K:epi1=S:wfirst" joined by "+"
+for _ent in filter(None, (e.strip() for e in os.environ.get("NBD_GEMM_PAIR_TUNE", "").split("+"))):
+    _k, _v = _ent.split("=")
+    _m, _n, _kk, _e = (int(v) for v in _k.split(":"))
+    _s, _o = (int(v) for v in _v.split(":"))
+    _PAIR_TUNED[(_m, _n, _kk, _e)] = _s | (_o << 4)
+
+
 def pair_schedule(M: int, N: int, K: int, tile: int = 128, epi1: int = EPI_NONE) -> int:
     """Split count and dispatch order of the grouped backward launch for dy [M, N], W [N, K]
     (dx = dy·W: (M/t)(K/t) units of N/64 K-steps; dW = dyᵀ·x: (N/t)(K/t)·S units of M/(64 S)),
