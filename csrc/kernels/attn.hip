@@ -896,7 +896,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::T
 void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                   const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
                   const at::Tensor& dk, const at::Tensor& dv, const c10::optional<at::Tensor>& rope_cos,
-                  const c10::optional<at::Tensor>& rope_sin) {
+                  const c10::optional<at::Tensor>& rope_sin, const c10::optional<at::Tensor>& delta_in) {
   check_shapes(q, k, v);
   const Rope rp = rope_of(rope_cos, rope_sin, q.size(2));
   TORCH_CHECK(dout.sizes() == q.sizes() && out.sizes() == q.sizes() && dq.sizes() == q.sizes() &&
@@ -918,7 +918,14 @@ void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
   }();
   const bool fd = fd_env >= 0 ? fd_env == 1 : nblk <= 2;
   at::Tensor delta;
-  if (!fd) {
+  if (!fd && delta_in.has_value() && delta_in->defined()) {
+    // δ computed by the producer of dout (gemm.hip EPI_ADELTA: the output projection's input
+    // gradient) — no pre-pass
+    TORCH_CHECK(delta_in->is_cuda() && delta_in->scalar_type() == at::kFloat && delta_in->is_contiguous() &&
+                    delta_in->numel() == (int64_t)B * H * T,
+                "attn_bwd: delta must be float32 [B, H, T]");
+    delta = *delta_in;
+  } else if (!fd) {
     delta = at::empty({B, H, T}, lse.options());
     const int64_t rows = (int64_t)B * H * T;
     hipLaunchKernelGGL(bwd_pre_kernel, dim3((unsigned)((rows + NT / 8 - 1) / (NT / 8))), dim3(NT), 0, st, dov, ov,

@@ -53,7 +53,7 @@ void gemm_hip(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, boo
 void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor& c1, int64_t epi1,
                    const c10::optional<at::Tensor>& aux_in1, const at::Tensor& a2, const at::Tensor& b2,
                    const at::Tensor& c2, int64_t epi2, const c10::optional<at::Tensor>& aux_out2, int64_t splits2,
-                   int64_t accum2);
+                   int64_t accum2, const c10::optional<at::Tensor>& delta1 = c10::nullopt, int64_t delta_T = 0);
 }  // namespace gemm
 namespace norm {
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ln_fwd_hip(const at::Tensor& x,
@@ -90,7 +90,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& q, const at::T
 void attn_bwd_hip(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                   const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
                   const at::Tensor& dk, const at::Tensor& dv, const c10::optional<at::Tensor>& rope_cos,
-                  const c10::optional<at::Tensor>& rope_sin);
+                  const c10::optional<at::Tensor>& rope_sin, const c10::optional<at::Tensor>& delta = c10::nullopt);
 }  // namespace attn
 
 namespace ag {
@@ -228,7 +228,8 @@ static GradOut grad_out(const Tensor& param, bool want, at::IntArrayRef shape, c
 // dx = dy·W [· act′(aux)], dW = dyᵀ·x [, db = Σ dy] in one grouped launch (gemm_pair_hip)
 static std::tuple<Tensor, Tensor, Tensor> pair(const Tensor& dy, const Tensor& w, const Tensor& x, int epi1,
                                                const optional<Tensor>& aux1, bool bias_grad, int64_t splits,
-                                               const Tensor& bparam = Tensor()) {
+                                               const Tensor& bparam = Tensor(), const Tensor& delta = Tensor(),
+                                               int64_t delta_T = 0) {
   const int64_t M = dy.size(0), N = dy.size(1), K = w.size(1);
   Tensor dx = at::empty({M, epi1 == EPI_DSWIGLU ? 2 * K : K}, dy.options());
   const GradOut dw = grad_out(w, true, {N, K}, dy.options());
@@ -238,7 +239,8 @@ static std::tuple<Tensor, Tensor, Tensor> pair(const Tensor& dy, const Tensor& w
   {
     const ht::Scope hs(ht::PAIR_CALL);
     gemm_pair_hip(dy, w, dx, epi1, aux1, dy, x, dw.t.view({N, K}), bias_grad ? EPI_ROWSUM : EPI_NONE,
-                  bias_grad ? optional<Tensor>(db.t.view({N})) : c10::nullopt, splits, dw.bit(1) | db.bit(2));
+                  bias_grad ? optional<Tensor>(db.t.view({N})) : c10::nullopt, splits, dw.bit(1) | db.bit(2),
+                  delta.defined() ? optional<Tensor>(delta) : c10::nullopt, delta_T);
   }
   return {dx, dw.done(), bias_grad ? db.done() : Tensor()};
 }
@@ -260,6 +262,60 @@ static std::vector<int64_t> out_shape(const Tensor& x, int64_t n) {
   s.back() = n;
   return s;
 }
+
+// ---- the flash backward's δ from the output projection (GPT-2: attention -> c_proj) ----------
+// δ = Σ_d dO·O per (query, head) is the attention backward's pre-pass; dO is the input gradient
+// of the Linear that consumes the attention output O, so that Linear's grouped backward launch
+// can produce δ in its epilogue (gemm.hip EPI_ADELTA) and the pre-pass launch goes away.  The
+// attention node registers its output here at forward time; the Linear's backward, finding its
+// input registered, fills δ; the attention's backward takes it only if its dout IS that Linear's
+// input gradient (a second consumer of O would have summed gradients into another tensor).
+namespace adelta {
+struct Req {
+  int64_t T = 0, H = 0;
+  Tensor delta;             // filled by the Linear's backward
+  const void* dx = nullptr;  // ... for this input gradient
+};
+std::mutex mu;
+std::unordered_map<const void*, Req> reqs;
+
+static bool enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NBD_ATTN_DELTA_EPI");  // 0: the pre-pass kernel (A/B)
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+static void want(const Tensor& o, int64_t T, int64_t H) {
+  std::lock_guard<std::mutex> lk(mu);
+  reqs[o.data_ptr()] = Req{T, H, Tensor(), nullptr};  // (a new forward resets a stale entry)
+}
+// the δ tensor to fill for the Linear input x2 [B·T, H·64], or undefined
+static Tensor request(const Tensor& x2) {
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = reqs.find(x2.data_ptr());
+  if (it == reqs.end()) return Tensor();
+  Req& r = it->second;
+  if (x2.dim() != 2 || x2.size(1) != r.H * 64 || r.T <= 0 || x2.size(0) % r.T != 0) return Tensor();
+  r.delta = at::empty({x2.size(0) / r.T, r.H, r.T}, x2.options().dtype(at::kFloat));
+  r.dx = nullptr;
+  return r.delta;
+}
+static void produced(const Tensor& x2, const Tensor& dx) {
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = reqs.find(x2.data_ptr());
+  if (it != reqs.end()) it->second.dx = dx.data_ptr();
+}
+// δ for the attention output o whose incoming gradient is dout (and forget the entry)
+static Tensor take(const Tensor& o, const Tensor& dout) {
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = reqs.find(o.data_ptr());
+  if (it == reqs.end()) return Tensor();
+  Tensor d = (it->second.delta.defined() && it->second.dx == dout.data_ptr()) ? it->second.delta : Tensor();
+  reqs.erase(it);
+  return d;
+}
+}  // namespace adelta
 
 // ------------------------------------------------------------------------------------- Linear
 static Tensor linear_forward(const Tensor& x2, const Tensor& w, const optional<Tensor>& b, at::IntArrayRef plan) {
@@ -320,7 +376,14 @@ struct LinearFn : public torch::autograd::Function<LinearFn> {
     }
     const Tensor dy = bf16c(grads[0]).view({-1, w.size(0)});
     if (nx && nw && plan[9] >= 0) {
-      std::tie(dx, dw, db) = pair(dy, w, x2, EPI_NONE, c10::nullopt, nb, plan[9], b);
+      // an attention output as this Linear's input: the flash backward's δ from this launch
+      const Tensor delta = adelta::enabled() ? adelta::request(x2) : Tensor();
+      if (delta.defined()) {
+        std::tie(dx, dw, db) = pair(dy, w, x2, EPI_ADELTA, x2, nb, plan[9], b, delta, delta.size(2));
+        adelta::produced(x2, dx);
+      } else {
+        std::tie(dx, dw, db) = pair(dy, w, x2, EPI_NONE, c10::nullopt, nb, plan[9], b);
+      }
     } else {
       if (nx) dx = run(dy, w, false, true, prod(plan, 1)).first;
       if (nw) std::tie(dw, db) = wgrad(dy, x2, w, b, nb, plan, 2);
@@ -552,6 +615,10 @@ struct AttnQKVFn : public torch::autograd::Function<AttnQKVFn> {
     auto [q, k, v] = split_qkv(qkv, H, Hkv);
     auto [o, lse] = attn::attn_fwd_hip(q, k, v, causal, scale, cos, sin);
     const bool rope = cos.has_value();
+    // sequences past two 128-query blocks get the pre-pass (attn.hip: fd off): offer δ to the
+    // consumer of the output (adelta above)
+    if (adelta::enabled() && q.size(3) == 64 && qkv.size(1) / 128 > 2 && qkv.size(1) % 128 == 0)
+      adelta::want(o, qkv.size(1), H);
     if (rope) ctx->save_for_backward({qkv, o, lse, *cos, *sin});
     else ctx->save_for_backward({qkv, o, lse});
     ctx->saved_data["H"] = H;
@@ -570,10 +637,12 @@ struct AttnQKVFn : public torch::autograd::Function<AttnQKVFn> {
     auto [q, k, v] = split_qkv(qkv, H, Hkv);
     Tensor dqkv = at::empty_like(qkv, at::MemoryFormat::Contiguous);
     auto [dq, dk, dv] = split_qkv(dqkv, H, Hkv);
+    const Tensor delta = adelta::enabled() ? adelta::take(o, grads[0]) : Tensor();
     const Tensor dout = grads[0].contiguous().view({B, T, H, D}).transpose(1, 2);
     attn::attn_bwd_hip(dout, q, k, v, o, lse, ctx->saved_data["causal"].toBool(), ctx->saved_data["scale"].toDouble(),
                        dq, dk, dv, rope ? optional<Tensor>(sv[3]) : c10::nullopt,
-                       rope ? optional<Tensor>(sv[4]) : c10::nullopt);
+                       rope ? optional<Tensor>(sv[4]) : c10::nullopt,
+                       delta.defined() ? optional<Tensor>(delta) : c10::nullopt);
     return {dqkv, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
   }
 };

@@ -471,6 +471,23 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
       load8<bf16_t>(reinterpret_cast<const bf16_t*>(p.aux_in) + off, h);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= dgelu_tanh(h[e]);
+    } else if constexpr (EPI == EPI_ADELTA) {
+      // δ of (row, head) from the 8 consecutive lanes holding that row's 64 columns of the head
+      // (CPR % 8 == 0 and BM·CPR % NTW == 0: every lane runs every iteration, groups aligned)
+      static_assert(CPR % 8 == 0 && (BM * CPR) % NTW == 0, "EPI_ADELTA: whole heads per 8 lanes, no idle lanes");
+      float o[8];
+      load8<bf16_t>(reinterpret_cast<const bf16_t*>(p.aux_in) + off, o);
+      float dsum = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum = fmaf(bf16_to_f32(f32_to_bf16(v[e])), o[e], dsum);
+      dsum += __shfl_xor(dsum, 1, 64);
+      dsum += __shfl_xor(dsum, 2, 64);
+      dsum += __shfl_xor(dsum, 4, 64);
+      if ((c & 7) == 0) {
+        const int64_t m = m0 + r;
+        const int64_t hh = (n0 + cn) / 64, H = p.ldc / 64;
+        p.delta[((m / p.dT) * H + hh) * p.dT + (m % p.dT)] = dsum;
+      }
     } else {
       if (p.accum & 1) {  // gradient accumulation: c += A·B (one bf16 rounding of the fp32 sum)
         float o[8];
@@ -1105,14 +1122,14 @@ void gemm_hip_one(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c,
 void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor& c1, int64_t epi1,
                    const c10::optional<at::Tensor>& aux_in1, const at::Tensor& a2, const at::Tensor& b2,
                    const at::Tensor& c2, int64_t epi2, const c10::optional<at::Tensor>& aux_out2, int64_t splits2,
-                   int64_t accum2) {
+                   int64_t accum2, const c10::optional<at::Tensor>& delta1, int64_t delta_T) {
   for (const at::Tensor* x : {&a1, &b1, &c1, &a2, &b2, &c2}) {
     TORCH_CHECK(x->dim() == 2 && x->scalar_type() == at::kBFloat16 && x->is_contiguous() && x->is_cuda() &&
                     reinterpret_cast<uintptr_t>(x->data_ptr()) % 16 == 0,
                 "nbd::gemm_pair: contiguous 16-B aligned bf16 2-D GPU operands");
   }
-  TORCH_CHECK(epi1 == EPI_NONE || epi1 == EPI_DGELU || epi1 == EPI_DSWIGLU,
-              "nbd::gemm_pair: epi1 must be none, GELU' or SwiGLU'");
+  TORCH_CHECK(epi1 == EPI_NONE || epi1 == EPI_DGELU || epi1 == EPI_DSWIGLU || epi1 == EPI_ADELTA,
+              "nbd::gemm_pair: epi1 must be none, GELU', SwiGLU' or the attention delta");
   TORCH_CHECK(epi2 == EPI_NONE || epi2 == EPI_ROWSUM, "nbd::gemm_pair: epi2 must be none or row sums");
   // product 1: dgrad layout
   const int M1 = a1.size(0), K1 = a1.size(1), N1 = b1.size(1);
@@ -1150,6 +1167,13 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   p1.aux_in = epi1 != EPI_NONE ? static_cast<const uint16_t*>(aux_in1->data_ptr()) : nullptr;
   p1.M = M1; p1.N = N1; p1.K = K1;
   p1.lda = a1.size(1); p1.ldb = b1.size(1); p1.ldc = c1N;
+  if (epi1 == EPI_ADELTA) {  // δ [M1 / T][N1 / 64][T] from dO (c1) and O (aux_in1)
+    TORCH_CHECK(delta1 && delta1->is_cuda() && delta1->scalar_type() == at::kFloat && delta1->is_contiguous() &&
+                    delta_T > 0 && M1 % delta_T == 0 && N1 % 64 == 0 && delta1->numel() == (int64_t)M1 / 64 * N1,
+                "nbd::gemm_pair: the attention delta needs delta float32 [M / T, N / 64, T] and T dividing M");
+    p1.delta = delta1->data_ptr<float>();
+    p1.dT = (int)delta_T;
+  }
   p1.tiles_m = M1 / TB; p1.tiles_n = N1 / TB;
   p2.a = static_cast<const uint16_t*>(a2.data_ptr());
   p2.b = static_cast<const uint16_t*>(b2.data_ptr());
@@ -1215,13 +1239,16 @@ void gemm_pair_hip(const at::Tensor& a1, const at::Tensor& b1, const at::Tensor&
   using I2 = std::integral_constant<int, EPI_DGELU>;
   using I3 = std::integral_constant<int, EPI_ROWSUM>;
   using I5 = std::integral_constant<int, EPI_DSWIGLU>;
+  using I6 = std::integral_constant<int, EPI_ADELTA>;
   if (epi2 == EPI_NONE) {
     if (epi1 == EPI_NONE) launch(I0{}, I0{});
     else if (epi1 == EPI_DGELU) launch(I2{}, I0{});
+    else if (epi1 == EPI_ADELTA) launch(I6{}, I0{});
     else launch(I5{}, I0{});
   } else {
     if (epi1 == EPI_NONE) launch(I0{}, I3{});
     else if (epi1 == EPI_DGELU) launch(I2{}, I3{});
+    else if (epi1 == EPI_ADELTA) launch(I6{}, I3{});
     else launch(I5{}, I3{});
   }
   C10_HIP_KERNEL_LAUNCH_CHECK();

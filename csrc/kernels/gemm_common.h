@@ -26,7 +26,11 @@ constexpr int BK = 64;
 // feature: c = silu(g)·u [M][I], aux_out = [g|u] pre-activations [M][2I].
 // EPI_DSWIGLU (dgrad layout, C = dact [M][I] never stored): aux_in = [g|u] [M][2I];
 // c = d[g|u] [M][2I] = [dact·u·σ(g)(1 + g(1−σ(g))) | dact·silu(g)].
-enum Epi : int { EPI_NONE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_ROWSUM = 3, EPI_SWIGLU = 4, EPI_DSWIGLU = 5 };
+// EPI_ADELTA (dgrad layout, the input gradient of an attention output projection: C = dO [M][H·64]):
+//   also δ[b][h][t] = Σ_d dO[m][64h + d]·O[m][64h + d] (m = b·T + t, O = aux_in, same layout as C)
+//   into `delta` — the flash backward's pre-pass, from the tile's rounded outputs (attn.hip)
+enum Epi : int { EPI_NONE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_ROWSUM = 3, EPI_SWIGLU = 4, EPI_DSWIGLU = 5,
+                 EPI_ADELTA = 6 };
 
 struct Args {
   const uint16_t* a;
@@ -47,6 +51,8 @@ struct Args {
   const uint8_t* pf;
   int64_t pf_lines;
   int warm_blocks;
+  float* delta;  // EPI_ADELTA: δ [M / dT][ldc / 64][dT] fp32
+  int dT;
 };
 
 // ---- swizzles ---------------------------------------------------------------------------------

@@ -12,7 +12,8 @@ TORCH_LIBRARY(nbd, m) {
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, Tensor? rope_cos=None, "
         "Tensor? rope_sin=None) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale, "
-        "Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor? rope_cos=None, Tensor? rope_sin=None) -> ()");
+        "Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor? rope_cos=None, Tensor? rope_sin=None, "
+        "Tensor? delta=None) -> ()");
   m.def("decode_attn(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor pos, int n_head, float scale, "
         "int kv_len_max, Tensor? rope_cos, Tensor? rope_sin, Tensor(c!) partials) -> Tensor");
   m.def("greedy_advance(Tensor logits, Tensor(a!) tok, Tensor(b!) pos, Tensor(c!) out, Tensor(d!)? done, int eos) -> ()");
@@ -40,7 +41,8 @@ TORCH_LIBRARY(nbd, m) {
   m.def("gemm(Tensor a, Tensor b, Tensor(a!) c, bool a_km, bool b_kn, Tensor? bias, int epi, Tensor? aux_in, "
         "Tensor(b!)? aux_out, int splits, int tile, int accum=0) -> ()");
   m.def("gemm_pair(Tensor a1, Tensor b1, Tensor(a!) c1, int epi1, Tensor? aux_in1, Tensor a2, Tensor b2, "
-        "Tensor(b!) c2, int epi2, Tensor(c!)? aux_out2, int splits2, int accum2=0) -> ()");
+        "Tensor(b!) c2, int epi2, Tensor(c!)? aux_out2, int splits2, int accum2=0, Tensor(d!)? delta1=None, "
+        "int delta_T=0) -> ()");
   // autograd nodes of the fused Linear / MLP paths (autograd.hip); plan = ops/gemm.py native_plan
   m.def("linear_ag(Tensor x, Tensor w, Tensor? b, int[] plan) -> Tensor");
   m.def("mlp_gelu_ag(Tensor x, Tensor w1, Tensor? b1, Tensor w2, Tensor? b2, int[] plan) -> Tensor");

@@ -231,3 +231,30 @@ def test_gqa_split_sum_repeatable(dev):
     ref.backward(do.float())
     for name, a, b in (("dq", outs[0][0], qr.grad), ("dk", outs[0][1], kr.grad), ("dv", outs[0][2], vr.grad)):
         assert _rel(a, b) < 3e-2, (name, _rel(a, b))
+
+
+@pytest.mark.parametrize("T", [512, 1024])
+def test_attention_out_projection_delta_epilogue(dev, T):
+    """GPT-2's attention -> c_proj on the native nodes: at T > 256 the projection's grouped
+    backward launch computes the flash backward's δ in its epilogue (gemm.hip EPI_ADELTA, no
+    pre-pass); q|k|v, weight and bias gradients against fp32 SDPA + Linear."""
+    import torch.nn.functional as F
+
+    B, H, D = 2, 4, 64
+    C = H * D
+    g = torch.Generator(device="cpu").manual_seed(T)
+    qkv = (torch.randn(B, T, 3 * C, generator=g) * 0.5).to(dev, torch.bfloat16).requires_grad_()
+    w = (torch.randn(C, C, generator=g) * 0.05).to(dev, torch.bfloat16).requires_grad_()
+    b = (torch.randn(C, generator=g) * 0.1).to(dev, torch.bfloat16).requires_grad_()
+    dy = torch.randn(B, T, C, generator=g).to(dev, torch.bfloat16)
+    y = ops.gemm_linear(ops.attention_qkv(qkv, H, causal=True), w, b)
+    y.backward(dy)
+    qr, wr, br = (t.detach().float().requires_grad_() for t in (qkv, w, b))
+    q, k, v = (t.view(B, T, H, D).transpose(1, 2) for t in qr.split(C, dim=-1))
+    a = F.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2).reshape(B, T, C)
+    yr = F.linear(a, wr, br)
+    yr.backward(dy.float())
+    torch.cuda.synchronize()
+    assert _rel(y, yr) < 2e-2
+    for name, x, r in (("dqkv", qkv.grad, qr.grad), ("dW", w.grad, wr.grad), ("db", b.grad, br.grad)):
+        assert _rel(x, r) < 3e-2, (name, _rel(x, r))
