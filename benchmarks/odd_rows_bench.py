@@ -47,3 +47,24 @@ for M in (8100, 8192):
             r["hip"].append(round(time_us(hip), 1))
             r["lib"].append(round(time_us(lib), 1))
         print(f"M={M} {name:12s} N={N:5d} K={K:5d}  hip(padded) fwd+bwd us {r['hip']}  hipBLASLt {r['lib']}", flush=True)
+
+
+# weight dims off the 64-grid (NBD_GEMM_PAD_DIMS=1 path) against the library
+G.PAD_DIMS = True
+for (M, N, K) in ((8192, 1000, 768), (8192, 768, 1000), (8192, 3000, 1000)):
+    x = torch.randn(M, K, device=dev).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16).requires_grad_()
+    b = torch.zeros(N, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+
+    def hip():
+        G.gemm_linear(x, w, b).backward(dy)
+
+    def lib():
+        F.linear(x, w, b).backward(dy)
+
+    r = {"hip": [], "lib": []}
+    for _ in range(3):
+        r["hip"].append(round(time_us(hip), 1))
+        r["lib"].append(round(time_us(lib), 1))
+    print(f"dims M={M} N={N:5d} K={K:5d}  hip(padded) fwd+bwd us {r['hip']}  hipBLASLt {r['lib']}", flush=True)

@@ -600,9 +600,38 @@ def _pad_rows(x, *ws):
     return F.pad(x.reshape(M, x.shape[-1]), (0, 0, 0, (-M) % 256)), M
 
 
+# weight dims (N outputs, K inputs) off the 64-grid: zero-pad the weight (N to 128, K to 64) and
+# the input's columns onto the HIP kernels (NBD_GEMM_PAD_DIMS=0: the library; faster than
+# hipBLASLt on the measured odd shapes despite the weight copy per call — FINDINGS §36)
+PAD_DIMS = os.environ.get("NBD_GEMM_PAD_DIMS", "1") != "0"
+
+
+def _pad_dims(x, weight, bias):
+    """(x, weight, bias) zero-padded so that N and K are multiples of 64, or None."""
+    import torch
+
+    if not (PAD_DIMS and ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+            and weight.dim() == 2 and not torch.is_autocast_enabled()
+            and (bias is None or bias.dtype == torch.bfloat16)):
+        return None
+    N, K = weight.shape
+    # N to a multiple of 128 (128-wide tiles; 64 left N = 3000 on 64-wide tiles, slower than the library)
+    pn, pk = (-N) % 128, (-K) % 64
+    if pn == 0 and pk == 0:
+        return None
+    import torch.nn.functional as F
+
+    return (F.pad(x, (0, pk)) if pk else x, F.pad(weight, (0, pk, 0, pn)),
+            F.pad(bias, (0, pn)) if (bias is not None and pn) else bias)
+
+
 def gemm_linear(x, weight, bias=None):
-    """``F.linear`` on the HIP MFMA GEMM (bf16; weight dims multiples of 64, a row count that is
-    not is padded); PyTorch otherwise."""
+    """``F.linear`` on the HIP MFMA GEMM (bf16; weight dims multiples of 64 — or padded with
+    NBD_GEMM_PAD_DIMS=1 —, a row count that is not is padded); PyTorch otherwise."""
+    pd = _pad_dims(x, weight, bias)
+    if pd is not None:
+        y = gemm_linear(*pd)
+        return y[..., :weight.shape[0]] if y.shape[-1] != weight.shape[0] else y
     pr = _pad_rows(x, weight)
     if pr is not None:
         return gemm_linear(pr[0], weight, bias)[:pr[1]].reshape(*x.shape[:-1], weight.shape[0])
@@ -678,8 +707,9 @@ def linear_any(x, weight, bias=None):
     is the forward ``parallel.DistributedDataParallel(fused_linear=True)`` gives ``nn.Linear``."""
     import torch
 
-    if (_fast(x, weight) or _pad_rows(x, weight) is not None) and _native(bias):
-        return gemm_linear(x, weight, bias)  # (a row count off the 64-grid is padded there)
+    if ((_fast(x, weight) or _pad_rows(x, weight) is not None or _pad_dims(x, weight, bias) is not None)
+            and _native(bias)):
+        return gemm_linear(x, weight, bias)  # (row counts / weight dims off the 64-grid are padded there)
     # bf16 heads with a tiny output dimension (classifiers: N <= 64): the tiny-linear kernels
     from .tiny import linear_tiny, supported as _tiny_ok
 

@@ -458,3 +458,29 @@ def test_gemm_linear_odd_rows_padded(M, bias):
     assert rel(y, yf) < 1e-2 and rel(x.grad, xf.grad) < 1e-2 and rel(w.grad, wf.grad) < 2e-2
     if bias:
         assert rel(b.grad, bf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1000, 1000), (256, 100, 320), (64, 192, 70)])
+def test_gemm_linear_odd_dims_padded(M, N, K, monkeypatch):
+    """Weight dims off the 64-grid zero-padded onto the HIP kernels (NBD_GEMM_PAD_DIMS) — output and
+    all gradients against fp32."""
+    import torch.nn.functional as F
+
+    monkeypatch.setattr(G, "PAD_DIMS", True)
+    torch.manual_seed(N + K)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(N, K, device="cuda") * 0.05).to(torch.bfloat16).requires_grad_()
+    b = (torch.randn(N, device="cuda") * 0.1).to(torch.bfloat16).requires_grad_()
+    assert G._pad_dims(x, w, b) is not None
+    y = G.gemm_linear(x, w, b)
+    assert y.shape == (M, N)
+    dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    y.backward(dy)
+    xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+    F.linear(xf, wf, bf).backward(dy.float())
+
+    def rel(a, r):
+        return float((a.float() - r).abs().max() / r.abs().max().clamp_min(1e-6))
+
+    assert rel(y, F.linear(xf, wf, bf)) < 1e-2
+    assert rel(x.grad, xf.grad) < 1e-2 and rel(w.grad, wf.grad) < 2e-2 and rel(b.grad, bf.grad) < 2e-2
