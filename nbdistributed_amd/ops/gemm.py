@@ -615,7 +615,7 @@ def _pad_dims(x, weight, bias):
             and (bias is None or bias.dtype == torch.bfloat16)):
         return None
     N, K = weight.shape
-    if N <= 64:  # (classifier heads: the tiny-linear kernels, ops/tiny.py)
+    if N <= 64 or (N % 64 == 0 and K % 64 == 0):  # (heads: tiny-linear kernels; aligned: as is)
         return None
     # N to a multiple of 128 (128-wide tiles; 64 left N = 3000 on 64-wide tiles, slower than the library)
     pn, pk = (-N) % 128, (-K) % 64
