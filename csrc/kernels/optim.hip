@@ -53,7 +53,7 @@ __device__ __forceinline__ void device_hyper(AdamArgs& a, const float* dstep, co
 
 // U = 8-element groups per thread per iteration (all their loads issued before any math: 112·U
 // bytes in flight per lane); NTL = non-temporal loads (every byte is read once per step).
-template <typename G, typename P, int U, bool NTL>
+template <typename G, typename P, int U, bool NTL, bool NTS = false>
 __global__ __launch_bounds__(256) void adamw_flat_kernel(const G* __restrict__ grad, P* __restrict__ param,
                                                          float* __restrict__ master, float* __restrict__ m,
                                                          float* __restrict__ v, const float* __restrict__ gscale,
@@ -91,9 +91,15 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(const G* __restrict__ g
         const float denom = sqrtf(vv[u][j]) * a.inv_sqrt_bc2 + a.eps;
         w[u][j] = w[u][j] * a.wd_factor - a.step_size * (mm[u][j] / denom);
       }
-      store8<float>(master + i, w[u]);
-      store8<float>(m + i, mm[u]);
-      store8<float>(v + i, vv[u]);
+      if constexpr (NTS) {  // (variant 4: every stream non-temporal)
+        store8_nt<float>(master + i, w[u]);
+        store8_nt<float>(m + i, mm[u]);
+        store8_nt<float>(v + i, vv[u]);
+      } else {
+        store8<float>(master + i, w[u]);
+        store8<float>(m + i, mm[u]);
+        store8<float>(v + i, vv[u]);
+      }
       if (sizeof(P) == 2) store8_nt<P>(param + i, w[u]);
       else store8<P>(param + i, w[u]);
     }
@@ -136,7 +142,8 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(const G* __restrict__ g
 // 0.648 ms against 0.700 for the former 2048-block grid-stride default, 124 M parameters,
 // profiles/adamw_grid_r5.txt);
 // NBD_ADAMW_VARIANT: 1 = two 8-element groups per thread per iteration, 2 = that with
-// non-temporal loads, 3 = one group with non-temporal loads (all measured slower: FINDINGS §31)
+// non-temporal loads, 3 = one group with non-temporal loads (all measured slower: FINDINGS §31),
+// 4 = one group with non-temporal stores
 static int adamw_env(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e == nullptr ? dflt : std::atoi(e);
@@ -150,14 +157,15 @@ static void launch_adamw(const at::Tensor& grad, const at::Tensor& param, const 
   static const int variant = adamw_env("NBD_ADAMW_VARIANT", 0);
   const int64_t work = (n + 7) / 8;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, cap));
-#define NBD_ADAMW(U_, NT_)                                                                                        \
-  hipLaunchKernelGGL((adamw_flat_kernel<G, P, U_, NT_>), dim3((unsigned)blocks), dim3(256), 0, st,                 \
+#define NBD_ADAMW(U_, NT_, ...)                                                                                   \
+  hipLaunchKernelGGL((adamw_flat_kernel<G, P, U_, NT_, ##__VA_ARGS__>), dim3((unsigned)blocks), dim3(256), 0, st,  \
                      static_cast<const G*>(grad.data_ptr()), static_cast<P*>(param.data_ptr()), master.data_ptr<float>(), \
                      m.data_ptr<float>(), v.data_ptr<float>(), gs, dstep, dlr, n, a)
   switch (variant) {
     case 1: NBD_ADAMW(2, false); break;
     case 2: NBD_ADAMW(2, true); break;
     case 3: NBD_ADAMW(1, true); break;
+    case 4: NBD_ADAMW(1, false, true); break;
     default: NBD_ADAMW(1, false); break;
   }
 #undef NBD_ADAMW
