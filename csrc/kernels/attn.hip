@@ -96,10 +96,10 @@ __device__ __forceinline__ s8v cat(s4v a, s4v b) {
 __device__ __forceinline__ uint16_t bf(float x) { return f32_to_bf16(x); }
 // registers 8s .. 8s+7 of a C tile -> bf16 B/A fragment of k-step s (k order as §3)
 __device__ __forceinline__ s8v pack_half(const f16x& c, int s) {
-  s8v r;
+  u32x4 w;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (short)bf(c[8 * s + j]);
-  return r;
+  for (int j = 0; j < 4; ++j) w[j] = pack2_bf16(c[8 * s + 2 * j], c[8 * s + 2 * j + 1]);
+  return __builtin_bit_cast(s8v, w);
 }
 __device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 __device__ __forceinline__ f16x zero16() {
@@ -114,8 +114,8 @@ __device__ __forceinline__ f16x zero16() {
 __device__ __forceinline__ void store_dT(uint16_t* rowp, const f16x& c, int db, int h, float mul) {
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    uint32_t lo = (uint32_t)bf(c[4 * g] * mul) | ((uint32_t)bf(c[4 * g + 1] * mul) << 16);
-    uint32_t hi = (uint32_t)bf(c[4 * g + 2] * mul) | ((uint32_t)bf(c[4 * g + 3] * mul) << 16);
+    const uint32_t lo = pack2_bf16(c[4 * g] * mul, c[4 * g + 1] * mul);
+    const uint32_t hi = pack2_bf16(c[4 * g + 2] * mul, c[4 * g + 3] * mul);
     const int d = db * 32 + 8 * g + 4 * h;
     *reinterpret_cast<uint2*>(rowp + d) = make_uint2(lo, hi);
   }

@@ -80,7 +80,7 @@ __device__ __forceinline__ void unpack8(const u32x4& w, float (&v)[8]) {
 __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
   u32x4 w;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) w[j] = (uint32_t)f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
+  for (int j = 0; j < 4; ++j) w[j] = pack2_bf16(v[2 * j], v[2 * j + 1]);
   return w;
 }
 

@@ -311,8 +311,8 @@ __device__ __forceinline__ void gemm_body(const Args& p, int bx, int by, int S, 
           const int m = wm * (BM / WM) + 16 * j + (lane & 15);
           const f4 v = acc[i][j];
           uint2 w;
-          w.x = (uint32_t)f32_to_bf16(v[0] + bv[0]) | ((uint32_t)f32_to_bf16(v[1] + bv[1]) << 16);
-          w.y = (uint32_t)f32_to_bf16(v[2] + bv[2]) | ((uint32_t)f32_to_bf16(v[3] + bv[3]) << 16);
+          w.x = pack2_bf16(v[0] + bv[0], v[1] + bv[1]);
+          w.y = pack2_bf16(v[2] + bv[2], v[3] + bv[3]);
           *reinterpret_cast<uint2*>(cb + m * LDB + n) = w;
         }
       }

@@ -113,7 +113,7 @@ __device__ __forceinline__ void vm_wait() {
 }
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
+  return pack2_bf16(a, b);
 }
 
 // NTS: the C tile leaves with non-temporal stores (an output far larger than the L2s and the

@@ -26,6 +26,16 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+// Two floats -> one dword of two bf16 (a in the low half) as a single v_cvt_pk_bf16_f32: the
+// vector conversion.  Packing two scalar casts with shift / or compiled to 3 instructions a pair
+// (the compiler converted each half separately, then merged them with v_and / v_lshl / v_or_sdwa).
+typedef float nbd_f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 nbd_b2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
+  const nbd_f2v f = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, nbd_b2v));
+}
+
 __device__ __forceinline__ float f16_to_f32(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
 __device__ __forceinline__ uint16_t f32_to_f16(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
 
@@ -100,7 +110,7 @@ __device__ __forceinline__ void store8<bf16_t>(bf16_t* p, const float (&v)[8]) {
   u32x4 w;
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    w[j] = (uint32_t)f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
+    w[j] = pack2_bf16(v[2 * j], v[2 * j + 1]);
   *reinterpret_cast<u32x4*>(p) = w;
 }
 template <>
@@ -156,7 +166,7 @@ __device__ __forceinline__ void store8_nt<bf16_t>(bf16_t* p, const float (&v)[8]
   u32x4 w;
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    w[j] = (uint32_t)f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
+    w[j] = pack2_bf16(v[2 * j], v[2 * j + 1]);
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
 }
 template <>

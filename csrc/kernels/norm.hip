@@ -69,8 +69,7 @@ template <typename T>
 __device__ __forceinline__ void store4(T* p, const float (&v)[4]);
 template <>
 __device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float (&v)[4]) {
-  *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16),
-                                            (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16));
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3]));
 }
 template <>
 __device__ __forceinline__ void store4<f16_t>(f16_t* p, const float (&v)[4]) {
