@@ -49,7 +49,8 @@ def test_flash_forward_backward(dev, causal, B, H, T):
         assert _rel(a, b) < 3e-2, (name, _rel(a, b))
 
 
-_GQA_CASES = [(2, 9, 3, 128), (4, 8, 2, 256), (1, 6, 1, 384), (16, 9, 3, 128), (64, 9, 3, 128)]
+_GQA_CASES = [(2, 9, 3, 128), (4, 8, 2, 256), (1, 6, 1, 384), (16, 9, 3, 128), (64, 9, 3, 128), (4, 9, 3, 256),
+              (3, 9, 3, 384)]
 
 
 def _gqa_case(dev, B, H, Hkv, T, causal):
@@ -67,8 +68,9 @@ def _gqa_case(dev, B, H, Hkv, T, causal):
 @pytest.mark.parametrize("B,H,Hkv,T", _GQA_CASES)
 def test_flash_gqa_backward(dev, causal, B, H, Hkv, T):
     """Grouped-query backward, incl. the query-head groups split over workgroups and summed by
-    gqa_reduce_kernel (B·Hkv·T/128 < 128), and one workgroup per key/value head sweeping its group
-    (B64: 192), against fp32 attention on repeated K/V."""
+    gqa_reduce_kernel (B·Hkv·T/128 < 128 — fused δ at T ≤ 256, the δ pre-pass at 384), and one
+    workgroup per key/value head sweeping its group (B64: 192), against fp32 attention on repeated
+    K/V."""
     (q, k, v, do), (out, dq, dk, dv) = _gqa_case(dev, B, H, Hkv, T, causal)
     rep = H // Hkv
     qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
