@@ -61,6 +61,9 @@ def check_ids(device=None) -> None:
 
 
 _EmbFn = None
+# the token embedding's gradient written into its DDP bucket slice (NBD_EMB_BUCKET=0: a dense
+# gradient tensor, copied into the bucket by DDP — A/B)
+_EMB_BUCKET = os.environ.get("NBD_EMB_BUCKET", "1") != "0"
 
 def _emb_fn():
     global _EmbFn
@@ -72,15 +75,33 @@ def _emb_fn():
             def forward(ctx, idx, weight):
                 ctx.save_for_backward(idx)
                 ctx.V = weight.shape[0]
+                # (the parameter itself, for its DDP bucket slice: a plain reference, never read)
+                ctx.weight = weight if isinstance(weight, torch.nn.Parameter) else None
                 return torch.nn.functional.embedding(idx, weight)
 
             @staticmethod
             def backward(ctx, dy):
+                from . import graddst
+
                 (idx,) = ctx.saved_tensors
                 C = dy.shape[-1]
                 dy2 = dy.reshape(-1, C)
                 dy2 = dy2 if dy2.is_contiguous() else dy2.contiguous()
-                return None, torch.ops.nbd.embedding_bwd(dy2, idx.reshape(-1).contiguous(), ctx.V)
+                ids = idx.reshape(-1).contiguous()
+                w = ctx.weight
+                if w is not None and dy2.dtype == w.dtype and _EMB_BUCKET:
+                    # straight into the DDP bucket slice (no dense gradient + flatten copy: 56 MB
+                    # each way for SmolLM2's table); a tied head that already wrote the slice in
+                    # this pass gets the token rows added
+                    dst = graddst.join(w)
+                    if dst is not None:
+                        torch.ops.nbd.embedding_bwd(dy2, ids, ctx.V, dst, True)
+                        return None, None
+                    dst, acc = graddst.claim(w)
+                    if dst is not None:
+                        torch.ops.nbd.embedding_bwd(dy2, ids, ctx.V, dst, acc)
+                        return None, graddst.hand_back(w, dst, acc)
+                return None, torch.ops.nbd.embedding_bwd(dy2, ids, ctx.V)
 
         _EmbFn = _Embedding
     return _EmbFn

@@ -129,6 +129,50 @@ pad_zero = bool((mv.module.wte.weight[5000:] == 0).all())
 (mv.stats["grad_views"] == len(list(mv.module.parameters())), rel1 < 2e-2, rel3 < 3e-2, pad_zero)
 """
 
+CODE_DDP_LLAMA = """
+import copy
+import contextlib
+from nbdistributed_amd.models.llama import LlamaConfig, LlamaForSequenceClassification, LlamaForCausalLM
+from nbdistributed_amd.parallel import DistributedDataParallel as NbdDDP
+from nbdistributed_amd.ops import graddst as GD
+got = []  # (parameter, a bucket slice was handed out for it) from the embedding's backward
+_claim, _join = GD.claim, GD.join
+def _spy_claim(p):
+    d, acc = _claim(p)
+    got.append((p, d is not None))
+    return d, acc
+def _spy_join(p):
+    d = _join(p)
+    got.append((p, d is not None))
+    return d
+GD.claim, GD.join = _spy_claim, _spy_join
+res = []
+for cls in (LlamaForSequenceClassification, LlamaForCausalLM):
+    torch.manual_seed(4)
+    cfg = LlamaConfig(vocab_size=1000, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                      num_attention_heads=2, num_key_value_heads=1, tie_word_embeddings=cls is LlamaForCausalLM)
+    base = cls(cfg).to(device, torch.bfloat16)
+    mv = NbdDDP(copy.deepcopy(base), flat_params=True, grad_mode="bucket", bucket_cap_mb=1.0)
+    mf = NbdDDP(copy.deepcopy(base), flat_params=True, grad_mode="bucket", bucket_cap_mb=1.0, grad_views=False)
+    ids = torch.randint(1, 1000, (2, 128), generator=torch.Generator().manual_seed(1)).to(device)
+    lab = torch.tensor([0, 1], device=device) if cls is LlamaForSequenceClassification else ids
+    def grads(m, k=1):
+        for i in range(k):
+            ctx = m.no_sync() if i < k - 1 else contextlib.nullcontext()
+            with ctx:
+                m(ids, labels=lab).loss.backward()
+        torch.cuda.synchronize()
+        return torch.cat([b.buffer.float() for b in m.buckets])
+    a, b = grads(mv), grads(mf)
+    a3, b3 = grads(mv, 3), grads(mf, 3)
+    emb = mv.module.model.embed_tokens.weight
+    home = any(p is emb and ok for p, ok in got)
+    got.clear()
+    res += [home, float((a - b).abs().max() / b.abs().max()) < 2e-2, float((a3 - b3).abs().max() / b3.abs().max()) < 3e-2]
+GD.claim, GD.join = _claim, _join
+tuple(res)
+"""
+
 CODE_LINEAR = """
 import copy
 import contextlib
@@ -168,6 +212,15 @@ def test_ddp_gpt2_grad_views_match_flatten_path(sess):
     r = sess.execute(CODE_DDP, render=False)
     assert r.ok, r.errors
     assert r.results[0]["echo"] == "(True, True, True, True)", r.results[0]
+
+
+def test_ddp_llama_embedding_grad_in_bucket_matches_flatten_path(sess):
+    """The token embedding's backward writes into its DDP bucket slice (``.grad`` is the bucket
+    view) — untied (sequence classifier) and tied to the LM head — matching the flatten path,
+    incl. accumulation over no_sync micro-batches."""
+    r = sess.execute(CODE_DDP_LLAMA, render=False)
+    assert r.ok, r.errors
+    assert r.results[0]["echo"] == str((True,) * 6), r.results[0]
 
 
 def test_ddp_fp32_linear_in_place_matches_torch_ddp(sess):
