@@ -21,6 +21,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "graddst.h"
@@ -42,12 +43,12 @@ struct SplitTable {
   int block0[kMaxD + 1];  // first workgroup of each descriptor
 };
 
-__global__ __launch_bounds__(256) void multi_splitk_kernel(SplitTable t, int nd) {
+__device__ __forceinline__ void splitk_body(const SplitTable& t, int nd, int blk) {
   int d = 0;  // block-uniform forward scan over <= 64 prefixes
-  while (d + 1 < nd && t.block0[d + 1] <= (int)blockIdx.x) ++d;
+  while (d + 1 < nd && t.block0[d + 1] <= blk) ++d;
   const int64_t n8 = t.n8[d], m8 = t.m8[d], slab = t.slab[d];
   const int splits = t.splits[d], accum = t.accum[d];
-  const int64_t base = (int64_t)((int)blockIdx.x - t.block0[d]) * kPer * 256;
+  const int64_t base = (int64_t)(blk - t.block0[d]) * kPer * 256;
 #pragma unroll
   for (int u = 0; u < kPer; ++u) {
     const int64_t i = base + u * 256 + threadIdx.x;
@@ -74,6 +75,8 @@ __global__ __launch_bounds__(256) void multi_splitk_kernel(SplitTable t, int nd)
   }
 }
 
+__global__ __launch_bounds__(256) void multi_splitk_kernel(SplitTable t, int nd) { splitk_body(t, nd, (int)blockIdx.x); }
+
 // ---- norm partial rows: out0[c] / out1[c - C] (+)= Σ_p part[p][c], c < W (row stride ld)
 // (col_reduce_kernel's shape: a workgroup = 16 columns x 16 partial-row groups, combined in LDS)
 struct ColTable {
@@ -84,14 +87,14 @@ struct ColTable {
   int block0[kMaxD + 1];
 };
 
-__global__ __launch_bounds__(256) void multi_colred_kernel(ColTable t, int nd) {
+__device__ __forceinline__ void colred_body(const ColTable& t, int nd, int blk) {
   __shared__ float red[16][17];
   int d = 0;
-  while (d + 1 < nd && t.block0[d + 1] <= (int)blockIdx.x) ++d;
+  while (d + 1 < nd && t.block0[d + 1] <= blk) ++d;
   const int nparts = t.nparts[d], ld = t.ld[d], W = t.W[d], C = t.C[d], accum = t.accum[d];
   const float* part = t.part[d];
   const int cx = threadIdx.x & 15, pg = threadIdx.x >> 4;
-  const int c = ((int)blockIdx.x - t.block0[d]) * 16 + cx;
+  const int c = (blk - t.block0[d]) * 16 + cx;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (c < W) {
     int p = pg;
@@ -115,6 +118,16 @@ __global__ __launch_bounds__(256) void multi_colred_kernel(ColTable t, int nd) {
     if (accum & (second ? 2 : 1)) s += Elem<bf16_t>::load(dst, j);
     Elem<bf16_t>::store(dst, j, s);
   }
+}
+
+__global__ __launch_bounds__(256) void multi_colred_kernel(ColTable t, int nd) { colred_body(t, nd, (int)blockIdx.x); }
+
+// both kinds of a flush in one launch: workgroups [0, sblocks) sum split-K slabs, the rest column
+// partials (the branch is per workgroup; the two sets of outputs are disjoint)
+__global__ __launch_bounds__(256) void multi_reduce_kernel(SplitTable st, int ns, int sblocks, ColTable ct, int nc) {
+  const int blk = (int)blockIdx.x;
+  if (blk < sblocks) splitk_body(st, ns, blk);
+  else colred_body(ct, nc, blk - sblocks);
 }
 
 // ---- queue -------------------------------------------------------------------------------------
@@ -156,27 +169,60 @@ std::atomic<bool> g_enabled{false};
 thread_local bool t_scope = false;
 bool q_callback = false;  // an end-of-backward flush is registered with the running backward
 
+// fill a table from items[pos..] (at most kMaxD): returns (descriptors, workgroups), advances pos
+std::pair<int, int> fill_split(SplitTable& tab, const std::vector<const Item*>& items, size_t& pos) {
+  int nd = 0, blocks = 0;
+  for (; pos < items.size() && nd < kMaxD; ++pos, ++nd) {
+    const Item& it = *items[pos];
+    tab.ws[nd] = it.buf.data_ptr<float>();
+    tab.out[nd] = it.out0;
+    tab.rs_out[nd] = it.out1;
+    tab.n8[nd] = it.a;
+    tab.m8[nd] = it.b;
+    tab.slab[nd] = it.c;
+    tab.splits[nd] = it.d;
+    tab.accum[nd] = it.accum;
+    tab.block0[nd] = blocks;
+    const int64_t nb = (it.a + it.b + kPer * 256 - 1) / (kPer * 256);
+    TORCH_CHECK(blocks + nb < (int64_t)INT32_MAX / 2, "grad_defer: too many workgroups in one flush");
+    blocks += (int)nb;
+  }
+  tab.block0[nd] = blocks;
+  return {nd, blocks};
+}
+
+std::pair<int, int> fill_col(ColTable& tab, const std::vector<const Item*>& items, size_t& pos) {
+  int nd = 0, blocks = 0;
+  for (; pos < items.size() && nd < kMaxD; ++pos, ++nd) {
+    const Item& it = *items[pos];
+    tab.part[nd] = it.buf.data_ptr<float>();
+    tab.out0[nd] = it.out0;
+    tab.out1[nd] = it.out1;
+    tab.nparts[nd] = (int)it.a;
+    tab.ld[nd] = (int)it.b;
+    tab.W[nd] = (int)it.c;
+    tab.C[nd] = it.d;
+    tab.accum[nd] = it.accum;
+    tab.block0[nd] = blocks;
+    blocks += (int)((it.c + 15) / 16);
+  }
+  tab.block0[nd] = blocks;
+  return {nd, blocks};
+}
+
+bool merge_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NBD_GRAD_DEFER_MERGE");  // 0: one launch per kind (A/B)
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 void launch_split(const std::vector<const Item*>& items) {
   size_t pos = 0;
   while (pos < items.size()) {
     SplitTable tab{};
-    int nd = 0, blocks = 0;
-    for (; pos < items.size() && nd < kMaxD; ++pos, ++nd) {
-      const Item& it = *items[pos];
-      tab.ws[nd] = it.buf.data_ptr<float>();
-      tab.out[nd] = it.out0;
-      tab.rs_out[nd] = it.out1;
-      tab.n8[nd] = it.a;
-      tab.m8[nd] = it.b;
-      tab.slab[nd] = it.c;
-      tab.splits[nd] = it.d;
-      tab.accum[nd] = it.accum;
-      tab.block0[nd] = blocks;
-      const int64_t nb = (it.a + it.b + kPer * 256 - 1) / (kPer * 256);
-      TORCH_CHECK(blocks + nb < (int64_t)INT32_MAX, "grad_defer: too many workgroups in one flush");
-      blocks += (int)nb;
-    }
-    tab.block0[nd] = blocks;
+    const auto [nd, blocks] = fill_split(tab, items, pos);
     hipLaunchKernelGGL(multi_splitk_kernel, dim3(blocks), dim3(256), 0, q_stream, tab, nd);
     C10_HIP_KERNEL_LAUNCH_CHECK();
   }
@@ -186,21 +232,7 @@ void launch_col(const std::vector<const Item*>& items) {
   size_t pos = 0;
   while (pos < items.size()) {
     ColTable tab{};
-    int nd = 0, blocks = 0;
-    for (; pos < items.size() && nd < kMaxD; ++pos, ++nd) {
-      const Item& it = *items[pos];
-      tab.part[nd] = it.buf.data_ptr<float>();
-      tab.out0[nd] = it.out0;
-      tab.out1[nd] = it.out1;
-      tab.nparts[nd] = (int)it.a;
-      tab.ld[nd] = (int)it.b;
-      tab.W[nd] = (int)it.c;
-      tab.C[nd] = it.d;
-      tab.accum[nd] = it.accum;
-      tab.block0[nd] = blocks;
-      blocks += (int)((it.c + 15) / 16);
-    }
-    tab.block0[nd] = blocks;
+    const auto [nd, blocks] = fill_col(tab, items, pos);
     hipLaunchKernelGGL(multi_colred_kernel, dim3(blocks), dim3(256), 0, q_stream, tab, nd);
     C10_HIP_KERNEL_LAUNCH_CHECK();
   }
@@ -237,8 +269,21 @@ void flush_locked() {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)q_device));
   std::vector<const Item*> split, col;
   for (const Item& it : q_items) (it.kind == 0 ? split : col).push_back(&it);
-  if (!split.empty()) launch_split(split);
-  if (!col.empty()) launch_col(col);
+  if (merge_enabled() && !split.empty() && !col.empty() && split.size() <= (size_t)kMaxD &&
+      col.size() <= (size_t)kMaxD) {
+    // one launch for both kinds (each table holds all its items)
+    SplitTable st{};
+    ColTable ct{};
+    size_t ps = 0, pc = 0;
+    const auto [ns, sblocks] = fill_split(st, split, ps);
+    const auto [nc, cblocks] = fill_col(ct, col, pc);
+    hipLaunchKernelGGL(multi_reduce_kernel, dim3((unsigned)(sblocks + cblocks)), dim3(256), 0, q_stream, st, ns,
+                       sblocks, ct, nc);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    if (!split.empty()) launch_split(split);
+    if (!col.empty()) launch_col(col);
+  }
   q_items.clear();  // the partials go back to the allocator (reuse is ordered after the flush)
   q_bytes = 0;
 }
