@@ -77,7 +77,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ln_bwd_into(const at::Tensor& x, 
 std::tuple<at::Tensor, at::Tensor> rms_bwd_into(const at::Tensor& x, const at::Tensor& dy,
                                                 const c10::optional<at::Tensor>& dres, const at::Tensor& weight,
                                                 const at::Tensor& rstd, const at::Tensor& dw_dst, int accum);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> embed_rms_fwd_hip(const at::Tensor& ids, const at::Tensor& table,
+                                                                 const at::Tensor& weight, double eps,
+                                                                 const c10::optional<at::Tensor>& err);
 }  // namespace norm
+namespace embed {
+at::Tensor embedding_bwd_hip(const at::Tensor& dy, const at::Tensor& idx, int64_t V,
+                             const c10::optional<at::Tensor>& grad_out, bool accumulate);
+}  // namespace embed
+namespace graddst {
+at::Tensor grad_dest_join(const at::Tensor& param);
+}  // namespace graddst
 namespace gemm {
 std::vector<at::Tensor> gemm_warm_take_refs();
 }  // namespace gemm
@@ -568,6 +578,65 @@ struct LNFn : public torch::autograd::Function<LNFn> {
     return {dx, add ? dx : Tensor(), gw.t.defined() ? gw.done() : dw, gb.t.defined() ? gb.done() : db, Tensor()};
   }
 };
+
+// Token embedding + the first RMSNorm (Llama): one forward launch (norm.hip embed_rms_kernel)
+// returning the residual stream x0 and h0 = RMSNorm(x0); in backward the two incoming gradients
+// meet here, so the norm's backward adds the residual stream's gradient in its own pass (no
+// separate add), and the table's gradient goes straight into its DDP bucket slice (graddst.h).
+struct EmbedRMSFn : public torch::autograd::Function<EmbedRMSFn> {
+  static variable_list forward(AutogradContext* ctx, const Tensor& ids, const Tensor& table, const Tensor& w,
+                               double eps, const optional<Tensor>& err) {
+    at::AutoDispatchBelowADInplaceOrView guard;
+    ctx->set_materialize_grads(false);
+    auto [x0, y, rstd] = norm::embed_rms_fwd_hip(ids, table, w, eps, err);
+    ctx->save_for_backward({ids, x0, w, rstd});
+    ctx->saved_data["table"] = table;  // (its bucket slice; the values are not read)
+    return {x0, y};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const auto sv = ctx->get_saved_variables();
+    const Tensor& ids = sv[0];
+    const Tensor& x0 = sv[1];
+    const Tensor& w = sv[2];
+    const Tensor table = ctx->saved_data["table"].toTensor();
+    const Tensor ds = grads[0], dy = grads[1];
+    Tensor dx = ds, dw_ret;
+    if (dy.defined()) {
+      const GradOut gw = grad_out(w, w.requires_grad(), w.sizes(), w.options());
+      const defer::Scope dsc(gw.claimed);
+      auto [dxx, dw] = norm::rms_bwd_into(x0, dy.contiguous(), opt(ds), w, sv[3], gw.t, gw.bit(1));
+      dx = dxx;
+      dw_ret = gw.t.defined() ? gw.done() : dw;
+    }
+    Tensor dtable;
+    if (dx.defined() && table.requires_grad()) {
+      const int64_t C = table.size(1), V = table.size(0);
+      const Tensor d2 = dx.reshape({-1, C}).contiguous(), id1 = ids.reshape({-1});
+      const Tensor j = graddst::grad_dest_join(table);
+      if (j.numel() > 0 && j.scalar_type() == d2.scalar_type()) {
+        // a tied head already wrote this pass's gradient into the slice: add the token rows
+        embed::embedding_bwd_hip(d2, id1, V, j.view({V, C}), true);
+      } else {
+        const GradOut gt = grad_out(table, true, table.sizes(), table.options());
+        embed::embedding_bwd_hip(d2, id1, V, gt.t, gt.acc);
+        dtable = gt.done();
+      }
+    }
+    return {Tensor(), dtable, dw_ret, Tensor(), Tensor()};
+  }
+};
+
+std::tuple<Tensor, Tensor> embed_rms_norm_ag(const Tensor& ids, const Tensor& table, const Tensor& w, double eps,
+                                             const optional<Tensor>& err) {
+  auto r = EmbedRMSFn::apply(ids, table, w, eps, err);
+  return {r[0], r[1]};
+}
+std::tuple<Tensor, Tensor> embed_rms_norm_noag(const Tensor& ids, const Tensor& table, const Tensor& w, double eps,
+                                               const optional<Tensor>& err) {
+  auto r = norm::embed_rms_fwd_hip(ids, table, w, eps, err);
+  return {std::get<0>(r), std::get<1>(r)};
+}
 
 Tensor rms_norm_ag(const Tensor& x, const Tensor& w, double eps) { return RMSFn::apply(x, c10::nullopt, w, eps)[0]; }
 std::tuple<Tensor, Tensor> add_rms_norm_ag(const Tensor& x, const Tensor& delta, const Tensor& w, double eps) {
@@ -1986,6 +2055,7 @@ TORCH_LIBRARY_IMPL(nbd, Autograd, m) {
   m.impl("add_rms_norm_ag", &nbd::ag::add_rms_norm_ag);
   m.impl("layer_norm_ag", &nbd::ag::layer_norm_ag);
   m.impl("add_layer_norm_ag", &nbd::ag::add_layer_norm_ag);
+  m.impl("embed_rms_norm_ag", &nbd::ag::embed_rms_norm_ag);
   m.impl("attn_qkv_ag", &nbd::ag::attn_qkv_ag);
   m.impl("llama_block_ag", &nbd::ag::llama_block_ag);
   m.impl("cast_group_ag", &nbd::ag::cast_group_ag);
@@ -1996,6 +2066,7 @@ TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
   m.impl("add_rms_norm_ag", &nbd::ag::add_rms_norm_noag);
   m.impl("layer_norm_ag", &nbd::ag::layer_norm_noag);
   m.impl("add_layer_norm_ag", &nbd::ag::add_layer_norm_noag);
+  m.impl("embed_rms_norm_ag", &nbd::ag::embed_rms_norm_noag);
   m.impl("attn_qkv_ag", &nbd::ag::attn_qkv_noag);
   m.impl("linear_ag", &nbd::ag::linear_noag);
   m.impl("mlp_gelu_ag", &nbd::ag::mlp_gelu_noag);

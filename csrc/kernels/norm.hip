@@ -500,6 +500,64 @@ __global__ __launch_bounds__(NT) void col_reduce_kernel(const float* __restrict_
 }
 
 // ============================================================================ host
+// A Llama model's token embedding and its first RMSNorm in one pass (a wave per row):
+// x0[r] = table[ids[r]] (stored: the residual stream) and y[r] = RMSNorm(x0[r])·g, with the same
+// arithmetic as F.embedding + ln_fwd_kernel<RMS> (identical bits).  Out-of-range ids read as zero
+// rows and set `err` (the host reads the flag lazily, ops/embedding.py), as embedding_tokpos does.
+template <typename T, typename W, int NCH>
+__global__ __launch_bounds__(NT) void embed_rms_kernel(const int64_t* __restrict__ ids, const T* __restrict__ table,
+                                                       int64_t V, const W* __restrict__ gamma, T* __restrict__ x0,
+                                                       T* __restrict__ y, float* __restrict__ rstd_out, int64_t rows,
+                                                       int C, float eps, int* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (NT / kWave) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int64_t id = ids[row];
+  const bool ok = id >= 0 && id < V;
+  if (!ok && err != nullptr && lane == 0) atomicOr(err, 1);  // (a vector-memory atomic)
+  const T* src = table + (ok ? id : 0) * (int64_t)C;
+  const int64_t base = row * C;
+  float v[NCH][4], g[NCH][4];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * lane + 256 * k;
+    if (c < C) {
+      load4<W>(gamma + c, g[k]);
+      if (ok) {
+        load4<T>(src + c, v[k]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[k][e] = 0.f;
+      }
+      store4<T>(x0 + base + c, v[k]);
+    }
+  }
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * lane + 256 * k;
+    if (c < C) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[k][e] - 0.f;
+        q = fmaf(d, d, q);
+      }
+    }
+  }
+  const float rstd = rsqrtf(wsum(q) / (float)C + eps);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * lane + 256 * k;
+    if (c < C) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = fmaf((v[k][e] - 0.f) * rstd, g[k][e], 0.f);
+      store4<T>(y + base + c, o);
+    }
+  }
+  if (lane == 0) rstd_out[row] = rstd;
+}
+
 static void check_rows(const at::Tensor& t, int64_t C, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.size(-1) == C, "norm: ", name, " must be contiguous [..., C]");
   TORCH_CHECK(((uintptr_t)t.data_ptr() & 15) == 0, "norm: ", name, " must be 16-B aligned");
@@ -738,6 +796,42 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rms_fwd_hip(const at::Tensor& x, 
   });
   C10_HIP_KERNEL_LAUNCH_CHECK();
   return {y, xsum, rstd};
+}
+
+// (x0, y, rstd) of embed_rms_kernel: x0 / y shaped ids.shape + [C]
+std::tuple<at::Tensor, at::Tensor, at::Tensor> embed_rms_fwd_hip(const at::Tensor& ids, const at::Tensor& table,
+                                                                 const at::Tensor& weight, double eps,
+                                                                 const c10::optional<at::Tensor>& err) {
+  TORCH_CHECK(ids.is_cuda() && table.is_cuda() && weight.is_cuda(), "embed_rms: GPU tensors expected");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous(), "embed_rms: contiguous int64 ids expected");
+  TORCH_CHECK(table.dim() == 2 && table.is_contiguous(), "embed_rms: contiguous [V, C] table expected");
+  const int64_t C = table.size(1), V = table.size(0);
+  TORCH_CHECK(C % 4 == 0 && C <= 256 * kMaxCh && C > 0, "embed_rms: C must be a multiple of 4 and <= 2048");
+  TORCH_CHECK(((uintptr_t)table.data_ptr() & 7) == 0, "embed_rms: 8-B aligned table expected");
+  TORCH_CHECK(weight.is_contiguous() && weight.numel() == C, "embed_rms: weight must be [C]");
+  if (err) TORCH_CHECK(err->is_cuda() && err->scalar_type() == at::kInt && err->numel() >= 1, "embed_rms: int32 error flag");
+  std::vector<int64_t> shape(ids.sizes().begin(), ids.sizes().end());
+  shape.push_back(C);
+  at::Tensor x0 = at::empty(shape, table.options()), y = at::empty(shape, table.options());
+  const int64_t rows = ids.numel();
+  at::Tensor rstd = at::empty({rows}, table.options().dtype(at::kFloat));
+  if (rows == 0) return {x0, y, rstd};
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  dispatch_tw(table.scalar_type(), weight.scalar_type(), [&](auto t, auto w) {
+   dispatch_nch(C, [&](auto nch) {
+    using T = decltype(t);
+    using W = decltype(w);
+    constexpr int N = decltype(nch)::value;
+    hipLaunchKernelGGL((embed_rms_kernel<T, W, N>), grid, dim3(NT), 0, st, ids.data_ptr<int64_t>(),
+                       static_cast<const T*>(table.data_ptr()), V, static_cast<const W*>(weight.data_ptr()),
+                       static_cast<T*>(x0.data_ptr()), static_cast<T*>(y.data_ptr()), rstd.data_ptr<float>(), rows,
+                       (int)C, (float)eps, err ? err->data_ptr<int>() : nullptr);
+   });
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return {x0, y, rstd};
 }
 
 std::tuple<at::Tensor, at::Tensor> rms_bwd_into(const at::Tensor& x, const at::Tensor& dy,

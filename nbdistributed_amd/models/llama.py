@@ -441,9 +441,10 @@ class LlamaModel(nn.Module):
         cd = self.cast_dtype(input_ids) if cache is None else None
         if cd is not None:
             return self._forward_cast(input_ids, cd, cos, sin)
-        x = ops.embedding(input_ids, self.embed_tokens.weight)
         # the residual stream: each block's two residual adds are fused with the RMSNorm after them
-        h = self.layers[0].input_layernorm(x)
+        # (and the embedding with the first one)
+        ln0 = self.layers[0].input_layernorm
+        x, h = ops.embed_rms_norm(input_ids, self.embed_tokens.weight, ln0.weight, ln0.eps)
         for i, layer in enumerate(self.layers):
             nxt = self.layers[i + 1].input_layernorm if i + 1 < len(self.layers) else self.norm
             at = layer.self_attn

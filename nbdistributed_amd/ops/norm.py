@@ -160,3 +160,29 @@ def add_rms_norm(x, delta, weight, eps: float = 1e-6):
         return _llama_fns()[1].apply(x, delta, weight, float(eps))
     s = x + delta
     return s, rms_norm(s, weight, eps)
+
+
+# the fused token embedding + first RMSNorm (NBD_EMBED_RMS=0: the two ops, A/B)
+_EMBED_RMS = __import__("os").environ.get("NBD_EMBED_RMS", "1") != "0"
+
+
+def embed_rms_norm(ids, table, weight, eps: float = 1e-6):
+    """``x = F.embedding(ids, table); return x, rms_norm(x, weight)`` — a Llama model's input: one
+    HIP pass forward (the gathered rows stored as the residual stream beside their norm) and, in
+    backward, one norm pass that also adds the residual stream's gradient, then the table's
+    gradient straight into its DDP bucket slice (``csrc/kernels/autograd.hip`` EmbedRMSFn).
+    Same bits as the two separate ops."""
+    import torch
+
+    from .embedding import _poll_ids, embedding
+
+    C = table.shape[-1]
+    if (_EMBED_RMS and table.is_cuda and _native() and ids.dtype == torch.int64 and table.dim() == 2
+            and table.dtype == weight.dtype and table.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and C % 4 == 0 and C <= 2048 and table.is_contiguous() and not torch.is_autocast_enabled()):
+        _require()
+        return torch.ops.nbd.embed_rms_norm_ag(ids if ids.is_contiguous() else ids.contiguous(), table, weight,
+                                               float(eps), _poll_ids(table.device))
+    x = embedding(ids, table)
+    return x, rms_norm(x, weight, eps)
+

@@ -45,6 +45,38 @@ def test_rms_norm(dev, res, C):
         assert _rel(ds.grad, dr.grad) < 3e-2
 
 
+@pytest.mark.parametrize("C", [576, 64])
+def test_embed_rms_norm_matches_separate_ops(dev, C):
+    """ops.embed_rms_norm (one forward launch; in backward the residual stream's gradient added in
+    the norm's pass) against F.embedding + ops.rms_norm: x0 and h bit-identical, the table and
+    weight gradients equal to the two-op path's, both gradients arriving (ds from the residual
+    stream, dh from the norm's output), a repeated id included."""
+    g = torch.Generator(device="cpu").manual_seed(C)
+    V = 300
+    table = torch.randn(V, C, generator=g).to(dev, torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(C, generator=g)).to(dev, torch.bfloat16)
+    ids = torch.randint(0, V, (3, 128), generator=g).to(dev)
+    ids[0, 5] = ids[1, 7]
+    ds = torch.randn(3, 128, C, generator=g).to(dev, torch.bfloat16)
+    dh = torch.randn(3, 128, C, generator=g).to(dev, torch.bfloat16)
+    t1, w1 = table.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    x1, h1 = ops.embed_rms_norm(ids, t1, w1, 1e-5)
+    torch.autograd.backward([x1, h1], [ds, dh])
+    t2, w2 = table.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    x2 = F.embedding(ids, t2)
+    h2 = ops.rms_norm(x2, w2, 1e-5)
+    torch.autograd.backward([x2, h2], [ds, dh])
+    torch.cuda.synchronize()
+    assert torch.equal(x1, x2) and torch.equal(h1, h2)
+    assert _rel(t1.grad, t2.grad) < 1e-2 and _rel(w1.grad, w2.grad) < 1e-2
+    # only the norm's output used: the residual-gradient path absent
+    t3 = table.clone().requires_grad_(True)
+    ops.embed_rms_norm(ids, t3, w, 1e-5)[1].backward(dh)
+    t4 = table.clone().requires_grad_(True)
+    ops.rms_norm(F.embedding(ids, t4), w, 1e-5).backward(dh)
+    assert _rel(t3.grad, t4.grad) < 1e-2
+
+
 def test_rope_forward_backward(dev):
     B, T, H, Hkv, D = 2, 128, 9, 3, 64
     x = torch.randn(B, T, (H + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
