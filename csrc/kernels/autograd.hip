@@ -80,10 +80,15 @@ std::tuple<at::Tensor, at::Tensor> rms_bwd_into(const at::Tensor& x, const at::T
 std::tuple<at::Tensor, at::Tensor, at::Tensor> embed_rms_fwd_hip(const at::Tensor& ids, const at::Tensor& table,
                                                                  const at::Tensor& weight, double eps,
                                                                  const c10::optional<at::Tensor>& err);
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tokpos_ln_fwd_hip(
+    const at::Tensor& idx, const at::Tensor& wte, const at::Tensor& pos, const at::Tensor& wpe, int64_t vocab,
+    const at::Tensor& weight, const at::Tensor& bias, double eps, const c10::optional<at::Tensor>& err);
 }  // namespace norm
 namespace embed {
 at::Tensor embedding_bwd_hip(const at::Tensor& dy, const at::Tensor& idx, int64_t V,
                              const c10::optional<at::Tensor>& grad_out, bool accumulate);
+at::Tensor embedding_pos_bwd_hip(const at::Tensor& dy, const at::Tensor& pos, int64_t P,
+                                 const c10::optional<at::Tensor>& out_opt, bool accumulate);
 }  // namespace embed
 namespace graddst {
 at::Tensor grad_dest_join(const at::Tensor& param);
@@ -579,6 +584,22 @@ struct LNFn : public torch::autograd::Function<LNFn> {
   }
 };
 
+// The gradient of an embedding table from the gradient at its gathered rows (ids < V; rows of the
+// table past V are padding and get zeros): into the table's DDP bucket slice when it has one — or,
+// when a tied LM head already wrote this pass's gradient there, added into it (nothing returned)
+static Tensor table_grad(const Tensor& table, const Tensor& dx, const Tensor& ids, int64_t V) {
+  const int64_t C = table.size(1);
+  const Tensor d2 = dx.reshape({-1, C}).contiguous(), id1 = ids.reshape({-1});
+  const Tensor j = graddst::grad_dest_join(table);
+  if (j.numel() > 0 && j.scalar_type() == d2.scalar_type()) {
+    embed::embedding_bwd_hip(d2, id1, V, j.view(table.sizes()), true);
+    return Tensor();
+  }
+  const GradOut gt = grad_out(table, true, table.sizes(), table.options());
+  embed::embedding_bwd_hip(d2, id1, V, gt.t, gt.acc);
+  return gt.done();
+}
+
 // Token embedding + the first RMSNorm (Llama): one forward launch (norm.hip embed_rms_kernel)
 // returning the residual stream x0 and h0 = RMSNorm(x0); in backward the two incoming gradients
 // meet here, so the norm's backward adds the residual stream's gradient in its own pass (no
@@ -609,23 +630,74 @@ struct EmbedRMSFn : public torch::autograd::Function<EmbedRMSFn> {
       dx = dxx;
       dw_ret = gw.t.defined() ? gw.done() : dw;
     }
-    Tensor dtable;
-    if (dx.defined() && table.requires_grad()) {
-      const int64_t C = table.size(1), V = table.size(0);
-      const Tensor d2 = dx.reshape({-1, C}).contiguous(), id1 = ids.reshape({-1});
-      const Tensor j = graddst::grad_dest_join(table);
-      if (j.numel() > 0 && j.scalar_type() == d2.scalar_type()) {
-        // a tied head already wrote this pass's gradient into the slice: add the token rows
-        embed::embedding_bwd_hip(d2, id1, V, j.view({V, C}), true);
-      } else {
-        const GradOut gt = grad_out(table, true, table.sizes(), table.options());
-        embed::embedding_bwd_hip(d2, id1, V, gt.t, gt.acc);
-        dtable = gt.done();
-      }
-    }
+    const Tensor dtable = dx.defined() && table.requires_grad() ? table_grad(table, dx, ids, table.size(0)) : Tensor();
     return {Tensor(), dtable, dw_ret, Tensor(), Tensor()};
   }
 };
+
+// GPT-2's token + position embedding + the first LayerNorm: one forward launch (norm.hip
+// tokpos_ln_kernel); in backward the norm's pass adds the residual stream's gradient, then the
+// token table's gradient (bucket slice / tied head: table_grad) and the position table's
+// (the batch summed per position, into its slice: embedding_pos_bwd).
+struct TokPosLNFn : public torch::autograd::Function<TokPosLNFn> {
+  static variable_list forward(AutogradContext* ctx, const Tensor& idx, const Tensor& wte, const Tensor& pos,
+                               const Tensor& wpe, const Tensor& w, const Tensor& b, int64_t vocab, double eps,
+                               const optional<Tensor>& err) {
+    at::AutoDispatchBelowADInplaceOrView guard;
+    ctx->set_materialize_grads(false);
+    auto [x0, y, mean, rstd] = norm::tokpos_ln_fwd_hip(idx, wte, pos, wpe, vocab, w, b, eps, err);
+    ctx->save_for_backward({idx, pos, x0, w, mean, rstd});
+    ctx->saved_data["wte"] = wte;  // (identities only: their gradients' bucket slices)
+    ctx->saved_data["wpe"] = wpe;
+    if (b.requires_grad()) ctx->saved_data["b"] = b;
+    ctx->saved_data["V"] = vocab > 0 ? std::min<int64_t>(vocab, wte.size(0)) : wte.size(0);
+    return {x0, y};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const auto sv = ctx->get_saved_variables();
+    const Tensor &idx = sv[0], &pos = sv[1], &x0 = sv[2], &w = sv[3];
+    const Tensor wte = ctx->saved_data["wte"].toTensor(), wpe = ctx->saved_data["wpe"].toTensor();
+    const Tensor ds = grads[0], dy = grads[1];
+    Tensor dx = ds, dw_ret, db_ret;
+    if (dy.defined()) {
+      const GradOut gw = grad_out(w, w.requires_grad(), w.sizes(), w.options());
+      const GradOut gb = grad_out(ctx->saved_data.count("b") ? ctx->saved_data["b"].toTensor() : Tensor(), true,
+                                  w.sizes(), w.options());
+      const defer::Scope dsc(gw.claimed && gb.claimed);
+      auto [dxx, dw, db] = norm::ln_bwd_into(x0, dy.contiguous(), opt(ds), w, sv[4], sv[5], gw.t, gb.t,
+                                             gw.bit(1) | gb.bit(2));
+      dx = dxx;
+      dw_ret = gw.t.defined() ? gw.done() : dw;
+      db_ret = gb.t.defined() ? gb.done() : db;
+    }
+    Tensor dwte, dwpe;
+    if (dx.defined()) {
+      if (wte.requires_grad()) dwte = table_grad(wte, dx, idx, ctx->saved_data["V"].toInt());
+      if (wpe.requires_grad()) {
+        const int64_t C = wpe.size(1), P = wpe.size(0);
+        const Tensor d2 = dx.reshape({-1, C}).contiguous();
+        const GradOut gp = grad_out(wpe, true, wpe.sizes(), wpe.options());
+        embed::embedding_pos_bwd_hip(d2, pos, P, gp.t, gp.acc);
+        dwpe = gp.done();
+      }
+    }
+    return {Tensor(), dwte, Tensor(), dwpe, dw_ret, db_ret, Tensor(), Tensor(), Tensor()};
+  }
+};
+
+std::tuple<Tensor, Tensor> tokpos_layer_norm_ag(const Tensor& idx, const Tensor& wte, const Tensor& pos,
+                                                const Tensor& wpe, const Tensor& w, const Tensor& b, int64_t vocab,
+                                                double eps, const optional<Tensor>& err) {
+  auto r = TokPosLNFn::apply(idx, wte, pos, wpe, w, b, vocab, eps, err);
+  return {r[0], r[1]};
+}
+std::tuple<Tensor, Tensor> tokpos_layer_norm_noag(const Tensor& idx, const Tensor& wte, const Tensor& pos,
+                                                  const Tensor& wpe, const Tensor& w, const Tensor& b, int64_t vocab,
+                                                  double eps, const optional<Tensor>& err) {
+  auto r = norm::tokpos_ln_fwd_hip(idx, wte, pos, wpe, vocab, w, b, eps, err);
+  return {std::get<0>(r), std::get<1>(r)};
+}
 
 std::tuple<Tensor, Tensor> embed_rms_norm_ag(const Tensor& ids, const Tensor& table, const Tensor& w, double eps,
                                              const optional<Tensor>& err) {
@@ -2056,6 +2128,7 @@ TORCH_LIBRARY_IMPL(nbd, Autograd, m) {
   m.impl("layer_norm_ag", &nbd::ag::layer_norm_ag);
   m.impl("add_layer_norm_ag", &nbd::ag::add_layer_norm_ag);
   m.impl("embed_rms_norm_ag", &nbd::ag::embed_rms_norm_ag);
+  m.impl("tokpos_layer_norm_ag", &nbd::ag::tokpos_layer_norm_ag);
   m.impl("attn_qkv_ag", &nbd::ag::attn_qkv_ag);
   m.impl("llama_block_ag", &nbd::ag::llama_block_ag);
   m.impl("cast_group_ag", &nbd::ag::cast_group_ag);
@@ -2067,6 +2140,7 @@ TORCH_LIBRARY_IMPL(nbd, CUDA, m) {
   m.impl("layer_norm_ag", &nbd::ag::layer_norm_noag);
   m.impl("add_layer_norm_ag", &nbd::ag::add_layer_norm_noag);
   m.impl("embed_rms_norm_ag", &nbd::ag::embed_rms_norm_noag);
+  m.impl("tokpos_layer_norm_ag", &nbd::ag::tokpos_layer_norm_noag);
   m.impl("attn_qkv_ag", &nbd::ag::attn_qkv_noag);
   m.impl("linear_ag", &nbd::ag::linear_noag);
   m.impl("mlp_gelu_ag", &nbd::ag::mlp_gelu_noag);

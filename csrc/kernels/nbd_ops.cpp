@@ -50,6 +50,8 @@ TORCH_LIBRARY(nbd, m) {
   m.def("rms_norm_ag(Tensor x, Tensor w, float eps) -> Tensor");
   m.def("add_rms_norm_ag(Tensor x, Tensor delta, Tensor w, float eps) -> (Tensor, Tensor)");
   m.def("embed_rms_norm_ag(Tensor ids, Tensor table, Tensor w, float eps, Tensor(a!)? err=None) -> (Tensor, Tensor)");
+  m.def("tokpos_layer_norm_ag(Tensor idx, Tensor wte, Tensor pos, Tensor wpe, Tensor w, Tensor b, int vocab, float eps, "
+        "Tensor(a!)? err=None) -> (Tensor, Tensor)");
   m.def("layer_norm_ag(Tensor x, Tensor w, Tensor b, float eps) -> Tensor");
   m.def("add_layer_norm_ag(Tensor x, Tensor delta, Tensor w, Tensor b, float eps) -> (Tensor, Tensor)");
   m.def("attn_qkv_ag(Tensor qkv, int n_head, int n_kv, bool causal, float scale, Tensor? cos, Tensor? sin) -> Tensor");

@@ -558,6 +558,86 @@ __global__ __launch_bounds__(NT) void embed_rms_kernel(const int64_t* __restrict
   if (lane == 0) rstd_out[row] = rstd;
 }
 
+// GPT-2's input and its first LayerNorm in one pass (a wave per row): x0[r] = wte[idx[r]] +
+// wpe[pos[r % Tp]] (fp32 add, stored rounded — embedding_tokpos's bits) and y[r] = LayerNorm(x0[r])
+// with ln_fwd_kernel's arithmetic on the rounded row.  Out-of-range ids (outside [0, V)) read as
+// zero rows and set `err`; out-of-range positions read as zero rows.
+template <typename T, typename W, int NCH>
+__global__ __launch_bounds__(NT) void tokpos_ln_kernel(const int64_t* __restrict__ idx, const T* __restrict__ wte,
+                                                       int64_t V, const int64_t* __restrict__ pos, int Tp,
+                                                       const T* __restrict__ wpe, int64_t P,
+                                                       const W* __restrict__ gamma, const W* __restrict__ beta,
+                                                       T* __restrict__ x0, T* __restrict__ y, float* __restrict__ mean_out,
+                                                       float* __restrict__ rstd_out, int64_t rows, int C, float eps,
+                                                       int* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (NT / kWave) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int64_t id = idx[row], q = pos[row % Tp];
+  const bool ok = id >= 0 && id < V, okp = q >= 0 && q < P;
+  if (!ok && err != nullptr && lane == 0) atomicOr(err, 1);  // (a vector-memory atomic)
+  const T* ta = wte + (ok ? id : 0) * (int64_t)C;
+  const T* tb = wpe + (okp ? q : 0) * (int64_t)C;
+  const int64_t base = row * C;
+  float v[NCH][4], g[NCH][4], b[NCH][4];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * lane + 256 * k;
+    if (c < C) {
+      load4<W>(gamma + c, g[k]);
+      load4<W>(beta + c, b[k]);
+      float e2[4];
+      if (ok) {
+        load4<T>(ta + c, v[k]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[k][e] = 0.f;
+      }
+      if (okp) {
+        load4<T>(tb + c, e2);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) e2[e] = 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[k][e] += e2[e];
+      store4<T>(x0 + base + c, v[k]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[k][e] = round_to<T>(v[k][e]);  // normalise what was stored
+      s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
+    }
+  }
+  const float mean = wsum(s) / (float)C;
+  float qq = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * lane + 256 * k;
+    if (c < C) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[k][e] - mean;
+        qq = fmaf(d, d, qq);
+      }
+    }
+  }
+  const float rstd = rsqrtf(wsum(qq) / (float)C + eps);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * lane + 256 * k;
+    if (c < C) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = fmaf((v[k][e] - mean) * rstd, g[k][e], b[k][e]);
+      store4<T>(y + base + c, o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
 static void check_rows(const at::Tensor& t, int64_t C, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.size(-1) == C, "norm: ", name, " must be contiguous [..., C]");
   TORCH_CHECK(((uintptr_t)t.data_ptr() & 15) == 0, "norm: ", name, " must be 16-B aligned");
@@ -832,6 +912,53 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> embed_rms_fwd_hip(const at::Tenso
   });
   C10_HIP_KERNEL_LAUNCH_CHECK();
   return {x0, y, rstd};
+}
+
+// (x0, y, mean, rstd) of tokpos_ln_kernel: x0 / y shaped idx.shape + [C]; vocab < wte rows: the
+// rows past it are padding (ids there are out of range)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tokpos_ln_fwd_hip(
+    const at::Tensor& idx, const at::Tensor& wte, const at::Tensor& pos, const at::Tensor& wpe, int64_t vocab,
+    const at::Tensor& weight, const at::Tensor& bias, double eps, const c10::optional<at::Tensor>& err) {
+  TORCH_CHECK(idx.is_cuda() && wte.is_cuda() && pos.is_cuda() && wpe.is_cuda(), "tokpos_ln: GPU tensors expected");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && pos.scalar_type() == at::kLong && idx.is_contiguous() &&
+                  pos.is_contiguous() && pos.dim() == 1 && pos.numel() > 0 && idx.numel() % pos.numel() == 0,
+              "tokpos_ln: int64 ids [..., T] and positions [T]");
+  TORCH_CHECK(wte.dim() == 2 && wpe.dim() == 2 && wte.size(1) == wpe.size(1) && wte.is_contiguous() &&
+                  wpe.is_contiguous() && wte.scalar_type() == wpe.scalar_type(),
+              "tokpos_ln: contiguous [V, C] / [P, C] tables of one dtype");
+  const int64_t C = wte.size(1);
+  TORCH_CHECK(C % 4 == 0 && C <= 256 * kMaxCh && C > 0, "tokpos_ln: C must be a multiple of 4 and <= 2048");
+  TORCH_CHECK(((uintptr_t)wte.data_ptr() & 7) == 0 && ((uintptr_t)wpe.data_ptr() & 7) == 0,
+              "tokpos_ln: 8-B aligned tables expected");
+  TORCH_CHECK(weight.is_contiguous() && bias.is_contiguous() && weight.numel() == C && bias.numel() == C,
+              "tokpos_ln: weight / bias must be [C]");
+  if (err) TORCH_CHECK(err->is_cuda() && err->scalar_type() == at::kInt && err->numel() >= 1, "tokpos_ln: int32 error flag");
+  const int64_t V = vocab > 0 ? std::min<int64_t>(vocab, wte.size(0)) : wte.size(0);
+  std::vector<int64_t> shape(idx.sizes().begin(), idx.sizes().end());
+  shape.push_back(C);
+  at::Tensor x0 = at::empty(shape, wte.options()), y = at::empty(shape, wte.options());
+  const int64_t rows = idx.numel();
+  auto fo = wte.options().dtype(at::kFloat);
+  at::Tensor mean = at::empty({rows}, fo), rstd = at::empty({rows}, fo);
+  if (rows == 0) return {x0, y, mean, rstd};
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(wte.device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  dispatch_tw(wte.scalar_type(), weight.scalar_type(), [&](auto t, auto w) {
+   dispatch_nch(C, [&](auto nch) {
+    using T = decltype(t);
+    using W = decltype(w);
+    constexpr int N = decltype(nch)::value;
+    hipLaunchKernelGGL((tokpos_ln_kernel<T, W, N>), grid, dim3(NT), 0, st, idx.data_ptr<int64_t>(),
+                       static_cast<const T*>(wte.data_ptr()), V, pos.data_ptr<int64_t>(), (int)pos.numel(),
+                       static_cast<const T*>(wpe.data_ptr()), wpe.size(0), static_cast<const W*>(weight.data_ptr()),
+                       static_cast<const W*>(bias.data_ptr()), static_cast<T*>(x0.data_ptr()),
+                       static_cast<T*>(y.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, (int)C,
+                       (float)eps, err ? err->data_ptr<int>() : nullptr);
+   });
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return {x0, y, mean, rstd};
 }
 
 std::tuple<at::Tensor, at::Tensor> rms_bwd_into(const at::Tensor& x, const at::Tensor& dy,

@@ -245,20 +245,30 @@ class GPT2(nn.Module):
         B, T = idx.shape
         pos_fn = getattr(self, "position_ids", None)  # set by parallel.context (global positions)
         pos = pos_fn(T, idx.device) if pos_fn is not None else torch.arange(T, device=idx.device)
-        if self._fast_ok(idx):
+        c = self.config
+        fused_in = (self._fast_ok(idx) and c.fused_norm and c.bias and c.n_embd % 8 == 0 and c.n_embd <= 2048
+                    and T % 128 == 0 and c.n_layer > 0)
+        if fused_in:
+            # the input and the first LayerNorm as one node (and one launch)
+            from .. import ops
+
+            ln = self.h[0].ln_1
+            x, h = ops.tokpos_layer_norm(idx, self.wte.weight, pos, self.wpe.weight, c.vocab_size, ln.weight,
+                                         ln.bias, ln.eps)
+        elif self._fast_ok(idx):
             from .. import ops
 
             x = ops.embedding_tok_pos(idx, self.wte.weight, pos, self.wpe.weight, self.config.vocab_size)
         else:
             x = self.wte(idx) + self.wpe(pos)
-        if self._fast(x):
+        if fused_in or self._fast(x):
             # residual stream through the HIP add+LayerNorm kernels: each block's two residual adds
             # are fused with the LayerNorm that follows them (ln_2, then the next block's ln_1 / ln_f)
             from .. import ops
 
-            c = self.config
-            ln = self.h[0].ln_1
-            h = ops.layer_norm(x, ln.weight, ln.bias, ln.eps)
+            if not fused_in:
+                ln = self.h[0].ln_1
+                h = ops.layer_norm(x, ln.weight, ln.bias, ln.eps)
             for i, blk in enumerate(self.h):
                 fa = self.fused_attn_ok
                 a = blk.attn(h, fast=fa) if cache is None else blk.attn(h, fast=fa, kv=(cache, i))

@@ -50,7 +50,7 @@ from .gemm import (block_graphs, block_graphs_memory, block_graphs_reset, block_
 from .llama import rope_, rope_tables, swiglu
 from .loss import cross_entropy, linear_cross_entropy
 from .mask import seqcls_prep
-from .norm import add_layer_norm, add_rms_norm, colsum, embed_rms_norm, layer_norm, linear, rms_norm
+from .norm import add_layer_norm, add_rms_norm, colsum, embed_rms_norm, layer_norm, linear, rms_norm, tokpos_layer_norm
 from .optim import _ref_adamw, adamw_flat
 from .tiny import linear_tiny
 from .summary import SUMMARY_FIELDS, _ref_summary, tensor_summary, tensor_summary_raw, tensor_summary_text
@@ -64,6 +64,6 @@ def __getattr__(name):
 
 __all__ = ["linear_tiny", "bucket_flatten", "bucket_unflatten", "local_prereduce", "prereduce_into_bucket", "graddst", "adamw_flat", "cross_entropy", "linear_cross_entropy",
            "flash_attention", "attention_qkv", "decode_attention", "decode_attention_reference", "linear_small", "linear_small_reference", "flash_supported", "layer_norm", "add_layer_norm", "linear",
-           "colsum", "embedding", "embedding_tok_pos", "gemm_linear", "llama_block", "block_graphs", "block_graphs_memory", "block_graphs_reset", "block_graphs_stats", "cast_buffers_memory", "mlp_gelu", "mlp_swiglu", "rms_norm", "add_rms_norm", "embed_rms_norm", "rope_", "rope_tables", "swiglu", "tensor_summary",
+           "colsum", "embedding", "embedding_tok_pos", "gemm_linear", "llama_block", "block_graphs", "block_graphs_memory", "block_graphs_reset", "block_graphs_stats", "cast_buffers_memory", "mlp_gelu", "mlp_swiglu", "rms_norm", "add_rms_norm", "embed_rms_norm", "tokpos_layer_norm", "rope_", "rope_tables", "swiglu", "tensor_summary",
            "tensor_summary_text", "tensor_summary_raw", "plan_offsets", "native_available", "load_library",
            "SUMMARY_FIELDS", "seqcls_prep"]

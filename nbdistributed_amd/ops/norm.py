@@ -186,3 +186,26 @@ def embed_rms_norm(ids, table, weight, eps: float = 1e-6):
     x = embedding(ids, table)
     return x, rms_norm(x, weight, eps)
 
+
+def tokpos_layer_norm(idx, wte, pos, wpe, vocab: int, weight, bias, eps: float = 1e-5):
+    """``x = embedding_tok_pos(idx, wte, pos, wpe, vocab); return x, layer_norm(x, weight, bias)`` —
+    GPT-2's input and its first LayerNorm in one HIP pass, their backward in one norm pass (the
+    residual stream's gradient added there) plus the two tables' gradients, each into its DDP
+    bucket slice (``csrc/kernels/autograd.hip`` TokPosLNFn).  Same bits forward as the two ops.
+    ``NBD_EMBED_RMS=0`` also turns this fusion off (A/B)."""
+    import torch
+
+    from .embedding import FUSED_EMBED, _poll_ids, embedding_tok_pos
+
+    C = wte.shape[-1]
+    if (_EMBED_RMS and FUSED_EMBED and wte.is_cuda and _native() and idx.dtype == torch.int64
+            and pos.dtype == torch.int64 and pos.dim() == 1 and idx.shape[-1] == pos.numel() and wte.dim() == 2
+            and wte.dtype == wpe.dtype == weight.dtype == bias.dtype and wte.dtype in (torch.bfloat16, torch.float16)
+            and C % 8 == 0 and C <= 2048 and wte.is_contiguous() and wpe.is_contiguous()
+            and not torch.is_autocast_enabled()):
+        _require()
+        return torch.ops.nbd.tokpos_layer_norm_ag(idx.contiguous(), wte, pos.contiguous(), wpe, weight, bias,
+                                                  int(vocab), float(eps), _poll_ids(wte.device))
+    x = embedding_tok_pos(idx, wte, pos, wpe, vocab)
+    return x, layer_norm(x, weight, bias, eps)
+

@@ -77,6 +77,40 @@ def test_embed_rms_norm_matches_separate_ops(dev, C):
     assert _rel(t3.grad, t4.grad) < 1e-2
 
 
+def test_tokpos_layer_norm_matches_separate_ops(dev):
+    """ops.tokpos_layer_norm (GPT-2's input + first LayerNorm as one node) against
+    embedding_tok_pos + layer_norm: x0 and h bit-identical; token table (padded past the
+    vocabulary: zero gradient there), position table, weight and bias gradients equal to the
+    two-op path's with both the residual and the norm gradient arriving."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    V, Vp, P, C, T = 500, 512, 256, 256, 128
+    wte = torch.randn(Vp, C, generator=g).to(dev, torch.bfloat16)
+    wte[V:] = 0
+    wpe = torch.randn(P, C, generator=g).to(dev, torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(C, generator=g)).to(dev, torch.bfloat16)
+    b = (0.1 * torch.randn(C, generator=g)).to(dev, torch.bfloat16)
+    idx = torch.randint(0, V, (2, T), generator=g).to(dev)
+    pos = torch.arange(T, device=dev)
+    ds = torch.randn(2, T, C, generator=g).to(dev, torch.bfloat16)
+    dh = torch.randn(2, T, C, generator=g).to(dev, torch.bfloat16)
+    outs = []
+    for fused in (True, False):
+        ps = [t.clone().requires_grad_(True) for t in (wte, wpe, w, b)]
+        if fused:
+            x, h = ops.tokpos_layer_norm(idx, ps[0], pos, ps[1], V, ps[2], ps[3], 1e-5)
+        else:
+            x = ops.embedding_tok_pos(idx, ps[0], pos, ps[1], V)
+            h = ops.layer_norm(x, ps[2], ps[3], 1e-5)
+        torch.autograd.backward([x, h], [ds, dh])
+        torch.cuda.synchronize()
+        outs.append((x, h, [p.grad for p in ps]))
+    (x1, h1, g1), (x2, h2, g2) = outs
+    assert torch.equal(x1, x2) and torch.equal(h1, h2)
+    for a, r in zip(g1, g2):
+        assert _rel(a, r) < 1e-2
+    assert (g1[0][V:] == 0).all()
+
+
 def test_rope_forward_backward(dev):
     B, T, H, Hkv, D = 2, 128, 9, 3, 64
     x = torch.randn(B, T, (H + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
