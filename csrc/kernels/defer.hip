@@ -264,10 +264,15 @@ void flush_carry_locked() {
 }
 
 void flush_locked() {
-  flush_carry_locked();
+  // a carried reduce on the queue's stream joins the queue's launch (the outputs are disjoint
+  // slices: a second claim of a slice flushes before it is written again)
+  const bool carry_joins = c_has && !q_items.empty() && c_stream == q_stream && c_device == q_device &&
+                           c_capturing == q_capturing && merge_enabled();
+  if (!carry_joins) flush_carry_locked();
   if (q_items.empty()) return;
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)q_device));
   std::vector<const Item*> split, col;
+  if (carry_joins) split.push_back(&c_item);
   for (const Item& it : q_items) (it.kind == 0 ? split : col).push_back(&it);
   if (merge_enabled() && !split.empty() && !col.empty() && split.size() <= (size_t)kMaxD &&
       col.size() <= (size_t)kMaxD) {
@@ -286,6 +291,10 @@ void flush_locked() {
   }
   q_items.clear();  // the partials go back to the allocator (reuse is ordered after the flush)
   q_bytes = 0;
+  if (carry_joins) {
+    c_item = Item{};
+    c_has = false;
+  }
 }
 
 thread_local std::vector<Item>* t_record = nullptr;  // record_begin(): queued for replays instead
