@@ -321,6 +321,69 @@ __device__ __forceinline__ float hsum(float v) {  // sum over the 32 lanes of a 
 
 constexpr int kRpi16 = 1;  // one row pair per wave iteration: 192 VGPRs (two pairs: 256, and slower — 16.8 vs 16.2 µs)
 
+// Forward with 16-B accesses (2-byte types, C a multiple of 256): a half-wave per row, NCH
+// 8-element chunks per lane (ln_fwd_kernel: a wave per row, 8-B chunks).  Same math; the partial
+// sums group 8 elements per lane, so the last bits can differ from ln_fwd_kernel's.
+template <typename T, typename W, bool RES, int NCH, bool RMS = false>
+__global__ __launch_bounds__(NT) void ln_fwd16_kernel(const T* __restrict__ x, const T* __restrict__ delta,
+                                                      T* __restrict__ xsum, const W* __restrict__ gamma,
+                                                      const W* __restrict__ beta, T* __restrict__ y,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      int64_t rows, int C, float eps) {
+  static_assert(sizeof(T) == 2, "ln_fwd16: 2-byte element types");
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int64_t row = ((int64_t)blockIdx.x * (NT / kWave) + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  if (row >= rows) return;  // (whole half-waves: the reductions below stay within the live half)
+  const int64_t base = row * C;
+  float v[NCH][8], g[NCH][8], b[NCH][8];
+  u32x4 xv[NCH], dv[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 8 * hl + 256 * k;
+    xv[k] = *reinterpret_cast<const u32x4*>(x + base + c);
+    if (RES) dv[k] = *reinterpret_cast<const u32x4*>(delta + base + c);
+    load8<W>(gamma + c, g[k]);
+    if (!RMS) load8<W>(beta + c, b[k]);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    unpack8v<T>(xv[k], v[k]);
+    if (RES) {
+      float d[8];
+      unpack8v<T>(dv[k], d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[k][e] += d[e];
+      store8<T>(xsum + base + 8 * hl + 256 * k, v[k]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[k][e] = round_to<T>(v[k][e]);  // normalise what was stored
+    }
+#pragma unroll
+    for (int e = 0; e < 8; e += 4) s += (v[k][e] + v[k][e + 1]) + (v[k][e + 2] + v[k][e + 3]);
+  }
+  const float mean = RMS ? 0.f : hsum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[k][e] - mean;
+      q = fmaf(d, d, q);
+    }
+  const float rstd = rsqrtf(hsum(q) / (float)C + eps);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = fmaf((v[k][e] - mean) * rstd, g[k][e], RMS ? 0.f : b[k][e]);
+    store8<T>(y + base + 8 * hl + 256 * k, o);
+  }
+  if (hl == 0) {
+    if (!RMS) mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
 template <typename T, typename W, bool RES, int NCH, bool RMS = false>
 __global__ __launch_bounds__(NT) void ln_bwd16_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                       const T* __restrict__ dres, const W* __restrict__ gamma,
@@ -688,6 +751,58 @@ static void reduce_into(const at::Tensor& part, int nparts, int ld, int W, int C
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
+// The 16-B forward (ln_fwd16_kernel) for 2-byte types, C a multiple of 256 (NCH = C / 256 in
+// {1, 2, 3, 4, 6, 8}) and 16-B aligned operands; false: use ln_fwd_kernel.  NBD_LN_FWD16=0 (A/B).
+template <bool RMS>
+static bool launch_fwd16(const at::Tensor& x, const c10::optional<at::Tensor>& delta, const at::Tensor& xsum,
+                         const at::Tensor& weight, const at::Tensor* bias, const at::Tensor& y, const at::Tensor& mean,
+                         const at::Tensor& rstd, int64_t rows, int64_t C, double eps, hipStream_t st) {
+  static const bool on = [] {
+    const char* e = std::getenv("NBD_LN_FWD16");
+    return e == nullptr || e[0] != '0';
+  }();
+  const auto dt = x.scalar_type();
+  if (!on || (dt != at::kBFloat16 && dt != at::kHalf) || weight.scalar_type() != dt || C % 256 != 0) return false;
+  const int nch = (int)(C / 256);
+  if (nch != 1 && nch != 2 && nch != 3 && nch != 4 && nch != 6 && nch != 8) return false;
+  const bool res = delta.has_value() && delta->defined();
+  auto a16 = [](const at::Tensor& t) { return !t.defined() || ((uintptr_t)t.data_ptr() & 15) == 0; };
+  if (!a16(x) || !a16(y) || !a16(weight) || (bias != nullptr && (bias->scalar_type() != dt || !a16(*bias))) ||
+      (res && (!a16(*delta) || !a16(xsum))))
+    return false;
+  const dim3 grid((unsigned)((rows + 7) / 8));
+  auto go = [&](auto t, auto nc) {
+    using T = decltype(t);
+    constexpr int N = decltype(nc)::value;
+    const T* dp = res ? static_cast<const T*>(delta->data_ptr()) : nullptr;
+    T* sp = res ? static_cast<T*>(xsum.data_ptr()) : nullptr;
+    const T* bp = bias != nullptr ? static_cast<const T*>(bias->data_ptr()) : nullptr;
+    float* mp = RMS ? nullptr : mean.data_ptr<float>();
+    if (res)
+      hipLaunchKernelGGL((ln_fwd16_kernel<T, T, true, N, RMS>), grid, dim3(NT), 0, st,
+                         static_cast<const T*>(x.data_ptr()), dp, sp, static_cast<const T*>(weight.data_ptr()), bp,
+                         static_cast<T*>(y.data_ptr()), mp, rstd.data_ptr<float>(), rows, (int)C, (float)eps);
+    else
+      hipLaunchKernelGGL((ln_fwd16_kernel<T, T, false, N, RMS>), grid, dim3(NT), 0, st,
+                         static_cast<const T*>(x.data_ptr()), dp, sp, static_cast<const T*>(weight.data_ptr()), bp,
+                         static_cast<T*>(y.data_ptr()), mp, rstd.data_ptr<float>(), rows, (int)C, (float)eps);
+  };
+  auto by_n = [&](auto t) {
+    switch (nch) {
+      case 1: go(t, std::integral_constant<int, 1>{}); break;
+      case 2: go(t, std::integral_constant<int, 2>{}); break;
+      case 3: go(t, std::integral_constant<int, 3>{}); break;
+      case 4: go(t, std::integral_constant<int, 4>{}); break;
+      case 6: go(t, std::integral_constant<int, 6>{}); break;
+      default: go(t, std::integral_constant<int, 8>{}); break;
+    }
+  };
+  if (dt == at::kBFloat16) by_n(bf16_t{});
+  else by_n(f16_t{});
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return true;
+}
+
 // returns (y, xsum or undefined, mean, rstd)
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ln_fwd_hip(const at::Tensor& x,
                                                                       const c10::optional<at::Tensor>& delta,
@@ -711,6 +826,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ln_fwd_hip(const at::
   if (rows == 0) return {y, xsum, mean, rstd};
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  if (launch_fwd16<false>(x, delta, xsum, weight, &bias, y, mean, rstd, rows, C, eps, st)) return {y, xsum, mean, rstd};
   const dim3 grid((unsigned)((rows + 3) / 4));
   dispatch_tw(x.scalar_type(), weight.scalar_type(), [&](auto t, auto w) {
    dispatch_nch(C, [&](auto nch) {
@@ -854,6 +970,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rms_fwd_hip(const at::Tensor& x, 
   if (rows == 0) return {y, xsum, rstd};
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  if (launch_fwd16<true>(x, delta, xsum, weight, nullptr, y, at::Tensor(), rstd, rows, C, eps, st)) return {y, xsum, rstd};
   const dim3 grid((unsigned)((rows + 3) / 4));
   dispatch_tw(x.scalar_type(), weight.scalar_type(), [&](auto t, auto w) {
    dispatch_nch(C, [&](auto nch) {

@@ -79,7 +79,7 @@ def test_embed_rms_norm_matches_separate_ops(dev, C):
 
 def test_tokpos_layer_norm_matches_separate_ops(dev):
     """ops.tokpos_layer_norm (GPT-2's input + first LayerNorm as one node) against
-    embedding_tok_pos + layer_norm: x0 and h bit-identical; token table (padded past the
+    embedding_tok_pos + layer_norm: x0 bit-identical, h equal to rounding; token table (padded past the
     vocabulary: zero gradient there), position table, weight and bias gradients equal to the
     two-op path's with both the residual and the norm gradient arriving."""
     g = torch.Generator(device="cpu").manual_seed(3)
@@ -105,7 +105,8 @@ def test_tokpos_layer_norm_matches_separate_ops(dev):
         torch.cuda.synchronize()
         outs.append((x, h, [p.grad for p in ps]))
     (x1, h1, g1), (x2, h2, g2) = outs
-    assert torch.equal(x1, x2) and torch.equal(h1, h2)
+    # (h: the separate LayerNorm may take the 16-B kernel, whose partial sums group differently)
+    assert torch.equal(x1, x2) and _rel(h1, h2) < 1e-2
     for a, r in zip(g1, g2):
         assert _rel(a, r) < 1e-2
     assert (g1[0][V:] == 0).all()
