@@ -1,6 +1,8 @@
 """LayerNorm / RMSNorm with fused residual adds, bias-gradient column sums, Linear (K8, K9, K11)."""
 from __future__ import annotations
 
+import os
+
 from ._lib import _require
 from .gemm import _native
 from .llama import _llama_fns
@@ -163,7 +165,7 @@ def add_rms_norm(x, delta, weight, eps: float = 1e-6):
 
 
 # the fused token embedding + first RMSNorm (NBD_EMBED_RMS=0: the two ops, A/B)
-_EMBED_RMS = __import__("os").environ.get("NBD_EMBED_RMS", "1") != "0"
+_EMBED_RMS = os.environ.get("NBD_EMBED_RMS", "1") != "0"
 
 
 def embed_rms_norm(ids, table, weight, eps: float = 1e-6):
