@@ -239,12 +239,24 @@ class GPT2(nn.Module):
         V = self.config.vocab_size
         return logits[..., :V] if logits.shape[-1] != V else logits
 
+    def _positions(self, T: int, device) -> torch.Tensor:
+        """``arange(T)`` on ``device``, kept between calls (one launch less per step; made only
+        outside a stream capture, so a captured graph never owns the kept tensor)."""
+        cache = self.__dict__.setdefault("_pos_cache", {})
+        key = (T, str(device))
+        p = cache.get(key)
+        if p is None:
+            p = torch.arange(T, device=device)
+            if not (p.is_cuda and torch.cuda.is_current_stream_capturing()):
+                cache[key] = p
+        return p
+
     def _trunk(self, idx: torch.Tensor, cache=None):
         """Final-normed hidden states [B, T, C] (and whether the HIP fast path ran); ``cache``
         (a ``generation.KVCache``) receives every layer's k / v."""
         B, T = idx.shape
         pos_fn = getattr(self, "position_ids", None)  # set by parallel.context (global positions)
-        pos = pos_fn(T, idx.device) if pos_fn is not None else torch.arange(T, device=idx.device)
+        pos = pos_fn(T, idx.device) if pos_fn is not None else self._positions(T, idx.device)
         c = self.config
         fused_in = (self._fast_ok(idx) and c.fused_norm and c.bias and c.n_embd % 8 == 0 and c.n_embd <= 2048
                     and T % 128 == 0 and c.n_layer > 0)
