@@ -138,6 +138,73 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(const G* __restrict__ g
   }
 }
 
+// Every bucket of FlatAdamW's step in one launch (adamw_flat_multi): workgroup w updates 256
+// 8-element groups of the bucket whose block range holds w (the last workgroup of a bucket also
+// its < 8 trailing elements) — the per-element math of adamw_flat_kernel<.., 1, false>, so the
+// update is bit-identical; one ramp and one tail instead of one per bucket.
+constexpr int kMaxBuckets = 16;
+template <typename G, typename P>
+struct BucketTable {
+  const G* grad[kMaxBuckets];
+  P* param[kMaxBuckets];
+  float* master[kMaxBuckets];
+  float* m[kMaxBuckets];
+  float* v[kMaxBuckets];
+  int64_t n[kMaxBuckets];
+  int block0[kMaxBuckets + 1];
+};
+
+template <typename G, typename P>
+__global__ __launch_bounds__(256) void adamw_multi_kernel(BucketTable<G, P> t, int nb,
+                                                          const float* __restrict__ gscale,
+                                                          const float* __restrict__ dstep,
+                                                          const float* __restrict__ dlr, AdamArgs a) {
+  if (gscale != nullptr) a.grad_scale *= *gscale;
+  device_hyper(a, dstep, dlr);
+  const int blk = (int)blockIdx.x;
+  int d = 0;  // block-uniform scan over <= 16 prefixes
+  while (d + 1 < nb && t.block0[d + 1] <= blk) ++d;
+  const int64_t n = t.n[d], nv = n / 8;
+  const G* grad = t.grad[d];
+  P* param = t.param[d];
+  float *master = t.master[d], *m = t.m[d], *v = t.v[d];
+  const int64_t k = (int64_t)(blk - t.block0[d]) * 256 + threadIdx.x;
+  if (k < nv) {
+    const int64_t i = k * 8;
+    float g[8], w[8], mm[8], vv[8];
+    load8<G>(grad + i, g);
+    load8<float>(master + i, w);
+    load8<float>(m + i, mm);
+    load8<float>(v + i, vv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gj = g[j] * a.grad_scale;
+      mm[j] = fmaf(a.beta1, mm[j], (1.f - a.beta1) * gj);
+      vv[j] = fmaf(a.beta2, vv[j], (1.f - a.beta2) * gj * gj);
+      const float denom = sqrtf(vv[j]) * a.inv_sqrt_bc2 + a.eps;
+      w[j] = w[j] * a.wd_factor - a.step_size * (mm[j] / denom);
+    }
+    store8<float>(master + i, w);
+    store8<float>(m + i, mm);
+    store8<float>(v + i, vv);
+    if (sizeof(P) == 2) store8_nt<P>(param + i, w);
+    else store8<P>(param + i, w);
+  }
+  if (blk == t.block0[d + 1] - 1) {  // the bucket's trailing elements
+    for (int64_t i = nv * 8 + threadIdx.x; i < n; i += 256) {
+      const float gj = Elem<G>::load(grad, i) * a.grad_scale;
+      const float mm = fmaf(a.beta1, m[i], (1.f - a.beta1) * gj);
+      const float vv = fmaf(a.beta2, v[i], (1.f - a.beta2) * gj * gj);
+      const float denom = sqrtf(vv) * a.inv_sqrt_bc2 + a.eps;
+      const float w = master[i] * a.wd_factor - a.step_size * (mm / denom);
+      m[i] = mm;
+      v[i] = vv;
+      master[i] = w;
+      Elem<P>::store(param, i, w);
+    }
+  }
+}
+
 // NBD_ADAMW_BLOCKS (A/B): grid cap in workgroups (default none: one thread per 8-element group —
 // 0.648 ms against 0.700 for the former 2048-block grid-stride default, 124 M parameters,
 // profiles/adamw_grid_r5.txt);
@@ -370,6 +437,99 @@ void adamw_tensors_hip(at::TensorList params, at::TensorList grads, at::TensorLi
   }
 }
 
+// All buckets in one adamw_multi_kernel launch when they allow it (<= 16 buckets, one gradient and
+// one parameter dtype, the default kernel variant); false: the caller loops over adamw_flat_hip,
+// which also validates every buffer.  NBD_ADAMW_MULTI=0 (A/B).
+static bool multi_launch(at::TensorList grads, at::TensorList params, at::TensorList masters, at::TensorList exp_avgs,
+                         at::TensorList exp_avg_sqs, double lr, double beta1, double beta2, double eps,
+                         double weight_decay, int64_t step, double grad_scale,
+                         const c10::optional<at::Tensor>& grad_scale_t, const c10::optional<at::Tensor>& step_t,
+                         const c10::optional<at::Tensor>& lr_t) {
+  static const bool on = [] {
+    const char* e = std::getenv("NBD_ADAMW_MULTI");
+    return e == nullptr || e[0] != '0';
+  }();
+  const size_t nb = params.size();
+  if (!on || nb < 2 || nb > (size_t)kMaxBuckets || adamw_env("NBD_ADAMW_VARIANT", 0) != 0 ||
+      adamw_env("NBD_ADAMW_BLOCKS", 0) > 0 || step < 1)
+    return false;
+  const auto gt = grads[0].scalar_type(), pt = params[0].scalar_type();
+  for (size_t i = 0; i < nb; ++i) {
+    const at::Tensor* ts[5] = {&grads[i], &params[i], &masters[i], &exp_avgs[i], &exp_avg_sqs[i]};
+    for (const at::Tensor* t : ts)
+      if (!t->is_cuda() || !t->is_contiguous() || (uintptr_t)t->data_ptr() % 16 != 0 ||
+          t->device() != params[0].device())
+        return false;
+    const int64_t n = params[i].numel();
+    if (grads[i].scalar_type() != gt || params[i].scalar_type() != pt || masters[i].scalar_type() != at::kFloat ||
+        exp_avgs[i].scalar_type() != at::kFloat || exp_avg_sqs[i].scalar_type() != at::kFloat ||
+        grads[i].numel() < n || masters[i].numel() != n || exp_avgs[i].numel() != n || exp_avg_sqs[i].numel() != n ||
+        n == 0)
+      return false;
+  }
+  auto dev_scalar = [](const c10::optional<at::Tensor>& t) -> const float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() == 1,
+                "adamw_flat_multi: step_t / lr_t / grad_scale_t must be 1-element float32 GPU tensors");
+    return t->data_ptr<float>();
+  };
+  const float* gs = dev_scalar(grad_scale_t);
+  const float* dstep = dev_scalar(step_t);
+  const float* dlr = dev_scalar(lr_t);
+  TORCH_CHECK((dstep == nullptr) == (dlr == nullptr), "adamw_flat_multi: step_t and lr_t go together (capturable mode)");
+  AdamArgs a;
+  a.weight_decay = (float)weight_decay;
+  a.lr = (float)lr;
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.wd_factor = (float)(1.0 - lr * weight_decay);
+  a.step_size = (float)(lr / (1.0 - std::pow(beta1, (double)step)));
+  a.inv_sqrt_bc2 = (float)(1.0 / std::sqrt(1.0 - std::pow(beta2, (double)step)));
+  a.grad_scale = (float)grad_scale;
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(params[0].device());
+  hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  bool done = false;
+  auto go = [&](auto gtag, auto ptag) {
+    using G = decltype(gtag);
+    using P = decltype(ptag);
+    BucketTable<G, P> t{};
+    int blocks = 0;
+    for (size_t i = 0; i < nb; ++i) {
+      t.grad[i] = static_cast<const G*>(grads[i].data_ptr());
+      t.param[i] = static_cast<P*>(params[i].data_ptr());
+      t.master[i] = masters[i].data_ptr<float>();
+      t.m[i] = exp_avgs[i].data_ptr<float>();
+      t.v[i] = exp_avg_sqs[i].data_ptr<float>();
+      t.n[i] = params[i].numel();
+      t.block0[i] = blocks;
+      const int64_t nbk = std::max<int64_t>(1, (t.n[i] / 8 + 255) / 256);
+      TORCH_CHECK(blocks + nbk < (int64_t)INT32_MAX / 2, "adamw_flat_multi: too many workgroups");
+      blocks += (int)nbk;
+    }
+    t.block0[nb] = blocks;
+    hipLaunchKernelGGL((adamw_multi_kernel<G, P>), dim3((unsigned)blocks), dim3(256), 0, st, t, (int)nb, gs, dstep,
+                       dlr, a);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    done = true;
+  };
+  auto by_p = [&](auto gtag) {
+    switch (pt) {
+      case at::kFloat: go(gtag, float{}); break;
+      case at::kBFloat16: go(gtag, bf16_t{}); break;
+      case at::kHalf: go(gtag, f16_t{}); break;
+      default: break;
+    }
+  };
+  switch (gt) {
+    case at::kFloat: by_p(float{}); break;
+    case at::kBFloat16: by_p(bf16_t{}); break;
+    case at::kHalf: by_p(f16_t{}); break;
+    default: break;
+  }
+  return done;
+}
+
 // Every bucket's update from one call (FlatAdamW.step's fast path): the same per-bucket kernels
 // in bucket order, without a Python round trip and an op dispatch per bucket (an eager small-model
 // step is host-bound: docs/FINDINGS.md §27).
@@ -381,6 +541,9 @@ void adamw_flat_multi_hip(at::TensorList grads, at::TensorList params, at::Tenso
   const size_t n = params.size();
   TORCH_CHECK(grads.size() == n && masters.size() == n && exp_avgs.size() == n && exp_avg_sqs.size() == n,
               "adamw_flat_multi: one gradient, master, exp_avg and exp_avg_sq per parameter buffer");
+  if (multi_launch(grads, params, masters, exp_avgs, exp_avg_sqs, lr, beta1, beta2, eps, weight_decay, step,
+                   grad_scale, grad_scale_t, step_t, lr_t))
+    return;
   for (size_t i = 0; i < n; ++i)
     adamw_flat_hip(grads[i], params[i], masters[i], exp_avgs[i], exp_avg_sqs[i], lr, beta1, beta2, eps, weight_decay,
                    step, grad_scale, grad_scale_t, step_t, lr_t);

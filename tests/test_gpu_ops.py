@@ -153,6 +153,41 @@ def test_adamw_flat_matches_reference(dev, gdt, pdt, n, clip):
     assert torch.equal(gpu[3].cpu(), gpu[0].cpu().to(DT[pdt]))
 
 
+@pytest.mark.parametrize("capturable", [False, True])
+def test_adamw_flat_multi_one_launch_matches_per_bucket(dev, capturable):
+    """adamw_flat_multi's single launch over all buckets (adamw_multi_kernel; sizes with and
+    without a < 8-element tail, one bucket of 7 elements) bit-identical to one adamw_flat launch per
+    bucket, incl. the device-side clip coefficient and the capturable step / lr scalars."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    sizes = [1 << 20, 7, 16389, 4096 + 3, (1 << 18) + 8]
+    coef = torch.tensor([0.37], device=dev)
+    sets = []
+    for _ in range(2):
+        bufs = []
+        for n in sizes:
+            master = torch.randn(n, generator=g).to(dev) if not sets else sets[0][len(bufs)][1].clone()
+            bufs.append([None, master, torch.zeros(n, device=dev), torch.zeros(n, device=dev),
+                         master.to(torch.bfloat16)])
+        sets.append(bufs)
+    grads = [[torch.randn(n, generator=g).to(dev, torch.bfloat16) for n in sizes] for _ in range(3)]
+    st = [torch.zeros(1, device=dev) for _ in range(2)]
+    lr_t = [torch.full((1,), 1e-3, device=dev) for _ in range(2)]
+    for step, gr in enumerate(grads, 1):
+        a, b = sets
+        for t in st:
+            t.add_(1.0)
+        torch.ops.nbd.adamw_flat_multi(gr, [x[4] for x in a], [x[1] for x in a], [x[2] for x in a],
+                                       [x[3] for x in a], 1e-3, 0.9, 0.95, 1e-8, 0.1, step, 0.5, coef,
+                                       st[0] if capturable else None, lr_t[0] if capturable else None)
+        for i, x in enumerate(b):
+            ops.adamw_flat(gr[i], x[4], x[1], x[2], x[3], 1e-3, 0.9, 0.95, 1e-8, 0.1, step, 0.5, coef,
+                           step_t=st[1] if capturable else None, lr_t=lr_t[1] if capturable else None)
+    torch.cuda.synchronize()
+    for x, y in zip(*sets):
+        for u, v in zip(x[1:], y[1:]):
+            assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("dt", ["f32", "bf16", "f16"])
 @pytest.mark.parametrize("V", [1, 7, 64, 1000, 50257])
 @pytest.mark.parametrize("inplace", [False, True])
